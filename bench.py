@@ -1,0 +1,260 @@
+#!/usr/bin/env python3
+"""bench.py -- batched 64x64-torus LifeState::Step() on MI355X.
+
+Headline workload (BASELINE.json configs[1], "config 2"): 1M random-fill
+64x64 universes x 1 generation per step, per GPU.  A step is one launch of
+the HIP step kernel over the rank's whole shard (device-resident, ping-pong
+buffers, so the state keeps evolving).  With N GPUs (one process per GPU,
+launched by torch.distributed.run) every rank steps its own contiguous shard
+of the global universe array -- no collective on the data path ("weak"
+scaling: per-GPU work fixed).  After the timed region the per-universe hashes
+are all-gathered over RCCL (result collection, timed and reported separately).
+
+Prints ONE JSON line on rank 0 (contract in the task brief / DESIGN.md).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "64x64 universe-generations/sec (+ cell-updates/sec) at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
+VALU_PEAK_TOPS = 39.3216    # 256 CU x 64 lanes x 2.4 GHz int32 ops (1 op/lane/clk)
+BYTES_PER_UNIVERSE_GEN = 1024  # 512 B read + 512 B write
+OPS_PER_UNIVERSE_GEN = 2688    # reference's ~21 u64 ops/column = 42 int32 x 64
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse_args():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--universes", type=int, default=1 << 20, help="universes per rank (config 2: 1M)")
+    p.add_argument("--gens-per-step", type=int, default=1)
+    p.add_argument("--seed", type=int, default=2)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=2.0, help="wall budget of the CPU baseline")
+    p.add_argument("--no-secondary", action="store_true", help="skip the config-3 side measurement")
+    p.add_argument("--no-verify", action="store_true")
+    return p.parse_args()
+
+
+def timed_launches(hip, bufs, steps, gens, stream):
+    """Run `steps` ping-pong launches; return (per-launch ms list, last buffer index)."""
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(steps)]
+    cur = 0
+    for k in range(steps):
+        evs[k][0].record(stream)
+        hip.step(bufs[cur], out=bufs[1 - cur], generations=gens, stream=stream)
+        evs[k][1].record(stream)
+        cur = 1 - cur
+    return evs, cur
+
+
+def cpu_baseline(x_host: np.ndarray, seconds: float):
+    """Reference CPU Step() (oracle/_ref, else the C port) on host cores."""
+    from oracle.oracle import Port, Ref
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    threads = max(1, min(threads, 16))
+    if Ref.available():
+        o, kind = Ref(), "reference"
+        run = lambda a, t: o.step_batch(a, 1, nthreads=t)  # noqa: E731
+    else:
+        o, kind = Port(), "port"
+        run = lambda a, t: o.step_batch(a, 1, nthreads=t)  # noqa: E731
+    n = x_host.shape[0]
+    out = {}
+    for t in sorted({1, threads}):
+        run(x_host[: min(n, 4096)], t)  # warm
+        passes, t0 = 0, time.perf_counter()
+        while True:
+            run(x_host, t)
+            passes += 1
+            el = time.perf_counter() - t0
+            if el >= seconds / 2:
+                break
+        out[t] = (n * passes / el, passes, el)
+    v, passes, el = out[threads]
+    cpu = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), "")
+    except OSError:
+        pass
+    return {
+        "value": v, "unit": "universe-gen/s", "cores": threads, "kind": kind,
+        "sample": f"config-2 input ({n} universes) x 1 gen, {passes} passes in {el:.2f}s, "
+                  f"{threads} threads, contiguous slices; CPU: {cpu}",
+        "value_1thread": out[1][0],
+    }
+
+
+def secondary_config3(hip, device, stream):
+    """Config 3: 64K universes x 1024 generations, state resident in VGPRs."""
+    n, gens = 1 << 16, 1024
+    a = hip.fill_random(n, seed=3, device=device, stream=stream)
+    b = torch.empty_like(a)
+    hip.step(a, out=b, generations=gens, stream=stream)  # warm
+    reps, ms = 5, []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        hip.step(a, out=b, generations=gens, stream=stream)
+        e1.record(stream)
+        e1.synchronize()
+        ms.append(e0.elapsed_time(e1))
+    t = min(ms) / 1e3
+    gps = n * gens / t
+    return {"workload": "config3: 64K universes x 1024 generations (one launch)",
+            "value": gps, "unit": "universe-gen/s", "cell_updates_per_s": gps * 4096,
+            "kernel_ms": min(ms), "kernel_ms_all": ms,
+            "roofline": {"bound": "valu", "achieved": OPS_PER_UNIVERSE_GEN * gps / 1e12,
+                         "peak": VALU_PEAK_TOPS, "unit": "Tops/s (reference-algorithm int32 ops)",
+                         "frac": OPS_PER_UNIVERSE_GEN * gps / 1e12 / VALU_PEAK_TOPS}}
+
+
+def load_pmc_traffic(n: int):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if it matches."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("universes") == n:
+            return d.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+    except (OSError, ValueError):
+        pass
+    return None, None
+
+
+def main():
+    args = parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+    import lifeapi_amd.hip as hip
+
+    n, gens = args.universes, args.gens_per_step
+    first = rank * n                         # contiguous shard of the global array
+    stream = torch.cuda.current_stream(device)
+    a = hip.fill_random(n, seed=args.seed, first_universe=first, device=device, stream=stream)
+    b = torch.empty_like(a)
+    x_head = a[: min(n, 2048)].cpu().numpy().view(np.uint64).copy()  # for the parity spot check
+    want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
+    x_full = a.cpu().numpy().view(np.uint64).copy() if want_cpu else None
+    bufs = [a, b]
+
+    # warmup (untimed)
+    _, cur = timed_launches(hip, bufs, args.warmup, gens, stream)
+    bufs = [bufs[cur], bufs[1 - cur]]
+    torch.cuda.synchronize(device)
+
+    # timed region: barrier + sync on both sides, max over ranks
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    evs, cur = timed_launches(hip, bufs, args.steps, gens, stream)
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    launch_ms = [e0.elapsed_time(e1) for e0, e1 in evs]
+    final = bufs[cur]
+
+    # result collection (not in the timed region): all-gather per-universe hashes
+    h = hip.hashes(final, stream=stream)
+    torch.cuda.synchronize(device)
+    collect = None
+    if world > 1:
+        gathered = torch.empty(world * n, dtype=torch.int64, device=device)
+        dist.barrier()
+        c0 = time.perf_counter()
+        dist.all_gather_into_tensor(gathered, h)
+        torch.cuda.synchronize(device)
+        cms = (time.perf_counter() - c0) * 1e3
+        collect = {"op": "all_gather(per-universe hash, RCCL)", "bytes_per_rank": n * 8,
+                   "ms": cms}
+
+    # parity spot check of the timed kernel's output against the oracle
+    verified = None
+    if not args.no_verify:
+        from oracle.oracle import Port
+        m = x_head.shape[0]
+        total_gens = (args.warmup + args.steps) * gens
+        got = final[:m].cpu().numpy().view(np.uint64)
+        want = Port().step_batch(x_head, total_gens, nthreads=8)
+        ok = bool((got == want).all())
+        if world > 1:
+            f = torch.tensor([0 if ok else 1], device=device)
+            dist.all_reduce(f)
+            ok = int(f.item()) == 0
+        verified = {"ok": ok, "universes_checked_per_rank": m, "generations": total_gens}
+
+    secondary = None
+    if rank == 0 and world == 1 and not args.no_secondary:
+        secondary = {"config3": secondary_config3(hip, device, stream)}
+
+    cpu = None
+    if want_cpu:
+        cpu = cpu_baseline(x_full, args.cpu_seconds)
+
+    if world > 1:
+        dist.barrier()
+    if rank == 0:
+        total = n * world * gens * args.steps
+        value = total / elapsed
+        avg_launch = sum(launch_ms) / len(launch_ms)
+        achieved = n * gens * BYTES_PER_UNIVERSE_GEN / (avg_launch / 1e3) / 1e9 if gens == 1 else None
+        traffic, tsrc = load_pmc_traffic(n)
+        cfg = hip.default_cfg(gens).as_dict()
+        line = {
+            "metric": METRIC, "value": value, "unit": "universe-gen/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+            "data": f"synthetic: splitmix64 uniform-fill universes (seed {args.seed}), generated on device",
+            "config": {"workload": f"config2: {n} random-fill 64x64 universes x {gens} generation "
+                                   f"per step per GPU", "universes_per_gpu": n,
+                       "global_universes": n * world, "gens_per_step": gens,
+                       "parallelism": f"dp{world} (contiguous universe shards, no collective)",
+                       "launch_cfg": cfg},
+            "cell_updates_per_s": value * 4096,
+            "kernel_ms_avg": avg_launch, "kernel_ms_min": min(launch_ms),
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                         "traffic": traffic, "traffic_source": tsrc,
+                         "algorithmic_bytes_per_launch": n * gens * BYTES_PER_UNIVERSE_GEN},
+            "cpu_baseline": cpu,
+            "verified": verified,
+            "collect": collect,
+            "secondary": secondary,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,114 @@
+/*
+ * lifeapi_hip.h -- C ABI of the MI355X (gfx950) batched LifeState::Step().
+ *
+ * The reference (scorbiclife/LifeAPI) is a header-only C++ library with no
+ * FFI; its "operator API" is the inline member functions of LifeState.  Each
+ * entry point below is the batched, device-resident replacement for one of
+ * them, cited as file:line into the reference snapshot:
+ *
+ *   lifeapi_step_batch[_dev]     LifeState::Step()          LifeAPI.hpp:1196-1216
+ *                                LifeState::Step(unsigned)  LifeAPI.hpp:877-881
+ *                                LifeState::Stepped(unsigned) LifeAPI.hpp:882-886
+ *   lifeapi_pop_batch_dev        LifeState::GetPop()        LifeAPI.hpp:290-298
+ *   lifeapi_contains_batch_dev   LifeState::Contains(const LifeTarget&)
+ *                                                           LifeTarget.hpp:44-51
+ *   lifeapi_fill_random_dev      LifeState::RandomState()   LifeAPI.hpp:63-69
+ *                                (seeded splitmix64; mode 1 = RandomState's
+ *                                 [2^61, 2^62) column distribution)
+ *   lifeapi_hash_batch_dev       (build-defined digest; stands in for
+ *                                 LifeState::GetHash, LifeAPI.hpp:373, which
+ *                                 needs the un-vendored xxHash)
+ *
+ * Data layout: a universe is the reference's LifeState, i.e. uint64_t[64]
+ * (word x = column x, bit y = row y; LifeAPI.hpp:39-40,131), 512 bytes.  A
+ * batch is a contiguous array of n universes = n*64 words.  Pointers must be
+ * 8-byte aligned (LifeState is 64-byte aligned, so a LifeState[] always is).
+ * in == out is allowed (in-place, like Step()); any other overlap is rejected.
+ *
+ * Conventions: every function returns 0 on success; a negative LIFEAPI_E_*
+ * for a caller error; a positive hipError_t from the HIP runtime otherwise.
+ * lifeapi_last_error() gives this thread's message for the last failure.
+ * Nothing throws across this ABI.  The library owns only internal staging
+ * buffers and streams (one per device, created lazily); the caller owns all
+ * arguments.  *_dev functions take device pointers and enqueue on `stream`
+ * (a hipStream_t; NULL = the null stream) without synchronising.  The host
+ * functions are synchronous and thread-safe (one lock per device).
+ */
+#ifndef LIFEAPI_HIP_H
+#define LIFEAPI_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LIFEAPI_ABI_VERSION 1
+
+#define LIFEAPI_OK 0
+#define LIFEAPI_E_INVALID (-1)   /* null/misaligned pointer, overlap, bad cfg */
+#define LIFEAPI_E_NODEVICE (-2)  /* no gfx950 device / bad device index */
+#define LIFEAPI_E_NOKERNEL (-3)  /* code object for this GPU missing */
+
+/* neighbour-column exchange used inside a wavefront */
+#define LIFEAPI_XCHG_DPP 0    /* DPP wave_ror:1 / wave_rol:1 (default) */
+#define LIFEAPI_XCHG_LDS 1    /* stage the column sums through LDS */
+#define LIFEAPI_XCHG_BPERM 2  /* ds_bpermute lane gather */
+
+typedef struct lifeapi_launch_cfg {
+  int xchg;                /* LIFEAPI_XCHG_*                                */
+  int universes_per_wave;  /* 1, 2, 4 or 8 universes in flight per wave     */
+  int blocks_per_cu;       /* grid = min(needed, CUs * blocks_per_cu); 0=auto */
+  int nontemporal;         /* 1: nt loads/stores (streaming, 1 generation)  */
+  int rule;                /* 0: adder network (bitop3), 1: plain and/or/xor */
+} lifeapi_launch_cfg;
+
+int lifeapi_abi_version(void);
+const char *lifeapi_last_error(void);
+int lifeapi_device_count(void);
+/* fills the default launch configuration (what a NULL cfg means) */
+void lifeapi_default_cfg(lifeapi_launch_cfg *cfg, uint32_t generations);
+
+/* ---- device-resident, stream-ordered (the hot path) -------------------- */
+
+/* out[u] = in[u] stepped `generations` times (0 = copy), for u < n.       */
+int lifeapi_step_batch_dev(const uint64_t *d_in, uint64_t *d_out, size_t n,
+                           uint32_t generations, void *stream);
+int lifeapi_step_batch_dev_cfg(const uint64_t *d_in, uint64_t *d_out, size_t n,
+                               uint32_t generations, void *stream,
+                               const lifeapi_launch_cfg *cfg);
+/* d_pop[u] = population of universe u                                     */
+int lifeapi_pop_batch_dev(const uint64_t *d_states, uint32_t *d_pop, size_t n, void *stream);
+/* d_hash[u] = build-defined 64-bit hash of universe u     */
+int lifeapi_hash_batch_dev(const uint64_t *d_states, uint64_t *d_hash, size_t n, void *stream);
+/* d_out[u] = Contains(target) for target = (wanted, unwanted), both device
+ * pointers to 64 words                                                    */
+int lifeapi_contains_batch_dev(const uint64_t *d_states, const uint64_t *d_wanted,
+                               const uint64_t *d_unwanted, uint8_t *d_out, size_t n,
+                               void *stream);
+/* fused Step^gens + Contains: d_out[u] = first generation g in 1..gens at
+ * which Stepped(g) contains the target, or 0 if none; d_final (may be NULL)
+ * receives Stepped(gens)                                                  */
+int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
+                                    const uint64_t *d_wanted, const uint64_t *d_unwanted,
+                                    uint32_t *d_first_gen, size_t n, uint32_t generations,
+                                    void *stream);
+/* synthetic universes: word w = u*64+x (u counted from first_universe) is
+ * splitmix64(seed + (w+1)*0x9E3779B97F4A7C15); mode 1 maps each column to
+ * [2^61, 2^62) like RandomState()                                         */
+int lifeapi_fill_random_dev(uint64_t *d_out, size_t n, uint64_t seed,
+                            uint64_t first_universe, int mode, void *stream);
+
+/* ---- host pointers, synchronous ----------------------------------------- */
+
+/* Stages through device memory of `device` (or of every visible device,
+ * contiguous shards, when device == -1).                                  */
+int lifeapi_step_batch(const uint64_t *in, uint64_t *out, size_t n, uint32_t generations,
+                       int device);
+int lifeapi_pop_batch(const uint64_t *states, uint32_t *pop, size_t n, int device);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LIFEAPI_HIP_H */

@@ -1,0 +1,648 @@
+// lifeapi_hip.hip -- MI355X (gfx950) batched LifeState::Step() and friends.
+//
+// One 64-lane wavefront steps one 64x64 torus universe: lane x owns column x
+// (the reference's state[x], LifeAPI.hpp:39-40) as two 32-bit VGPRs.  The
+// vertical (in-column) neighbours are a 1-bit rotate of the lane's own word
+// (v_alignbit_b32); the horizontal neighbours are the adjacent lanes' column
+// sums, fetched with DPP wave_ror:1 / wave_rol:1 (64-lane rotates, so the torus
+// wrap at columns 0/63 is free), or -- as ablations -- through LDS or
+// ds_bpermute.  The B3/S23 rule is the reference's bitsliced adder network
+// (CountRows LifeAPI.hpp:897-907 feeding the FullAdd form of StepAlt,
+// LifeAPI.hpp:1218-1254, which the reference proves equal to Step()'s
+// Rokicki form in tests/StepAltTest.cpp:5-13), evaluated with gfx950's
+// 3-input v_bitop3_b32.  A wave keeps U universes in flight; the grid
+// strides over the batch.  No MFMA: the work is pure integer/bitwise.
+//
+// All entry points are the C ABI in include/lifeapi_hip.h.
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "lifeapi_hip.h"
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr int kBlock = 256;
+constexpr int kWavesPerBlock = kBlock / kWave;
+constexpr uint64_t kGolden = 0x9E3779B97F4A7C15ULL;
+
+// ------------------------------------------------------------------------
+// lane-level primitives
+// ------------------------------------------------------------------------
+
+struct W {  // one column word, split in VGPR halves: bits 0-31 / 32-63
+  uint32_t lo, hi;
+};
+
+__device__ __forceinline__ W split(uint64_t v) { return W{(uint32_t)v, (uint32_t)(v >> 32)}; }
+__device__ __forceinline__ uint64_t join(W w) { return (uint64_t)w.lo | ((uint64_t)w.hi << 32); }
+
+// 64-bit rotates by one row: rotl(a,1) (cell y <- y-1) and rotr(a,1).
+__device__ __forceinline__ W rot_up(W a) {
+  return W{__builtin_amdgcn_alignbit(a.lo, a.hi, 31), __builtin_amdgcn_alignbit(a.hi, a.lo, 31)};
+}
+__device__ __forceinline__ W rot_dn(W a) {
+  return W{__builtin_amdgcn_alignbit(a.hi, a.lo, 1), __builtin_amdgcn_alignbit(a.lo, a.hi, 1)};
+}
+
+// v_bitop3_b32 truth tables: bit i of the table is f(bit i of 0xF0, 0xCC, 0xAA)
+// for (src0, src1, src2).
+constexpr uint32_t TA = 0xF0, TB = 0xCC, TC = 0xAA;
+constexpr uint32_t kXor3 = (TA ^ TB ^ TC) & 0xFF;                     // 0x96
+constexpr uint32_t kMaj = ((TA & TB) | (TA & TC) | (TB & TC)) & 0xFF;  // 0xE8
+constexpr uint32_t kCarry2 = (TA ^ (TB & TC)) & 0xFF;                 // a ^ (b & c)
+constexpr uint32_t kLive = ((TA ^ TB) & (TC | TA)) & 0xFF;            // (a ^ b) & (c | a)
+
+template <uint32_t TT>
+__device__ __forceinline__ uint32_t lut3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, TT);
+}
+template <uint32_t TT>
+__device__ __forceinline__ W lut3(W a, W b, W c) {
+  return W{lut3<TT>(a.lo, b.lo, c.lo), lut3<TT>(a.hi, b.hi, c.hi)};
+}
+
+// ------------------------------------------------------------------------
+// neighbour-column exchange (lane x <- lanes x-1 and x+1, mod 64)
+// ------------------------------------------------------------------------
+
+enum Xchg { XDPP = LIFEAPI_XCHG_DPP, XLDS = LIFEAPI_XCHG_LDS, XBPERM = LIFEAPI_XCHG_BPERM };
+
+// A full-wave rotate has no out-of-range source lane, so bound_ctrl (read 0
+// for invalid lanes) never fires; it lets the compiler skip the old-value init.
+__device__ __forceinline__ uint32_t dpp_prev(uint32_t v) {  // wave_ror:1
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x13C, 0xF, 0xF, true);
+}
+__device__ __forceinline__ uint32_t dpp_next(uint32_t v) {  // wave_rol:1
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x134, 0xF, 0xF, true);
+}
+
+// slot: 128 words of this wave's LDS scratch (only used by XLDS)
+template <int X>
+__device__ __forceinline__ void neighbours(W c0, W c1, W &L0, W &R0, W &L1, W &R1,
+                                           uint64_t *slot, int lane) {
+  if constexpr (X == XDPP) {
+    L0 = W{dpp_prev(c0.lo), dpp_prev(c0.hi)};
+    R0 = W{dpp_next(c0.lo), dpp_next(c0.hi)};
+    L1 = W{dpp_prev(c1.lo), dpp_prev(c1.hi)};
+    R1 = W{dpp_next(c1.lo), dpp_next(c1.hi)};
+  } else if constexpr (X == XBPERM) {
+    const int ap = ((lane + kWave - 1) & (kWave - 1)) << 2;
+    const int an = ((lane + 1) & (kWave - 1)) << 2;
+    L0 = W{(uint32_t)__builtin_amdgcn_ds_bpermute(ap, (int)c0.lo),
+           (uint32_t)__builtin_amdgcn_ds_bpermute(ap, (int)c0.hi)};
+    R0 = W{(uint32_t)__builtin_amdgcn_ds_bpermute(an, (int)c0.lo),
+           (uint32_t)__builtin_amdgcn_ds_bpermute(an, (int)c0.hi)};
+    L1 = W{(uint32_t)__builtin_amdgcn_ds_bpermute(ap, (int)c1.lo),
+           (uint32_t)__builtin_amdgcn_ds_bpermute(ap, (int)c1.hi)};
+    R1 = W{(uint32_t)__builtin_amdgcn_ds_bpermute(an, (int)c1.lo),
+           (uint32_t)__builtin_amdgcn_ds_bpermute(an, (int)c1.hi)};
+  } else {
+    // Stage the two column-sum planes through LDS: [0,64) plane 0, [64,128)
+    // plane 1, one 8-byte word per lane (ds_write_b64 / ds_read_b64, bank-
+    // conflict free: consecutive lanes, consecutive 8-byte words).  DS ops of
+    // one wave complete in order, so a wave only needs compiler ordering.
+    volatile uint64_t *s = slot;
+    s[lane] = join(c0);
+    s[kWave + lane] = join(c1);
+    __builtin_amdgcn_wave_barrier();
+    const int xp = (lane + kWave - 1) & (kWave - 1), xn = (lane + 1) & (kWave - 1);
+    L0 = split(s[xp]);
+    R0 = split(s[xn]);
+    L1 = split(s[kWave + xp]);
+    R1 = split(s[kWave + xn]);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// ------------------------------------------------------------------------
+// one generation of one universe (this lane's column)
+// ------------------------------------------------------------------------
+
+template <int X, int RULE>
+__device__ __forceinline__ W life_gen(W a, uint64_t *slot, int lane) {
+  const W up = rot_up(a), dn = rot_dn(a);
+  if constexpr (RULE == 0) {
+    // CountRows (LifeAPI.hpp:897-907): vertical 3-sum as two planes
+    const W c0 = lut3<kXor3>(up, dn, a);
+    const W c1 = lut3<kMaj>(up, dn, a);
+    W L0, R0, L1, R1;
+    neighbours<X>(c0, c1, L0, R0, L1, R1, slot, lane);
+    // FullAdd x2 (LifeAPI.hpp:826-833, StepAlt :1246-1249): 3x3 inclusive
+    // count = fs + 2(fc + cs) + 4cc
+    const W fs = lut3<kXor3>(L0, c0, R0), fc = lut3<kMaj>(L0, c0, R0);
+    const W cs = lut3<kXor3>(L1, c1, R1), cc = lut3<kMaj>(L1, c1, R1);
+    // StepAlt :1251-1252: cc ^= fc & cs;  next = (fs^cc) & (fc^cs^cc) & (a|fs)
+    const W b2 = lut3<kCarry2>(cc, fc, cs);
+    const W p = lut3<kLive>(fs, b2, a);
+    const W q = lut3<kXor3>(fc, cs, b2);
+    return W{p.lo & q.lo, p.hi & q.hi};
+  } else {
+    // the same network in plain and/or/xor (the compiler folds the DPP moves
+    // into v_*_dpp consumers); kept as an ablation of the bitop3 form
+    const uint64_t av = join(a), u = join(up), d = join(dn);
+    const uint64_t c0v = u ^ d ^ av, c1v = (u & d) | ((u ^ d) & av);
+    W L0, R0, L1, R1;
+    neighbours<X>(split(c0v), split(c1v), L0, R0, L1, R1, slot, lane);
+    const uint64_t l0 = join(L0), r0 = join(R0), l1 = join(L1), r1 = join(R1);
+    const uint64_t h0 = l0 ^ c0v, h1 = l1 ^ c1v;
+    const uint64_t fs = h0 ^ r0, fc = (l0 & c0v) | (r0 & h0);
+    const uint64_t cs = h1 ^ r1;
+    uint64_t cc = (l1 & c1v) | (r1 & h1);
+    cc ^= fc & cs;
+    return split((fs ^ cc) & (fc ^ cs ^ cc) & (av | fs));
+  }
+}
+
+template <bool NT>
+__device__ __forceinline__ W ld(const uint64_t *p) {
+  if constexpr (NT) return split(__builtin_nontemporal_load(p));
+  else return split(*p);
+}
+template <bool NT>
+__device__ __forceinline__ void st(uint64_t *p, W v) {
+  if constexpr (NT) __builtin_nontemporal_store(join(v), p);
+  else *p = join(v);
+}
+
+// ------------------------------------------------------------------------
+// kernels
+// ------------------------------------------------------------------------
+
+// out[u] = in[u] stepped `gens` times.  Wave w of the grid takes groups of U
+// consecutive universes, grid-strided.  All branches are wave-uniform.
+template <int X, int U, bool NT, int RULE>
+__global__ __launch_bounds__(kBlock) void k_step(const uint64_t *__restrict__ in,
+                                                 uint64_t *__restrict__ out, uint64_t n,
+                                                 uint32_t gens) {
+  __shared__ uint64_t lds[X == XLDS ? kWavesPerBlock * U * 2 * kWave : 1];
+  const int lane = threadIdx.x & (kWave - 1);
+  // wave index in the block, made provably wave-uniform so that the tail
+  // tests below are scalar branches
+  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock * U;
+  for (uint64_t u0 = ((uint64_t)blockIdx.x * kWavesPerBlock + wib) * U; u0 < n; u0 += stride) {
+    W a[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k)
+      a[k] = (u0 + k < n) ? ld<NT>(in + (u0 + k) * kWave + lane) : W{0u, 0u};
+    for (uint32_t g = 0; g < gens; ++g) {
+#pragma unroll
+      for (int k = 0; k < U; ++k)
+        a[k] = life_gen<X, RULE>(a[k], lds + (wib * U + k) * 2 * kWave, lane);
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k)
+      if (u0 + k < n) st<NT>(out + (u0 + k) * kWave + lane, a[k]);
+  }
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+  return v;
+}
+
+// GetPop (LifeAPI.hpp:290-298), one wave per universe
+__global__ __launch_bounds__(kBlock) void k_pop(const uint64_t *__restrict__ s,
+                                                uint32_t *__restrict__ pop, uint64_t n) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock;
+  for (uint64_t u = (uint64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave; u < n; u += stride) {
+    const uint32_t c = wave_sum_u32((uint32_t)__popcll(s[u * kWave + lane]));
+    if (lane == 0) pop[u] = c;
+  }
+}
+
+// build-defined universe hash: mix(sum_x mix(s[x] + (x+1)*G))
+__global__ __launch_bounds__(kBlock) void k_hash(const uint64_t *__restrict__ s,
+                                                 uint64_t *__restrict__ h, uint64_t n) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock;
+  for (uint64_t u = (uint64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave; u < n; u += stride) {
+    const uint64_t m = mix64(s[u * kWave + lane] + (uint64_t)(lane + 1) * kGolden);
+    const uint64_t t = wave_sum_u64(m);
+    if (lane == 0) h[u] = mix64(t);
+  }
+}
+
+// Contains(LifeTarget) (LifeTarget.hpp:44-51): (s ^ w) & (w | u) == 0 on all columns
+__device__ __forceinline__ bool wave_contains(W s, W w, W u) {
+  const uint32_t dlo = (s.lo ^ w.lo) & (w.lo | u.lo), dhi = (s.hi ^ w.hi) & (w.hi | u.hi);
+  return __ballot((dlo | dhi) != 0u) == 0ull;
+}
+
+__global__ __launch_bounds__(kBlock) void k_contains(const uint64_t *__restrict__ s,
+                                                     const uint64_t *__restrict__ wanted,
+                                                     const uint64_t *__restrict__ unwanted,
+                                                     uint8_t *__restrict__ out, uint64_t n) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const W w = split(wanted[lane]), uw = split(unwanted[lane]);
+  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock;
+  for (uint64_t u = (uint64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave; u < n; u += stride) {
+    const bool c = wave_contains(split(s[u * kWave + lane]), w, uw);
+    if (lane == 0) out[u] = c ? 1 : 0;
+  }
+}
+
+// Step + Contains fused: first generation in 1..gens whose state contains the
+// target (0 = never); the state keeps stepping to `gens` for d_final.
+__global__ __launch_bounds__(kBlock) void k_step_contains(const uint64_t *__restrict__ in,
+                                                          uint64_t *__restrict__ fin,
+                                                          const uint64_t *__restrict__ wanted,
+                                                          const uint64_t *__restrict__ unwanted,
+                                                          uint32_t *__restrict__ first,
+                                                          uint64_t n, uint32_t gens) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const W w = split(wanted[lane]), uw = split(unwanted[lane]);
+  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock;
+  for (uint64_t u = (uint64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave; u < n; u += stride) {
+    W a = split(in[u * kWave + lane]);
+    uint32_t hit = 0;
+    for (uint32_t g = 1; g <= gens; ++g) {
+      a = life_gen<XDPP, 0>(a, nullptr, lane);
+      if (hit == 0 && wave_contains(a, w, uw)) hit = g;
+    }
+    if (fin) fin[u * kWave + lane] = join(a);
+    if (lane == 0) first[u] = hit;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_fill(uint64_t *__restrict__ out, uint64_t nwords,
+                                                 uint64_t seed, uint64_t first_word, int mode) {
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < nwords; i += stride) {
+    uint64_t v = mix64(seed + (first_word + i + 1) * kGolden);
+    if (mode == 1) v = (v & ((1ULL << 61) - 1)) | (1ULL << 61);
+    out[i] = v;
+  }
+}
+
+// ------------------------------------------------------------------------
+// host side: errors, device info, dispatch
+// ------------------------------------------------------------------------
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, const char *arg = nullptr) {
+  char buf[512];
+  std::snprintf(buf, sizeof buf, fmt, arg ? arg : "");
+  g_err = buf;
+  return code;
+}
+int fail_hip(hipError_t e, const char *what) {
+  char buf[512];
+  std::snprintf(buf, sizeof buf, "%s: %s (hipError %d)", what, hipGetErrorString(e), (int)e);
+  g_err = buf;
+  if (e == hipErrorNoBinaryForGpu || e == hipErrorInvalidDeviceFunction ||
+      e == hipErrorInvalidImage || e == hipErrorSharedObjectInitFailed)
+    return LIFEAPI_E_NOKERNEL;
+  return (int)e;
+}
+
+struct DevInfo {
+  int cus = 0;
+  bool ok = false;
+};
+std::mutex g_info_mu;
+std::vector<DevInfo> g_info;
+
+int device_cus(int &cus) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return fail_hip(e, "hipGetDevice");
+  std::lock_guard<std::mutex> lk(g_info_mu);
+  if ((int)g_info.size() <= dev) g_info.resize(dev + 1);
+  if (!g_info[dev].ok) {
+    hipDeviceProp_t p;
+    e = hipGetDeviceProperties(&p, dev);
+    if (e != hipSuccess) return fail_hip(e, "hipGetDeviceProperties");
+    if (std::strncmp(p.gcnArchName, "gfx950", 6) != 0)
+      return fail(LIFEAPI_E_NODEVICE, "device is %s, this library is built for gfx950 only",
+                  p.gcnArchName);
+    g_info[dev].cus = p.multiProcessorCount;
+    g_info[dev].ok = true;
+  }
+  cus = g_info[dev].cus;
+  return LIFEAPI_OK;
+}
+
+bool aligned8(const void *p) { return ((uintptr_t)p & 7u) == 0; }
+
+int check_batch(const void *in, const void *out, size_t n) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!in || !out) return fail(LIFEAPI_E_INVALID, "null universe pointer%s");
+  if (!aligned8(in) || !aligned8(out)) return fail(LIFEAPI_E_INVALID, "universe pointers must be 8-byte aligned%s");
+  if (n > (SIZE_MAX / 512)) return fail(LIFEAPI_E_INVALID, "n too large%s");
+  const uintptr_t a = (uintptr_t)in, b = (uintptr_t)out, bytes = (uintptr_t)n * 512u;
+  if (a != b && a < b + bytes && b < a + bytes)
+    return fail(LIFEAPI_E_INVALID, "input and output batches overlap (only in == out is allowed)%s");
+  return LIFEAPI_OK;
+}
+
+unsigned grid_for(uint64_t waves_needed, int cus, int blocks_per_cu) {
+  uint64_t blocks = (waves_needed + kWavesPerBlock - 1) / kWavesPerBlock;
+  if (blocks_per_cu > 0) blocks = std::min<uint64_t>(blocks, (uint64_t)cus * blocks_per_cu);
+  blocks = std::min<uint64_t>(blocks, 1u << 30);
+  return (unsigned)std::max<uint64_t>(blocks, 1);
+}
+
+using StepFn = void (*)(const uint64_t *, uint64_t *, uint64_t, uint32_t);
+
+template <int X, int U, bool NT, int RULE>
+constexpr StepFn step_ptr() { return k_step<X, U, NT, RULE>; }
+
+template <int X, bool NT, int RULE>
+StepFn pick_u(int u) {
+  switch (u) {
+    case 1: return step_ptr<X, 1, NT, RULE>();
+    case 2: return step_ptr<X, 2, NT, RULE>();
+    case 4: return step_ptr<X, 4, NT, RULE>();
+    case 8: return step_ptr<X, 8, NT, RULE>();
+    default: return nullptr;
+  }
+}
+template <int X, int RULE>
+StepFn pick_nt(int u, bool nt) { return nt ? pick_u<X, true, RULE>(u) : pick_u<X, false, RULE>(u); }
+template <int X>
+StepFn pick_rule(int u, bool nt, int rule) {
+  return rule == 1 ? pick_nt<X, 1>(u, nt) : pick_nt<X, 0>(u, nt);
+}
+StepFn pick_step(const lifeapi_launch_cfg &c) {
+  switch (c.xchg) {
+    case LIFEAPI_XCHG_DPP: return pick_rule<XDPP>(c.universes_per_wave, c.nontemporal != 0, c.rule);
+    case LIFEAPI_XCHG_LDS: return pick_rule<XLDS>(c.universes_per_wave, c.nontemporal != 0, c.rule);
+    case LIFEAPI_XCHG_BPERM: return pick_rule<XBPERM>(c.universes_per_wave, c.nontemporal != 0, c.rule);
+    default: return nullptr;
+  }
+}
+
+int launched(const char *what) {
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? LIFEAPI_OK : fail_hip(e, what);
+}
+
+// ---- host-pointer staging: one context per device ----
+struct HostCtx {
+  std::mutex mu;
+  hipStream_t stream = nullptr;
+  uint64_t *buf = nullptr;
+  size_t cap = 0;  // universes
+};
+std::mutex g_ctx_mu;
+std::vector<HostCtx *> g_ctx;
+
+HostCtx *ctx_for(int dev) {
+  std::lock_guard<std::mutex> lk(g_ctx_mu);
+  if ((int)g_ctx.size() <= dev) g_ctx.resize(dev + 1, nullptr);
+  if (!g_ctx[dev]) g_ctx[dev] = new HostCtx();  // lives for the process
+  return g_ctx[dev];
+}
+
+struct DeviceGuard {
+  int prev = -1;
+  DeviceGuard() { (void)hipGetDevice(&prev); }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+constexpr size_t kChunk = size_t(1) << 21;  // 2M universes = 1 GiB per staging pass
+
+int host_step_one_device(const uint64_t *in, uint64_t *out, size_t n, uint32_t gens, int dev) {
+  DeviceGuard guard;
+  hipError_t e = hipSetDevice(dev);
+  if (e != hipSuccess) return fail_hip(e, "hipSetDevice");
+  HostCtx *c = ctx_for(dev);
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (!c->stream) {
+    e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) return fail_hip(e, "hipStreamCreate");
+  }
+  const size_t want = std::min(n, kChunk);
+  if (c->cap < want) {
+    if (c->buf) (void)hipFree(c->buf);
+    c->buf = nullptr;
+    c->cap = 0;
+    e = hipMalloc(&c->buf, want * 512);
+    if (e != hipSuccess) return fail_hip(e, "hipMalloc(staging)");
+    c->cap = want;
+  }
+  for (size_t off = 0; off < n; off += kChunk) {
+    const size_t m = std::min(kChunk, n - off);
+    e = hipMemcpyAsync(c->buf, in + off * 64, m * 512, hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) return fail_hip(e, "hipMemcpyAsync(H2D)");
+    int rc = lifeapi_step_batch_dev(c->buf, c->buf, m, gens, c->stream);
+    if (rc != LIFEAPI_OK) return rc;
+    e = hipMemcpyAsync(out + off * 64, c->buf, m * 512, hipMemcpyDeviceToHost, c->stream);
+    if (e != hipSuccess) return fail_hip(e, "hipMemcpyAsync(D2H)");
+    e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return fail_hip(e, "hipStreamSynchronize");
+  }
+  return LIFEAPI_OK;
+}
+
+}  // namespace
+
+// ==========================================================================
+// C ABI
+// ==========================================================================
+
+extern "C" {
+
+int lifeapi_abi_version(void) { return LIFEAPI_ABI_VERSION; }
+
+const char *lifeapi_last_error(void) { return g_err.c_str(); }
+
+int lifeapi_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+void lifeapi_default_cfg(lifeapi_launch_cfg *cfg, uint32_t generations) {
+  if (!cfg) return;
+  cfg->xchg = LIFEAPI_XCHG_DPP;
+  cfg->rule = 0;
+  if (generations <= 1) {  // HBM-streaming regime
+    cfg->universes_per_wave = 4;
+    cfg->blocks_per_cu = 8;
+    cfg->nontemporal = 1;
+  } else {  // VALU regime: state resident in VGPRs for all generations
+    cfg->universes_per_wave = 2;
+    cfg->blocks_per_cu = 0;
+    cfg->nontemporal = 0;
+  }
+}
+
+int lifeapi_step_batch_dev_cfg(const uint64_t *d_in, uint64_t *d_out, size_t n,
+                               uint32_t generations, void *stream,
+                               const lifeapi_launch_cfg *cfg) {
+  int rc = check_batch(d_in, d_out, n);
+  if (rc != LIFEAPI_OK || n == 0) return rc;
+  lifeapi_launch_cfg c;
+  if (cfg) c = *cfg;
+  else lifeapi_default_cfg(&c, generations);
+  StepFn fn = pick_step(c);
+  if (!fn) return fail(LIFEAPI_E_INVALID, "unsupported launch cfg%s");
+  int cus = 0;
+  rc = device_cus(cus);
+  if (rc != LIFEAPI_OK) return rc;
+  const uint64_t waves = (n + c.universes_per_wave - 1) / c.universes_per_wave;
+  const unsigned grid = grid_for(waves, cus, c.blocks_per_cu);
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, d_in, d_out,
+                     (uint64_t)n, generations);
+  return launched("k_step launch");
+}
+
+int lifeapi_step_batch_dev(const uint64_t *d_in, uint64_t *d_out, size_t n,
+                           uint32_t generations, void *stream) {
+  return lifeapi_step_batch_dev_cfg(d_in, d_out, n, generations, stream, nullptr);
+}
+
+int lifeapi_pop_batch_dev(const uint64_t *d_states, uint32_t *d_pop, size_t n, void *stream) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!d_states || !d_pop || !aligned8(d_states) || ((uintptr_t)d_pop & 3u))
+    return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_pop_batch_dev%s");
+  int cus = 0, rc = device_cus(cus);
+  if (rc != LIFEAPI_OK) return rc;
+  hipLaunchKernelGGL(k_pop, dim3(grid_for(n, cus, 8)), dim3(kBlock), 0, (hipStream_t)stream,
+                     d_states, d_pop, (uint64_t)n);
+  return launched("k_pop launch");
+}
+
+int lifeapi_hash_batch_dev(const uint64_t *d_states, uint64_t *d_hash, size_t n, void *stream) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!d_states || !d_hash || !aligned8(d_states) || !aligned8(d_hash))
+    return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_hash_batch_dev%s");
+  int cus = 0, rc = device_cus(cus);
+  if (rc != LIFEAPI_OK) return rc;
+  hipLaunchKernelGGL(k_hash, dim3(grid_for(n, cus, 8)), dim3(kBlock), 0, (hipStream_t)stream,
+                     d_states, d_hash, (uint64_t)n);
+  return launched("k_hash launch");
+}
+
+int lifeapi_contains_batch_dev(const uint64_t *d_states, const uint64_t *d_wanted,
+                               const uint64_t *d_unwanted, uint8_t *d_out, size_t n,
+                               void *stream) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!d_states || !d_wanted || !d_unwanted || !d_out || !aligned8(d_states) ||
+      !aligned8(d_wanted) || !aligned8(d_unwanted))
+    return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_contains_batch_dev%s");
+  int cus = 0, rc = device_cus(cus);
+  if (rc != LIFEAPI_OK) return rc;
+  hipLaunchKernelGGL(k_contains, dim3(grid_for(n, cus, 8)), dim3(kBlock), 0,
+                     (hipStream_t)stream, d_states, d_wanted, d_unwanted, d_out, (uint64_t)n);
+  return launched("k_contains launch");
+}
+
+int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
+                                    const uint64_t *d_wanted, const uint64_t *d_unwanted,
+                                    uint32_t *d_first_gen, size_t n, uint32_t generations,
+                                    void *stream) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!d_in || !d_wanted || !d_unwanted || !d_first_gen || !aligned8(d_in) ||
+      !aligned8(d_wanted) || !aligned8(d_unwanted) || ((uintptr_t)d_first_gen & 3u))
+    return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_step_contains_batch_dev%s");
+  if (d_final) {
+    int rc = check_batch(d_in, d_final, n);
+    if (rc != LIFEAPI_OK) return rc;
+  }
+  int cus = 0, rc = device_cus(cus);
+  if (rc != LIFEAPI_OK) return rc;
+  hipLaunchKernelGGL(k_step_contains, dim3(grid_for(n, cus, 0)), dim3(kBlock), 0,
+                     (hipStream_t)stream, d_in, d_final, d_wanted, d_unwanted, d_first_gen,
+                     (uint64_t)n, generations);
+  return launched("k_step_contains launch");
+}
+
+int lifeapi_fill_random_dev(uint64_t *d_out, size_t n, uint64_t seed, uint64_t first_universe,
+                            int mode, void *stream) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!d_out || !aligned8(d_out) || (mode != 0 && mode != 1))
+    return fail(LIFEAPI_E_INVALID, "bad argument to lifeapi_fill_random_dev%s");
+  int cus = 0, rc = device_cus(cus);
+  if (rc != LIFEAPI_OK) return rc;
+  const uint64_t words = (uint64_t)n * kWave;
+  hipLaunchKernelGGL(k_fill, dim3(grid_for(words / kWave, cus, 8)), dim3(kBlock), 0,
+                     (hipStream_t)stream, d_out, words, seed, first_universe * kWave, mode);
+  return launched("k_fill launch");
+}
+
+int lifeapi_step_batch(const uint64_t *in, uint64_t *out, size_t n, uint32_t generations,
+                       int device) {
+  int rc = check_batch(in, out, n);
+  if (rc != LIFEAPI_OK || n == 0) return rc;
+  const int ndev = lifeapi_device_count();
+  if (ndev <= 0) return fail(LIFEAPI_E_NODEVICE, "no HIP device visible%s");
+  if (device >= ndev || device < -1) return fail(LIFEAPI_E_NODEVICE, "bad device index%s");
+  if (device >= 0 || ndev == 1)
+    return host_step_one_device(in, out, n, generations, device < 0 ? 0 : device);
+  // every visible device, contiguous shards, one host thread each
+  std::vector<int> rcs(ndev, LIFEAPI_OK);
+  std::vector<std::string> errs(ndev);
+  std::vector<std::thread> pool;
+  for (int d = 0; d < ndev; ++d) {
+    const size_t lo = n * d / ndev, hi = n * (d + 1) / ndev;
+    pool.emplace_back([&, d, lo, hi] {
+      if (hi > lo) rcs[d] = host_step_one_device(in + lo * 64, out + lo * 64, hi - lo, generations, d);
+      errs[d] = g_err;
+    });
+  }
+  for (auto &t : pool) t.join();
+  for (int d = 0; d < ndev; ++d)
+    if (rcs[d] != LIFEAPI_OK) {
+      g_err = errs[d];
+      return rcs[d];
+    }
+  return LIFEAPI_OK;
+}
+
+int lifeapi_pop_batch(const uint64_t *states, uint32_t *pop, size_t n, int device) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!states || !pop || !aligned8(states)) return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_pop_batch%s");
+  const int ndev = lifeapi_device_count();
+  if (ndev <= 0) return fail(LIFEAPI_E_NODEVICE, "no HIP device visible%s");
+  if (device < 0) device = 0;
+  if (device >= ndev) return fail(LIFEAPI_E_NODEVICE, "bad device index%s");
+  DeviceGuard guard;
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return fail_hip(e, "hipSetDevice");
+  uint64_t *ds = nullptr;
+  uint32_t *dp = nullptr;
+  if ((e = hipMalloc(&ds, n * 512)) != hipSuccess) return fail_hip(e, "hipMalloc");
+  if ((e = hipMalloc(&dp, n * 4)) != hipSuccess) {
+    (void)hipFree(ds);
+    return fail_hip(e, "hipMalloc");
+  }
+  int rc = LIFEAPI_OK;
+  if ((e = hipMemcpy(ds, states, n * 512, hipMemcpyHostToDevice)) != hipSuccess) rc = fail_hip(e, "hipMemcpy");
+  if (rc == LIFEAPI_OK) rc = lifeapi_pop_batch_dev(ds, dp, n, nullptr);
+  if (rc == LIFEAPI_OK && (e = hipMemcpy(pop, dp, n * 4, hipMemcpyDeviceToHost)) != hipSuccess)
+    rc = fail_hip(e, "hipMemcpy");
+  (void)hipFree(ds);
+  (void)hipFree(dp);
+  return rc;
+}
+
+}  // extern "C"

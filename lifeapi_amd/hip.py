@@ -1,0 +1,212 @@
+"""ctypes binding of the C ABI in include/lifeapi_hip.h.
+
+Import order matters: torch is imported first so that its bundled HIP runtime
+(SONAME ``libamdhip64.so.7``) is the one ``liblifeapi_hip.so`` binds to --
+device pointers and streams handed over from torch then belong to the same
+runtime.  There is no fallback of any kind: a missing or unloadable library
+raises ImportError, and every failed call raises :class:`LifeApiError`.
+
+Universes are int64 tensors of shape (n, 64) holding the reference's
+``LifeState::state`` words bit-for-bit (LifeAPI.hpp:39-40).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+import torch  # noqa: F401  (must precede loading the HIP library)
+
+from .layout import N
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "liblifeapi_hip.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"{LIB_PATH} is missing: build it with "
+        "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950)")
+lib = ctypes.CDLL(LIB_PATH)
+
+XCHG_DPP, XCHG_LDS, XCHG_BPERM = 0, 1, 2
+
+
+class LaunchCfg(ctypes.Structure):
+    """lifeapi_launch_cfg (include/lifeapi_hip.h)."""
+
+    _fields_ = [("xchg", ctypes.c_int), ("universes_per_wave", ctypes.c_int),
+                ("blocks_per_cu", ctypes.c_int), ("nontemporal", ctypes.c_int),
+                ("rule", ctypes.c_int)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class LifeApiError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"lifeapi error {code}: {msg}")
+        self.code = code
+
+
+_vp, _sz, _u32, _u64, _int = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+_SIGS = {
+    "lifeapi_abi_version": ([], _int),
+    "lifeapi_last_error": ([], ctypes.c_char_p),
+    "lifeapi_device_count": ([], _int),
+    "lifeapi_default_cfg": ([ctypes.POINTER(LaunchCfg), _u32], None),
+    "lifeapi_step_batch_dev": ([_vp, _vp, _sz, _u32, _vp], _int),
+    "lifeapi_step_batch_dev_cfg": ([_vp, _vp, _sz, _u32, _vp, ctypes.POINTER(LaunchCfg)], _int),
+    "lifeapi_pop_batch_dev": ([_vp, _vp, _sz, _vp], _int),
+    "lifeapi_hash_batch_dev": ([_vp, _vp, _sz, _vp], _int),
+    "lifeapi_contains_batch_dev": ([_vp, _vp, _vp, _vp, _sz, _vp], _int),
+    "lifeapi_step_contains_batch_dev": ([_vp, _vp, _vp, _vp, _vp, _sz, _u32, _vp], _int),
+    "lifeapi_fill_random_dev": ([_vp, _sz, _u64, _u64, _int, _vp], _int),
+    "lifeapi_step_batch": ([_vp, _vp, _sz, _u32, _int], _int),
+    "lifeapi_pop_batch": ([_vp, _vp, _sz, _int], _int),
+}
+for _name, (_args, _res) in _SIGS.items():
+    _f = getattr(lib, _name)
+    _f.argtypes = _args
+    _f.restype = _res
+
+EXPORTS = tuple(_SIGS)
+
+
+def _check(rc: int) -> None:
+    if rc != 0:
+        raise LifeApiError(rc, lib.lifeapi_last_error().decode(errors="replace"))
+
+
+def abi_version() -> int:
+    return lib.lifeapi_abi_version()
+
+
+def device_count() -> int:
+    return lib.lifeapi_device_count()
+
+
+def default_cfg(generations: int = 1) -> LaunchCfg:
+    c = LaunchCfg()
+    lib.lifeapi_default_cfg(ctypes.byref(c), generations)
+    return c
+
+
+def _stream(stream) -> int:
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+
+
+def _universes(t: torch.Tensor, name: str = "states") -> int:
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a device tensor")
+    if t.dtype not in (torch.int64, torch.uint64) or not t.is_contiguous() or t.numel() % N:
+        raise ValueError(f"{name} must be a contiguous int64 tensor of shape (n, 64)")
+    return t.numel() // N
+
+
+def empty_universes(n: int, device=None) -> torch.Tensor:
+    return torch.empty((n, N), dtype=torch.int64, device=device or "cuda")
+
+
+def step(states: torch.Tensor, out: torch.Tensor | None = None, generations: int = 1,
+         cfg: LaunchCfg | None = None, stream=None) -> torch.Tensor:
+    """Batched ``Stepped(generations)`` (LifeAPI.hpp:882-886); ``out`` may be ``states``."""
+    n = _universes(states)
+    if out is None:
+        out = torch.empty_like(states)
+    if _universes(out, "out") != n:
+        raise ValueError("out has a different number of universes")
+    s = _stream(stream)
+    if cfg is None:
+        _check(lib.lifeapi_step_batch_dev(states.data_ptr(), out.data_ptr(), n, generations, s))
+    else:
+        _check(lib.lifeapi_step_batch_dev_cfg(states.data_ptr(), out.data_ptr(), n, generations, s,
+                                              ctypes.byref(cfg)))
+    return out
+
+
+def pop(states: torch.Tensor, stream=None) -> torch.Tensor:
+    """Per-universe ``GetPop()`` (LifeAPI.hpp:290-298) as int32."""
+    n = _universes(states)
+    out = torch.empty(n, dtype=torch.int32, device=states.device)
+    _check(lib.lifeapi_pop_batch_dev(states.data_ptr(), out.data_ptr(), n, _stream(stream)))
+    return out
+
+
+def hashes(states: torch.Tensor, stream=None) -> torch.Tensor:
+    """Per-universe build-defined 64-bit hash (bit pattern in an int64 tensor)."""
+    n = _universes(states)
+    out = torch.empty(n, dtype=torch.int64, device=states.device)
+    _check(lib.lifeapi_hash_batch_dev(states.data_ptr(), out.data_ptr(), n, _stream(stream)))
+    return out
+
+
+def contains(states: torch.Tensor, wanted: torch.Tensor, unwanted: torch.Tensor,
+             stream=None) -> torch.Tensor:
+    """Per-universe ``Contains(LifeTarget{wanted, unwanted})`` (LifeTarget.hpp:44-51)."""
+    n = _universes(states)
+    _universes(wanted, "wanted"), _universes(unwanted, "unwanted")
+    out = torch.empty(n, dtype=torch.uint8, device=states.device)
+    _check(lib.lifeapi_contains_batch_dev(states.data_ptr(), wanted.data_ptr(), unwanted.data_ptr(),
+                                          out.data_ptr(), n, _stream(stream)))
+    return out
+
+
+def step_contains(states: torch.Tensor, wanted: torch.Tensor, unwanted: torch.Tensor,
+                  generations: int, final: torch.Tensor | None = None, stream=None):
+    """First generation (1..gens, 0 = never) at which each universe contains the target."""
+    n = _universes(states)
+    first = torch.empty(n, dtype=torch.int32, device=states.device)
+    fptr = 0 if final is None else final.data_ptr()
+    if final is not None and _universes(final, "final") != n:
+        raise ValueError("final has a different number of universes")
+    _check(lib.lifeapi_step_contains_batch_dev(states.data_ptr(), fptr or None, wanted.data_ptr(),
+                                               unwanted.data_ptr(), first.data_ptr(), n,
+                                               generations, _stream(stream)))
+    return first, final
+
+
+def fill_random(n: int, seed: int, first_universe: int = 0, mode: int = 0,
+                out: torch.Tensor | None = None, device=None, stream=None) -> torch.Tensor:
+    """Seeded synthetic universes (see lifeapi_fill_random_dev)."""
+    if out is None:
+        out = empty_universes(n, device)
+    if _universes(out, "out") != n:
+        raise ValueError("out has a different number of universes")
+    _check(lib.lifeapi_fill_random_dev(out.data_ptr(), n, seed & (2**64 - 1), first_universe,
+                                       mode, _stream(stream)))
+    return out
+
+
+def _host_u64(a: np.ndarray) -> np.ndarray:
+    a = np.ascontiguousarray(a, dtype=np.uint64)
+    if a.size % N:
+        raise ValueError("host batch must hold whole universes (multiples of 64 words)")
+    return a
+
+
+def step_host(states: np.ndarray, generations: int = 1, device: int = 0,
+              out: np.ndarray | None = None) -> np.ndarray:
+    """Host-pointer ``lifeapi_step_batch`` (synchronous, PCIe-staged)."""
+    src = _host_u64(states)
+    dst = np.empty_like(src) if out is None else out
+    _check(lib.lifeapi_step_batch(src.ctypes.data, dst.ctypes.data, src.size // N, generations, device))
+    return dst
+
+
+def pop_host(states: np.ndarray, device: int = 0) -> np.ndarray:
+    src = _host_u64(states)
+    out = np.empty(src.size // N, dtype=np.uint32)
+    _check(lib.lifeapi_pop_batch(src.ctypes.data, out.ctypes.data, src.size // N, device))
+    return out
+
+
+def loaded_hip_runtimes() -> list[str]:
+    """Paths of every libamdhip64 mapped into this process (must be exactly one)."""
+    paths = set()
+    with open("/proc/self/maps") as f:
+        for line in f:
+            p = line.split()[-1] if len(line.split()) >= 6 else ""
+            if "libamdhip64" in p:
+                paths.add(p)
+    return sorted(paths)

@@ -1,0 +1,265 @@
+/*
+ * lifeapi_oracle.c -- CPU restatement of the reference's Step() path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see lifeapi_oracle.h).  Never linked into the
+ * product library; the product fails loudly if its HIP code object is absent.
+ *
+ * Every function names the reference lines it restates.  Paths are relative
+ * to the reference snapshot (scorbiclife/LifeAPI, 2025-02-22).
+ */
+#include "lifeapi_oracle.h"
+
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+static inline uint64_t rotl64(uint64_t v, unsigned k) { return (v << k) | (v >> ((64 - k) & 63)); }
+static inline uint64_t rotr64(uint64_t v, unsigned k) { return (v >> k) | (v << ((64 - k) & 63)); }
+
+/* Vertical (in-column) 3-cell sum as two bit planes.
+ * LifeAPI.hpp:897-907 (LifeState::CountRows). */
+void oracle_count_rows(const uint64_t s[64], uint64_t col0[64], uint64_t col1[64]) {
+  for (int x = 0; x < ORACLE_N; ++x) {
+    const uint64_t a = s[x];
+    const uint64_t up = rotl64(a, 1), dn = rotr64(a, 1);
+    col0[x] = up ^ dn ^ a;
+    col1[x] = ((up ^ dn) & a) | (up & dn);
+  }
+}
+
+/* B3/S23 from the centre column and the neighbour columns' 2-bit sums.
+ * LifeAPI.hpp:837-848 (LifeState::Rokicki). */
+uint64_t oracle_rokicki(uint64_t a, uint64_t bU0, uint64_t bU1, uint64_t bB0, uint64_t bB1) {
+  const uint64_t aw = rotl64(a, 1), ae = rotr64(a, 1);
+  const uint64_t s0 = aw ^ ae, s1 = aw & ae;
+  const uint64_t ts0 = bB0 ^ bU0;
+  const uint64_t ts1 = (bB0 & bU0) | (ts0 & s0);
+  return (bB1 ^ bU1 ^ ts1 ^ s1) & ((bB1 | bU1) ^ (ts1 | s1)) & ((ts0 ^ s0) | a);
+}
+
+/* One generation in place, torus wrap on the column index.
+ * LifeAPI.hpp:1196-1216 (LifeState::Step). */
+void oracle_step(uint64_t s[64]) {
+  uint64_t c0[64], c1[64];
+  oracle_count_rows(s, c0, c1);
+  for (int x = 0; x < ORACLE_N; ++x) {
+    const int xl = (x + ORACLE_N - 1) & (ORACLE_N - 1); /* idxU */
+    const int xr = (x + 1) & (ORACLE_N - 1);            /* idxB */
+    s[x] = oracle_rokicki(s[x], c0[xl], c1[xl], c0[xr], c1[xr]);
+  }
+}
+
+/* Same generation via two full adders on the bit planes.
+ * LifeAPI.hpp:1218-1254 (LifeState::StepAlt), adders from :822-833. */
+void oracle_step_alt(uint64_t s[64]) {
+  uint64_t c0[64], c1[64];
+  oracle_count_rows(s, c0, c1);
+  for (int x = 0; x < ORACLE_N; ++x) {
+    const int xl = (x + ORACLE_N - 1) & (ORACLE_N - 1);
+    const int xr = (x + 1) & (ORACLE_N - 1);
+    const uint64_t a = s[x];
+    /* FullAdd(final_sum, final_carry, u_on0, c_on0, l_on0) */
+    uint64_t h = c0[xl] ^ c0[x];
+    const uint64_t fs = h ^ c0[xr];
+    const uint64_t fc = (c0[xl] & c0[x]) | (c0[xr] & h);
+    /* FullAdd(carry_sum, carry_carry, u_on1, c_on1, l_on1) */
+    h = c1[xl] ^ c1[x];
+    const uint64_t cs = h ^ c1[xr];
+    uint64_t cc = (c1[xl] & c1[x]) | (c1[xr] & h);
+    cc ^= fc & cs;
+    s[x] = (fs ^ cc) & (fc ^ cs ^ cc) & (a | fs);
+  }
+}
+
+/* Inclusive 3x3 count 0..9 as four planes.
+ * NeighbourCount.hpp:25-38 (halo CountRows) and :40-70 (adder chain). */
+void oracle_neighbour_count(const uint64_t s[64], uint64_t bit3[64], uint64_t bit2[64],
+                            uint64_t bit1[64], uint64_t bit0[64]) {
+  uint64_t c0[66], c1[66];
+  oracle_count_rows(s, c0 + 1, c1 + 1);
+  c0[0] = c0[64]; c0[65] = c0[1];
+  c1[0] = c1[64]; c1[65] = c1[1];
+  for (int x = 0; x < ORACLE_N; ++x) {
+    const uint64_t u0 = c0[x], m0 = c0[x + 1], l0 = c0[x + 2];
+    const uint64_t u1 = c1[x], m1 = c1[x + 1], l1 = c1[x + 2];
+    /* HalfAdd(uc0, uc_carry0, u_on0, c_on0) */
+    const uint64_t uc0 = u0 ^ m0, ucc0 = u0 & m0;
+    /* FullAdd(uc1, uc2, u_on1, c_on1, uc_carry0) */
+    const uint64_t hh = u1 ^ m1;
+    const uint64_t uc1 = hh ^ ucc0, uc2 = (u1 & m1) | (ucc0 & hh);
+    /* HalfAdd(on0, on_carry0, uc0, l_on0) */
+    const uint64_t on0 = uc0 ^ l0, occ0 = uc0 & l0;
+    /* FullAdd(on1, on_carry1, uc1, l_on1, on_carry0) */
+    const uint64_t h2 = uc1 ^ l1;
+    const uint64_t on1 = h2 ^ occ0, occ1 = (uc1 & l1) | (occ0 & h2);
+    /* HalfAdd(on2, on3, uc2, on_carry1) */
+    bit0[x] = on0;
+    bit1[x] = on1;
+    bit2[x] = uc2 ^ occ1;
+    bit3[x] = uc2 & occ1;
+  }
+}
+
+/* Life via WithExactly(3) | (s & WithExactly(4)) on the inclusive count.
+ * NeighbourCount.hpp:93-102 (WithExactly). */
+void oracle_step_nc(uint64_t s[64]) {
+  uint64_t b3[64], b2[64], b1[64], b0[64];
+  oracle_neighbour_count(s, b3, b2, b1, b0);
+  for (int x = 0; x < ORACLE_N; ++x) {
+    const uint64_t exactly3 = ~b3[x] & ~b2[x] & b1[x] & b0[x];
+    const uint64_t exactly4 = ~b3[x] & b2[x] & ~b1[x] & ~b0[x];
+    s[x] = exactly3 | (s[x] & exactly4);
+  }
+}
+
+/* LifeAPI.hpp:877-881 (LifeState::Step(unsigned)). */
+void oracle_step_n(uint64_t s[64], unsigned gens) {
+  for (unsigned g = 0; g < gens; ++g) oracle_step(s);
+}
+
+typedef struct {
+  const uint64_t *in;
+  uint64_t *out;
+  size_t lo, hi;
+  unsigned gens;
+  int formulation;
+} batch_job;
+
+static void *batch_worker(void *p) {
+  const batch_job *j = (const batch_job *)p;
+  uint64_t s[64] __attribute__((aligned(64)));
+  for (size_t u = j->lo; u < j->hi; ++u) {
+    memcpy(s, j->in + u * 64, sizeof s);
+    for (unsigned g = 0; g < j->gens; ++g) {
+      if (j->formulation == ORACLE_FULLADD) oracle_step_alt(s);
+      else if (j->formulation == ORACLE_NCOUNT) oracle_step_nc(s);
+      else oracle_step(s);
+    }
+    memcpy(j->out + u * 64, s, sizeof s);
+  }
+  return NULL;
+}
+
+/* Batched form of LifeAPI.hpp:882-886 (Stepped(unsigned)) over independent
+ * universes; each thread owns a contiguous slice. */
+void oracle_step_batch(const uint64_t *in, uint64_t *out, size_t n, unsigned gens,
+                       int formulation, int nthreads) {
+  if (nthreads < 1) nthreads = 1;
+  if ((size_t)nthreads > n) nthreads = n ? (int)n : 1;
+  batch_job jobs[256];
+  pthread_t tid[256];
+  if (nthreads > 256) nthreads = 256;
+  for (int t = 0; t < nthreads; ++t) {
+    jobs[t].in = in; jobs[t].out = out;
+    jobs[t].lo = n * (size_t)t / (size_t)nthreads;
+    jobs[t].hi = n * (size_t)(t + 1) / (size_t)nthreads;
+    jobs[t].gens = gens; jobs[t].formulation = formulation;
+  }
+  if (nthreads == 1) { batch_worker(&jobs[0]); return; }
+  for (int t = 0; t < nthreads; ++t) pthread_create(&tid[t], NULL, batch_worker, &jobs[t]);
+  for (int t = 0; t < nthreads; ++t) pthread_join(tid[t], NULL);
+}
+
+/* LifeAPI.hpp:290-298 (LifeState::GetPop). */
+unsigned oracle_pop(const uint64_t s[64]) {
+  unsigned p = 0;
+  for (int x = 0; x < ORACLE_N; ++x) p += (unsigned)__builtin_popcountll(s[x]);
+  return p;
+}
+
+void oracle_pop_batch(const uint64_t *s, uint32_t *pop, size_t n) {
+  for (size_t u = 0; u < n; ++u) pop[u] = oracle_pop(s + u * 64);
+}
+
+/* LifeTarget.hpp:44-51 (LifeState::Contains(const LifeTarget&)). */
+int oracle_contains_target(const uint64_t s[64], const uint64_t wanted[64],
+                           const uint64_t unwanted[64]) {
+  uint64_t diff = 0;
+  for (int x = 0; x < ORACLE_N; ++x) diff |= (s[x] ^ wanted[x]) & (wanted[x] | unwanted[x]);
+  return diff == 0;
+}
+
+/* Parsing.hpp:143-198 (GenericParse + LifeState::Parse): header lines that
+ * start with 'x' are dropped, '$' with no count means 1, a count of 129 on
+ * '$' stops parsing, any non-'o' cell char is dead.  Coordinates are NOT
+ * wrapped by the reference (Set at LifeAPI.hpp:131); out-of-board cells are
+ * reported as an error here instead of writing out of bounds. */
+int oracle_parse_rle(const char *rle, uint64_t out[64]) {
+  memset(out, 0, 64 * sizeof(uint64_t));
+  int cnt = 0, x = 0, y = 0, bad = 0;
+  const char *p = rle;
+  while (*p) {
+    const char *eol = strchr(p, '\n');
+    const size_t len = eol ? (size_t)(eol - p) : strlen(p);
+    if (len == 0 || p[0] != 'x') {
+      for (size_t i = 0; i < len; ++i) {
+        const char ch = p[i];
+        if (ch >= '0' && ch <= '9') {
+          cnt = cnt * 10 + (ch - '0');
+        } else if (ch == '$') {
+          if (cnt == 0) cnt = 1;
+          if (cnt == 129) return bad ? -1 : 0;
+          y += cnt; x = 0; cnt = 0;
+        } else if (ch == '!') {
+          return bad ? -1 : 0;
+        } else if (ch == '\r' || ch == ' ') {
+          continue;
+        } else {
+          if (cnt == 0) cnt = 1;
+          for (int j = 0; j < cnt; ++j, ++x) {
+            if (ch != 'o') continue;
+            if (x < 0 || x >= 64 || y < 0 || y >= 64) { bad = 1; continue; }
+            out[x] |= 1ULL << y;
+          }
+          cnt = 0;
+        }
+      }
+    }
+    if (!eol) break;
+    p = eol + 1;
+  }
+  return bad ? -1 : 0;
+}
+
+/* ---- build-defined synthetic input and digests (no reference analogue) ---- */
+
+#define GOLDEN 0x9E3779B97F4A7C15ULL
+
+uint64_t oracle_splitmix64_mix(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+/* Word w (global index u*64+x) = splitmix64 output number w+1 of `seed`.
+ * mode 0: uniform density-0.5 columns.
+ * mode 1: RandomState()-shaped columns, uniform on [2^61, 2^62) like
+ *         LifeAPI.hpp:18-23,63-69 (row 61 on, rows 62-63 off). */
+void oracle_fill(uint64_t *out, size_t n, uint64_t seed, uint64_t first_universe, int mode) {
+  for (size_t i = 0; i < n * 64; ++i) {
+    const uint64_t w = first_universe * 64 + i;
+    uint64_t v = oracle_splitmix64_mix(seed + (w + 1) * GOLDEN);
+    if (mode == 1) v = (v & ((1ULL << 61) - 1)) | (1ULL << 61);
+    out[i] = v;
+  }
+}
+
+/* Per-universe hash: mix(sum_x mix(s[x] + (x+1)*GOLDEN)), order sensitive in x. */
+uint64_t oracle_universe_hash(const uint64_t s[64]) {
+  uint64_t acc = 0;
+  for (int x = 0; x < ORACLE_N; ++x) acc += oracle_splitmix64_mix(s[x] + (uint64_t)(x + 1) * GOLDEN);
+  return oracle_splitmix64_mix(acc);
+}
+
+void oracle_hash_batch(const uint64_t *s, uint64_t *h, size_t n) {
+  for (size_t u = 0; u < n; ++u) h[u] = oracle_universe_hash(s + u * 64);
+}
+
+/* Batch digest: sum_u mix(h_u + (u_global+1)*GOLDEN) -- additive, so shard
+ * digests combine by 64-bit addition. */
+uint64_t oracle_batch_digest(const uint64_t *hashes, size_t n, uint64_t first_universe) {
+  uint64_t acc = 0;
+  for (size_t u = 0; u < n; ++u)
+    acc += oracle_splitmix64_mix(hashes[u] + (first_universe + u + 1) * GOLDEN);
+  return acc;
+}

@@ -1,0 +1,191 @@
+"""ctypes bindings for the parity oracle.  TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s cpu_baseline
+leg import this module, and only as the checker / the timed CPU baseline.
+The product package ``lifeapi_amd`` never imports it.
+
+Two oracles live here:
+
+* ``Port``  -- ``oracle/liboracle.so``: the plain-C restatement
+  (``lifeapi_oracle.c``) of LifeAPI.hpp:822-907,1196-1254 and
+  NeighbourCount.hpp:25-102.
+* ``Ref``   -- ``oracle/_ref/libref_v{3,4}.so``: the reference's OWN
+  ``LifeState::Step()`` etc., compiled from /root/reference by
+  ``oracle/Makefile`` (target ``ref``).  Present on the GPU box only as the
+  prebuilt .so (the reference tree itself is not there).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+
+
+def _p64(a: np.ndarray):
+    assert a.dtype == np.uint64 and a.flags.c_contiguous
+    return a.ctypes.data_as(_u64p)
+
+
+def _cpu_has_avx512() -> bool:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("flags"):
+                    fl = set(line.split(":", 1)[1].split())
+                    return {"avx512f", "avx512bw", "avx512dq", "avx512vl", "avx512cd"} <= fl
+    except OSError:
+        pass
+    return False
+
+
+def universes(n: int) -> np.ndarray:
+    """Zeroed, 64-byte aligned (n, 64) uint64 array (LifeState[] layout)."""
+    raw = np.zeros(n * 64 + 8, dtype=np.uint64)
+    off = (-raw.ctypes.data % 64) // 8
+    return raw[off:off + n * 64].reshape(n, 64)
+
+
+class Port:
+    """The C restatement (oracle/lifeapi_oracle.c)."""
+
+    ROKICKI, FULLADD, NCOUNT = 0, 1, 2
+
+    def __init__(self, path: str | None = None):
+        path = path or os.path.join(HERE, "liboracle.so")
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"{path} missing: run `make -C oracle`")
+        L = self.lib = ctypes.CDLL(path)
+        L.oracle_step_batch.argtypes = [_u64p, _u64p, ctypes.c_size_t, ctypes.c_uint,
+                                        ctypes.c_int, ctypes.c_int]
+        L.oracle_pop_batch.argtypes = [_u64p, _u32p, ctypes.c_size_t]
+        L.oracle_contains_target.argtypes = [_u64p, _u64p, _u64p]
+        L.oracle_parse_rle.argtypes = [ctypes.c_char_p, _u64p]
+        L.oracle_fill.argtypes = [_u64p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64,
+                                  ctypes.c_int]
+        L.oracle_hash_batch.argtypes = [_u64p, _u64p, ctypes.c_size_t]
+        L.oracle_batch_digest.argtypes = [_u64p, ctypes.c_size_t, ctypes.c_uint64]
+        L.oracle_batch_digest.restype = ctypes.c_uint64
+        L.oracle_neighbour_count.argtypes = [_u64p] * 5
+        for name in ("oracle_step", "oracle_step_alt", "oracle_step_nc"):
+            getattr(L, name).argtypes = [_u64p]
+
+    def step_batch(self, states: np.ndarray, gens: int = 1, formulation: int = 0,
+                   nthreads: int = 1) -> np.ndarray:
+        src = np.ascontiguousarray(states, dtype=np.uint64).reshape(-1, 64)
+        out = universes(src.shape[0])
+        self.lib.oracle_step_batch(_p64(src), _p64(out), src.shape[0], gens, formulation, nthreads)
+        return out
+
+    def fill(self, n: int, seed: int, first_universe: int = 0, mode: int = 0) -> np.ndarray:
+        out = universes(n)
+        self.lib.oracle_fill(_p64(out), n, seed, first_universe, mode)
+        return out
+
+    def pop(self, states: np.ndarray) -> np.ndarray:
+        src = np.ascontiguousarray(states, dtype=np.uint64).reshape(-1, 64)
+        out = np.zeros(src.shape[0], dtype=np.uint32)
+        self.lib.oracle_pop_batch(_p64(src), out.ctypes.data_as(_u32p), src.shape[0])
+        return out
+
+    def hashes(self, states: np.ndarray) -> np.ndarray:
+        src = np.ascontiguousarray(states, dtype=np.uint64).reshape(-1, 64)
+        out = np.zeros(src.shape[0], dtype=np.uint64)
+        self.lib.oracle_hash_batch(_p64(src), _p64(out), src.shape[0])
+        return out
+
+    def digest(self, hashes: np.ndarray, first_universe: int = 0) -> int:
+        h = np.ascontiguousarray(hashes, dtype=np.uint64)
+        return int(self.lib.oracle_batch_digest(_p64(h), h.shape[0], first_universe))
+
+    def contains(self, state, wanted, unwanted) -> bool:
+        a, w, u = (np.ascontiguousarray(x, dtype=np.uint64).reshape(64) for x in (state, wanted, unwanted))
+        return bool(self.lib.oracle_contains_target(_p64(a), _p64(w), _p64(u)))
+
+    def parse(self, rle: str) -> np.ndarray:
+        out = np.zeros(64, dtype=np.uint64)
+        rc = self.lib.oracle_parse_rle(rle.encode(), _p64(out))
+        if rc != 0:
+            raise ValueError(f"RLE places a cell outside the 64x64 board: {rle!r}")
+        return out
+
+    def neighbour_count(self, state) -> np.ndarray:
+        s = np.ascontiguousarray(state, dtype=np.uint64).reshape(64)
+        b = np.zeros((4, 64), dtype=np.uint64)
+        self.lib.oracle_neighbour_count(_p64(s), _p64(b[0]), _p64(b[1]), _p64(b[2]), _p64(b[3]))
+        return b  # bit3, bit2, bit1, bit0
+
+
+class Ref:
+    """The reference's own code (oracle/_ref/libref_v*.so)."""
+
+    def __init__(self, path: str | None = None):
+        if path is None:
+            v = "v4" if _cpu_has_avx512() else "v3"
+            path = os.path.join(HERE, "_ref", f"libref_{v}.so")
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"{path} missing: run `make -C oracle ref` where /root/reference exists")
+        self.path = path
+        L = self.lib = ctypes.CDLL(path)
+        for name in ("ref_step", "ref_step_alt", "ref_step_nc", "ref_random_state"):
+            getattr(L, name).argtypes = [_u64p]
+        L.ref_step_n.argtypes = [_u64p, ctypes.c_uint]
+        L.ref_step_batch.argtypes = [_u64p, _u64p, ctypes.c_size_t, ctypes.c_uint, ctypes.c_int]
+        L.ref_pop.argtypes = [_u64p]
+        L.ref_pop.restype = ctypes.c_uint
+        L.ref_contains_target.argtypes = [_u64p, _u64p, _u64p]
+        L.ref_parse.argtypes = [ctypes.c_char_p, _u64p]
+        L.ref_neighbour_count.argtypes = [_u64p] * 5
+        L.ref_count_neighbourhood.argtypes = [_u64p] * 5
+
+    @staticmethod
+    def available() -> bool:
+        v = "v4" if _cpu_has_avx512() else "v3"
+        return os.path.exists(os.path.join(HERE, "_ref", f"libref_{v}.so"))
+
+    def step_batch(self, states: np.ndarray, gens: int = 1, nthreads: int = 1) -> np.ndarray:
+        src = np.ascontiguousarray(states, dtype=np.uint64).reshape(-1, 64)
+        out = universes(src.shape[0])
+        self.lib.ref_step_batch(_p64(src), _p64(out), src.shape[0], gens, nthreads)
+        return out
+
+    def _each(self, fn, states):
+        out = universes(np.asarray(states).reshape(-1, 64).shape[0])
+        out[:] = np.asarray(states, dtype=np.uint64).reshape(-1, 64)
+        for u in range(out.shape[0]):
+            fn(_p64(out[u]))
+        return out
+
+    def step_alt(self, states):
+        return self._each(self.lib.ref_step_alt, states)
+
+    def step_nc(self, states):
+        return self._each(self.lib.ref_step_nc, states)
+
+    def random_state(self) -> np.ndarray:
+        out = np.zeros(64, dtype=np.uint64)
+        self.lib.ref_random_state(_p64(out))
+        return out
+
+    def parse(self, rle: str) -> np.ndarray:
+        out = np.zeros(64, dtype=np.uint64)
+        self.lib.ref_parse(rle.encode(), _p64(out))
+        return out
+
+    def pop(self, state) -> int:
+        s = np.ascontiguousarray(state, dtype=np.uint64).reshape(64)
+        return int(self.lib.ref_pop(_p64(s)))
+
+    def contains(self, state, wanted, unwanted) -> bool:
+        a, w, u = (np.ascontiguousarray(x, dtype=np.uint64).reshape(64) for x in (state, wanted, unwanted))
+        return bool(self.lib.ref_contains_target(_p64(a), _p64(w), _p64(u)))
+
+    def neighbour_count(self, state) -> np.ndarray:
+        s = np.ascontiguousarray(state, dtype=np.uint64).reshape(64)
+        b = np.zeros((4, 64), dtype=np.uint64)
+        self.lib.ref_neighbour_count(_p64(s), _p64(b[0]), _p64(b[1]), _p64(b[2]), _p64(b[3]))
+        return b

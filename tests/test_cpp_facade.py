@@ -1,0 +1,25 @@
+"""Runs the C++ facade tests (tests/cpp/*.cpp, built by __graft_entry__.build())."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_facade_compiles_without_gpu():
+    """The facade header is self-contained C++20 (CPU: syntax + layout asserts)."""
+    src = os.path.join(ROOT, "tests", "cpp", "step_batch_test.cpp")
+    subprocess.run(["g++", "-std=c++20", "-fsyntax-only", "-Wall", "-Wextra", "-Werror",
+                    "-I" + os.path.join(ROOT, "include"), src], check=True)
+
+
+@pytest.mark.gpu
+def test_step_batch_cpp():
+    exe = os.path.join(ROOT, "build", "step_batch_test")
+    if not os.path.exists(exe):
+        import __graft_entry__ as g
+        g.build_cpp_tests()
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    print(r.stdout, r.stderr)
+    assert r.returncode == 0, r.stderr[-4000:]

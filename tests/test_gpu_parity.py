@@ -1,0 +1,183 @@
+"""GPU parity: the HIP path through the C ABI vs the CPU oracle.
+
+Bit-exact on every word (integer work, no tolerance).  Oracle = the C
+restatement (oracle/lifeapi_oracle.c) pinned against the reference's own
+Step() (oracle/_ref, tests/test_oracle.py).  Mirrors tests/StepAltTest.cpp:5-13
+(differential Step vs an independent formulation) on seeded inputs.
+"""
+import itertools
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+ALL_CFGS = list(itertools.product((0, 1, 2), (1, 2, 4, 8), (0, 1), (0, 1)))
+
+
+def to_dev(a: np.ndarray) -> torch.Tensor:
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.int64).reshape(-1, 64).copy()).cuda()
+
+
+def to_host(t: torch.Tensor) -> np.ndarray:
+    torch.cuda.synchronize()
+    return t.cpu().numpy().view(np.uint64).reshape(-1, 64)
+
+
+def seam_cases(port):
+    """Universes with cells on the torus seams (columns 0/63, rows 0/63)."""
+    out = []
+    s = np.zeros(64, np.uint64)
+    s[0] = s[63] = s[1] = np.uint64(0x8000000000000003)
+    out.append(s.copy())
+    s = np.zeros(64, np.uint64)
+    s[62] = s[63] = s[0] = np.uint64((1 << 63) | 1)       # blinker/block across both seams
+    out.append(s.copy())
+    out.append(np.full(64, np.uint64(2**64 - 1)))            # all on -> empty
+    chk = np.array([0xAAAAAAAAAAAAAAAA if x % 2 == 0 else 0x5555555555555555 for x in range(64)],
+                   dtype=np.uint64)
+    out.append(chk)                                          # checkerboard -> empty
+    g = port.parse("bo$2bo$3o!")                             # glider
+    out.append(np.roll(g, 62))                               # glider straddling column seam
+    out.append(np.array([int(w) << 62 | int(w) >> 2 for w in g], dtype=np.uint64))  # row seam
+    out.append(np.zeros(64, np.uint64))
+    return np.stack(out)
+
+
+def test_single_runtime(hip):
+    assert len(hip.loaded_hip_runtimes()) == 1, hip.loaded_hip_runtimes()
+
+
+@pytest.mark.parametrize("xchg,upw,nt,rule", ALL_CFGS)
+def test_step_all_cfgs(hip, port, xchg, upw, nt, rule):
+    n = 2048 + 3                               # ragged vs every U
+    x = port.fill(n, seed=1000 + xchg * 100 + upw * 10 + nt * 2 + rule)
+    x = np.concatenate([seam_cases(port), x])
+    cfg = hip.LaunchCfg(xchg, upw, 1, nt, rule)  # 1 block/CU: forces grid-striding
+    d = to_dev(x)
+    for gens in (1, 5):
+        got = to_host(hip.step(d, generations=gens, cfg=cfg))
+        want = port.step_batch(x, gens)
+        bad = np.nonzero((got != want).any(axis=1))[0]
+        assert bad.size == 0, f"gens={gens}: {bad.size} universes differ, first {bad[:8]}"
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 63, 64, 65, 4097])
+def test_ragged_default(hip, port, n):
+    x = port.fill(n, seed=n)
+    for gens in (1, 3):
+        got = to_host(hip.step(to_dev(x), generations=gens))
+        assert (got == port.step_batch(x, gens)).all()
+
+
+def test_zero_gens_and_empty(hip, port):
+    x = port.fill(17, seed=5)
+    assert (to_host(hip.step(to_dev(x), generations=0)) == x).all()
+    e = torch.empty((0, 64), dtype=torch.int64, device="cuda")
+    hip.step(e, generations=1)
+
+
+def test_inplace(hip, port):
+    x = port.fill(3001, seed=77)
+    d = to_dev(x)
+    hip.step(d, out=d, generations=1)
+    assert (to_host(d) == port.step_batch(x, 1)).all()
+    hip.step(d, out=d, generations=9)
+    assert (to_host(d) == port.step_batch(x, 10)).all()
+
+
+def test_overlap_rejected(hip):
+    d = torch.zeros((10, 64), dtype=torch.int64, device="cuda")
+    with pytest.raises(hip.LifeApiError) as e:
+        hip.step(d[:8], out=d[1:9], generations=1)
+    assert e.value.code == -1
+
+
+def test_iterated_randomstate_shaped(hip, port):
+    """Config-3 shape at small n: RandomState()-shaped columns, many gens."""
+    x = port.fill(1024, seed=3, mode=1)
+    got = to_host(hip.step(to_dev(x), generations=300))
+    assert (got == port.step_batch(x, 300, nthreads=8)).all()
+
+
+def test_rpentomino_1103(hip, port):
+    r = port.parse("b2o$2o$bo!")
+    got = to_host(hip.step(to_dev(r[None]), generations=1103))[0]
+    assert int(sum(bin(int(w)).count("1") for w in got)) == 113
+    assert (got == port.step_batch(r[None], 1103)[0]).all()
+
+
+def test_fill_matches_oracle(hip, port):
+    for mode in (0, 1):
+        got = to_host(hip.fill_random(1000, seed=42, first_universe=12345, mode=mode))
+        assert (got == port.fill(1000, 42, 12345, mode)).all()
+
+
+def test_pop_hash_digest(hip, port):
+    x = port.fill(5000, seed=9)
+    d = to_dev(x)
+    assert (hip.pop(d).cpu().numpy().astype(np.uint32) == port.pop(x)).all()
+    h = hip.hashes(d).cpu().numpy().view(np.uint64)
+    assert (h == port.hashes(x)).all()
+
+
+def test_contains(hip, port):
+    x = port.fill(600, seed=11)
+    block = port.parse("2o$2o!")
+    x[:200] = 0
+    x[:100, 10] |= np.uint64(3 << 20)
+    x[:100, 11] |= np.uint64(3 << 20)
+    wanted = np.roll(block, 10) << np.uint64(20)
+    unwanted = np.zeros(64, np.uint64)
+    for c in (9, 12):
+        unwanted[c] = np.uint64(0xF << 19)
+    unwanted[10] |= np.uint64(0x9 << 19)
+    unwanted[11] |= np.uint64(0x9 << 19)
+    got = hip.contains(to_dev(x), to_dev(wanted[None]), to_dev(unwanted[None])).cpu().numpy()
+    want = np.array([port.contains(x[u], wanted, unwanted) for u in range(len(x))])
+    assert (got.astype(bool) == want).all() and want[:100].all() and not want[100:200].any()
+
+
+def test_step_contains(hip, port):
+    # blinkers: contained every second generation
+    b = np.zeros(64, np.uint64)
+    b[30] = b[31] = b[32] = np.uint64(1 << 20)          # horizontal blinker
+    vert = port.step_batch(b[None], 1)[0]
+    x = np.stack([b, vert, port.fill(1, 5)[0]])
+    wanted = vert
+    unwanted = np.zeros(64, np.uint64)
+    first, final = hip.step_contains(to_dev(x), to_dev(wanted[None]), to_dev(unwanted[None]), 6,
+                                     final=torch.empty((3, 64), dtype=torch.int64, device="cuda"))
+    f = first.cpu().numpy()
+    exp = []
+    for u in range(3):
+        s, hit = x[u].copy(), 0
+        for g in range(1, 7):
+            s = port.step_batch(s[None], 1)[0]
+            if hit == 0 and port.contains(s, wanted, unwanted):
+                hit = g
+        exp.append(hit)
+    assert list(f) == exp and exp[0] == 1 and exp[1] == 2
+    assert (to_host(final) == port.step_batch(x, 6)).all()
+
+
+def test_host_api(hip, port):
+    x = port.fill(2500, seed=8)
+    assert (hip.step_host(x, 4, device=0).reshape(-1, 64) == port.step_batch(x, 4)).all()
+    assert (hip.step_host(x, 1, device=-1).reshape(-1, 64) == port.step_batch(x, 1)).all()
+    assert (hip.pop_host(x) == port.pop(x)).all()
+
+
+def test_full_size_config2(hip, port):
+    """Config 2 at full size (1M universes x 1 gen): every word vs the oracle."""
+    n = 1 << 20
+    d = hip.fill_random(n, seed=2)
+    x = to_host(d)
+    assert (x[:4096] == port.fill(4096, 2)).all()
+    got = to_host(hip.step(d, generations=1))
+    want = port.step_batch(x, 1, nthreads=16)
+    assert (got == want).all()
+    # checksum of checksums agrees too
+    assert port.digest(hip.hashes(hip.step(d)).cpu().numpy().view(np.uint64)) == \
+        port.digest(port.hashes(want))
