@@ -1,0 +1,158 @@
+#!/usr/bin/env python3
+"""Generates the golden fixtures in tests/golden/ FROM THE REFERENCE ITSELF.
+
+Run in the build container (needs oracle/_ref, i.e. /root/reference at build
+time):  make -C oracle ref && python tests/golden/make_golden.py
+
+Every expected output below is produced by the reference's own code
+(LifeState::Step / StepAlt / NeighbourCount / Parse / RandomState / GetPop /
+Contains, compiled from /root/reference by oracle/Makefile).  Inputs come from
+the build-defined splitmix64 generator (oracle_fill), from the reference's
+own RandomState(), or are hand-placed seam cases.  The fixtures are data only
+(inputs + expected outputs).  Digest fixtures use the build-defined hash
+(oracle_universe_hash / oracle_batch_digest), applied to reference outputs.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from oracle.oracle import Port, Ref  # noqa: E402
+
+P, R = Port(), Ref()
+
+
+def pop_words(s):
+    return int(sum(bin(int(w)).count("1") for w in s))
+
+
+def edge_cases():
+    names, out = [], []
+
+    def add(name, s):
+        names.append(name)
+        out.append(np.asarray(s, dtype=np.uint64).reshape(64))
+
+    add("empty", np.zeros(64))
+    add("all_on", np.full(64, 2**64 - 1, dtype=np.uint64))
+    add("checkerboard", [0xAAAAAAAAAAAAAAAA if x % 2 == 0 else 0x5555555555555555 for x in range(64)])
+    g = R.parse("bo$2bo$3o!")
+    add("glider", g)
+    add("glider_col_seam", np.roll(g, 62))
+    add("glider_row_seam", [((int(w) << 62) | (int(w) >> 2)) & (2**64 - 1) for w in g])
+    add("glider_corner", [((int(w) << 62) | (int(w) >> 2)) & (2**64 - 1) for w in np.roll(g, 62)])
+    s = np.zeros(64, np.uint64)
+    s[63] = s[0] = s[1] = np.uint64(1 << 63)          # blinker across column seam on row 63
+    add("blinker_both_seams", s)
+    s = np.zeros(64, np.uint64)
+    s[0] = np.uint64((1 << 63) | 1)
+    s[63] = np.uint64((1 << 63) | 1)                  # block split over all four corners
+    add("block_corners", s)
+    s = np.zeros(64, np.uint64)
+    s[0] = s[63] = np.uint64(0xFFFFFFFFFFFFFFFF)      # two full columns on the seam
+    add("full_seam_columns", s)
+    s = np.zeros(64, np.uint64)
+    for x in range(64):
+        s[x] = np.uint64(1 << 0) | np.uint64(1 << 63)  # full rows 0 and 63
+    add("full_seam_rows", s)
+    add("single_cell_corner", [1 if x == 0 else 0 for x in range(64)])
+    add("rpentomino", R.parse("b2o$2o$bo!"))
+    add("eater_pair", (R.parse("2b2o$bobo$bo$2o!") | np.roll(R.parse("2b2o$bobo$bo$2o!"), 5)))
+    add("randomstate_like", P.fill(1, 77, 0, 1)[0])
+    add("dense_random", P.fill(1, 78)[0] | P.fill(1, 79)[0])
+    return names, np.stack(out)
+
+
+def main():
+    meta = {"generator": "tests/golden/make_golden.py", "reference_lib": os.path.basename(R.path),
+            "reference": "scorbiclife/LifeAPI snapshot 2025-02-22 (/root/reference)"}
+
+    # 1. R-pentomino known answer, LifeAPI.hpp:1196 Step(), population trace 0..1103
+    r = R.parse("b2o$2o$bo!")
+    trace, s = [pop_words(r)], r.copy()
+    for _ in range(1103):
+        s = R.step_batch(s[None], 1)[0]
+        trace.append(pop_words(s))
+    np.savez(os.path.join(HERE, "rpentomino.npz"), initial=r, final=s,
+             pop_trace=np.array(trace, dtype=np.uint16))
+    meta["rpentomino"] = {"rle": "b2o$2o$bo!", "generations": 1103, "final_pop": trace[-1],
+                          "pop_at": {g: trace[g] for g in (0, 1, 2, 10, 100, 500, 1000, 1103)}}
+
+    # 2. seeded uniform random universes: Step^1, Step^1024
+    x = P.fill(256, seed=12345)
+    np.savez(os.path.join(HERE, "random_step.npz"), input=x, step1=R.step_batch(x, 1),
+             step1024=R.step_batch(x, 1024))
+    meta["random_step"] = {"n": 256, "seed": 12345, "mode": "uniform", "gens": [1, 1024]}
+
+    # 3. seam / edge cases: Step^g for g in 1, 2, 3, 4, 64, 256
+    names, e = edge_cases()
+    gens = [1, 2, 3, 4, 64, 256]
+    np.savez(os.path.join(HERE, "edge_cases.npz"), input=e, gens=np.array(gens),
+             **{f"step{g}": R.step_batch(e, g) for g in gens})
+    meta["edge_cases"] = {"names": names, "gens": gens}
+
+    # 4. the reference's own RandomState() distribution (StepAltTest.cpp:5-13):
+    #    Step, StepAlt and the NeighbourCount rule all from the reference
+    rs = np.stack([R.random_state() for _ in range(256)])
+    st = R.step_batch(rs, 1)
+    assert (R.step_alt(rs) == st).all() and (R.step_nc(rs) == st).all()
+    nc = np.stack([R.neighbour_count(rs[u]) for u in range(32)])
+    np.savez(os.path.join(HERE, "randomstate_kat.npz"), input=rs, step=st,
+             neighbour_count=nc)
+    meta["randomstate_kat"] = {"n": 256, "source": "LifeState::RandomState() (random_device seeded)",
+                               "neighbour_count_for_first": 32, "planes": "bit3,bit2,bit1,bit0"}
+
+    # 5. Contains(LifeTarget) (LifeTarget.hpp:44-51) on stepped random states
+    w = R.parse("2o$2o!")
+    wanted = np.roll(w, 20)
+    unwanted = np.zeros(64, np.uint64)
+    unwanted[19] = unwanted[22] = np.uint64(0xF)
+    unwanted[20] |= np.uint64(0x4)
+    unwanted[21] |= np.uint64(0x4)
+    y = P.fill(64, seed=31337)
+    y[:16] = 0
+    y[:8, 20] = y[:8, 21] = np.uint64(3)
+    y[8:12, 20] = y[8:12, 21] = np.uint64(3)
+    y[8:12, 19] = np.uint64(1)   # neighbouring cell -> unwanted violated
+    cont = np.array([R.contains(y[u], wanted, unwanted) for u in range(64)], dtype=np.uint8)
+    np.savez(os.path.join(HERE, "contains.npz"), states=y, wanted=wanted, unwanted=unwanted,
+             contains=cont)
+    meta["contains"] = {"n": 64, "true": int(cont.sum())}
+
+    # 6. full-size batch digests (checksum of checksums over reference outputs)
+    dig = {}
+    for name, n, seed, g in (("config2", 1 << 20, 2, 1), ("config3", 1 << 16, 3, 1024)):
+        xin = P.fill(n, seed=seed)
+        out = R.step_batch(xin, g, nthreads=8)
+        dig[name] = {"universes": n, "seed": seed, "generations": g,
+                     "input_digest": f"{P.digest(P.hashes(xin)):016x}",
+                     "output_digest": f"{P.digest(P.hashes(out)):016x}",
+                     "output_pop_total": int(P.pop(out).astype(np.uint64).sum())}
+    # config 4: 16M universes, 8 shards of 2M; additive digests per shard
+    shard, total, totin = [], 0, 0
+    for k in range(8):
+        xin = P.fill(1 << 21, seed=4, first_universe=k << 21)
+        out = R.step_batch(xin, 1, nthreads=8)
+        di = P.digest(P.hashes(xin), k << 21)
+        do = P.digest(P.hashes(out), k << 21)
+        shard.append(f"{do:016x}")
+        total = (total + do) % 2**64
+        totin = (totin + di) % 2**64
+    dig["config4"] = {"universes": 1 << 24, "seed": 4, "generations": 1, "shards": 8,
+                      "input_digest": f"{totin:016x}", "output_digest": f"{total:016x}",
+                      "shard_output_digests": shard}
+    meta["digests"] = dig
+    with open(os.path.join(HERE, "golden.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+    print(json.dumps(meta["digests"], indent=1))
+
+
+if __name__ == "__main__":
+    main()

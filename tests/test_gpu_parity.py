@@ -40,7 +40,8 @@ def seam_cases(port):
     out.append(chk)                                          # checkerboard -> empty
     g = port.parse("bo$2bo$3o!")                             # glider
     out.append(np.roll(g, 62))                               # glider straddling column seam
-    out.append(np.array([int(w) << 62 | int(w) >> 2 for w in g], dtype=np.uint64))  # row seam
+    out.append(np.array([(int(w) << 62 | int(w) >> 2) & (2**64 - 1) for w in g],
+                        dtype=np.uint64))                    # glider straddling row seam
     out.append(np.zeros(64, np.uint64))
     return np.stack(out)
 

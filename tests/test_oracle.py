@@ -1,0 +1,152 @@
+"""CPU: pin the oracle (C restatement) against the reference's golden vectors.
+
+The fixtures in tests/golden/ were produced by the reference's OWN code
+(tests/golden/make_golden.py, via oracle/_ref).  Where oracle/_ref is present
+(build container and GPU box) the restatement is also compared with the live
+reference on fresh seeded inputs.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def load(name):
+    return np.load(os.path.join(GOLD, name))  # allow_pickle=False (default)
+
+
+@pytest.fixture(scope="module")
+def meta():
+    with open(os.path.join(GOLD, "golden.json")) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("form", [0, 1, 2])
+def test_random_step_golden(port, form):
+    g = load("random_step.npz")
+    assert (port.step_batch(g["input"], 1, formulation=form) == g["step1"]).all()
+    assert (port.step_batch(g["input"], 1024, formulation=form) == g["step1024"]).all()
+
+
+def test_edge_cases_golden(port, meta):
+    g = load("edge_cases.npz")
+    for k in g["gens"]:
+        got = port.step_batch(g["input"], int(k))
+        bad = [meta["edge_cases"]["names"][i] for i in np.nonzero((got != g[f"step{k}"]).any(1))[0]]
+        assert not bad, f"gen {k}: {bad}"
+
+
+def test_edge_case_semantics(port, meta):
+    """Known behaviour of the fixtures themselves (not just self-consistency)."""
+    g = load("edge_cases.npz")
+    names = meta["edge_cases"]["names"]
+    x = dict(zip(names, g["input"]))
+    s1 = dict(zip(names, g["step1"]))
+    assert not s1["all_on"].any() and not s1["checkerboard"].any() and not s1["empty"].any()
+    assert (dict(zip(names, g["step2"]))["blinker_both_seams"] == x["blinker_both_seams"]).all()
+    assert (s1["block_corners"] == x["block_corners"]).all()
+    # glider: +1 column, +1 row every 4 generations, through both seams
+    s4 = dict(zip(names, g["step4"]))
+    for nm in ("glider", "glider_col_seam", "glider_row_seam", "glider_corner"):
+        moved = np.roll(x[nm], 1)
+        moved = np.array([((int(w) << 1) | (int(w) >> 63)) & (2**64 - 1) for w in moved], np.uint64)
+        assert (s4[nm] == moved).all(), nm
+    assert (dict(zip(names, g["step256"]))["glider"] == x["glider"]).all()
+
+
+def test_rpentomino_known_answer(port, meta):
+    g = load("rpentomino.npz")
+    r = port.parse("b2o$2o$bo!")
+    assert (r == g["initial"]).all()
+    s, trace = r.copy(), [int(port.pop(r[None])[0])]
+    for _ in range(1103):
+        s = port.step_batch(s[None], 1)[0]
+        trace.append(int(port.pop(s[None])[0]))
+    assert trace == g["pop_trace"].tolist()
+    assert (s == g["final"]).all()
+    assert trace[1103] == 113 and meta["rpentomino"]["final_pop"] == 113
+
+
+def test_randomstate_kat(port):
+    """StepAltTest.cpp:5-13 on the reference's own RandomState() draws."""
+    g = load("randomstate_kat.npz")
+    for form in (0, 1, 2):
+        assert (port.step_batch(g["input"], 1, formulation=form) == g["step"]).all()
+    # RandomState shape: row 61 always on, rows 62-63 off (LifeAPI.hpp:18-23)
+    assert ((g["input"] >> np.uint64(61)) == 1).all()
+    for u in range(g["neighbour_count"].shape[0]):
+        assert (port.neighbour_count(g["input"][u]) == g["neighbour_count"][u]).all()
+
+
+def test_contains_golden(port):
+    g = load("contains.npz")
+    got = [port.contains(g["states"][u], g["wanted"], g["unwanted"]) for u in range(64)]
+    assert np.array(got, dtype=np.uint8).tolist() == g["contains"].tolist()
+    assert g["contains"][:8].all() and not g["contains"][8:16].any()
+
+
+def test_digest_config3_golden(port, meta):
+    """Full config-3 workload (64K x 1024 gens) digest matches the reference's."""
+    d = meta["digests"]["config3"]
+    x = port.fill(d["universes"], d["seed"])
+    assert f"{port.digest(port.hashes(x)):016x}" == d["input_digest"]
+    out = port.step_batch(x, d["generations"], nthreads=8)
+    assert f"{port.digest(port.hashes(out)):016x}" == d["output_digest"]
+    assert int(port.pop(out).astype(np.uint64).sum()) == d["output_pop_total"]
+
+
+def test_digest_config2_input(port, meta):
+    d = meta["digests"]["config2"]
+    x = port.fill(d["universes"], d["seed"])
+    assert f"{port.digest(port.hashes(x)):016x}" == d["input_digest"]
+    out = port.step_batch(x, 1, nthreads=4)
+    assert f"{port.digest(port.hashes(out)):016x}" == d["output_digest"]
+    assert int(port.pop(out).astype(np.uint64).sum()) == d["output_pop_total"]
+
+
+def test_shard_digests_additive(port, meta):
+    """Config-4 sharding: shard digests (first_universe offsets) add to the global one."""
+    d = meta["digests"]["config4"]
+    k = 3
+    x = port.fill(4096, d["seed"], first_universe=k << 21)
+    h = port.hashes(x)
+    whole = port.digest(h, k << 21)
+    parts = (port.digest(h[:1000], k << 21) + port.digest(h[1000:], (k << 21) + 1000)) % 2**64
+    assert whole == parts
+
+
+def test_parse_semantics(port):
+    r = port.parse("x = 3, y = 3, rule = B3/S23\nb2o$2o$bo!")
+    assert (r == port.parse("b2o$2o$bo!")).all()
+    assert port.parse("o$$o!")[0] == 0b101       # bare '$' counts as 1 (Parsing.hpp:161-162)
+    assert port.parse("3o!")[2] == 1
+    with pytest.raises(ValueError):
+        port.parse("65bo!")
+
+
+# ---- live reference (present where oracle/_ref was built) ----
+
+def test_port_equals_reference_live(port, ref):
+    for seed, mode in ((101, 0), (102, 1)):
+        x = port.fill(3000, seed, mode=mode)
+        for gens in (1, 7):
+            assert (port.step_batch(x, gens) == ref.step_batch(x, gens)).all()
+    x = port.fill(200, 103)
+    assert (ref.step_alt(x) == port.step_batch(x, 1, formulation=1)).all()
+    assert (ref.step_nc(x) == port.step_batch(x, 1, formulation=2)).all()
+    for u in range(20):
+        assert (ref.neighbour_count(x[u]) == port.neighbour_count(x[u])).all()
+
+
+def test_reference_random_state_shape(ref, port):
+    rs = np.stack([ref.random_state() for _ in range(64)])
+    assert ((rs >> np.uint64(61)) == 1).all()
+    assert (port.step_batch(rs, 1) == ref.step_batch(rs, 1)).all()
+
+
+def test_parse_equals_reference(port, ref):
+    for rle in ("b2o$2o$bo!", "bo$2bo$3o!", "2b2o$bobo$bo$2o!", "x = 1\n3o$b2o3$o!", "o2$3bo!"):
+        assert (port.parse(rle) == ref.parse(rle)).all(), rle
