@@ -27,6 +27,9 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from lifeapi_amd.digest import batch_digest  # noqa: E402
+from lifeapi_amd.shard import gather_hashes, weak_shard  # noqa: E402
+
 METRIC = "64x64 universe-generations/sec (+ cell-updates/sec) at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
 VALU_PEAK_TOPS = 39.3216    # 256 CU x 64 lanes x 2.4 GHz int32 ops (1 op/lane/clk)
@@ -128,6 +131,29 @@ def secondary_config3(hip, device, stream):
                          "frac": OPS_PER_UNIVERSE_GEN * gps / 1e12 / VALU_PEAK_TOPS}}
 
 
+def verify_first_launch(hip, out, first, n, gens, seed, stream, world, device):
+    """Digest of the first launch's output vs the reference's (golden.json)."""
+    gold = os.path.join(ROOT, "tests", "golden", "golden.json")
+    want = None
+    try:
+        with open(gold) as f:
+            d = json.load(f)["digests"]["weak_shards_seed2"]
+        k = first // n
+        if (gens == 1 and seed == d["seed"] and n == d["universes_per_rank"]
+                and k < len(d["shard_output_digests"])):
+            want = d["shard_output_digests"][k]
+    except (OSError, ValueError, KeyError):
+        pass
+    got = f"{batch_digest(hip.hashes(out, stream=stream).cpu().numpy(), first):016x}"
+    ok = None if want is None else got == want
+    if world > 1 and ok is not None:
+        f = torch.tensor([0 if ok else 1], device=device)
+        dist.all_reduce(f)
+        ok = int(f.item()) == 0
+    return {"ok": ok, "first_launch_digest_rank0": got, "expected": want,
+            "against": "tests/golden/golden.json weak_shards_seed2 (reference Step(), all ranks)"}
+
+
 def load_pmc_traffic(n: int):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, if it matches."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -153,18 +179,22 @@ def main():
     import lifeapi_amd.hip as hip
 
     n, gens = args.universes, args.gens_per_step
-    first = rank * n                         # contiguous shard of the global array
+    first, _ = weak_shard(rank, n)           # contiguous shard of the global array
     stream = torch.cuda.current_stream(device)
     a = hip.fill_random(n, seed=args.seed, first_universe=first, device=device, stream=stream)
     b = torch.empty_like(a)
-    x_head = a[: min(n, 2048)].cpu().numpy().view(np.uint64).copy()  # for the parity spot check
     want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
     x_full = a.cpu().numpy().view(np.uint64).copy() if want_cpu else None
     bufs = [a, b]
 
-    # warmup (untimed)
-    _, cur = timed_launches(hip, bufs, args.warmup, gens, stream)
-    bufs = [bufs[cur], bufs[1 - cur]]
+    # warmup (untimed); the first launch's output is checked against the
+    # reference-generated digest of this shard (tests/golden/golden.json)
+    hip.step(bufs[0], out=bufs[1], generations=gens, stream=stream)
+    verified = None
+    if not args.no_verify:
+        verified = verify_first_launch(hip, bufs[1], first, n, gens, args.seed, stream, world, device)
+    _, cur = timed_launches(hip, [bufs[1], bufs[0]], max(args.warmup - 1, 0), gens, stream)
+    bufs = [bufs[1], bufs[0]] if cur == 0 else [bufs[0], bufs[1]]
     torch.cuda.synchronize(device)
 
     # timed region: barrier + sync on both sides, max over ranks
@@ -189,29 +219,15 @@ def main():
     torch.cuda.synchronize(device)
     collect = None
     if world > 1:
-        gathered = torch.empty(world * n, dtype=torch.int64, device=device)
         dist.barrier()
         c0 = time.perf_counter()
-        dist.all_gather_into_tensor(gathered, h)
+        gathered = gather_hashes(h, world)
         torch.cuda.synchronize(device)
         cms = (time.perf_counter() - c0) * 1e3
         collect = {"op": "all_gather(per-universe hash, RCCL)", "bytes_per_rank": n * 8,
                    "ms": cms}
-
-    # parity spot check of the timed kernel's output against the oracle
-    verified = None
-    if not args.no_verify:
-        from oracle.oracle import Port
-        m = x_head.shape[0]
-        total_gens = (args.warmup + args.steps) * gens
-        got = final[:m].cpu().numpy().view(np.uint64)
-        want = Port().step_batch(x_head, total_gens, nthreads=8)
-        ok = bool((got == want).all())
-        if world > 1:
-            f = torch.tensor([0 if ok else 1], device=device)
-            dist.all_reduce(f)
-            ok = int(f.item()) == 0
-        verified = {"ok": ok, "universes_checked_per_rank": m, "generations": total_gens}
+        if rank == 0:
+            collect["final_digest"] = f"{batch_digest(gathered.cpu().numpy()):016x}"
 
     secondary = None
     if rank == 0 and world == 1 and not args.no_secondary:

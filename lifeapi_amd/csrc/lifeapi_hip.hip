@@ -484,13 +484,14 @@ void lifeapi_default_cfg(lifeapi_launch_cfg *cfg, uint32_t generations) {
   if (!cfg) return;
   cfg->xchg = LIFEAPI_XCHG_DPP;
   cfg->rule = 0;
-  if (generations <= 1) {  // HBM-streaming regime
+  // Measured on MI355X (profiles/r01/tune.jsonl): a one-shot grid (no
+  // grid-stride cap) beats every capped grid in both regimes.
+  cfg->blocks_per_cu = 0;
+  if (generations <= 1) {  // HBM-streaming regime: 4 x 512 B loads in flight per wave
     cfg->universes_per_wave = 4;
-    cfg->blocks_per_cu = 8;
     cfg->nontemporal = 1;
   } else {  // VALU regime: state resident in VGPRs for all generations
-    cfg->universes_per_wave = 2;
-    cfg->blocks_per_cu = 0;
+    cfg->universes_per_wave = 1;
     cfg->nontemporal = 0;
   }
 }

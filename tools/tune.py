@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""Launch-configuration sweep for the step kernel (measurement tool).
+
+Times every lifeapi_launch_cfg variant on the config-2 (1M x 1 gen) and
+config-3 (64K x 1024 gens) workloads in ONE process, interleaving rounds so
+that clock drift hits all variants alike (cdna_hip_programming.md rule 24),
+and checks each variant's output against the default variant bit-for-bit.
+Prints one JSON line per (workload, variant) with best/median kernel time.
+"""
+from __future__ import annotations
+
+import argparse
+import itertools
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import lifeapi_amd.hip as hip  # noqa: E402
+
+
+def timeit(fn, reps):
+    out = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        e1.synchronize()
+        out.append(e0.elapsed_time(e1))
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", choices=["c2", "c3", "both"], default="both")
+    ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--quick", action="store_true")
+    args = ap.parse_args()
+
+    work = []
+    if args.workload in ("c2", "both"):
+        n, g = 1 << 20, 1
+        xs = [0, 1, 2]
+        us = [1, 2, 4, 8]
+        bpcs = [4, 8, 16, 0] if not args.quick else [8, 0]
+        nts = [0, 1]
+        rules = [0] if args.quick else [0, 1]
+        work.append(("c2", n, g, list(itertools.product(xs, us, bpcs, nts, rules))))
+    if args.workload in ("c3", "both"):
+        n, g = 1 << 16, 1024
+        work.append(("c3", n, g, list(itertools.product([0, 1, 2], [1, 2, 4, 8], [2, 4, 8, 0], [0], [0, 1]))))
+
+    for name, n, g, cfgs in work:
+        a = hip.fill_random(n, seed=2)
+        ref = hip.step(a, generations=g)
+        b = torch.empty_like(a)
+        ms = {c: [] for c in cfgs}
+        ok = {}
+        if name == "c2":  # stream-copy ceiling of the same bytes, for context
+            copy_ms = []
+        for r in range(args.rounds):
+            for c in cfgs:
+                cfg = hip.LaunchCfg(*c)
+                ms[c] += timeit(lambda: hip.step(a, out=b, generations=g, cfg=cfg), args.reps)
+                if r == 0:
+                    torch.cuda.synchronize()
+                    ok[c] = bool(torch.equal(b, ref))
+            if name == "c2":
+                copy_ms += timeit(lambda: b.copy_(a), args.reps)
+        for c in cfgs:
+            t = sorted(ms[c])
+            best, med = t[0], t[len(t) // 2]
+            rec = {"workload": name, "n": n, "gens": g, "xchg": c[0], "universes_per_wave": c[1],
+                   "blocks_per_cu": c[2], "nontemporal": c[3], "rule": c[4], "ms_best": best,
+                   "ms_median": med, "gen_per_s_median": n * g / (med / 1e3), "bit_exact": ok[c]}
+            if name == "c2":
+                rec["GBps_median"] = n * 1024 / (med / 1e3) / 1e9
+            print(json.dumps(rec), flush=True)
+        if name == "c2":
+            t = sorted(copy_ms)
+            print(json.dumps({"workload": "c2-torch-copy", "ms_best": t[0], "ms_median": t[len(t) // 2],
+                              "GBps_median": n * 1024 / (t[len(t) // 2] / 1e3) / 1e9}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
