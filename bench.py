@@ -154,6 +154,29 @@ def verify_first_launch(hip, out, first, n, gens, seed, stream, world, device):
             "against": "tests/golden/golden.json weak_shards_seed2 (reference Step(), all ranks)"}
 
 
+def secondary_config5(hip, device, stream):
+    """Config 5: unknown_step_refined ternary step, 256K universes, one launch."""
+    n = 1 << 18
+    planes = hip.fill_random(n * 11, seed=6, device=device, stream=stream).reshape(n, 11 * 64)
+    out = torch.empty((n, 3 * 64), dtype=torch.int64, device=device)
+    hip.refined_step(planes, out=out, stream=stream)  # warm
+    ms = []
+    for _ in range(10):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        hip.refined_step(planes, out=out, stream=stream)
+        e1.record(stream)
+        e1.synchronize()
+        ms.append(e0.elapsed_time(e1))
+    t = sorted(ms)[len(ms) // 2] / 1e3
+    ups = n / t
+    return {"workload": "config5: 256K universes, unknown_step_refined (11 planes in, 3 out)",
+            "value": ups, "unit": "universe-steps/s", "kernel_ms_median": t * 1e3,
+            "roofline": {"bound": "hbm", "achieved": n * 7168 / t / 1e9, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": n * 7168 / t / 1e9 / HBM_PEAK_GBS,
+                         "algorithmic_bytes_per_universe": 7168}}
+
+
 def load_pmc_traffic(n: int):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, if it matches."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -231,7 +254,8 @@ def main():
 
     secondary = None
     if rank == 0 and world == 1 and not args.no_secondary:
-        secondary = {"config3": secondary_config3(hip, device, stream)}
+        secondary = {"config3": secondary_config3(hip, device, stream),
+                     "config5": secondary_config5(hip, device, stream)}
 
     cpu = None
     if want_cpu:

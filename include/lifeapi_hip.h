@@ -94,6 +94,14 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
                                     const uint64_t *d_wanted, const uint64_t *d_unwanted,
                                     uint32_t *d_first_gen, size_t n, uint32_t generations,
                                     void *stream);
+/* Config-5 ternary step: bitslicing/unknown_step_refined.hpp:1-85 applied
+ * per column with s2..s0 / on2..on0 = bits 2..0 of NeighbourCount
+ * (NeighbourCount.hpp:40-70) of stable.state / current.state.
+ * d_in: n x 11 planes x 64 words (stable.state, current.state,
+ * current.unknown, live2, live3, dead0, dead1, dead2, dead4, dead5, dead6;
+ * option planes 1 = ruled out, LifeStable.hpp:41-53).  d_out: n x 3 planes
+ * (next_on, next_unknown, next_unknown_stable).  No overlap allowed.      */
+int lifeapi_refined_step_batch_dev(const uint64_t *d_in, uint64_t *d_out, size_t n, void *stream);
 /* synthetic universes: word w = u*64+x (u counted from first_universe) is
  * splitmix64(seed + (w+1)*0x9E3779B97F4A7C15); mode 1 maps each column to
  * [2^61, 2^62) like RandomState()                                         */

@@ -288,6 +288,61 @@ __global__ __launch_bounds__(kBlock) void k_step_contains(const uint64_t *__rest
   }
 }
 
+// ---- config 5: the unknown_step_refined ternary step --------------------
+// Bits 2..0 of the inclusive 3x3 count of this lane's column: the
+// NeighbourCount adder chain (NeighbourCount.hpp:40-70) as CountRows + DPP
+// neighbour planes + two FullAdds (count = fs + 2(fc+cs) + 4cc).
+__device__ __forceinline__ void ncount3(W a, W &b2, W &b1, W &b0) {
+  const W up = rot_up(a), dn = rot_dn(a);
+  const W c0 = lut3<kXor3>(up, dn, a), c1 = lut3<kMaj>(up, dn, a);
+  W L0, R0, L1, R1;
+  neighbours<XDPP>(c0, c1, L0, R0, L1, R1, nullptr, 0);
+  const W fs = lut3<kXor3>(L0, c0, R0), fc = lut3<kMaj>(L0, c0, R0);
+  const W cs = lut3<kXor3>(L1, c1, R1), cc = lut3<kMaj>(L1, c1, R1);
+  b0 = fs;
+  b1 = W{fc.lo ^ cs.lo, fc.hi ^ cs.hi};
+  b2 = lut3<kCarry2>(cc, fc, cs);
+}
+
+// bitslicing/unknown_step_refined.hpp:1-85 as a v_bitop3 network.  The
+// network is generated (tools/synth_bitop3.py) from the fragment's complete
+// truth table, which tests/golden/make_golden.py extracts from the reference
+// build, and is verified against all 2^16 input combinations when generated.
+__device__ __forceinline__ void refined_circuit(const W (&x)[16], W &next_on, W &next_unknown,
+                                                W &next_unknown_stable) {
+#include "refined_circuit.inc"
+}
+
+// One wave per universe.  In: 11 planes x 64 words (stable.state,
+// current.state, current.unknown, live2, live3, dead0, dead1, dead2, dead4,
+// dead5, dead6 -- LifeStable.hpp:41-53 with options stored as "1 = ruled
+// out").  Out: 3 planes (next_on, next_unknown, next_unknown_stable).
+__global__ __launch_bounds__(kBlock) void k_refined(const uint64_t *__restrict__ in,
+                                                    uint64_t *__restrict__ out, uint64_t n) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock;
+  for (uint64_t u = (uint64_t)blockIdx.x * kWavesPerBlock + wib; u < n; u += stride) {
+    const uint64_t *p = in + u * 11 * kWave + lane;
+    W pl[11];
+#pragma unroll
+    for (int k = 0; k < 11; ++k) pl[k] = ld<true>(p + k * kWave);
+    W x[16];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = pl[3 + k];  // l2 l3 d0 d1 d2 d4 d5 d6
+    x[8] = pl[2];                                  // current_unknown
+    x[9] = pl[1];                                  // current_on
+    ncount3(pl[0], x[10], x[11], x[12]);           // s2 s1 s0
+    ncount3(pl[1], x[13], x[14], x[15]);           // on2 on1 on0
+    W o0, o1, o2;
+    refined_circuit(x, o0, o1, o2);
+    uint64_t *q = out + u * 3 * kWave + lane;
+    st<true>(q, o0);
+    st<true>(q + kWave, o1);
+    st<true>(q + 2 * kWave, o2);
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_fill(uint64_t *__restrict__ out, uint64_t nwords,
                                                  uint64_t seed, uint64_t first_word, int mode) {
   const uint64_t stride = (uint64_t)gridDim.x * kBlock;
@@ -575,6 +630,20 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
                      (hipStream_t)stream, d_in, d_final, d_wanted, d_unwanted, d_first_gen,
                      (uint64_t)n, generations);
   return launched("k_step_contains launch");
+}
+
+int lifeapi_refined_step_batch_dev(const uint64_t *d_in, uint64_t *d_out, size_t n, void *stream) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!d_in || !d_out || !aligned8(d_in) || !aligned8(d_out))
+    return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_refined_step_batch_dev%s");
+  const uintptr_t a = (uintptr_t)d_in, b = (uintptr_t)d_out;
+  if (a < b + n * 3 * 512 && b < a + n * 11 * 512)
+    return fail(LIFEAPI_E_INVALID, "refined step input and output overlap%s");
+  int cus = 0, rc = device_cus(cus);
+  if (rc != LIFEAPI_OK) return rc;
+  hipLaunchKernelGGL(k_refined, dim3(grid_for(n, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream,
+                     d_in, d_out, (uint64_t)n);
+  return launched("k_refined launch");
 }
 
 int lifeapi_fill_random_dev(uint64_t *d_out, size_t n, uint64_t seed, uint64_t first_universe,

@@ -60,6 +60,7 @@ _SIGS = {
     "lifeapi_contains_batch_dev": ([_vp, _vp, _vp, _vp, _sz, _vp], _int),
     "lifeapi_step_contains_batch_dev": ([_vp, _vp, _vp, _vp, _vp, _sz, _u32, _vp], _int),
     "lifeapi_fill_random_dev": ([_vp, _sz, _u64, _u64, _int, _vp], _int),
+    "lifeapi_refined_step_batch_dev": ([_vp, _vp, _sz, _vp], _int),
     "lifeapi_step_batch": ([_vp, _vp, _sz, _u32, _int], _int),
     "lifeapi_pop_batch": ([_vp, _vp, _sz, _int], _int),
 }
@@ -210,3 +211,16 @@ def loaded_hip_runtimes() -> list[str]:
             if "libamdhip64" in p:
                 paths.add(p)
     return sorted(paths)
+
+
+def refined_step(planes: torch.Tensor, out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+    """Config-5 ternary step: (n, 11*64) int64 planes -> (n, 3*64) planes
+    (see lifeapi_refined_step_batch_dev)."""
+    if not planes.is_cuda or planes.dtype not in (torch.int64, torch.uint64) or \
+            not planes.is_contiguous() or planes.numel() % (11 * N):
+        raise ValueError("planes must be a contiguous int64 device tensor of shape (n, 11*64)")
+    n = planes.numel() // (11 * N)
+    if out is None:
+        out = torch.empty((n, 3 * N), dtype=torch.int64, device=planes.device)
+    _check(lib.lifeapi_refined_step_batch_dev(planes.data_ptr(), out.data_ptr(), n, _stream(stream)))
+    return out

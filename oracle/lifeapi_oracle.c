@@ -263,3 +263,41 @@ uint64_t oracle_batch_digest(const uint64_t *hashes, size_t n, uint64_t first_un
     acc += oracle_splitmix64_mix(hashes[u] + (first_universe + u + 1) * GOLDEN);
   return acc;
 }
+
+/* ---- config 5: the unknown_step_refined harness ----
+ * bitslicing/unknown_step_refined.hpp:1-85 is an espresso sum-of-products
+ * over 16 per-cell inputs.  The oracle evaluates that function by TABLE
+ * LOOKUP: tt holds the fragment's complete truth table (3 x 65536 bytes of
+ * 0/1, index bit i = input i in the order l2 l3 d0 d1 d2 d4 d5 d6
+ * current_unknown current_on s2 s1 s0 on2 on1 on0), extracted from the
+ * reference build by tests/golden/make_golden.py.  Inputs per universe: 11
+ * planes (stable.state, current.state, current.unknown, live2, live3, dead0,
+ * dead1, dead2, dead4, dead5, dead6); s* / on* = bits 2..0 of the inclusive
+ * NeighbourCount (NeighbourCount.hpp:40-70) of stable.state / current.state.
+ * Output: next_on, next_unknown, next_unknown_stable planes. */
+void oracle_refined_step_batch(const uint64_t *in, uint64_t *out, size_t n, const uint8_t *tt) {
+  for (size_t u = 0; u < n; ++u) {
+    const uint64_t *p = in + u * 11 * 64;
+    uint64_t *o = out + u * 3 * 64;
+    uint64_t s3[64], s2[64], s1[64], s0[64], c3[64], c2[64], c1[64], c0[64];
+    oracle_neighbour_count(p, s3, s2, s1, s0);
+    oracle_neighbour_count(p + 64, c3, c2, c1, c0);
+    for (int x = 0; x < 64; ++x) {
+      const uint64_t planes[16] = {p[3 * 64 + x], p[4 * 64 + x], p[5 * 64 + x], p[6 * 64 + x],
+                                   p[7 * 64 + x], p[8 * 64 + x], p[9 * 64 + x], p[10 * 64 + x],
+                                   p[2 * 64 + x], p[1 * 64 + x], s2[x], s1[x], s0[x],
+                                   c2[x], c1[x], c0[x]};
+      uint64_t r0 = 0, r1 = 0, r2 = 0;
+      for (int y = 0; y < 64; ++y) {
+        unsigned idx = 0;
+        for (int i = 0; i < 16; ++i) idx |= (unsigned)((planes[i] >> y) & 1u) << i;
+        r0 |= (uint64_t)(tt[idx] & 1u) << y;
+        r1 |= (uint64_t)(tt[65536 + idx] & 1u) << y;
+        r2 |= (uint64_t)(tt[2 * 65536 + idx] & 1u) << y;
+      }
+      o[x] = r0;
+      o[64 + x] = r1;
+      o[128 + x] = r2;
+    }
+  }
+}

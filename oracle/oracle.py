@@ -71,6 +71,9 @@ class Port:
         L.oracle_batch_digest.argtypes = [_u64p, ctypes.c_size_t, ctypes.c_uint64]
         L.oracle_batch_digest.restype = ctypes.c_uint64
         L.oracle_neighbour_count.argtypes = [_u64p] * 5
+        L.oracle_refined_step_batch.argtypes = [_u64p, _u64p, ctypes.c_size_t,
+                                                ctypes.POINTER(ctypes.c_uint8)]
+        self._tt = None
         for name in ("oracle_step", "oracle_step_alt", "oracle_step_nc"):
             getattr(L, name).argtypes = [_u64p]
 
@@ -119,6 +122,21 @@ class Port:
         self.lib.oracle_neighbour_count(_p64(s), _p64(b[0]), _p64(b[1]), _p64(b[2]), _p64(b[3]))
         return b  # bit3, bit2, bit1, bit0
 
+    def refined_truth_table(self) -> np.ndarray:
+        if self._tt is None:
+            path = os.path.join(os.path.dirname(HERE), "tests", "golden", "unknown_step_refined_tt.npz")
+            self._tt = np.ascontiguousarray(np.load(path)["tt"].astype(np.uint8))
+        return self._tt
+
+    def refined_step(self, planes: np.ndarray) -> np.ndarray:
+        """Config-5 harness: (n, 11*64) input planes -> (n, 3*64) output planes."""
+        src = np.ascontiguousarray(planes, dtype=np.uint64).reshape(-1, 11 * 64)
+        out = np.zeros((src.shape[0], 3 * 64), dtype=np.uint64)
+        tt = self.refined_truth_table()
+        self.lib.oracle_refined_step_batch(_p64(src), _p64(out), src.shape[0],
+                                           tt.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
+        return out
+
 
 class Ref:
     """The reference's own code (oracle/_ref/libref_v*.so)."""
@@ -141,6 +159,8 @@ class Ref:
         L.ref_parse.argtypes = [ctypes.c_char_p, _u64p]
         L.ref_neighbour_count.argtypes = [_u64p] * 5
         L.ref_count_neighbourhood.argtypes = [_u64p] * 5
+        L.ref_unknown_step_refined.argtypes = [_u64p, _u64p]
+        L.ref_refined_step_batch.argtypes = [_u64p, _u64p, ctypes.c_size_t]
 
     @staticmethod
     def available() -> bool:
@@ -189,3 +209,10 @@ class Ref:
         b = np.zeros((4, 64), dtype=np.uint64)
         self.lib.ref_neighbour_count(_p64(s), _p64(b[0]), _p64(b[1]), _p64(b[2]), _p64(b[3]))
         return b
+
+    def refined_step(self, planes: np.ndarray) -> np.ndarray:
+        """Config-5 harness around the reference's own fragment (ref_shim.cpp)."""
+        src = np.ascontiguousarray(planes, dtype=np.uint64).reshape(-1, 11 * 64)
+        out = np.zeros((src.shape[0], 3 * 64), dtype=np.uint64)
+        self.lib.ref_refined_step_batch(_p64(src), _p64(out), src.shape[0])
+        return out

@@ -62,6 +62,51 @@ void ref_parse(const char *rle, uint64_t *out) { store(LifeState::Parse(std::str
 // LifeState::RandomState  LifeAPI.hpp:63-69 (non-deterministic, random_device seeded)
 void ref_random_state(uint64_t *out) { store(LifeState::RandomState(), out); }
 
+// ---- config 5: bitslicing/unknown_step_refined.hpp (the espresso fragment)
+// Inputs in the fragment's own variable names, 64 cells per word, in the
+// order of bitslicing/unknown_step_refined.py:105-113 (innames) with the
+// older live-count encoding on2..on0 (bits 2..0 of the inclusive live count,
+// :99) that this fragment was generated from.
+void ref_unknown_step_refined(const uint64_t *in16, uint64_t *out3) {
+  const uint64_t l2 = in16[0], l3 = in16[1], d0 = in16[2], d1 = in16[3], d2 = in16[4],
+                 d4 = in16[5], d5 = in16[6], d6 = in16[7], current_unknown = in16[8],
+                 current_on = in16[9], s2 = in16[10], s1 = in16[11], s0 = in16[12],
+                 on2 = in16[13], on1 = in16[14], on0 = in16[15];
+  uint64_t next_on = 0, next_unknown = 0, next_unknown_stable = 0;
+#include "bitslicing/unknown_step_refined.hpp"
+  out3[0] = next_on;
+  out3[1] = next_unknown;
+  out3[2] = next_unknown_stable;
+}
+
+// Config-5 harness (build-defined; the reference has no consumer of this
+// fragment).  Per universe, 11 input planes of 64 words:
+//   0 stable.state  1 current.state (ON)  2 current.unknown
+//   3..10 live2 live3 dead0 dead1 dead2 dead4 dead5 dead6 (LifeStable.hpp:44-53,
+//         1 = ruled out)
+// s2..s0  = bits 2..0 of NeighbourCount(stable.state)    (NeighbourCount.hpp:40-70)
+// on2..on0 = bits 2..0 of NeighbourCount(current.state)
+// Output per universe, 3 planes: next_on, next_unknown, next_unknown_stable.
+void ref_refined_step_batch(const uint64_t *in, uint64_t *out, size_t n) {
+  for (size_t u = 0; u < n; ++u) {
+    const uint64_t *p = in + u * 11 * 64;
+    uint64_t *o = out + u * 3 * 64;
+    NeighbourCount ns(load(p + 0 * 64)), nc(load(p + 1 * 64));
+    for (unsigned i = 0; i < 64; ++i) {
+      const uint64_t in16[16] = {p[3 * 64 + i], p[4 * 64 + i], p[5 * 64 + i], p[6 * 64 + i],
+                                 p[7 * 64 + i], p[8 * 64 + i], p[9 * 64 + i], p[10 * 64 + i],
+                                 p[2 * 64 + i], p[1 * 64 + i],
+                                 ns.bit2[i], ns.bit1[i], ns.bit0[i],
+                                 nc.bit2[i], nc.bit1[i], nc.bit0[i]};
+      uint64_t r[3];
+      ref_unknown_step_refined(in16, r);
+      o[0 * 64 + i] = r[0];
+      o[1 * 64 + i] = r[1];
+      o[2 * 64 + i] = r[2];
+    }
+  }
+}
+
 // Batched Stepped(gens) (LifeAPI.hpp:882-886) over independent universes, one
 // contiguous slice per std::thread: the reference algorithm on host cores.
 void ref_step_batch(const uint64_t *in, uint64_t *out, size_t n, unsigned gens, int nthreads) {

@@ -28,6 +28,38 @@ from oracle.oracle import Port, Ref  # noqa: E402
 
 P, R = Port(), Ref()
 
+import ctypes  # noqa: E402
+
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+R.lib.ref_unknown_step_refined.argtypes = [_u64p, _u64p]
+R.lib.ref_refined_step_batch.argtypes = [_u64p, _u64p, ctypes.c_size_t]
+
+# the fragment's input variables, in bitslicing/unknown_step_refined.py:105-113
+# order with the live-count encoding the fragment was generated from
+REFINED_INPUTS = ["l2", "l3", "d0", "d1", "d2", "d4", "d5", "d6", "current_unknown",
+                  "current_on", "s2", "s1", "s0", "on2", "on1", "on0"]
+REFINED_OUTPUTS = ["next_on", "next_unknown", "next_unknown_stable"]
+
+
+def _p64(a):
+    return a.ctypes.data_as(_u64p)
+
+
+def refined_truth_table() -> np.ndarray:
+    """(3, 65536) uint8: output bits of the reference fragment for every input
+    combination c (bit i of c = REFINED_INPUTS[i]), evaluated 64 at a time."""
+    c = np.arange(1 << 16, dtype=np.uint64).reshape(1024, 64)
+    shifts = np.arange(64, dtype=np.uint64)
+    words = np.stack([(((c >> np.uint64(i)) & np.uint64(1)) << shifts).sum(axis=1, dtype=np.uint64)
+                      for i in range(16)])  # (16, 1024)
+    out = np.zeros((3, 1024), np.uint64)
+    for w in range(1024):
+        a = np.ascontiguousarray(words[:, w])
+        o = np.zeros(3, np.uint64)
+        R.lib.ref_unknown_step_refined(_p64(a), _p64(o))
+        out[:, w] = o
+    return np.unpackbits(out.view(np.uint8), bitorder="little").reshape(3, 1 << 16)
+
 
 def pop_words(s):
     return int(sum(bin(int(w)).count("1") for w in s))
@@ -130,6 +162,23 @@ def main():
     np.savez(os.path.join(HERE, "contains.npz"), states=y, wanted=wanted, unwanted=unwanted,
              contains=cont)
     meta["contains"] = {"n": 64, "true": int(cont.sum())}
+
+    # 5b. config 5: bitslicing/unknown_step_refined.hpp (the reference's espresso
+    #     fragment) as a complete truth table over its 16 inputs, plus seeded
+    #     11-plane universes through the build-defined harness (ref_shim.cpp)
+    tt = refined_truth_table()
+    np.savez_compressed(os.path.join(HERE, "unknown_step_refined_tt.npz"), tt=tt,
+                        inputs=np.array(REFINED_INPUTS), outputs=np.array(REFINED_OUTPUTS))
+    xin = P.fill(64 * 11, seed=5).reshape(64, 11 * 64)
+    rout = np.zeros((64, 3 * 64), np.uint64)
+    R.lib.ref_refined_step_batch(_p64(xin), _p64(rout), 64)
+    np.savez(os.path.join(HERE, "refined_step.npz"), input=xin, output=rout)
+    meta["unknown_step_refined"] = {"inputs": REFINED_INPUTS, "outputs": REFINED_OUTPUTS,
+                                    "ones_per_output": [int(v) for v in tt.sum(axis=1)],
+                                    "harness_universes": 64, "harness_seed": 5,
+                                    "planes_in": ["stable.state", "current.state", "current.unknown",
+                                                  "live2", "live3", "dead0", "dead1", "dead2",
+                                                  "dead4", "dead5", "dead6"]}
 
     # 6. full-size batch digests (checksum of checksums over reference outputs)
     dig = {}

@@ -182,3 +182,34 @@ def test_full_size_config2(hip, port):
     # checksum of checksums agrees too
     assert port.digest(hip.hashes(hip.step(d)).cpu().numpy().view(np.uint64)) == \
         port.digest(port.hashes(want))
+
+
+# ---- config 5: unknown_step_refined ternary step ----
+
+def test_refined_step_golden(hip, port):
+    import os
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "refined_step.npz"))
+    got = hip.refined_step(to_dev(g["input"]).reshape(-1, 11 * 64))
+    torch.cuda.synchronize()
+    assert (got.cpu().numpy().view(np.uint64) == g["output"]).all()
+
+
+@pytest.mark.parametrize("n", [1, 5, 1000, 4099])
+def test_refined_step_vs_oracle(hip, port, n):
+    x = port.fill(n * 11, seed=500 + n).reshape(n, 11 * 64)
+    if n > 5:  # realistic-ish planes: sparse states, dense option masks
+        x[: n // 2, :64] &= port.fill(n // 2, seed=1)[:, :] & port.fill(n // 2, seed=2)
+    got = hip.refined_step(to_dev(x).reshape(n, 11 * 64))
+    torch.cuda.synchronize()
+    assert (got.cpu().numpy().view(np.uint64) == port.refined_step(x)).all()
+
+
+def test_refined_step_full_size_sample(hip, port):
+    """Config 5 at full size (256K universes): prefix and strided sample vs the oracle."""
+    n = 1 << 18
+    d = hip.fill_random(n * 11, seed=6).reshape(n, 11 * 64)
+    got = hip.refined_step(d)
+    torch.cuda.synchronize()
+    idx = np.r_[0:512, 511 * np.arange(1, 500)]
+    x = d.cpu().numpy().view(np.uint64)[idx]
+    assert (got.cpu().numpy().view(np.uint64)[idx] == port.refined_step(x)).all()
