@@ -127,6 +127,40 @@ def test_parse_semantics(port):
         port.parse("65bo!")
 
 
+def test_refined_truth_table_fixture(port, meta):
+    """Config 5: the fragment's truth table fixture and the harness outputs."""
+    tt = port.refined_truth_table()
+    assert tt.shape == (3, 1 << 16)
+    assert [int(v) for v in tt.sum(axis=1)] == meta["unknown_step_refined"]["ones_per_output"]
+    g = load("refined_step.npz")
+    assert (port.refined_step(g["input"]) == g["output"]).all()
+
+
+def test_refined_circuit_is_the_table():
+    """The generated bitop3 network (lifeapi_amd/csrc/refined_circuit.inc),
+    simulated on all 2^16 inputs, is exactly the reference fragment's table."""
+    import re
+    tt = load("unknown_step_refined_tt.npz")["tt"].astype(bool)
+    src = open(os.path.join(os.path.dirname(GOLD), "..", "lifeapi_amd", "csrc",
+                            "refined_circuit.inc")).read()
+    idx = np.arange(1 << 16, dtype=np.uint32)
+    val = {f"x[{i}]": ((idx >> i) & 1).astype(bool) for i in range(16)}
+    A, B, C = 0xF0, 0xCC, 0xAA
+    for tab, a, b, c, name in [(int(m[1], 16), m[2], m[3], m[4], m[0]) for m in
+                               re.findall(r"const W (t\d+) = lut3<0x([0-9A-F]{2})>\(([^,]+), ([^,]+), ([^)]+)\);", src)]:
+        va, vb, vc = val[a], val[b], val[c]
+        out = np.zeros(1 << 16, bool)
+        for bit in range(8):
+            if (tab >> bit) & 1:
+                out |= (va == bool((A >> bit) & 1)) & (vb == bool((B >> bit) & 1)) & (vc == bool((C >> bit) & 1))
+        val[name] = out
+    outs = []
+    for nm in ("next_on", "next_unknown", "next_unknown_stable"):
+        m = re.search(rf"{nm} = (W{{~(t\d+)\.lo, ~t\d+\.hi}}|(t\d+|x\[\d+\]));", src)
+        outs.append(~val[m[2]] if m[2] else val[m[3]])
+    assert (np.stack(outs) == tt).all()
+
+
 # ---- live reference (present where oracle/_ref was built) ----
 
 def test_port_equals_reference_live(port, ref):
@@ -145,6 +179,12 @@ def test_reference_random_state_shape(ref, port):
     rs = np.stack([ref.random_state() for _ in range(64)])
     assert ((rs >> np.uint64(61)) == 1).all()
     assert (port.step_batch(rs, 1) == ref.step_batch(rs, 1)).all()
+
+
+def test_refined_oracle_equals_reference_fragment(port, ref):
+    x = port.fill(200 * 11, seed=909).reshape(200, 11 * 64)
+    x[:100, :64] &= port.fill(100, seed=1)           # sparser stable states
+    assert (port.refined_step(x) == ref.refined_step(x)).all()
 
 
 def test_parse_equals_reference(port, ref):
