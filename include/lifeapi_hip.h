@@ -102,6 +102,11 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
  * option planes 1 = ruled out, LifeStable.hpp:41-53).  d_out: n x 3 planes
  * (next_on, next_unknown, next_unknown_stable).  No overlap allowed.      */
 int lifeapi_refined_step_batch_dev(const uint64_t *d_in, uint64_t *d_out, size_t n, void *stream);
+/* tuning form: cfg->universes_per_wave 1 = no prefetch / 2 = prefetch the
+ * next universe; cfg->blocks_per_cu = grid cap (0 = one wave per universe);
+ * cfg->rule = 0 or 4 (request >= 4 waves per SIMD from the allocator)     */
+int lifeapi_refined_step_batch_dev_cfg(const uint64_t *d_in, uint64_t *d_out, size_t n,
+                                       void *stream, const lifeapi_launch_cfg *cfg);
 /* synthetic universes: word w = u*64+x (u counted from first_universe) is
  * splitmix64(seed + (w+1)*0x9E3779B97F4A7C15); mode 1 maps each column to
  * [2^61, 2^62) like RandomState()                                         */

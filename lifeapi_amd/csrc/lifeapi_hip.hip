@@ -308,38 +308,80 @@ __device__ __forceinline__ void ncount3(W a, W &b2, W &b1, W &b0) {
 // network is generated (tools/synth_bitop3.py) from the fragment's complete
 // truth table, which tests/golden/make_golden.py extracts from the reference
 // build, and is verified against all 2^16 input combinations when generated.
-__device__ __forceinline__ void refined_circuit(const W (&x)[16], W &next_on, W &next_unknown,
-                                                W &next_unknown_stable) {
+template <class T>
+__device__ __forceinline__ void refined_circuit(const T (&x)[16], T &next_on, T &next_unknown,
+                                                T &next_unknown_stable) {
 #include "refined_circuit.inc"
 }
 
-// One wave per universe.  In: 11 planes x 64 words (stable.state,
-// current.state, current.unknown, live2, live3, dead0, dead1, dead2, dead4,
-// dead5, dead6 -- LifeStable.hpp:41-53 with options stored as "1 = ruled
-// out").  Out: 3 planes (next_on, next_unknown, next_unknown_stable).
-__global__ __launch_bounds__(kBlock) void k_refined(const uint64_t *__restrict__ in,
-                                                    uint64_t *__restrict__ out, uint64_t n) {
+__device__ __forceinline__ void refined_load(W (&pl)[11], const uint64_t *in, uint64_t u, int lane) {
+  const uint64_t *p = in + u * 11 * kWave + lane;
+#pragma unroll
+  for (int k = 0; k < 11; ++k) pl[k] = ld<true>(p + k * kWave);
+}
+
+__device__ __forceinline__ void refined_one(const W (&pl)[11], uint64_t *out, uint64_t u, int lane) {
+  W x[16];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) x[k] = pl[3 + k];  // l2 l3 d0 d1 d2 d4 d5 d6
+  x[8] = pl[2];                                  // current_unknown
+  x[9] = pl[1];                                  // current_on
+  ncount3(pl[0], x[10], x[11], x[12]);           // s2 s1 s0
+  ncount3(pl[1], x[13], x[14], x[15]);           // on2 on1 on0
+  // Evaluate the ~500-node network on the low and then the high 32 bits of
+  // the column: the scheduling barrier keeps the two halves from being
+  // interleaved, which halves the live temporaries (VGPR pressure).
+  uint32_t xl[16], xh[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    xl[k] = x[k].lo;
+    xh[k] = x[k].hi;
+  }
+  W o0, o1, o2;
+  refined_circuit(xl, o0.lo, o1.lo, o2.lo);
+  __builtin_amdgcn_sched_barrier(0);
+  refined_circuit(xh, o0.hi, o1.hi, o2.hi);
+  uint64_t *q = out + u * 3 * kWave + lane;
+  st<true>(q, o0);
+  st<true>(q + kWave, o1);
+  st<true>(q + 2 * kWave, o2);
+}
+
+// One wave per universe at a time, grid-strided.  In: 11 planes x 64 words
+// (stable.state, current.state, current.unknown, live2, live3, dead0, dead1,
+// dead2, dead4, dead5, dead6 -- LifeStable.hpp:41-53 with options stored as
+// "1 = ruled out").  Out: 3 planes (next_on, next_unknown,
+// next_unknown_stable).  PF = 1: the next universe's 11 loads are issued
+// before this one's ~1000-instruction network runs (register double buffer),
+// so HBM traffic overlaps the VALU work of the same wave.  OCC = minimum
+// waves per SIMD requested from the register allocator (0 = no bound).
+template <int PF, int OCC>
+__global__ __launch_bounds__(kBlock, OCC > 0 ? OCC : 1) void k_refined(
+    const uint64_t *__restrict__ in, uint64_t *__restrict__ out, uint64_t n) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock;
-  for (uint64_t u = (uint64_t)blockIdx.x * kWavesPerBlock + wib; u < n; u += stride) {
-    const uint64_t *p = in + u * 11 * kWave + lane;
-    W pl[11];
+  uint64_t u = (uint64_t)blockIdx.x * kWavesPerBlock + wib;
+  if (u >= n) return;
+  if constexpr (PF == 0) {
+    for (; u < n; u += stride) {
+      W pl[11];
+      refined_load(pl, in, u, lane);
+      refined_one(pl, out, u, lane);
+    }
+  } else {
+    W cur[11];
+    refined_load(cur, in, u, lane);
+    for (; u < n; u += stride) {
+      const uint64_t un = u + stride;
+      W nxt[11];
+      if (un < n) refined_load(nxt, in, un, lane);
+      refined_one(cur, out, u, lane);
+      if (un < n) {
 #pragma unroll
-    for (int k = 0; k < 11; ++k) pl[k] = ld<true>(p + k * kWave);
-    W x[16];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) x[k] = pl[3 + k];  // l2 l3 d0 d1 d2 d4 d5 d6
-    x[8] = pl[2];                                  // current_unknown
-    x[9] = pl[1];                                  // current_on
-    ncount3(pl[0], x[10], x[11], x[12]);           // s2 s1 s0
-    ncount3(pl[1], x[13], x[14], x[15]);           // on2 on1 on0
-    W o0, o1, o2;
-    refined_circuit(x, o0, o1, o2);
-    uint64_t *q = out + u * 3 * kWave + lane;
-    st<true>(q, o0);
-    st<true>(q + kWave, o1);
-    st<true>(q + 2 * kWave, o2);
+        for (int k = 0; k < 11; ++k) cur[k] = nxt[k];
+      }
+    }
   }
 }
 
@@ -632,18 +674,35 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
   return launched("k_step_contains launch");
 }
 
-int lifeapi_refined_step_batch_dev(const uint64_t *d_in, uint64_t *d_out, size_t n, void *stream) {
+int lifeapi_refined_step_batch_dev_cfg(const uint64_t *d_in, uint64_t *d_out, size_t n,
+                                       void *stream, const lifeapi_launch_cfg *cfg) {
   if (n == 0) return LIFEAPI_OK;
   if (!d_in || !d_out || !aligned8(d_in) || !aligned8(d_out))
     return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_refined_step_batch_dev%s");
   const uintptr_t a = (uintptr_t)d_in, b = (uintptr_t)d_out;
   if (a < b + n * 3 * 512 && b < a + n * 11 * 512)
     return fail(LIFEAPI_E_INVALID, "refined step input and output overlap%s");
+  // cfg: universes_per_wave 1 = no prefetch, 2 = prefetch next universe;
+  // blocks_per_cu = grid cap; rule = 0 (no occupancy bound) or 4 (>= 4 waves/SIMD)
+  int pf = 1, bpc = 3, occ = 0;
+  if (cfg) {
+    pf = cfg->universes_per_wave >= 2 ? 1 : 0;
+    bpc = cfg->blocks_per_cu;
+    occ = cfg->rule;
+    if (occ != 0 && occ != 4) return fail(LIFEAPI_E_INVALID, "unsupported refined cfg%s");
+  }
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
-  hipLaunchKernelGGL(k_refined, dim3(grid_for(n, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream,
-                     d_in, d_out, (uint64_t)n);
+  using Fn = void (*)(const uint64_t *, uint64_t *, uint64_t);
+  Fn fn = pf ? (occ ? (Fn)k_refined<1, 4> : (Fn)k_refined<1, 0>)
+             : (occ ? (Fn)k_refined<0, 4> : (Fn)k_refined<0, 0>);
+  hipLaunchKernelGGL(fn, dim3(grid_for(n, cus, bpc)), dim3(kBlock), 0, (hipStream_t)stream, d_in,
+                     d_out, (uint64_t)n);
   return launched("k_refined launch");
+}
+
+int lifeapi_refined_step_batch_dev(const uint64_t *d_in, uint64_t *d_out, size_t n, void *stream) {
+  return lifeapi_refined_step_batch_dev_cfg(d_in, d_out, n, stream, nullptr);
 }
 
 int lifeapi_fill_random_dev(uint64_t *d_out, size_t n, uint64_t seed, uint64_t first_universe,

@@ -61,6 +61,7 @@ _SIGS = {
     "lifeapi_step_contains_batch_dev": ([_vp, _vp, _vp, _vp, _vp, _sz, _u32, _vp], _int),
     "lifeapi_fill_random_dev": ([_vp, _sz, _u64, _u64, _int, _vp], _int),
     "lifeapi_refined_step_batch_dev": ([_vp, _vp, _sz, _vp], _int),
+    "lifeapi_refined_step_batch_dev_cfg": ([_vp, _vp, _sz, _vp, ctypes.POINTER(LaunchCfg)], _int),
     "lifeapi_step_batch": ([_vp, _vp, _sz, _u32, _int], _int),
     "lifeapi_pop_batch": ([_vp, _vp, _sz, _int], _int),
 }

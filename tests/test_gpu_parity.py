@@ -213,3 +213,17 @@ def test_refined_step_full_size_sample(hip, port):
     idx = np.r_[0:512, 511 * np.arange(1, 500)]
     x = d.cpu().numpy().view(np.uint64)[idx]
     assert (got.cpu().numpy().view(np.uint64)[idx] == port.refined_step(x)).all()
+
+
+@pytest.mark.parametrize("pf,bpc,occ", [(1, 0, 0), (2, 1, 0), (2, 3, 4), (1, 2, 4)])
+def test_refined_step_cfgs(hip, port, pf, bpc, occ):
+    import ctypes
+    n = 3001
+    x = port.fill(n * 11, seed=77 + pf + bpc).reshape(n, 11 * 64)
+    d = to_dev(x).reshape(n, 11 * 64)
+    out = torch.empty((n, 3 * 64), dtype=torch.int64, device="cuda")
+    cfg = hip.LaunchCfg(0, pf, bpc, 1, occ)
+    hip._check(hip.lib.lifeapi_refined_step_batch_dev_cfg(
+        d.data_ptr(), out.data_ptr(), n, torch.cuda.current_stream().cuda_stream, ctypes.byref(cfg)))
+    torch.cuda.synchronize()
+    assert (out.cpu().numpy().view(np.uint64) == port.refined_step(x)).all()

@@ -147,7 +147,7 @@ def test_refined_circuit_is_the_table():
     val = {f"x[{i}]": ((idx >> i) & 1).astype(bool) for i in range(16)}
     A, B, C = 0xF0, 0xCC, 0xAA
     for tab, a, b, c, name in [(int(m[1], 16), m[2], m[3], m[4], m[0]) for m in
-                               re.findall(r"const W (t\d+) = lut3<0x([0-9A-F]{2})>\(([^,]+), ([^,]+), ([^)]+)\);", src)]:
+                               re.findall(r"const T (t\d+) = lut3<0x([0-9A-F]{2})>\(([^,]+), ([^,]+), ([^)]+)\);", src)]:
         va, vb, vc = val[a], val[b], val[c]
         out = np.zeros(1 << 16, bool)
         for bit in range(8):
@@ -156,7 +156,7 @@ def test_refined_circuit_is_the_table():
         val[name] = out
     outs = []
     for nm in ("next_on", "next_unknown", "next_unknown_stable"):
-        m = re.search(rf"{nm} = (W{{~(t\d+)\.lo, ~t\d+\.hi}}|(t\d+|x\[\d+\]));", src)
+        m = re.search(rf"{nm} = (~(t\d+)|(t\d+|x\[\d+\]));", src)
         outs.append(~val[m[2]] if m[2] else val[m[3]])
     assert (np.stack(outs) == tt).all()
 

@@ -153,13 +153,13 @@ class Circuit:
                 C = 0xFF if lneg else 0x00
                 ln = a
             table = ((TA & B) | (~TA & C)) & 0xFF
-            lines.append(f"  const W t{nid} = lut3<0x{table:02X}>({a}, {hn}, {ln});")
+            lines.append(f"  const T t{nid} = lut3<0x{table:02X}>({a}, {hn}, {ln});")
         for name, r in zip(out_names, outs):
             n, neg = ref(r)
             if n is None:
-                lines.append(f"  {name} = W{{{'0xFFFFFFFFu, 0xFFFFFFFFu' if neg else '0u, 0u'}}};")
+                lines.append(f"  {name} = {'~T(0)' if neg else 'T(0)'};")
             elif neg:
-                lines.append(f"  {name} = W{{~{n}.lo, ~{n}.hi}};")
+                lines.append(f"  {name} = ~{n};")
             else:
                 lines.append(f"  {name} = {n};")
         return lines

@@ -33,16 +33,48 @@ def timeit(fn, reps):
     return out
 
 
+def tune_c5(args):
+    """Config 5 (refined ternary step): prefetch x grid cap x occupancy bound."""
+    import ctypes
+    n = 1 << 18
+    planes = hip.fill_random(n * 11, seed=6).reshape(n, 11 * 64)
+    ref = hip.refined_step(planes)
+    out = torch.empty_like(ref)
+    s = torch.cuda.current_stream().cuda_stream
+    cfgs = list(itertools.product([1, 2], [2, 3, 4, 5, 6, 8, 0], [0, 4]))
+    ms = {c: [] for c in cfgs}
+    ok = {}
+    for r in range(args.rounds):
+        for c in cfgs:
+            cfg = hip.LaunchCfg(0, c[0], c[1], 1, c[2])
+            run = lambda: hip._check(hip.lib.lifeapi_refined_step_batch_dev_cfg(  # noqa: E731
+                planes.data_ptr(), out.data_ptr(), n, s, ctypes.byref(cfg)))
+            ms[c] += timeit(run, args.reps)
+            if r == 0:
+                torch.cuda.synchronize()
+                ok[c] = bool(torch.equal(out, ref))
+    for c in cfgs:
+        t = sorted(ms[c])
+        med = t[len(t) // 2]
+        print(json.dumps({"workload": "c5", "n": n, "prefetch": c[0] - 1, "blocks_per_cu": c[1],
+                          "occ": c[2], "ms_best": t[0], "ms_median": med,
+                          "GBps_median": n * 7168 / (med / 1e3) / 1e9, "bit_exact": ok[c]}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=["c2", "c3", "both"], default="both")
+    ap.add_argument("--workload", choices=["c2", "c3", "c5", "both", "all"], default="both")
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--quick", action="store_true")
     args = ap.parse_args()
 
+    if args.workload in ("c5", "all"):
+        tune_c5(args)
+        if args.workload == "c5":
+            return
     work = []
-    if args.workload in ("c2", "both"):
+    if args.workload in ("c2", "both", "all"):
         n, g = 1 << 20, 1
         xs = [0, 1, 2]
         us = [1, 2, 4, 8]
@@ -50,7 +82,7 @@ def main():
         nts = [0, 1]
         rules = [0] if args.quick else [0, 1]
         work.append(("c2", n, g, list(itertools.product(xs, us, bpcs, nts, rules))))
-    if args.workload in ("c3", "both"):
+    if args.workload in ("c3", "both", "all"):
         n, g = 1 << 16, 1024
         work.append(("c3", n, g, list(itertools.product([0, 1, 2], [1, 2, 4, 8], [2, 4, 8, 0], [0], [0, 1]))))
 
