@@ -94,6 +94,16 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
                                     const uint64_t *d_wanted, const uint64_t *d_unwanted,
                                     uint32_t *d_first_gen, size_t n, uint32_t generations,
                                     void *stream);
+/* Inclusive 3x3 neighbourhood count of each universe as 4 planes:
+ * d_out = n x {bit3, bit2, bit1, bit0} x 64 words.
+ * Replaces NeighbourCount(const LifeState&) (NeighbourCount.hpp:40-70) and
+ * LifeState::CountNeighbourhood (LifeAPI.hpp:909-952).                    */
+int lifeapi_neighbour_count_batch_dev(const uint64_t *d_in, uint64_t *d_out, size_t n, void *stream);
+/* LifeState::InteractionCounts (LifeAPI.hpp:956-993): d_out = n x {out1,
+ * out2, outMore} x 64 words; with_next != 0: InteractionCountsAndNext
+ * (LifeAPI.hpp:997-1040), d_out = n x {out1, out2, outMore, next} x 64.     */
+int lifeapi_interaction_counts_batch_dev(const uint64_t *d_in, uint64_t *d_out, size_t n,
+                                         int with_next, void *stream);
 /* Config-5 ternary step: bitslicing/unknown_step_refined.hpp:1-85 applied
  * per column with s2..s0 / on2..on0 = bits 2..0 of NeighbourCount
  * (NeighbourCount.hpp:40-70) of stable.state / current.state.

@@ -288,6 +288,52 @@ __global__ __launch_bounds__(kBlock) void k_step_contains(const uint64_t *__rest
   }
 }
 
+// ---- neighbourhood counters --------------------------
+// Same stencil as Step(), different output planes.  The two FullAdds of the
+// vertical planes give the inclusive 3x3 count = fs + 2(fc + cs) + 4cc.
+// MODE 0: NeighbourCount / CountNeighbourhood (NeighbourCount.hpp:40-70,
+//         LifeAPI.hpp:909-952): planes bit3, bit2, bit1, bit0.
+// MODE 1: InteractionCounts (LifeAPI.hpp:956-993): out1, out2, outMore.
+// MODE 2: InteractionCountsAndNext (LifeAPI.hpp:997-1040): out1, out2,
+//         outMore, next.
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_counts(const uint64_t *__restrict__ in,
+                                                   uint64_t *__restrict__ out, uint64_t n) {
+  constexpr int P = MODE == 1 ? 3 : 4;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock;
+  for (uint64_t u = (uint64_t)blockIdx.x * kWavesPerBlock + wib; u < n; u += stride) {
+    const W a = ld<true>(in + u * kWave + lane);
+    const W up = rot_up(a), dn = rot_dn(a);
+    const W c0 = lut3<kXor3>(up, dn, a), c1 = lut3<kMaj>(up, dn, a);
+    W L0, R0, L1, R1;
+    neighbours<XDPP>(c0, c1, L0, R0, L1, R1, nullptr, lane);
+    const W fs = lut3<kXor3>(L0, c0, R0), fc = lut3<kMaj>(L0, c0, R0);
+    const W cs = lut3<kXor3>(L1, c1, R1), cc = lut3<kMaj>(L1, c1, R1);
+    uint64_t *q = out + u * P * kWave + lane;
+    const uint64_t s = join(a), vfs = join(fs), vfc = join(fc), vcs = join(cs), vcc = join(cc);
+    if constexpr (MODE == 0) {
+      const uint64_t carry = vfc & vcs;
+      st<true>(q + 0 * kWave, split(vcc & carry));          // bit3
+      st<true>(q + 1 * kWave, split(vcc ^ carry));          // bit2
+      st<true>(q + 2 * kWave, split(vfc ^ vcs));            // bit1
+      st<true>(q + 3 * kWave, fs);                          // bit0
+    } else {
+      const uint64_t o1 = ~s & ~vcc & vfs & ~vcs & ~vfc;
+      const uint64_t o2 = ~s & ~vcc & ~vfs & (vcs ^ vfc);
+      const uint64_t om = ~s & ~o2 & (vfc | vcs | vcc);
+      st<true>(q + 0 * kWave, split(o1));
+      st<true>(q + 1 * kWave, split(o2));
+      st<true>(q + 2 * kWave, split(om));
+      if constexpr (MODE == 2) {
+        const uint64_t c2 = vcc ^ (vcs & vfc);
+        st<true>(q + 3 * kWave, split((vfs ^ c2) & (vfc ^ vcs ^ c2) & (s | vfs)));
+      }
+    }
+  }
+}
+
 // ---- config 5: the unknown_step_refined ternary step --------------------
 // Bits 2..0 of the inclusive 3x3 count of this lane's column: the
 // NeighbourCount adder chain (NeighbourCount.hpp:40-70) as CountRows + DPP
@@ -672,6 +718,32 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
                      (hipStream_t)stream, d_in, d_final, d_wanted, d_unwanted, d_first_gen,
                      (uint64_t)n, generations);
   return launched("k_step_contains launch");
+}
+
+static int counts_launch(const uint64_t *d_in, uint64_t *d_out, size_t n, int mode, void *stream) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!d_in || !d_out || !aligned8(d_in) || !aligned8(d_out))
+    return fail(LIFEAPI_E_INVALID, "bad pointer to a neighbourhood-count entry point%s");
+  const size_t planes = mode == 1 ? 3 : 4;
+  const uintptr_t a = (uintptr_t)d_in, b = (uintptr_t)d_out;
+  if (a < b + n * planes * 512 && b < a + n * 512)
+    return fail(LIFEAPI_E_INVALID, "count input and output overlap%s");
+  int cus = 0, rc = device_cus(cus);
+  if (rc != LIFEAPI_OK) return rc;
+  using Fn = void (*)(const uint64_t *, uint64_t *, uint64_t);
+  Fn fn = mode == 0 ? (Fn)k_counts<0> : mode == 1 ? (Fn)k_counts<1> : (Fn)k_counts<2>;
+  hipLaunchKernelGGL(fn, dim3(grid_for(n, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream, d_in,
+                     d_out, (uint64_t)n);
+  return launched("k_counts launch");
+}
+
+int lifeapi_neighbour_count_batch_dev(const uint64_t *d_in, uint64_t *d_out, size_t n, void *stream) {
+  return counts_launch(d_in, d_out, n, 0, stream);
+}
+
+int lifeapi_interaction_counts_batch_dev(const uint64_t *d_in, uint64_t *d_out, size_t n,
+                                         int with_next, void *stream) {
+  return counts_launch(d_in, d_out, n, with_next ? 2 : 1, stream);
 }
 
 int lifeapi_refined_step_batch_dev_cfg(const uint64_t *d_in, uint64_t *d_out, size_t n,

@@ -60,6 +60,8 @@ _SIGS = {
     "lifeapi_contains_batch_dev": ([_vp, _vp, _vp, _vp, _sz, _vp], _int),
     "lifeapi_step_contains_batch_dev": ([_vp, _vp, _vp, _vp, _vp, _sz, _u32, _vp], _int),
     "lifeapi_fill_random_dev": ([_vp, _sz, _u64, _u64, _int, _vp], _int),
+    "lifeapi_neighbour_count_batch_dev": ([_vp, _vp, _sz, _vp], _int),
+    "lifeapi_interaction_counts_batch_dev": ([_vp, _vp, _sz, _int, _vp], _int),
     "lifeapi_refined_step_batch_dev": ([_vp, _vp, _sz, _vp], _int),
     "lifeapi_refined_step_batch_dev_cfg": ([_vp, _vp, _sz, _vp, ctypes.POINTER(LaunchCfg)], _int),
     "lifeapi_step_batch": ([_vp, _vp, _sz, _u32, _int], _int),
@@ -224,4 +226,22 @@ def refined_step(planes: torch.Tensor, out: torch.Tensor | None = None, stream=N
     if out is None:
         out = torch.empty((n, 3 * N), dtype=torch.int64, device=planes.device)
     _check(lib.lifeapi_refined_step_batch_dev(planes.data_ptr(), out.data_ptr(), n, _stream(stream)))
+    return out
+
+
+def neighbour_count(states: torch.Tensor, stream=None) -> torch.Tensor:
+    """NeighbourCount planes (NeighbourCount.hpp:40-70): (n, 4, 64) = bit3..bit0."""
+    n = _universes(states)
+    out = torch.empty((n, 4, N), dtype=torch.int64, device=states.device)
+    _check(lib.lifeapi_neighbour_count_batch_dev(states.data_ptr(), out.data_ptr(), n, _stream(stream)))
+    return out
+
+
+def interaction_counts(states: torch.Tensor, with_next: bool = False, stream=None) -> torch.Tensor:
+    """InteractionCounts[AndNext] (LifeAPI.hpp:956-1040): (n, 3|4, 64) planes
+    out1, out2, outMore[, next]."""
+    n = _universes(states)
+    out = torch.empty((n, 4 if with_next else 3, N), dtype=torch.int64, device=states.device)
+    _check(lib.lifeapi_interaction_counts_batch_dev(states.data_ptr(), out.data_ptr(), n,
+                                                    1 if with_next else 0, _stream(stream)))
     return out

@@ -112,6 +112,31 @@ void oracle_step_nc(uint64_t s[64]) {
   }
 }
 
+/* OFF cells with exactly 1, exactly 2, and more neighbours, plus (optionally)
+ * the next generation.  LifeAPI.hpp:956-993 (InteractionCounts) and
+ * :997-1040 (InteractionCountsAndNext). */
+void oracle_interaction_counts(const uint64_t s[64], uint64_t out1[64], uint64_t out2[64],
+                               uint64_t out_more[64], uint64_t next[64]) {
+  uint64_t c0[64], c1[64];
+  oracle_count_rows(s, c0, c1);
+  for (int x = 0; x < ORACLE_N; ++x) {
+    const int xl = (x + ORACLE_N - 1) & (ORACLE_N - 1), xr = (x + 1) & (ORACLE_N - 1);
+    uint64_t h = c0[xl] ^ c0[x];
+    const uint64_t fsum = h ^ c0[xr], fcar = (c0[xl] & c0[x]) | (c0[xr] & h);
+    h = c1[xl] ^ c1[x];
+    const uint64_t csum = h ^ c1[xr];
+    uint64_t ccar = (c1[xl] & c1[x]) | (c1[xr] & h);
+    const uint64_t dead = ~s[x];
+    out1[x] = dead & ~ccar & fsum & ~csum & ~fcar;
+    out2[x] = dead & ~ccar & ~fsum & (csum ^ fcar);
+    out_more[x] = dead & ~out2[x] & (fcar | csum | ccar);
+    if (next) {
+      ccar ^= csum & fcar;
+      next[x] = (fsum ^ ccar) & (fcar ^ csum ^ ccar) & (s[x] | fsum);
+    }
+  }
+}
+
 /* LifeAPI.hpp:877-881 (LifeState::Step(unsigned)). */
 void oracle_step_n(uint64_t s[64], unsigned gens) {
   for (unsigned g = 0; g < gens; ++g) oracle_step(s);

@@ -71,6 +71,7 @@ class Port:
         L.oracle_batch_digest.argtypes = [_u64p, ctypes.c_size_t, ctypes.c_uint64]
         L.oracle_batch_digest.restype = ctypes.c_uint64
         L.oracle_neighbour_count.argtypes = [_u64p] * 5
+        L.oracle_interaction_counts.argtypes = [_u64p] * 5
         L.oracle_refined_step_batch.argtypes = [_u64p, _u64p, ctypes.c_size_t,
                                                 ctypes.POINTER(ctypes.c_uint8)]
         self._tt = None
@@ -122,6 +123,14 @@ class Port:
         self.lib.oracle_neighbour_count(_p64(s), _p64(b[0]), _p64(b[1]), _p64(b[2]), _p64(b[3]))
         return b  # bit3, bit2, bit1, bit0
 
+    def interaction_counts(self, state, with_next: bool = True) -> np.ndarray:
+        """(4, 64): out1, out2, outMore, next (LifeAPI.hpp:956-1040)."""
+        s = np.ascontiguousarray(state, dtype=np.uint64).reshape(64)
+        b = np.zeros((4, 64), dtype=np.uint64)
+        self.lib.oracle_interaction_counts(_p64(s), _p64(b[0]), _p64(b[1]), _p64(b[2]),
+                                           _p64(b[3]) if with_next else None)
+        return b if with_next else b[:3]
+
     def refined_truth_table(self) -> np.ndarray:
         if self._tt is None:
             path = os.path.join(os.path.dirname(HERE), "tests", "golden", "unknown_step_refined_tt.npz")
@@ -159,6 +168,7 @@ class Ref:
         L.ref_parse.argtypes = [ctypes.c_char_p, _u64p]
         L.ref_neighbour_count.argtypes = [_u64p] * 5
         L.ref_count_neighbourhood.argtypes = [_u64p] * 5
+        L.ref_interaction_counts.argtypes = [_u64p] * 5
         L.ref_unknown_step_refined.argtypes = [_u64p, _u64p]
         L.ref_refined_step_batch.argtypes = [_u64p, _u64p, ctypes.c_size_t]
 
@@ -208,6 +218,12 @@ class Ref:
         s = np.ascontiguousarray(state, dtype=np.uint64).reshape(64)
         b = np.zeros((4, 64), dtype=np.uint64)
         self.lib.ref_neighbour_count(_p64(s), _p64(b[0]), _p64(b[1]), _p64(b[2]), _p64(b[3]))
+        return b
+
+    def interaction_counts(self, state) -> np.ndarray:
+        s = np.ascontiguousarray(state, dtype=np.uint64).reshape(64)
+        b = np.zeros((4, 64), dtype=np.uint64)
+        self.lib.ref_interaction_counts(_p64(s), _p64(b[0]), _p64(b[1]), _p64(b[2]), _p64(b[3]))
         return b
 
     def refined_step(self, planes: np.ndarray) -> np.ndarray:

@@ -50,6 +50,15 @@ void ref_neighbour_count(const uint64_t *s, uint64_t *b3, uint64_t *b2, uint64_t
   NeighbourCount nc(load(s));
   store(nc.bit3, b3); store(nc.bit2, b2); store(nc.bit1, b1); store(nc.bit0, b0);
 }
+// LifeState::InteractionCountsAndNext  LifeAPI.hpp:997-1040 (and
+// InteractionCounts :956-993, which must agree on the first three planes)
+void ref_interaction_counts(const uint64_t *s, uint64_t *o1, uint64_t *o2, uint64_t *om, uint64_t *nx) {
+  LifeState t = load(s), a1, a2, am, an, b1, b2, bm;
+  t.InteractionCountsAndNext(a1, a2, am, an);
+  t.InteractionCounts(b1, b2, bm);
+  if (!(a1 == b1 && a2 == b2 && am == bm)) std::abort();
+  store(a1, o1); store(a2, o2); store(am, om); store(an, nx);
+}
 // LifeState::GetPop  LifeAPI.hpp:290-298
 unsigned ref_pop(const uint64_t *s) { return load(s).GetPop(); }
 // LifeState::Contains(const LifeTarget&)  LifeTarget.hpp:44-51

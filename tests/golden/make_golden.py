@@ -163,6 +163,17 @@ def main():
              contains=cont)
     meta["contains"] = {"n": 64, "true": int(cont.sum())}
 
+    # 5a. neighbourhood counters: NeighbourCount planes and
+    #     InteractionCountsAndNext planes, from the reference, on edge cases +
+    #     32 seeded universes
+    cin = np.concatenate([e, P.fill(32, seed=4242)])
+    ncs = np.stack([R.neighbour_count(cin[u]) for u in range(len(cin))])
+    ics = np.stack([R.interaction_counts(cin[u]) for u in range(len(cin))])
+    np.savez(os.path.join(HERE, "counts.npz"), input=cin, neighbour_count=ncs,
+             interaction_counts=ics)
+    meta["counts"] = {"n": int(len(cin)), "neighbour_count_planes": "bit3,bit2,bit1,bit0",
+                      "interaction_planes": "out1,out2,outMore,next"}
+
     # 5b. config 5: bitslicing/unknown_step_refined.hpp (the reference's espresso
     #     fragment) as a complete truth table over its 16 inputs, plus seeded
     #     11-plane universes through the build-defined harness (ref_shim.cpp)

@@ -184,6 +184,32 @@ def test_full_size_config2(hip, port):
         port.digest(port.hashes(want))
 
 
+# ---- neighbourhood counters ----
+
+def test_counts_golden_gpu(hip):
+    import os
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "counts.npz"))
+    d = to_dev(g["input"])
+    nc = hip.neighbour_count(d)
+    ic = hip.interaction_counts(d, with_next=True)
+    ic3 = hip.interaction_counts(d, with_next=False)
+    torch.cuda.synchronize()
+    assert (nc.cpu().numpy().view(np.uint64) == g["neighbour_count"]).all()
+    assert (ic.cpu().numpy().view(np.uint64) == g["interaction_counts"]).all()
+    assert (ic3.cpu().numpy().view(np.uint64) == g["interaction_counts"][:, :3]).all()
+
+
+def test_counts_vs_oracle_ragged(hip, port):
+    x = np.concatenate([seam_cases(port), port.fill(2001, seed=8080)])
+    d = to_dev(x)
+    nc = hip.neighbour_count(d).cpu().numpy().view(np.uint64)
+    ic = hip.interaction_counts(d, with_next=True).cpu().numpy().view(np.uint64)
+    for u in range(0, len(x), 7):
+        assert (nc[u] == port.neighbour_count(x[u])).all()
+        assert (ic[u] == port.interaction_counts(x[u])).all()
+    assert (ic[:, 3] == port.step_batch(x, 1)).all()
+
+
 # ---- config 5: unknown_step_refined ternary step ----
 
 def test_refined_step_golden(hip, port):

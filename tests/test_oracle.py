@@ -127,6 +127,17 @@ def test_parse_semantics(port):
         port.parse("65bo!")
 
 
+def test_counts_golden(port):
+    """NeighbourCount (NeighbourCount.hpp:40-70) and InteractionCountsAndNext
+    (LifeAPI.hpp:997-1040) planes vs the reference-generated fixture."""
+    g = load("counts.npz")
+    for u in range(g["input"].shape[0]):
+        assert (port.neighbour_count(g["input"][u]) == g["neighbour_count"][u]).all()
+        assert (port.interaction_counts(g["input"][u]) == g["interaction_counts"][u]).all()
+    # the 'next' plane is Step()
+    assert (g["interaction_counts"][:, 3] == port.step_batch(g["input"], 1)).all()
+
+
 def test_refined_truth_table_fixture(port, meta):
     """Config 5: the fragment's truth table fixture and the harness outputs."""
     tt = port.refined_truth_table()
@@ -179,6 +190,12 @@ def test_reference_random_state_shape(ref, port):
     rs = np.stack([ref.random_state() for _ in range(64)])
     assert ((rs >> np.uint64(61)) == 1).all()
     assert (port.step_batch(rs, 1) == ref.step_batch(rs, 1)).all()
+
+
+def test_counts_equal_reference_live(port, ref):
+    x = port.fill(100, seed=4343)
+    for u in range(100):
+        assert (port.interaction_counts(x[u]) == ref.interaction_counts(x[u])).all()
 
 
 def test_refined_oracle_equals_reference_fragment(port, ref):

@@ -6,3 +6,4 @@ timeout -k 10 600 python -m pytest tests/test_gpu_parity.py -q -k refined -p no:
 tail -2 gpurun_out/pytest_refined.log
 timeout -k 10 600 python tools/tune.py --workload c5 --rounds 3 --reps 4 > gpurun_out/tune_c5.jsonl 2> gpurun_out/tune_c5.err || { tail gpurun_out/tune_c5.err; exit 3; }
 echo tuned
+timeout -k 10 300 ./build/valu_probe > gpurun_out/valu_probe.jsonl 2>&1 || exit 4
