@@ -128,8 +128,53 @@ __device__ __forceinline__ void neighbours(W c0, W c1, W &L0, W &R0, W &L1, W &R
 // one generation of one universe (this lane's column)
 // ------------------------------------------------------------------------
 
+// one 64-bit neighbour word from lanes x-1 / x+1 (used by the row-first rule)
+template <int X>
+__device__ __forceinline__ void neighbour_cols(W a, W &L, W &R, uint64_t *slot, int lane) {
+  if constexpr (X == XDPP) {
+    L = W{dpp_prev(a.lo), dpp_prev(a.hi)};
+    R = W{dpp_next(a.lo), dpp_next(a.hi)};
+  } else if constexpr (X == XBPERM) {
+    const int ap = ((lane + kWave - 1) & (kWave - 1)) << 2;
+    const int an = ((lane + 1) & (kWave - 1)) << 2;
+    L = W{(uint32_t)__builtin_amdgcn_ds_bpermute(ap, (int)a.lo),
+          (uint32_t)__builtin_amdgcn_ds_bpermute(ap, (int)a.hi)};
+    R = W{(uint32_t)__builtin_amdgcn_ds_bpermute(an, (int)a.lo),
+          (uint32_t)__builtin_amdgcn_ds_bpermute(an, (int)a.hi)};
+  } else {
+    volatile uint64_t *s = slot;
+    s[lane] = join(a);
+    __builtin_amdgcn_wave_barrier();
+    L = split(s[(lane + kWave - 1) & (kWave - 1)]);
+    R = split(s[(lane + 1) & (kWave - 1)]);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 template <int X, int RULE>
 __device__ __forceinline__ W life_gen(W a, uint64_t *slot, int lane) {
+  if constexpr (RULE == 2) {
+    // Row-first form of the same adder network.  A DPP move issues at half
+    // the VALU rate on gfx950 (tools/valu_probe.hip: 8 DPP of 32 instructions
+    // cost 25 % of the loop), so exchange the raw column (4 DPP) instead of
+    // its two vertical-sum planes (8 DPP):
+    //   horizontal 3-sums  H0 = xor3(L,a,R), H1 = maj(L,a,R)   (2-bit, 0..3)
+    //   vertical    FullAdd(H0 up, H0, H0 down) -> fs, fc
+    //               FullAdd(H1 up, H1, H1 down) -> cs, cc
+    // and the 3x3 count is again fs + 2(fc + cs) + 4cc, so the rule tail is
+    // StepAlt's (LifeAPI.hpp:1251-1252).  Addition is commutative, so this is
+    // bit-identical to CountRows-then-columns (LifeAPI.hpp:897-907,1218-1254).
+    W L, R;
+    neighbour_cols<X>(a, L, R, slot, lane);
+    const W h0 = lut3<kXor3>(L, a, R), h1 = lut3<kMaj>(L, a, R);
+    const W h0u = rot_up(h0), h0d = rot_dn(h0), h1u = rot_up(h1), h1d = rot_dn(h1);
+    const W fs = lut3<kXor3>(h0u, h0, h0d), fc = lut3<kMaj>(h0u, h0, h0d);
+    const W cs = lut3<kXor3>(h1u, h1, h1d), cc = lut3<kMaj>(h1u, h1, h1d);
+    const W b2 = lut3<kCarry2>(cc, fc, cs);
+    const W p = lut3<kLive>(fs, b2, a);
+    const W q = lut3<kXor3>(fc, cs, b2);
+    return W{p.lo & q.lo, p.hi & q.hi};
+  }
   const W up = rot_up(a), dn = rot_dn(a);
   if constexpr (RULE == 0) {
     // CountRows (LifeAPI.hpp:897-907): vertical 3-sum as two planes
@@ -529,7 +574,12 @@ template <int X, int RULE>
 StepFn pick_nt(int u, bool nt) { return nt ? pick_u<X, true, RULE>(u) : pick_u<X, false, RULE>(u); }
 template <int X>
 StepFn pick_rule(int u, bool nt, int rule) {
-  return rule == 1 ? pick_nt<X, 1>(u, nt) : pick_nt<X, 0>(u, nt);
+  switch (rule) {
+    case 0: return pick_nt<X, 0>(u, nt);
+    case 1: return pick_nt<X, 1>(u, nt);
+    case 2: return pick_nt<X, 2>(u, nt);
+    default: return nullptr;
+  }
 }
 StepFn pick_step(const lifeapi_launch_cfg &c) {
   switch (c.xchg) {
@@ -755,19 +805,22 @@ int lifeapi_refined_step_batch_dev_cfg(const uint64_t *d_in, uint64_t *d_out, si
   if (a < b + n * 3 * 512 && b < a + n * 11 * 512)
     return fail(LIFEAPI_E_INVALID, "refined step input and output overlap%s");
   // cfg: universes_per_wave 1 = no prefetch, 2 = prefetch next universe;
-  // blocks_per_cu = grid cap; rule = 0 (no occupancy bound) or 4 (>= 4 waves/SIMD)
-  int pf = 1, bpc = 3, occ = 0;
+  // blocks_per_cu = grid cap; rule = minimum waves per SIMD requested from the
+  // register allocator (0 = none, 4, 6).  Default = the measured best
+  // (profiles/r01/tune_c5.jsonl): no prefetch, 8 blocks per CU.
+  int pf = 0, bpc = 8, occ = 0;
   if (cfg) {
     pf = cfg->universes_per_wave >= 2 ? 1 : 0;
     bpc = cfg->blocks_per_cu;
     occ = cfg->rule;
-    if (occ != 0 && occ != 4) return fail(LIFEAPI_E_INVALID, "unsupported refined cfg%s");
+    if (occ != 0 && occ != 4 && occ != 6)
+      return fail(LIFEAPI_E_INVALID, "unsupported refined cfg%s");
   }
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
   using Fn = void (*)(const uint64_t *, uint64_t *, uint64_t);
-  Fn fn = pf ? (occ ? (Fn)k_refined<1, 4> : (Fn)k_refined<1, 0>)
-             : (occ ? (Fn)k_refined<0, 4> : (Fn)k_refined<0, 0>);
+  Fn fn = pf ? (occ == 4 ? (Fn)k_refined<1, 4> : occ == 6 ? (Fn)k_refined<1, 6> : (Fn)k_refined<1, 0>)
+             : (occ == 4 ? (Fn)k_refined<0, 4> : occ == 6 ? (Fn)k_refined<0, 6> : (Fn)k_refined<0, 0>);
   hipLaunchKernelGGL(fn, dim3(grid_for(n, cus, bpc)), dim3(kBlock), 0, (hipStream_t)stream, d_in,
                      d_out, (uint64_t)n);
   return launched("k_refined launch");

@@ -13,7 +13,7 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-ALL_CFGS = list(itertools.product((0, 1, 2), (1, 2, 4, 8), (0, 1), (0, 1)))
+ALL_CFGS = list(itertools.product((0, 1, 2), (1, 2, 4, 8), (0, 1), (0, 1, 2)))
 
 
 def to_dev(a: np.ndarray) -> torch.Tensor:
@@ -182,6 +182,42 @@ def test_full_size_config2(hip, port):
     # checksum of checksums agrees too
     assert port.digest(hip.hashes(hip.step(d)).cpu().numpy().view(np.uint64)) == \
         port.digest(port.hashes(want))
+
+
+def test_config4_all_shards_vs_reference_digests(hip):
+    """Config 4 (16M universes x 1 gen, 8 shards of 2M): every shard's output
+    digest equals the reference's (tests/golden/golden.json), one GPU doing
+    the shards in turn -- the same contiguous shards the 8 ranks own."""
+    import json
+    import os
+
+    from lifeapi_amd.digest import batch_digest, combine
+    with open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")) as f:
+        d = json.load(f)["digests"]["config4"]
+    per = d["universes"] // d["shards"]
+    a = torch.empty((per, 64), dtype=torch.int64, device="cuda")
+    b = torch.empty_like(a)
+    got = []
+    for k in range(d["shards"]):
+        hip.fill_random(per, seed=d["seed"], first_universe=k * per, out=a)
+        hip.step(a, out=b, generations=1)
+        got.append(batch_digest(hip.hashes(b).cpu().numpy(), k * per))
+    assert [f"{g:016x}" for g in got] == d["shard_output_digests"]
+    assert f"{combine(got):016x}" == d["output_digest"]
+
+
+def test_config3_full_size_vs_reference_digest(hip):
+    """Config 3 (64K x 1024 generations, one launch) vs the reference's digest."""
+    import json
+    import os
+
+    from lifeapi_amd.digest import batch_digest
+    with open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")) as f:
+        d = json.load(f)["digests"]["config3"]
+    x = hip.fill_random(d["universes"], seed=d["seed"])
+    out = hip.step(x, generations=d["generations"])
+    assert f"{batch_digest(hip.hashes(out).cpu().numpy()):016x}" == d["output_digest"]
+    assert int(hip.pop(out).sum().item()) == d["output_pop_total"]
 
 
 # ---- neighbourhood counters (SURVEY 8(f) row 2) ----

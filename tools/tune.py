@@ -41,7 +41,7 @@ def tune_c5(args):
     ref = hip.refined_step(planes)
     out = torch.empty_like(ref)
     s = torch.cuda.current_stream().cuda_stream
-    cfgs = list(itertools.product([1, 2], [2, 3, 4, 5, 6, 8, 0], [0, 4]))
+    cfgs = list(itertools.product([1, 2], [4, 6, 8, 12, 0], [0, 4, 6]))
     ms = {c: [] for c in cfgs}
     ok = {}
     for r in range(args.rounds):
@@ -76,15 +76,15 @@ def main():
     work = []
     if args.workload in ("c2", "both", "all"):
         n, g = 1 << 20, 1
-        xs = [0, 1, 2]
-        us = [1, 2, 4, 8]
-        bpcs = [4, 8, 16, 0] if not args.quick else [8, 0]
-        nts = [0, 1]
-        rules = [0] if args.quick else [0, 1]
+        xs = [0, 2]
+        us = [2, 4, 8]
+        bpcs = [0]
+        nts = [1]
+        rules = [0, 2]
         work.append(("c2", n, g, list(itertools.product(xs, us, bpcs, nts, rules))))
     if args.workload in ("c3", "both", "all"):
         n, g = 1 << 16, 1024
-        work.append(("c3", n, g, list(itertools.product([0, 1, 2], [1, 2, 4, 8], [2, 4, 8, 0], [0], [0, 1]))))
+        work.append(("c3", n, g, list(itertools.product([0], [1, 2], [8, 0], [0], [0, 2]))))
 
     for name, n, g, cfgs in work:
         a = hip.fill_random(n, seed=2)
