@@ -37,6 +37,9 @@ BYTES_PER_UNIVERSE_GEN = 1024  # 512 B read + 512 B write
 OPS_PER_UNIVERSE_GEN = 2688    # reference's ~21 u64 ops/column = 42 int32 x 64
 
 
+COLL_DEV = None  # device the collectives' tensors live on (set in main)
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -57,16 +60,18 @@ def parse_args():
 
 
 def timed_launches(hip, bufs, steps, gens, stream):
-    """Run `steps` ping-pong launches; return (per-launch ms list, last buffer index)."""
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(steps)]
+    """Run `steps` back-to-back ping-pong launches on `stream`, bracketed by one
+    pair of HIP events on that same stream (no events between launches, so
+    none of their cost lands between kernels).  Returns ((start, end), index
+    of the buffer holding the latest state)."""
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     cur = 0
-    for k in range(steps):
-        evs[k][0].record(stream)
+    e0.record(stream)
+    for _ in range(steps):
         hip.step(bufs[cur], out=bufs[1 - cur], generations=gens, stream=stream)
-        evs[k][1].record(stream)
         cur = 1 - cur
-    return evs, cur
+    e1.record(stream)
+    return (e0, e1), cur
 
 
 def cpu_baseline(x_host: np.ndarray, seconds: float):
@@ -147,7 +152,7 @@ def verify_first_launch(hip, out, first, n, gens, seed, stream, world, device):
     got = f"{batch_digest(hip.hashes(out, stream=stream).cpu().numpy(), first):016x}"
     ok = None if want is None else got == want
     if world > 1 and ok is not None:
-        f = torch.tensor([0 if ok else 1], device=device)
+        f = torch.tensor([0 if ok else 1], device=COLL_DEV)
         dist.all_reduce(f)
         ok = int(f.item()) == 0
     return {"ok": ok, "first_launch_digest_rank0": got, "expected": want,
@@ -195,10 +200,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    # one process per GPU; the modulo only matters for a rehearsal with more
+    # ranks than GPUs (LIFEAPI_BENCH_BACKEND=gloo), never for the real run
+    ndev = torch.cuda.device_count()
+    device = torch.device("cuda", local % max(ndev, 1))
+    torch.cuda.set_device(device)
+    backend = os.environ.get("LIFEAPI_BENCH_BACKEND", "nccl")  # nccl == RCCL on ROCm
+    global COLL_DEV
+    COLL_DEV = device if backend == "nccl" else torch.device("cpu")
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
     import lifeapi_amd.hip as hip
 
     n, gens = args.universes, args.gens_per_step
@@ -231,10 +245,10 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=COLL_DEV)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    launch_ms = [e0.elapsed_time(e1) for e0, e1 in evs]
+    span_ms = evs[0].elapsed_time(evs[1])   # GPU time of the K launches on their stream
     final = bufs[cur]
 
     # result collection (not in the timed region): all-gather per-universe hashes
@@ -244,10 +258,11 @@ def main():
     if world > 1:
         dist.barrier()
         c0 = time.perf_counter()
-        gathered = gather_hashes(h, world)
+        gathered = gather_hashes(h.to(COLL_DEV), world)
         torch.cuda.synchronize(device)
         cms = (time.perf_counter() - c0) * 1e3
-        collect = {"op": "all_gather(per-universe hash, RCCL)", "bytes_per_rank": n * 8,
+        collect = {"op": f"all_gather(per-universe hash, {'RCCL' if backend == 'nccl' else backend})",
+                   "bytes_per_rank": n * 8,
                    "ms": cms}
         if rank == 0:
             collect["final_digest"] = f"{batch_digest(gathered.cpu().numpy()):016x}"
@@ -266,7 +281,7 @@ def main():
     if rank == 0:
         total = n * world * gens * args.steps
         value = total / elapsed
-        avg_launch = sum(launch_ms) / len(launch_ms)
+        avg_launch = span_ms / args.steps  # includes the ~1-2 us launch gaps: conservative
         achieved = n * gens * BYTES_PER_UNIVERSE_GEN / (avg_launch / 1e3) / 1e9 if gens == 1 else None
         traffic, tsrc = load_pmc_traffic(n)
         cfg = hip.default_cfg(gens).as_dict()
@@ -281,7 +296,8 @@ def main():
                        "parallelism": f"dp{world} (contiguous universe shards, no collective)",
                        "launch_cfg": cfg},
             "cell_updates_per_s": value * 4096,
-            "kernel_ms_avg": avg_launch, "kernel_ms_min": min(launch_ms),
+            "kernel_ms_avg": avg_launch,
+            "kernel_timing": "HIP events on the launch stream around the K timed launches / K",
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                          "traffic": traffic, "traffic_source": tsrc,

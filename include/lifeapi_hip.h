@@ -61,7 +61,10 @@ typedef struct lifeapi_launch_cfg {
   int universes_per_wave;  /* 1, 2, 4 or 8 universes in flight per wave     */
   int blocks_per_cu;       /* grid = min(needed, CUs * blocks_per_cu); 0=auto */
   int nontemporal;         /* 1: nt loads/stores (streaming, 1 generation)  */
-  int rule;                /* 0: adder network (bitop3), 1: plain and/or/xor */
+  int rule;                /* 0: column-first adder network (bitop3),
+                              1: the same in plain and/or/xor,
+                              2: row-first adder network (bitop3, half the
+                                 DPP moves; default)                     */
 } lifeapi_launch_cfg;
 
 int lifeapi_abi_version(void);

@@ -676,7 +676,7 @@ int lifeapi_device_count(void) {
 void lifeapi_default_cfg(lifeapi_launch_cfg *cfg, uint32_t generations) {
   if (!cfg) return;
   cfg->xchg = LIFEAPI_XCHG_DPP;
-  cfg->rule = 0;
+  cfg->rule = 2;  // row-first network: 4 DPP moves per generation instead of 8
   // Measured on MI355X (profiles/r01/tune.jsonl): a one-shot grid (no
   // grid-stride cap) beats every capped grid in both regimes.
   cfg->blocks_per_cu = 0;
@@ -807,8 +807,8 @@ int lifeapi_refined_step_batch_dev_cfg(const uint64_t *d_in, uint64_t *d_out, si
   // cfg: universes_per_wave 1 = no prefetch, 2 = prefetch next universe;
   // blocks_per_cu = grid cap; rule = minimum waves per SIMD requested from the
   // register allocator (0 = none, 4, 6).  Default = the measured best
-  // (profiles/r01/tune_c5.jsonl): no prefetch, 8 blocks per CU.
-  int pf = 0, bpc = 8, occ = 0;
+  // (profiles/r01/tune_all.jsonl): no prefetch, 12 blocks per CU.
+  int pf = 0, bpc = 12, occ = 0;
   if (cfg) {
     pf = cfg->universes_per_wave >= 2 ? 1 : 0;
     bpc = cfg->blocks_per_cu;
