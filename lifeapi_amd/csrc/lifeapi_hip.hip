@@ -807,8 +807,9 @@ int lifeapi_refined_step_batch_dev_cfg(const uint64_t *d_in, uint64_t *d_out, si
   // cfg: universes_per_wave 1 = no prefetch, 2 = prefetch next universe;
   // blocks_per_cu = grid cap; rule = minimum waves per SIMD requested from the
   // register allocator (0 = none, 4, 6).  Default = the measured best
-  // (profiles/r01/tune_all.jsonl): no prefetch, 12 blocks per CU.
-  int pf = 0, bpc = 12, occ = 0;
+  // with the 192-op SOP network (profiles/r01/tune_c5.jsonl): prefetch the
+  // next universe, one-shot grid, no occupancy bound -> 6.3 TB/s.
+  int pf = 1, bpc = 0, occ = 0;
   if (cfg) {
     pf = cfg->universes_per_wave >= 2 ? 1 : 0;
     bpc = cfg->blocks_per_cu;
