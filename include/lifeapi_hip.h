@@ -107,6 +107,10 @@ int lifeapi_neighbour_count_batch_dev(const uint64_t *d_in, uint64_t *d_out, siz
  * (LifeAPI.hpp:997-1040), d_out = n x {out1, out2, outMore, next} x 64.     */
 int lifeapi_interaction_counts_batch_dev(const uint64_t *d_in, uint64_t *d_out, size_t n,
                                          int with_next, void *stream);
+/* LifeWeld::Step() (LifeWeld.hpp:169-186) `generations` times, in place on
+ * LifeWeld[n] = {state, frozen2, frozen1, frozen0} x 64 words (the struct's
+ * member order, LifeWeld.hpp:18-20); only the state planes change.        */
+int lifeapi_weld_step_batch_dev(uint64_t *d_welds, size_t n, uint32_t generations, void *stream);
 /* Config-5 ternary step: bitslicing/unknown_step_refined.hpp:1-85 applied
  * per column with s2..s0 / on2..on0 = bits 2..0 of NeighbourCount
  * (NeighbourCount.hpp:40-70) of stable.state / current.state.

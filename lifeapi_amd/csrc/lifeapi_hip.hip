@@ -334,6 +334,21 @@ __global__ __launch_bounds__(kBlock) void k_step_contains(const uint64_t *__rest
 }
 
 // ---- neighbourhood counters --------------------------
+
+// Bits 2..0 of the inclusive 3x3 count of this lane's column: the
+// NeighbourCount adder chain (NeighbourCount.hpp:40-70) in the row-first
+// order of life_gen<RULE 2> (4 DPP moves): count = fs + 2(fc+cs) + 4cc.
+__device__ __forceinline__ void ncount3(W a, W &b2, W &b1, W &b0) {
+  W L, R;
+  neighbour_cols<XDPP>(a, L, R, nullptr, 0);
+  const W h0 = lut3<kXor3>(L, a, R), h1 = lut3<kMaj>(L, a, R);
+  const W h0u = rot_up(h0), h0d = rot_dn(h0), h1u = rot_up(h1), h1d = rot_dn(h1);
+  const W fs = lut3<kXor3>(h0u, h0, h0d), fc = lut3<kMaj>(h0u, h0, h0d);
+  const W cs = lut3<kXor3>(h1u, h1, h1d), cc = lut3<kMaj>(h1u, h1, h1d);
+  b0 = fs;
+  b1 = W{fc.lo ^ cs.lo, fc.hi ^ cs.hi};
+  b2 = lut3<kCarry2>(cc, fc, cs);
+}
 // Same stencil as Step(), different output planes.  The two FullAdds of the
 // vertical planes give the inclusive 3x3 count = fs + 2(fc + cs) + 4cc.
 // MODE 0: NeighbourCount / CountNeighbourhood (NeighbourCount.hpp:40-70,
@@ -379,24 +394,40 @@ __global__ __launch_bounds__(kBlock) void k_counts(const uint64_t *__restrict__ 
   }
 }
 
-// ---- config 5: the unknown_step_refined ternary step --------------------
-// Bits 2..0 of the inclusive 3x3 count of this lane's column: the
-// NeighbourCount adder chain (NeighbourCount.hpp:40-70) as CountRows + DPP
-// neighbour planes + two FullAdds (count = fs + 2(fc+cs) + 4cc).
-__device__ __forceinline__ void ncount3(W a, W &b2, W &b1, W &b0) {
-  const W up = rot_up(a), dn = rot_dn(a);
-  const W c0 = lut3<kXor3>(up, dn, a), c1 = lut3<kMaj>(up, dn, a);
-  W L0, R0, L1, R1;
-  neighbours<XDPP>(c0, c1, L0, R0, L1, R1, nullptr, 0);
-  const W fs = lut3<kXor3>(L0, c0, R0), fc = lut3<kMaj>(L0, c0, R0);
-  const W cs = lut3<kXor3>(L1, c1, R1), cc = lut3<kMaj>(L1, c1, R1);
-  b0 = fs;
-  b1 = W{fc.lo ^ cs.lo, fc.hi ^ cs.hi};
-  b2 = lut3<kCarry2>(cc, fc, cs);
+// ---- LifeWeld::Step ----------------------------------
+// LifeWeld.hpp:169-186: inclusive count bits 2..0 (CountNeighbourhood, bit3
+// dropped) + the frozen 3-bit count (HalfAdd, FullAdd, FullAdd), then the
+// Life rule on the sum.  The frozen planes are loop-invariant, so `gens`
+// generations run in registers.  In place on LifeWeld[] = {state, frozen2,
+// frozen1, frozen0} x 64 words; only the state plane is written back.
+__device__ __forceinline__ W weld_gen(W s, W f2, W f1, W f0) {
+  W b2, b1, b0;
+  ncount3(s, b2, b1, b0);
+  const W s0 = W{b0.lo ^ f0.lo, b0.hi ^ f0.hi}, k0 = W{b0.lo & f0.lo, b0.hi & f0.hi};
+  const W s1 = lut3<kXor3>(b1, f1, k0), k1 = lut3<kMaj>(b1, f1, k0);
+  const W s2 = lut3<kXor3>(b2, f2, k1);
+  const W p = lut3<kLive>(s0, s2, s);  // (s0 ^ s2) & (s | s0)
+  return W{p.lo & (s1.lo ^ s2.lo), p.hi & (s1.hi ^ s2.hi)};
 }
 
+__global__ __launch_bounds__(kBlock) void k_weld(uint64_t *__restrict__ welds, uint64_t n,
+                                                 uint32_t gens) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock;
+  for (uint64_t u = (uint64_t)blockIdx.x * kWavesPerBlock + wib; u < n; u += stride) {
+    uint64_t *p = welds + u * 4 * kWave + lane;
+    W s = ld<false>(p);
+    const W f2 = ld<false>(p + kWave), f1 = ld<false>(p + 2 * kWave), f0 = ld<false>(p + 3 * kWave);
+    for (uint32_t g = 0; g < gens; ++g) s = weld_gen(s, f2, f1, f0);
+    st<false>(p, s);
+  }
+}
+
+// ---- config 5: the unknown_step_refined ternary step --------------------
+
 // bitslicing/unknown_step_refined.hpp:1-85 as a v_bitop3 network.  The
-// network is generated (tools/synth_bitop3.py) from the fragment's complete
+// network is generated (tools/synth_sop.py) from the fragment's complete
 // truth table, which tests/golden/make_golden.py extracts from the reference
 // build, and is verified against all 2^16 input combinations when generated.
 template <class T>
@@ -785,6 +816,17 @@ static int counts_launch(const uint64_t *d_in, uint64_t *d_out, size_t n, int mo
   hipLaunchKernelGGL(fn, dim3(grid_for(n, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream, d_in,
                      d_out, (uint64_t)n);
   return launched("k_counts launch");
+}
+
+int lifeapi_weld_step_batch_dev(uint64_t *d_welds, size_t n, uint32_t generations, void *stream) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!d_welds || !aligned8(d_welds))
+    return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_weld_step_batch_dev%s");
+  int cus = 0, rc = device_cus(cus);
+  if (rc != LIFEAPI_OK) return rc;
+  hipLaunchKernelGGL(k_weld, dim3(grid_for(n, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream,
+                     d_welds, (uint64_t)n, generations);
+  return launched("k_weld launch");
 }
 
 int lifeapi_neighbour_count_batch_dev(const uint64_t *d_in, uint64_t *d_out, size_t n, void *stream) {

@@ -60,6 +60,7 @@ _SIGS = {
     "lifeapi_contains_batch_dev": ([_vp, _vp, _vp, _vp, _sz, _vp], _int),
     "lifeapi_step_contains_batch_dev": ([_vp, _vp, _vp, _vp, _vp, _sz, _u32, _vp], _int),
     "lifeapi_fill_random_dev": ([_vp, _sz, _u64, _u64, _int, _vp], _int),
+    "lifeapi_weld_step_batch_dev": ([_vp, _sz, _u32, _vp], _int),
     "lifeapi_neighbour_count_batch_dev": ([_vp, _vp, _sz, _vp], _int),
     "lifeapi_interaction_counts_batch_dev": ([_vp, _vp, _sz, _int, _vp], _int),
     "lifeapi_refined_step_batch_dev": ([_vp, _vp, _sz, _vp], _int),
@@ -227,6 +228,17 @@ def refined_step(planes: torch.Tensor, out: torch.Tensor | None = None, stream=N
         out = torch.empty((n, 3 * N), dtype=torch.int64, device=planes.device)
     _check(lib.lifeapi_refined_step_batch_dev(planes.data_ptr(), out.data_ptr(), n, _stream(stream)))
     return out
+
+
+def weld_step(welds: torch.Tensor, generations: int = 1, stream=None) -> torch.Tensor:
+    """LifeWeld::Step()^generations in place on (n, 4*64) {state, frozen2,
+    frozen1, frozen0} planes (LifeWeld.hpp:169-186)."""
+    if not welds.is_cuda or welds.dtype not in (torch.int64, torch.uint64) or \
+            not welds.is_contiguous() or welds.numel() % (4 * N):
+        raise ValueError("welds must be a contiguous int64 device tensor of shape (n, 4*64)")
+    _check(lib.lifeapi_weld_step_batch_dev(welds.data_ptr(), welds.numel() // (4 * N), generations,
+                                           _stream(stream)))
+    return welds
 
 
 def neighbour_count(states: torch.Tensor, stream=None) -> torch.Tensor:

@@ -137,6 +137,26 @@ void oracle_interaction_counts(const uint64_t s[64], uint64_t out1[64], uint64_t
   }
 }
 
+/* LifeWeld::Step (LifeWeld.hpp:169-186), `gens` times, in place on the
+ * LifeWeld layout {state, frozen2, frozen1, frozen0} (4 x 64 words): the
+ * inclusive count's low three bits (CountNeighbourhood, bit3 dropped) plus
+ * the frozen 3-bit count, then the Life rule on the sum. */
+void oracle_weld_step(uint64_t w[256], unsigned gens) {
+  uint64_t *s = w;
+  const uint64_t *f2 = w + 64, *f1 = w + 128, *f0 = w + 192;
+  for (unsigned g = 0; g < gens; ++g) {
+    uint64_t b3[64], b2[64], b1[64], b0[64];
+    oracle_neighbour_count(s, b3, b2, b1, b0);
+    for (int x = 0; x < ORACLE_N; ++x) {
+      const uint64_t s0 = b0[x] ^ f0[x], k0 = b0[x] & f0[x];
+      const uint64_t h1 = b1[x] ^ f1[x];
+      const uint64_t s1 = h1 ^ k0, k1 = (b1[x] & f1[x]) | (k0 & h1);
+      const uint64_t s2 = b2[x] ^ f2[x] ^ k1;
+      s[x] = (s0 ^ s2) & (s1 ^ s2) & (s[x] | s0);
+    }
+  }
+}
+
 /* LifeAPI.hpp:877-881 (LifeState::Step(unsigned)). */
 void oracle_step_n(uint64_t s[64], unsigned gens) {
   for (unsigned g = 0; g < gens; ++g) oracle_step(s);

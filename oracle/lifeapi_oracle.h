@@ -69,6 +69,9 @@ uint64_t oracle_batch_digest(const uint64_t *hashes, size_t n, uint64_t first_un
 void oracle_interaction_counts(const uint64_t s[64], uint64_t out1[64], uint64_t out2[64],
                                uint64_t out_more[64], uint64_t next[64]);
 
+/* LifeWeld.hpp:169-186: in place on {state, frozen2, frozen1, frozen0} */
+void oracle_weld_step(uint64_t w[256], unsigned gens);
+
 /* config 5 harness (see lifeapi_oracle.c): 11 planes in, 3 planes out per
  * universe; tt = the reference fragment's truth table, 3 x 65536 bytes */
 void oracle_refined_step_batch(const uint64_t *in, uint64_t *out, size_t n, const uint8_t *tt);

@@ -72,6 +72,7 @@ class Port:
         L.oracle_batch_digest.restype = ctypes.c_uint64
         L.oracle_neighbour_count.argtypes = [_u64p] * 5
         L.oracle_interaction_counts.argtypes = [_u64p] * 5
+        L.oracle_weld_step.argtypes = [_u64p, ctypes.c_uint]
         L.oracle_refined_step_batch.argtypes = [_u64p, _u64p, ctypes.c_size_t,
                                                 ctypes.POINTER(ctypes.c_uint8)]
         self._tt = None
@@ -131,6 +132,13 @@ class Port:
                                            _p64(b[3]) if with_next else None)
         return b if with_next else b[:3]
 
+    def weld_step(self, welds: np.ndarray, gens: int = 1) -> np.ndarray:
+        """LifeWeld::Step^gens on (n, 4*64) {state, frozen2, frozen1, frozen0}."""
+        out = np.ascontiguousarray(welds, dtype=np.uint64).reshape(-1, 256).copy()
+        for u in range(out.shape[0]):
+            self.lib.oracle_weld_step(_p64(out[u]), gens)
+        return out
+
     def refined_truth_table(self) -> np.ndarray:
         if self._tt is None:
             path = os.path.join(os.path.dirname(HERE), "tests", "golden", "unknown_step_refined_tt.npz")
@@ -169,6 +177,7 @@ class Ref:
         L.ref_neighbour_count.argtypes = [_u64p] * 5
         L.ref_count_neighbourhood.argtypes = [_u64p] * 5
         L.ref_interaction_counts.argtypes = [_u64p] * 5
+        L.ref_weld_step.argtypes = [_u64p, ctypes.c_uint]
         L.ref_unknown_step_refined.argtypes = [_u64p, _u64p]
         L.ref_refined_step_batch.argtypes = [_u64p, _u64p, ctypes.c_size_t]
 
@@ -225,6 +234,12 @@ class Ref:
         b = np.zeros((4, 64), dtype=np.uint64)
         self.lib.ref_interaction_counts(_p64(s), _p64(b[0]), _p64(b[1]), _p64(b[2]), _p64(b[3]))
         return b
+
+    def weld_step(self, welds: np.ndarray, gens: int = 1) -> np.ndarray:
+        out = np.ascontiguousarray(welds, dtype=np.uint64).reshape(-1, 256).copy()
+        for u in range(out.shape[0]):
+            self.lib.ref_weld_step(_p64(out[u]), gens)
+        return out
 
     def refined_step(self, planes: np.ndarray) -> np.ndarray:
         """Config-5 harness around the reference's own fragment (ref_shim.cpp)."""

@@ -10,6 +10,7 @@
 #include "NeighbourCount.hpp"
 #include "LifeTarget.hpp"
 #include "Parsing.hpp"
+#include "LifeWeld.hpp"
 
 static_assert(sizeof(LifeState) == 512 && alignof(LifeState) == 64,
               "LifeState layout (LifeAPI.hpp:39-40)");
@@ -58,6 +59,27 @@ void ref_interaction_counts(const uint64_t *s, uint64_t *o1, uint64_t *o2, uint6
   t.InteractionCounts(b1, b2, bm);
   if (!(a1 == b1 && a2 == b2 && am == bm)) std::abort();
   store(a1, o1); store(a2, o2); store(am, om); store(an, nx);
+}
+// LifeWeld::Step  LifeWeld.hpp:169-186, `gens` times, in place on
+// {state, frozen2, frozen1, frozen0} (4 x 64 words, the struct's member order)
+void ref_weld_step(uint64_t *w, unsigned gens) {
+  LifeWeld weld(load(w), load(w + 64), load(w + 128), load(w + 192));
+  for (unsigned g = 0; g < gens; ++g) weld.Step();
+  store(weld.state, w);
+  store(weld.frozen2, w + 64);
+  store(weld.frozen1, w + 128);
+  store(weld.frozen0, w + 192);
+}
+// LifeWeld::FromRequired  LifeWeld.hpp:133-159 (tests/LifeWeldTest.cpp:19-33
+// shape, with Parse instead of the `$`-buggy ConstantParse)
+void ref_weld_from_required(const char *state_rle, const char *required_rle, int dx, int dy,
+                            uint64_t *w) {
+  LifeWeld weld = LifeWeld::FromRequired(LifeState::Parse(std::string(state_rle)),
+                                         LifeState::Parse(std::string(required_rle)).Moved(dx, dy));
+  store(weld.state, w);
+  store(weld.frozen2, w + 64);
+  store(weld.frozen1, w + 128);
+  store(weld.frozen0, w + 192);
 }
 // LifeState::GetPop  LifeAPI.hpp:290-298
 unsigned ref_pop(const uint64_t *s) { return load(s).GetPop(); }

@@ -174,6 +174,27 @@ def main():
     meta["counts"] = {"n": int(len(cin)), "neighbour_count_planes": "bit3,bit2,bit1,bit0",
                       "interaction_planes": "out1,out2,outMore,next"}
 
+    # 5c. LifeWeld::Step (LifeWeld.hpp:169-186): the RequiredTest welds of
+    #     tests/LifeWeldTest.cpp:19-33 built by the reference's FromRequired
+    #     (must be invariant), plus seeded random welds stepped 1 and 7 times
+    R.lib.ref_weld_from_required.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
+                                             ctypes.c_int, _u64p]
+    req = [("2b2o$bobo$bo$2o!", "2b2o$b3o$b4o$5o$4o$4o!"),
+           ("2o$o2bob2o$b3obobo$5bobo$b5ob3o$bo4bo3bo$4bobo2b2o$4b2o!",
+            "4o$5o2bo$4o$5o4bo$b5ob5o$b12o$b12o$b12o$4b9o$4b4o!"),
+           ("4b2ob2o$3bobobobo$b3o3bobo$o4bobob3o$b3ob2obo3bo$3bo4bo2b2o$5b3o$4b2o!",
+            "4b2o$3b2o2bo2b2o$b4o6bo$6obob5o$15o$15o$b14o$3b12o$4b6o$4b4o!")]
+    req_welds = np.zeros((len(req), 256), np.uint64)
+    for i, (srle, rrle) in enumerate(req):
+        R.lib.ref_weld_from_required(srle.encode(), rrle.encode(), -1, -1, _p64(req_welds[i]))
+    rw = P.fill(64 * 4, seed=6060).reshape(64, 256)
+    rw[:, 64:] &= P.fill(64 * 3, seed=6061).reshape(64, 192) & P.fill(64 * 3, seed=6062).reshape(64, 192)
+    wel = np.concatenate([req_welds, rw])
+    np.savez(os.path.join(HERE, "weld.npz"), input=wel, step1=R.weld_step(wel, 1),
+             step7=R.weld_step(wel, 7), n_required=len(req))
+    meta["weld"] = {"n": int(len(wel)), "required_examples": len(req),
+                    "layout": "state,frozen2,frozen1,frozen0"}
+
     # 5b. config 5: bitslicing/unknown_step_refined.hpp (the reference's espresso
     #     fragment) as a complete truth table over its 16 inputs, plus seeded
     #     11-plane universes through the build-defined harness (ref_shim.cpp)

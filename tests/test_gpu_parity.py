@@ -246,6 +246,28 @@ def test_counts_vs_oracle_ragged(hip, port):
     assert (ic[:, 3] == port.step_batch(x, 1)).all()
 
 
+# ---- LifeWeld::Step ----
+
+def test_weld_golden_gpu(hip):
+    import os
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "weld.npz"))
+    for gens, key in ((1, "step1"), (7, "step7")):
+        d = to_dev(g["input"]).reshape(-1, 256)
+        hip.weld_step(d, gens)
+        torch.cuda.synchronize()
+        assert (d.cpu().numpy().view(np.uint64) == g[key]).all()
+
+
+def test_weld_vs_oracle_ragged(hip, port):
+    n = 3003
+    w = port.fill(n * 4, seed=9191).reshape(n, 256)
+    w[:, 64:] &= port.fill(n * 3, seed=9192).reshape(n, 192)
+    d = to_dev(w).reshape(n, 256)
+    hip.weld_step(d, 4)
+    torch.cuda.synchronize()
+    assert (d.cpu().numpy().view(np.uint64) == port.weld_step(w, 4)).all()
+
+
 # ---- config 5: unknown_step_refined ternary step ----
 
 def test_refined_step_golden(hip, port):

@@ -138,6 +138,22 @@ def test_counts_golden(port):
     assert (g["interaction_counts"][:, 3] == port.step_batch(g["input"], 1)).all()
 
 
+def test_weld_golden(port):
+    """LifeWeld::Step (LifeWeld.hpp:169-186) vs the reference-generated
+    fixture; the FromRequired welds of LifeWeldTest.cpp:19-33 are invariant."""
+    g = load("weld.npz")
+    assert (port.weld_step(g["input"], 1) == g["step1"]).all()
+    assert (port.weld_step(g["input"], 7) == g["step7"]).all()
+    k = int(g["n_required"])
+    assert (g["step1"][:k] == g["input"][:k]).all() and g["input"][:k, 64:].any()
+
+
+def test_weld_equals_reference_live(port, ref):
+    w = port.fill(50 * 4, seed=7171).reshape(50, 256)
+    w[:, 64:] &= port.fill(150, seed=7172).reshape(50, 192)
+    assert (port.weld_step(w, 3) == ref.weld_step(w, 3)).all()
+
+
 def test_refined_truth_table_fixture(port, meta):
     """Config 5: the fragment's truth table fixture and the harness outputs."""
     tt = port.refined_truth_table()
