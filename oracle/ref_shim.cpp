@@ -81,6 +81,71 @@ void ref_weld_from_required(const char *state_rle, const char *required_rle, int
   store(weld.frozen1, w + 128);
   store(weld.frozen0, w + 192);
 }
+// ---- LifeStable passes (LifeStable.hpp:41-53,526-729): 10 planes in the
+// class's member order {state, unknown, live2, live3, dead0, dead1, dead2,
+// dead4, dead5, dead6}; options stored as "1 = ruled out".
+static LifeStable load_stable(const uint64_t *p) {
+  LifeStable s;
+  s.state = load(p);
+  s.unknown = load(p + 64);
+  s.live2 = load(p + 128);
+  s.live3 = load(p + 192);
+  s.dead0 = load(p + 256);
+  s.dead1 = load(p + 320);
+  s.dead2 = load(p + 384);
+  s.dead4 = load(p + 448);
+  s.dead5 = load(p + 512);
+  s.dead6 = load(p + 576);
+  return s;
+}
+static void store_stable(const LifeStable &s, uint64_t *p) {
+  store(s.state, p);
+  store(s.unknown, p + 64);
+  store(s.live2, p + 128);
+  store(s.live3, p + 192);
+  store(s.dead0, p + 256);
+  store(s.dead1, p + 320);
+  store(s.dead2, p + 384);
+  store(s.dead4, p + 448);
+  store(s.dead5, p + 512);
+  store(s.dead6, p + 576);
+}
+// which: 0 SynchroniseStateKnown (:526-556), 1 UpdateOptions (:558-615),
+// 2 SignalNeighbours (:617-675), 3 PropagateStep (:695-716),
+// 4 Propagate (:718-729).  Returns consistent | changed << 1.
+int ref_stable_pass(uint64_t *planes, int which) {
+  LifeStable s = load_stable(planes);
+  LifeStable::PropagateResult r{};
+  switch (which) {
+    case 0: r = s.SynchroniseStateKnown(); break;
+    case 1: r = s.UpdateOptions(); break;
+    case 2: r = s.SignalNeighbours(); break;
+    case 3: r = s.PropagateStep(); break;
+    default: r = s.Propagate(); break;
+  }
+  store_stable(s, planes);
+  return (r.consistent ? 1 : 0) | (r.changed ? 2 : 0);
+}
+// The two espresso fragments the passes include, evaluated on 64 cells.
+// stable_count.hpp (included at LifeStable.hpp:591): 9 inputs -> 9 outputs
+void ref_stable_count_frag(const uint64_t *in, uint64_t *out) {
+  const uint64_t on2 = in[0], on1 = in[1], on0 = in[2], off3 = in[3], off2 = in[4], off1 = in[5],
+                 off0 = in[6], known_on = in[7], known_off = in[8];
+  uint64_t abort = 0, l2 = 0, l3 = 0, d0 = 0, d1 = 0, d2 = 0, d4 = 0, d5 = 0, d6 = 0;
+#include "bitslicing/stable_count.hpp"
+  const uint64_t r[9] = {l2, l3, d0, d1, d2, d4, d5, d6, abort};
+  std::memcpy(out, r, sizeof r);
+}
+// stable_signal.hpp (included at LifeStable.hpp:654): 17 inputs -> 4 outputs
+void ref_stable_signal_frag(const uint64_t *in, uint64_t *out) {
+  const uint64_t l2 = in[0], l3 = in[1], d0 = in[2], d1 = in[3], d2 = in[4], d4 = in[5], d5 = in[6],
+                 d6 = in[7], s2 = in[8], s1 = in[9], s0 = in[10], m3 = in[11], m2 = in[12],
+                 m1 = in[13], m0 = in[14], stateon = in[15], stateunk = in[16];
+  uint64_t signaloff = 0, signalon = 0, centeroff = 0, centeron = 0;
+#include "bitslicing/stable_signal.hpp"
+  const uint64_t r[4] = {signaloff, signalon, centeroff, centeron};
+  std::memcpy(out, r, sizeof r);
+}
 // LifeState::GetPop  LifeAPI.hpp:290-298
 unsigned ref_pop(const uint64_t *s) { return load(s).GetPop(); }
 // LifeState::Contains(const LifeTarget&)  LifeTarget.hpp:44-51

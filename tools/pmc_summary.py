@@ -36,24 +36,30 @@ def main(prof_dir: str, out_json: str, universes: int = 1 << 20):
     known = 1 << 29  # calib copy: 2^20 universes x 512 B each way
     cf, ncf = mean_counter(p("calib_FETCH_SIZE", "calib_counter_collection.csv"), "k_copy", "FETCH_SIZE")
     cw, ncw = mean_counter(p("calib_WRITE_SIZE", "calib_counter_collection.csv"), "k_copy", "WRITE_SIZE")
-    sf, nsf = mean_counter(p("pmc_FETCH_SIZE", "bench_counter_collection.csv"), "k_step", "FETCH_SIZE")
-    sw, nsw = mean_counter(p("pmc_WRITE_SIZE", "bench_counter_collection.csv"), "k_step", "WRITE_SIZE")
     ff, wf = known / (cf * 1024), known / (cw * 1024)
-    fetch_b, write_b = sf * 1024 * ff, sw * 1024 * wf
-    algo = universes * 1024
-    d = {
-        "kernel": "k_step<DPP, U=4, nt, bitop3> (config 2: 1M universes x 1 gen)",
-        "universes": universes,
-        "raw": {"FETCH_SIZE_KiB_mean": sf, "WRITE_SIZE_KiB_mean": sw, "dispatches": [nsf, nsw]},
-        "calibration": {"kernel": "tools/membw.hip calib: dwordx2 U=4 nt copy, 512 MiB each way",
+
+    def entry(name_sub, label, algo):
+        sf, nsf = mean_counter(p("pmc_FETCH_SIZE", "bench_counter_collection.csv"), name_sub, "FETCH_SIZE")
+        sw, nsw = mean_counter(p("pmc_WRITE_SIZE", "bench_counter_collection.csv"), name_sub, "WRITE_SIZE")
+        fetch_b, write_b = sf * 1024 * ff, sw * 1024 * wf
+        return {"kernel": label, "kernel_name_match": name_sub,
+                "raw": {"FETCH_SIZE_KiB_mean": sf, "WRITE_SIZE_KiB_mean": sw, "dispatches": [nsf, nsw]},
+                "hbm_read_bytes_per_launch": fetch_b, "hbm_write_bytes_per_launch": write_b,
+                "hbm_bytes_per_launch": fetch_b + write_b, "algorithmic_bytes_per_launch": algo,
+                "traffic_over_algorithmic": (fetch_b + write_b) / algo}
+
+    c2 = entry("k_step<0, 4, true, 2>", "k_step<DPP, U=4, nt, row-first> (config 2: 1M universes x 1 gen)",
+               universes * 1024)
+    d = dict(c2)
+    d["universes"] = universes
+    d["calibration"] = {"kernel": "tools/membw.hip calib: dwordx2 U=4 nt copy, 512 MiB each way",
                         "FETCH_SIZE_KiB_mean": cf, "WRITE_SIZE_KiB_mean": cw,
-                        "fetch_factor": ff, "write_factor": wf, "dispatches": [ncf, ncw]},
-        "hbm_read_bytes_per_launch": fetch_b,
-        "hbm_write_bytes_per_launch": write_b,
-        "hbm_bytes_per_launch": fetch_b + write_b,
-        "algorithmic_bytes_per_launch": algo,
-        "traffic_over_algorithmic": (fetch_b + write_b) / algo,
-    }
+                        "fetch_factor": ff, "write_factor": wf, "dispatches": [ncf, ncw]}
+    try:  # config 5 (present when the bench ran its secondaries under the PMC passes)
+        d["config5"] = entry("k_refined<1, 0>", "k_refined (config 5: 256K universes, 11 planes in, 3 out)",
+                             (1 << 18) * 7168)
+    except SystemExit:
+        pass
     with open(out_json, "w") as f:
         json.dump(d, f, indent=1)
     print(json.dumps(d, indent=1))
