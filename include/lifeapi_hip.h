@@ -107,6 +107,17 @@ int lifeapi_neighbour_count_batch_dev(const uint64_t *d_in, uint64_t *d_out, siz
  * (LifeAPI.hpp:997-1040), d_out = n x {out1, out2, outMore, next} x 64.     */
 int lifeapi_interaction_counts_batch_dev(const uint64_t *d_in, uint64_t *d_out, size_t n,
                                          int with_next, void *stream);
+/* LifeStable propagation passes, in place on LifeStable[n] = {state,
+ * unknown, live2, live3, dead0, dead1, dead2, dead4, dead5, dead6} x 64
+ * words (member order, LifeStable.hpp:41-53; option planes 1 = ruled out).
+ * pass: 0 SynchroniseStateKnown (LifeStable.hpp:526-556), 1 UpdateOptions
+ * (:558-615), 2 SignalNeighbours (:617-675), 3 PropagateStep (:695-716),
+ * 4 Propagate (:718-729, at most max_iters steps; 0 = 2^20).
+ * d_flags[u] = consistent | changed << 1 (| 4 if max_iters stopped pass 4),
+ * i.e. the PropagateResult; planes are left exactly as the reference leaves
+ * them, including on an inconsistent early return.                        */
+int lifeapi_stable_pass_batch_dev(uint64_t *d_planes, uint8_t *d_flags, size_t n, int pass,
+                                  uint32_t max_iters, void *stream);
 /* LifeWeld::Step() (LifeWeld.hpp:169-186) `generations` times, in place on
  * LifeWeld[n] = {state, frozen2, frozen1, frozen0} x 64 words (the struct's
  * member order, LifeWeld.hpp:18-20); only the state planes change.        */

@@ -61,6 +61,7 @@ _SIGS = {
     "lifeapi_step_contains_batch_dev": ([_vp, _vp, _vp, _vp, _vp, _sz, _u32, _vp], _int),
     "lifeapi_fill_random_dev": ([_vp, _sz, _u64, _u64, _int, _vp], _int),
     "lifeapi_weld_step_batch_dev": ([_vp, _sz, _u32, _vp], _int),
+    "lifeapi_stable_pass_batch_dev": ([_vp, _vp, _sz, _int, _u32, _vp], _int),
     "lifeapi_neighbour_count_batch_dev": ([_vp, _vp, _sz, _vp], _int),
     "lifeapi_interaction_counts_batch_dev": ([_vp, _vp, _sz, _int, _vp], _int),
     "lifeapi_refined_step_batch_dev": ([_vp, _vp, _sz, _vp], _int),
@@ -239,6 +240,24 @@ def weld_step(welds: torch.Tensor, generations: int = 1, stream=None) -> torch.T
     _check(lib.lifeapi_weld_step_batch_dev(welds.data_ptr(), welds.numel() // (4 * N), generations,
                                            _stream(stream)))
     return welds
+
+
+STABLE_PASSES = ("sync", "options", "signal", "step", "propagate")
+
+
+def stable_pass(planes: torch.Tensor, which: str | int, max_iters: int = 0,
+                stream=None) -> torch.Tensor:
+    """LifeStable pass in place on (n, 10*64) planes; returns uint8 flags
+    (bit0 consistent, bit1 changed, bit2 stopped by max_iters)."""
+    w = STABLE_PASSES.index(which) if isinstance(which, str) else int(which)
+    if not planes.is_cuda or planes.dtype not in (torch.int64, torch.uint64) or \
+            not planes.is_contiguous() or planes.numel() % (10 * N):
+        raise ValueError("planes must be a contiguous int64 device tensor of shape (n, 10*64)")
+    n = planes.numel() // (10 * N)
+    flags = torch.empty(n, dtype=torch.uint8, device=planes.device)
+    _check(lib.lifeapi_stable_pass_batch_dev(planes.data_ptr(), flags.data_ptr(), n, w, max_iters,
+                                             _stream(stream)))
+    return flags
 
 
 def neighbour_count(states: torch.Tensor, stream=None) -> torch.Tensor:

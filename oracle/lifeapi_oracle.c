@@ -309,6 +309,153 @@ uint64_t oracle_batch_digest(const uint64_t *hashes, size_t n, uint64_t first_un
   return acc;
 }
 
+/* ---- LifeStable passes (LifeStable.hpp:526-729) ----
+ * planes: {state, unknown, live2, live3, dead0, dead1, dead2, dead4, dead5,
+ * dead6} x 64 words (class member order, LifeStable.hpp:41-53; options are
+ * "1 = ruled out").  The espresso fragments stable_count.hpp / stable_signal.hpp
+ * are evaluated by TABLE LOOKUP in their complete truth tables (tests/golden/
+ * stable_{count,signal}_tt.npz, extracted from the reference build):
+ * tt_count = 9 x 512 bytes, tt_signal = 4 x 131072 bytes.  Returns
+ * consistent | changed << 1, like LifeStable::PropagateResult. */
+enum { ST, UN, L2, L3, D0, D1, D2, D4, D5, D6 };
+#define PL(p, k) ((p) + (k) * 64)
+
+/* LifeStable.hpp:526-556 */
+static int stable_sync(uint64_t *p) {
+  uint64_t changes = 0, abort_ = 0, ml[64], md[64];
+  for (int x = 0; x < 64; ++x) {
+    const uint64_t known_on = ~PL(p, UN)[x] & PL(p, ST)[x];
+    md[x] = ~(PL(p, D0)[x] & PL(p, D1)[x] & PL(p, D2)[x] & PL(p, D4)[x] & PL(p, D5)[x] & PL(p, D6)[x]);
+    changes |= md[x] & known_on;
+    for (int k = D0; k <= D6; ++k) PL(p, k)[x] |= known_on;
+    const uint64_t known_off = ~PL(p, UN)[x] & ~PL(p, ST)[x];
+    ml[x] = ~(PL(p, L2)[x] & PL(p, L3)[x]);
+    changes |= ml[x] & known_off;
+    PL(p, L2)[x] |= known_off;
+    PL(p, L3)[x] |= known_off;
+    abort_ |= ~ml[x] & ~md[x];
+  }
+  if (abort_) return 0;
+  for (int x = 0; x < 64; ++x) {
+    changes |= ~PL(p, ST)[x] & (ml[x] & ~md[x]);
+    PL(p, ST)[x] |= ml[x] & ~md[x];
+    changes |= ~PL(p, UN)[x] & (ml[x] & md[x]);
+    PL(p, UN)[x] &= ml[x] & md[x];
+  }
+  return 1 | (changes ? 2 : 0);
+}
+
+static unsigned cell_index(const uint64_t *w, int nin, int y) {
+  unsigned idx = 0;
+  for (int i = 0; i < nin; ++i) idx |= (unsigned)((w[i] >> y) & 1u) << i;
+  return idx;
+}
+
+/* LifeStable.hpp:558-615 */
+static int stable_options(uint64_t *p, const uint8_t *tt) {
+  uint64_t off[64], s3[64], s2[64], s1[64], s0[64], o3[64], o2[64], o1[64], o0[64];
+  for (int x = 0; x < 64; ++x) off[x] = ~PL(p, UN)[x] & ~PL(p, ST)[x];
+  oracle_neighbour_count(PL(p, ST), s3, s2, s1, s0);
+  oracle_neighbour_count(off, o3, o2, o1, o0);
+  uint64_t has_abort = 0, changes = 0;
+  for (int x = 0; x < 64; ++x) {
+    const uint64_t in[9] = {s2[x], s1[x], s0[x], o3[x], o2[x], o1[x], o0[x], PL(p, ST)[x], off[x]};
+    uint64_t r[9] = {0};
+    for (int y = 0; y < 64; ++y) {
+      const unsigned idx = cell_index(in, 9, y);
+      for (int k = 0; k < 9; ++k) r[k] |= (uint64_t)(tt[k * 512 + idx] & 1u) << y;
+    }
+    for (int k = 0; k < 8; ++k) {  /* l2 l3 d0 d1 d2 d4 d5 d6 -> planes L2.. D6 */
+      changes |= r[k] & ~PL(p, L2 + k)[x];
+      PL(p, L2 + k)[x] |= r[k];
+    }
+    has_abort |= r[8];
+  }
+  return (has_abort == 0) | (changes ? 2 : 0);
+}
+
+/* LifeAPI.hpp:541-562 (ZOIHollow) */
+static void zoi_hollow(const uint64_t *s, uint64_t *out) {
+  uint64_t t[64], m[64];
+  for (int x = 0; x < 64; ++x) {
+    m[x] = rotl64(s[x], 1) | rotr64(s[x], 1);
+    t[x] = s[x] | m[x];
+  }
+  for (int x = 0; x < 64; ++x) out[x] = t[(x + 63) & 63] | m[x] | t[(x + 1) & 63];
+}
+
+/* LifeStable.hpp:617-675 */
+static int stable_signal(uint64_t *p, const uint8_t *tt) {
+  uint64_t mx[64], s3[64], s2[64], s1[64], s0[64], m3[64], m2[64], m1[64], m0[64];
+  uint64_t soff[64], son[64], coff[64], con[64], offz[64], onz[64];
+  for (int x = 0; x < 64; ++x) mx[x] = PL(p, ST)[x] | PL(p, UN)[x];
+  oracle_neighbour_count(PL(p, ST), s3, s2, s1, s0);
+  oracle_neighbour_count(mx, m3, m2, m1, m0);
+  for (int x = 0; x < 64; ++x) {
+    const uint64_t in[17] = {PL(p, L2)[x], PL(p, L3)[x], PL(p, D0)[x], PL(p, D1)[x], PL(p, D2)[x],
+                             PL(p, D4)[x], PL(p, D5)[x], PL(p, D6)[x], s2[x], s1[x], s0[x],
+                             m3[x], m2[x], m1[x], m0[x], PL(p, ST)[x], PL(p, UN)[x]};
+    uint64_t r[4] = {0};
+    for (int y = 0; y < 64; ++y) {
+      const unsigned idx = cell_index(in, 17, y);
+      for (int k = 0; k < 4; ++k) r[k] |= (uint64_t)(tt[k * 131072 + idx] & 1u) << y;
+    }
+    soff[x] = r[0]; son[x] = r[1]; coff[x] = r[2]; con[x] = r[3];
+  }
+  zoi_hollow(soff, offz);
+  zoi_hollow(son, onz);
+  uint64_t clash = 0, changes = 0;
+  for (int x = 0; x < 64; ++x) {
+    offz[x] |= coff[x];
+    onz[x] |= con[x];
+    clash |= offz[x] & onz[x] & PL(p, UN)[x];
+  }
+  if (clash) return 0;
+  for (int x = 0; x < 64; ++x) {
+    changes |= (offz[x] & PL(p, UN)[x]) | (onz[x] & PL(p, UN)[x]);
+    const uint64_t w_off = offz[x] & PL(p, UN)[x];   /* SetOff, LifeStable.hpp:330-335 */
+    PL(p, ST)[x] &= ~w_off;
+    PL(p, UN)[x] &= ~w_off;
+    PL(p, L2)[x] |= w_off;
+    PL(p, L3)[x] |= w_off;
+    const uint64_t w_on = onz[x] & PL(p, UN)[x];     /* SetOn, LifeStable.hpp:320-329 */
+    PL(p, ST)[x] |= w_on;
+    PL(p, UN)[x] &= ~w_on;
+    for (int k = D0; k <= D6; ++k) PL(p, k)[x] |= w_on;
+  }
+  return 1 | (changes ? 2 : 0);
+}
+
+/* LifeStable.hpp:695-716 */
+static int stable_step(uint64_t *p, const uint8_t *ttc, const uint8_t *tts) {
+  const int k = stable_sync(p);
+  if (!(k & 1)) return 0;
+  const int o = stable_options(p, ttc);
+  if (!(o & 1)) return 0;
+  const int s = stable_signal(p, tts);
+  if (!(s & 1)) return 0;
+  return 1 | ((k | o | s) & 2);
+}
+
+int oracle_stable_pass(uint64_t *planes, int which, const uint8_t *tt_count,
+                       const uint8_t *tt_signal) {
+  switch (which) {
+    case 0: return stable_sync(planes);
+    case 1: return stable_options(planes, tt_count);
+    case 2: return stable_signal(planes, tt_signal);
+    case 3: return stable_step(planes, tt_count, tt_signal);
+    default: { /* LifeStable.hpp:718-729 */
+      int ever = 0;
+      for (;;) {
+        const int r = stable_step(planes, tt_count, tt_signal);
+        if (!(r & 1)) return 0;
+        if (!(r & 2)) return 1 | ever;
+        ever = 2;
+      }
+    }
+  }
+}
+
 /* ---- config 5: the unknown_step_refined harness ----
  * bitslicing/unknown_step_refined.hpp:1-85 is an espresso sum-of-products
  * over 16 per-cell inputs.  The oracle evaluates that function by TABLE

@@ -72,6 +72,12 @@ void oracle_interaction_counts(const uint64_t s[64], uint64_t out1[64], uint64_t
 /* LifeWeld.hpp:169-186: in place on {state, frozen2, frozen1, frozen0} */
 void oracle_weld_step(uint64_t w[256], unsigned gens);
 
+/* LifeStable passes, in place on 10 planes (see lifeapi_oracle.c):
+ * which = 0 SynchroniseStateKnown, 1 UpdateOptions, 2 SignalNeighbours,
+ * 3 PropagateStep, 4 Propagate.  Returns consistent | changed << 1. */
+int oracle_stable_pass(uint64_t *planes, int which, const uint8_t *tt_count,
+                       const uint8_t *tt_signal);
+
 /* config 5 harness (see lifeapi_oracle.c): 11 planes in, 3 planes out per
  * universe; tt = the reference fragment's truth table, 3 x 65536 bytes */
 void oracle_refined_step_batch(const uint64_t *in, uint64_t *out, size_t n, const uint8_t *tt);

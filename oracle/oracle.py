@@ -73,6 +73,8 @@ class Port:
         L.oracle_neighbour_count.argtypes = [_u64p] * 5
         L.oracle_interaction_counts.argtypes = [_u64p] * 5
         L.oracle_weld_step.argtypes = [_u64p, ctypes.c_uint]
+        L.oracle_stable_pass.argtypes = [_u64p, ctypes.c_int, ctypes.POINTER(ctypes.c_uint8),
+                                         ctypes.POINTER(ctypes.c_uint8)]
         L.oracle_refined_step_batch.argtypes = [_u64p, _u64p, ctypes.c_size_t,
                                                 ctypes.POINTER(ctypes.c_uint8)]
         self._tt = None
@@ -138,6 +140,23 @@ class Port:
         for u in range(out.shape[0]):
             self.lib.oracle_weld_step(_p64(out[u]), gens)
         return out
+
+    STABLE_PASSES = ("sync", "options", "signal", "step", "propagate")
+
+    def stable_pass(self, planes: np.ndarray, which: int):
+        """LifeStable pass `which` (0..4, see lifeapi_oracle.h) on (n, 640)
+        planes; returns (planes, flags: bit0 consistent, bit1 changed)."""
+        gold = os.path.join(os.path.dirname(HERE), "tests", "golden")
+        if not hasattr(self, "_stt"):
+            self._stt = tuple(np.ascontiguousarray(np.load(os.path.join(gold, f))["tt"].astype(np.uint8))
+                              for f in ("stable_count_tt.npz", "stable_signal_tt.npz"))
+        u8 = ctypes.POINTER(ctypes.c_uint8)
+        out = np.ascontiguousarray(planes, dtype=np.uint64).reshape(-1, 640).copy()
+        flags = np.zeros(out.shape[0], np.uint8)
+        for u in range(out.shape[0]):
+            flags[u] = self.lib.oracle_stable_pass(_p64(out[u]), which, self._stt[0].ctypes.data_as(u8),
+                                                   self._stt[1].ctypes.data_as(u8))
+        return out, flags
 
     def refined_truth_table(self) -> np.ndarray:
         if self._tt is None:

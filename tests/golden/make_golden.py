@@ -45,20 +45,81 @@ def _p64(a):
     return a.ctypes.data_as(_u64p)
 
 
-def refined_truth_table() -> np.ndarray:
-    """(3, 65536) uint8: output bits of the reference fragment for every input
-    combination c (bit i of c = REFINED_INPUTS[i]), evaluated 64 at a time."""
-    c = np.arange(1 << 16, dtype=np.uint64).reshape(1024, 64)
+def fragment_truth_table(fn, nin: int, nout: int) -> np.ndarray:
+    """(nout, 2^nin) uint8: output bits of a reference fragment wrapper `fn`
+    (in words -> out words) for every input combination c (bit i of c = input
+    i), evaluated 64 combinations per call."""
+    rows = 1 << nin
+    c = np.arange(rows, dtype=np.uint64).reshape(rows // 64, 64)
     shifts = np.arange(64, dtype=np.uint64)
     words = np.stack([(((c >> np.uint64(i)) & np.uint64(1)) << shifts).sum(axis=1, dtype=np.uint64)
-                      for i in range(16)])  # (16, 1024)
-    out = np.zeros((3, 1024), np.uint64)
-    for w in range(1024):
+                      for i in range(nin)])  # (nin, rows/64)
+    out = np.zeros((nout, rows // 64), np.uint64)
+    for w in range(rows // 64):
         a = np.ascontiguousarray(words[:, w])
-        o = np.zeros(3, np.uint64)
-        R.lib.ref_unknown_step_refined(_p64(a), _p64(o))
+        o = np.zeros(nout, np.uint64)
+        fn(_p64(a), _p64(o))
         out[:, w] = o
-    return np.unpackbits(out.view(np.uint8), bitorder="little").reshape(3, 1 << 16)
+    return np.unpackbits(out.view(np.uint8), bitorder="little").reshape(nout, rows)
+
+
+def refined_truth_table() -> np.ndarray:
+    return fragment_truth_table(R.lib.ref_unknown_step_refined, 16, 3)
+
+
+STABLE_COUNT_INPUTS = ["on2", "on1", "on0", "off3", "off2", "off1", "off0", "known_on", "known_off"]
+STABLE_COUNT_OUTPUTS = ["l2", "l3", "d0", "d1", "d2", "d4", "d5", "d6", "abort"]
+STABLE_SIGNAL_INPUTS = ["l2", "l3", "d0", "d1", "d2", "d4", "d5", "d6", "s2", "s1", "s0",
+                        "m3", "m2", "m1", "m0", "stateon", "stateunk"]
+STABLE_SIGNAL_OUTPUTS = ["signaloff", "signalon", "centeroff", "centeron"]
+
+
+def moved(s, dx, dy):
+    """LifeState::Move on the torus (columns x+dx, rows y+dy)."""
+    s = np.roll(np.asarray(s, np.uint64), dx)
+    k = dy % 64
+    return np.array([((int(w) << k) | (int(w) >> (64 - k))) & (2**64 - 1) if k else int(w)
+                     for w in s], dtype=np.uint64)
+
+
+def rect(x0, y0, w, h):
+    col = ((1 << h) - 1) << y0
+    s = np.zeros(64, np.uint64)
+    s[x0:x0 + w] = np.uint64(col & (2**64 - 1))
+    return s
+
+
+def stable_inputs(n: int, seed: int = 8080) -> np.ndarray:
+    """Seeded LifeStable planes {state, unknown, live2, live3, dead0, dead1,
+    dead2, dead4, dead5, dead6}: still lifes around an unknown window with
+    fresh options, sparse random soups around a window, and random planes."""
+    rng = np.random.default_rng(seed)
+    lifes = [R.parse(r) for r in ("2o$2o!", "b2o$o2bo$b2o!", "2o$obo$bo!", "2b2o$bobo$bo$2o!",
+                                   "b2o$o2bo$bobo$2bo!", "bo$obo$bo!")]
+    out = np.zeros((n, 10, 64), np.uint64)
+    for u in range(n):
+        kind = u % 3
+        w, h = int(rng.integers(6, 24)), int(rng.integers(6, 24))
+        x0, y0 = int(rng.integers(0, 64 - w)), int(rng.integers(0, 64 - h))
+        unk = rect(x0, y0, w, h)
+        if kind == 0:
+            st = np.zeros(64, np.uint64)
+            for _ in range(int(rng.integers(4, 12))):
+                st |= moved(lifes[int(rng.integers(len(lifes)))], int(rng.integers(64)), int(rng.integers(64)))
+            out[u, 0] = st & ~unk
+            out[u, 1] = unk
+        elif kind == 1:
+            f = P.fill(2, seed=int(rng.integers(1 << 30)))
+            out[u, 0] = f[0] & f[1] & ~unk
+            out[u, 1] = unk
+        else:
+            f = P.fill(10, seed=int(rng.integers(1 << 30)))
+            g = P.fill(10, seed=int(rng.integers(1 << 30)))
+            h2 = P.fill(10, seed=int(rng.integers(1 << 30)))
+            out[u, 0] = f[0]
+            out[u, 1] = g[1] & unk
+            out[u, 2:] = f[2:] & g[2:] & h2[2:]
+    return out.reshape(n, 640)
 
 
 def pop_words(s):
@@ -194,6 +255,35 @@ def main():
              step7=R.weld_step(wel, 7), n_required=len(req))
     meta["weld"] = {"n": int(len(wel)), "required_examples": len(req),
                     "layout": "state,frozen2,frozen1,frozen0"}
+
+    # 5d. LifeStable passes: the two espresso fragments as
+    #     complete truth tables, and seeded 10-plane LifeStables through the
+    #     reference's SynchroniseStateKnown / UpdateOptions / SignalNeighbours /
+    #     PropagateStep / Propagate
+    R.lib.ref_stable_count_frag.argtypes = [_u64p, _u64p]
+    R.lib.ref_stable_signal_frag.argtypes = [_u64p, _u64p]
+    R.lib.ref_stable_pass.argtypes = [_u64p, ctypes.c_int]
+    sc = fragment_truth_table(R.lib.ref_stable_count_frag, 9, 9)
+    np.savez_compressed(os.path.join(HERE, "stable_count_tt.npz"), tt=sc,
+                        inputs=np.array(STABLE_COUNT_INPUTS), outputs=np.array(STABLE_COUNT_OUTPUTS))
+    ss = fragment_truth_table(R.lib.ref_stable_signal_frag, 17, 4)
+    np.savez_compressed(os.path.join(HERE, "stable_signal_tt.npz"), tt=ss,
+                        inputs=np.array(STABLE_SIGNAL_INPUTS), outputs=np.array(STABLE_SIGNAL_OUTPUTS))
+    st_in = stable_inputs(48)
+    res = {}
+    for which, name in enumerate(["sync", "options", "signal", "step", "propagate"]):
+        planes = st_in.copy()
+        flags = np.array([R.lib.ref_stable_pass(_p64(planes[u]), which) for u in range(len(planes))],
+                         dtype=np.uint8)
+        res[name] = planes
+        res[name + "_flags"] = flags
+    np.savez_compressed(os.path.join(HERE, "stable.npz"), input=st_in, **res)
+    meta["stable"] = {"n": int(len(st_in)), "passes": ["sync", "options", "signal", "step", "propagate"],
+                      "flags": "bit0 consistent, bit1 changed",
+                      "step_consistent": int((res["step_flags"] & 1).sum()),
+                      "propagate_consistent": int((res["propagate_flags"] & 1).sum()),
+                      "stable_count_ones": [int(v) for v in sc.sum(axis=1)],
+                      "stable_signal_ones": [int(v) for v in ss.sum(axis=1)]}
 
     # 5b. config 5: bitslicing/unknown_step_refined.hpp (the reference's espresso
     #     fragment) as a complete truth table over its 16 inputs, plus seeded

@@ -268,6 +268,49 @@ def test_weld_vs_oracle_ragged(hip, port):
     assert (d.cpu().numpy().view(np.uint64) == port.weld_step(w, 4)).all()
 
 
+# ---- LifeStable passes ----
+
+def test_stable_passes_golden_gpu(hip):
+    import os
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "stable.npz"))
+    for name in hip.STABLE_PASSES:
+        d = to_dev(g["input"]).reshape(-1, 640)
+        fl = hip.stable_pass(d, name)
+        torch.cuda.synchronize()
+        assert (d.cpu().numpy().view(np.uint64) == g[name]).all(), name
+        assert (fl.cpu().numpy() == g[name + "_flags"]).all(), name
+
+
+def test_stable_passes_vs_oracle(hip, port):
+    """Seeded still-life neighbourhoods with an unknown window (mostly
+    consistent) and random planes (mostly inconsistent), every pass."""
+    rng = np.random.default_rng(5)
+    n = 300
+    x = np.zeros((n, 10, 64), np.uint64)
+    blocks = port.parse("2o$2o!")
+    for u in range(n):
+        st = np.zeros(64, np.uint64)
+        for _ in range(6):  # well separated blocks on a 16x16 lattice: a still life
+            bx, by = int(rng.integers(4)) * 16, int(rng.integers(4)) * 16
+            st |= np.roll(blocks, bx) << np.uint64(by)
+        w0, h0 = int(rng.integers(4, 20)), int(rng.integers(4, 20))
+        x0, y0 = int(rng.integers(0, 64 - w0)), int(rng.integers(0, 64 - h0))
+        unk = np.zeros(64, np.uint64)
+        unk[x0:x0 + w0] = np.uint64(((1 << h0) - 1) << y0)
+        x[u, 0], x[u, 1] = st & ~unk, unk
+        if u % 4 == 3:
+            f = port.fill(10, seed=u)
+            x[u, 2:] = f[2:] & port.fill(8, seed=u + 1000)
+    x = x.reshape(n, 640)
+    for w, name in enumerate(hip.STABLE_PASSES):
+        d = to_dev(x).reshape(n, 640)
+        fl = hip.stable_pass(d, name).cpu().numpy()
+        want, wfl = port.stable_pass(x, w)
+        assert (d.cpu().numpy().view(np.uint64) == want).all(), name
+        assert (fl == wfl).all(), name
+    assert (wfl & 1).sum() > n // 3  # the propagate loop ran to a fixpoint on many
+
+
 # ---- config 5: unknown_step_refined ternary step ----
 
 def test_refined_step_golden(hip, port):

@@ -163,29 +163,44 @@ def test_refined_truth_table_fixture(port, meta):
     assert (port.refined_step(g["input"]) == g["output"]).all()
 
 
-def test_refined_circuit_is_the_table():
-    """The generated bitop3 network (lifeapi_amd/csrc/refined_circuit.inc),
-    simulated on all 2^16 inputs, is exactly the reference fragment's table."""
+@pytest.mark.parametrize("inc,ttfile", [("refined_circuit.inc", "unknown_step_refined_tt.npz"),
+                                         ("stable_count_circuit.inc", "stable_count_tt.npz"),
+                                         ("stable_signal_circuit.inc", "stable_signal_tt.npz")])
+def test_generated_circuit_is_the_table(inc, ttfile):
+    """A generated bitop3 network (lifeapi_amd/csrc/*.inc), simulated on every
+    input combination, is exactly the reference fragment's truth table."""
     import re
-    tt = load("unknown_step_refined_tt.npz")["tt"].astype(bool)
-    src = open(os.path.join(os.path.dirname(GOLD), "..", "lifeapi_amd", "csrc",
-                            "refined_circuit.inc")).read()
-    idx = np.arange(1 << 16, dtype=np.uint32)
-    val = {f"x[{i}]": ((idx >> i) & 1).astype(bool) for i in range(16)}
+    d = load(ttfile)
+    tt = d["tt"].astype(bool)
+    nin = tt.shape[1].bit_length() - 1
+    src = open(os.path.join(os.path.dirname(GOLD), "..", "lifeapi_amd", "csrc", inc)).read()
+    idx = np.arange(1 << nin, dtype=np.uint32)
+    val = {f"x[{i}]": ((idx >> i) & 1).astype(bool) for i in range(nin)}
     A, B, C = 0xF0, 0xCC, 0xAA
     for tab, a, b, c, name in [(int(m[1], 16), m[2], m[3], m[4], m[0]) for m in
                                re.findall(r"const T (t\d+) = lut3<0x([0-9A-F]{2})>\(([^,]+), ([^,]+), ([^)]+)\);", src)]:
         va, vb, vc = val[a], val[b], val[c]
-        out = np.zeros(1 << 16, bool)
+        out = np.zeros(1 << nin, bool)
         for bit in range(8):
             if (tab >> bit) & 1:
                 out |= (va == bool((A >> bit) & 1)) & (vb == bool((B >> bit) & 1)) & (vc == bool((C >> bit) & 1))
         val[name] = out
     outs = []
-    for nm in ("next_on", "next_unknown", "next_unknown_stable"):
-        m = re.search(rf"{nm} = (~(t\d+)|(t\d+|x\[\d+\]));", src)
+    for nm in (str(s) for s in d["outputs"]):
+        m = re.search(rf"\b{nm} = (~(t\d+)|(t\d+|x\[\d+\]));", src)
         outs.append(~val[m[2]] if m[2] else val[m[3]])
     assert (np.stack(outs) == tt).all()
+
+
+def test_stable_passes_golden(port):
+    """LifeStable passes (LifeStable.hpp:526-729) vs the reference-generated
+    fixture: every plane and the PropagateResult flags, all five passes."""
+    g = load("stable.npz")
+    for w, name in enumerate(port.STABLE_PASSES):
+        out, fl = port.stable_pass(g["input"], w)
+        assert (out == g[name]).all(), name
+        assert (fl == g[name + "_flags"]).all(), name
+    assert (g["propagate_flags"] & 1).sum() >= 5  # some candidates stay consistent
 
 
 # ---- live reference (present where oracle/_ref was built) ----
