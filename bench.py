@@ -32,7 +32,6 @@ from lifeapi_amd.shard import gather_hashes, weak_shard  # noqa: E402
 
 METRIC = "64x64 universe-generations/sec (+ cell-updates/sec) at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
-VALU_PEAK_TOPS = 39.3216    # 256 CU x 64 lanes x 2.4 GHz int32 ops (1 op/lane/clk)
 BYTES_PER_UNIVERSE_GEN = 1024  # 512 B read + 512 B write
 OPS_PER_UNIVERSE_GEN = 2688    # reference's ~21 u64 ops/column = 42 int32 x 64
 
@@ -128,12 +127,18 @@ def secondary_config3(hip, device, stream):
         ms.append(e0.elapsed_time(e1))
     t = min(ms) / 1e3
     gps = n * gens / t
+    # VALU issue model of the generation loop (build/asm): 28
+    # full-rate VALU + 4 DPP moves, a DPP move taking two issue slots
+    # (tools/valu_probe.hip) = 36 slots per universe-generation per wave.
+    slots = 36
+    peak_slots = 1024 * 2.4e9 / 2  # 1024 SIMDs, one wave64 VALU op per 2 clk at 2.4 GHz
     return {"workload": "config3: 64K universes x 1024 generations (one launch)",
             "value": gps, "unit": "universe-gen/s", "cell_updates_per_s": gps * 4096,
             "kernel_ms": min(ms), "kernel_ms_all": ms,
-            "roofline": {"bound": "valu", "achieved": OPS_PER_UNIVERSE_GEN * gps / 1e12,
-                         "peak": VALU_PEAK_TOPS, "unit": "Tops/s (reference-algorithm int32 ops)",
-                         "frac": OPS_PER_UNIVERSE_GEN * gps / 1e12 / VALU_PEAK_TOPS}}
+            "roofline": {"bound": "valu", "achieved": gps * slots / 1e12, "peak": peak_slots / 1e12,
+                         "unit": "T VALU issue slots/s (36 per universe-gen)",
+                         "frac": gps * slots / peak_slots},
+            "reference_op_equivalent_Tops": OPS_PER_UNIVERSE_GEN * gps / 1e12}
 
 
 def verify_first_launch(hip, out, first, n, gens, seed, stream, world, device):
