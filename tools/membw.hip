@@ -1,8 +1,12 @@
 // membw.hip -- HBM streaming ceilings for the access shapes the step kernel
 // can use (measurement tool, not product code).  Copies 2^20 universes (512
 // MiB in + 512 MiB out) with wave-contiguous 512-B (dwordx2) or 1-KiB
-// (dwordx4) accesses, U loads in flight per lane, plain or nontemporal, for
-// several grid sizes, and prints one JSON line per variant.
+// (dwordx4) accesses, U loads in flight per lane, plain or nontemporal loads
+// and stores, for several grid sizes; plus read-only and write-only streams
+// of the same 512 MiB.  Prints one JSON line per variant.
+//   membw         the full sweep
+//   membw calib   only the step kernel's shape (dwordx2, U=4, nt, one-shot
+//                 grid): the byte-counter calibration run for rocprofv3
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -24,35 +28,47 @@ typedef unsigned long long u64;
 typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 
-template <class T, int U, bool NT>
+// MODE bit 0: nontemporal loads, bit 1: nontemporal stores,
+//      bit 2: read only (xor-reduce, one store per wave), bit 3: write only
+template <class T, int U, int MODE>
 __global__ __launch_bounds__(256) void k_copy(const T *__restrict__ in, T *__restrict__ out,
                                               u64 nvec) {
   // a "row" = 64 lanes x sizeof(T); waves take U rows at a time, grid-strided
   const int lane = threadIdx.x & 63;
   const u64 wave = (u64)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const u64 rows = nvec / 64, stride = (u64)gridDim.x * 4 * U;
+  T acc = T(0);
   for (u64 r0 = wave * U; r0 < rows; r0 += stride) {
     T v[U];
 #pragma unroll
-    for (int k = 0; k < U; ++k)
-      if (r0 + k < rows) v[k] = NT ? __builtin_nontemporal_load(in + (r0 + k) * 64 + lane)
-                                   : in[(r0 + k) * 64 + lane];
+    for (int k = 0; k < U; ++k) {
+      if (MODE & 8) v[k] = T((unsigned)(r0 + k));
+      else if (r0 + k < rows)
+        v[k] = (MODE & 1) ? __builtin_nontemporal_load(in + (r0 + k) * 64 + lane) : in[(r0 + k) * 64 + lane];
+    }
+    if constexpr ((MODE & 4) != 0) {
 #pragma unroll
-    for (int k = 0; k < U; ++k)
-      if (r0 + k < rows) {
-        if (NT) __builtin_nontemporal_store(v[k], out + (r0 + k) * 64 + lane);
-        else out[(r0 + k) * 64 + lane] = v[k];
-      }
+      for (int k = 0; k < U; ++k) acc ^= v[k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < U; ++k)
+        if (r0 + k < rows) {
+          if (MODE & 2) __builtin_nontemporal_store(v[k], out + (r0 + k) * 64 + lane);
+          else out[(r0 + k) * 64 + lane] = v[k];
+        }
+    }
   }
+  if constexpr ((MODE & 4) != 0) out[wave * 64 + lane] = acc;  // keep the loads live
 }
 
-static bool g_calib = false;  // `membw calib`: only the step kernel's access shape
+static bool g_calib = false;
 
-template <class T, int U, bool NT>
+template <class T, int U, int MODE>
 int run(const char *name, void *a, void *b, size_t bytes, int cus) {
   const u64 nvec = bytes / sizeof(T);
   const u64 rows = nvec / 64;
-  for (int bpc : {2, 4, 8, 16, 32, 0}) {
+  const double moved = (MODE & 12) ? (double)bytes : 2.0 * bytes;
+  for (int bpc : {4, 16, 0}) {
     if (g_calib && bpc != 0) continue;
     u64 blocks = (rows / U + 3) / 4;
     if (bpc) blocks = std::min<u64>(blocks, (u64)cus * bpc);
@@ -62,7 +78,7 @@ int run(const char *name, void *a, void *b, size_t bytes, int cus) {
     std::vector<float> ms;
     for (int rep = 0; rep < 25; ++rep) {
       CHECK(hipEventRecord(e0, 0));
-      hipLaunchKernelGGL((k_copy<T, U, NT>), dim3(blocks), dim3(256), 0, 0, (const T *)a, (T *)b, nvec);
+      hipLaunchKernelGGL((k_copy<T, U, MODE>), dim3(blocks), dim3(256), 0, 0, (const T *)a, (T *)b, nvec);
       CHECK(hipEventRecord(e1, 0));
       CHECK(hipEventSynchronize(e1));
       float t;
@@ -70,11 +86,10 @@ int run(const char *name, void *a, void *b, size_t bytes, int cus) {
       if (rep >= 5) ms.push_back(t);
     }
     std::sort(ms.begin(), ms.end());
-    const double gbs_best = 2.0 * bytes / (ms.front() * 1e-3) / 1e9;
-    const double gbs_med = 2.0 * bytes / (ms[ms.size() / 2] * 1e-3) / 1e9;
-    std::printf("{\"variant\": \"%s\", \"U\": %d, \"nt\": %d, \"blocks_per_cu\": %d, \"blocks\": %llu, "
+    std::printf("{\"variant\": \"%s\", \"U\": %d, \"mode\": %d, \"blocks_per_cu\": %d, \"blocks\": %llu, "
                 "\"ms_best\": %.4f, \"ms_median\": %.4f, \"GBps_best\": %.1f, \"GBps_median\": %.1f}\n",
-                name, U, (int)NT, bpc, blocks, ms.front(), ms[ms.size() / 2], gbs_best, gbs_med);
+                name, U, MODE, bpc, blocks, ms.front(), ms[ms.size() / 2], moved / (ms.front() * 1e-3) / 1e9,
+                moved / (ms[ms.size() / 2] * 1e-3) / 1e9);
     CHECK(hipEventDestroy(e0));
     CHECK(hipEventDestroy(e1));
   }
@@ -92,17 +107,20 @@ int main(int argc, char **argv) {
   hipDeviceProp_t p;
   CHECK(hipGetDeviceProperties(&p, 0));
   const int cus = p.multiProcessorCount;
+  if (g_calib) return run<u32x2, 4, 3>("dwordx2", a, b, bytes, cus);
   int rc = 0;
-  if (g_calib) return run<u32x2, 4, true>("dwordx2", a, b, bytes, cus);
-  rc |= run<u32x2, 1, false>("dwordx2", a, b, bytes, cus);
-  rc |= run<u32x2, 4, false>("dwordx2", a, b, bytes, cus);
-  rc |= run<u32x2, 4, true>("dwordx2", a, b, bytes, cus);
-  rc |= run<u32x2, 8, true>("dwordx2", a, b, bytes, cus);
-  rc |= run<u32x2, 8, false>("dwordx2", a, b, bytes, cus);
-  rc |= run<u32x4, 1, false>("dwordx4", a, b, bytes, cus);
-  rc |= run<u32x4, 2, false>("dwordx4", a, b, bytes, cus);
-  rc |= run<u32x4, 2, true>("dwordx4", a, b, bytes, cus);
-  rc |= run<u32x4, 4, true>("dwordx4", a, b, bytes, cus);
-  rc |= run<u32x4, 4, false>("dwordx4", a, b, bytes, cus);
+  rc |= run<u32x2, 4, 0>("dwordx2", a, b, bytes, cus);
+  rc |= run<u32x2, 4, 1>("dwordx2", a, b, bytes, cus);
+  rc |= run<u32x2, 4, 2>("dwordx2", a, b, bytes, cus);
+  rc |= run<u32x2, 4, 3>("dwordx2", a, b, bytes, cus);
+  rc |= run<u32x2, 8, 3>("dwordx2", a, b, bytes, cus);
+  rc |= run<u32x2, 16, 3>("dwordx2", a, b, bytes, cus);
+  rc |= run<u32x4, 2, 3>("dwordx4", a, b, bytes, cus);
+  rc |= run<u32x4, 4, 3>("dwordx4", a, b, bytes, cus);
+  rc |= run<u32x4, 8, 3>("dwordx4", a, b, bytes, cus);
+  rc |= run<u32x2, 4, 5>("dwordx2-readonly", a, b, bytes, cus);
+  rc |= run<u32x4, 4, 5>("dwordx4-readonly", a, b, bytes, cus);
+  rc |= run<u32x2, 4, 10>("dwordx2-writeonly", a, b, bytes, cus);
+  rc |= run<u32x4, 4, 10>("dwordx4-writeonly", a, b, bytes, cus);
   return rc;
 }

@@ -42,8 +42,26 @@ __device__ __forceinline__ uint32_t xr(uint32_t v) {
   else if constexpr (V == 2) return v ^ 0x7654321u;
   else return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x134, 0xF, 0xF, true);
 }
+__device__ __forceinline__ W rup(W a) {
+  return W{__builtin_amdgcn_alignbit(a.lo, a.hi, 31), __builtin_amdgcn_alignbit(a.hi, a.lo, 31)};
+}
+__device__ __forceinline__ W rdn(W a) {
+  return W{__builtin_amdgcn_alignbit(a.hi, a.lo, 1), __builtin_amdgcn_alignbit(a.lo, a.hi, 1)};
+}
+
 template <int V>
 __device__ __forceinline__ W gen(W a) {
+  if constexpr (V >= 3) {  // row-first (the product's default rule): 4 DPP
+    const W L{xl<0>(a.lo), xl<0>(a.hi)}, R{xr<0>(a.lo), xr<0>(a.hi)};
+    const W h0 = l3<0x96>(L, a, R), h1 = l3<0xE8>(L, a, R);
+    const W h0u = rup(h0), h0d = rdn(h0), h1u = rup(h1), h1d = rdn(h1);
+    const W fs = l3<0x96>(h0u, h0, h0d), fc = l3<0xE8>(h0u, h0, h0d);
+    const W cs = l3<0x96>(h1u, h1, h1d), cc = l3<0xE8>(h1u, h1, h1d);
+    const W b2 = l3<0x78>(cc, fc, cs);
+    const W p = l3<0x38>(fs, b2, a);
+    const W q = l3<0x96>(fc, cs, b2);
+    return W{p.lo & q.lo, p.hi & q.hi};
+  }
   const W up{__builtin_amdgcn_alignbit(a.lo, a.hi, 31), __builtin_amdgcn_alignbit(a.hi, a.lo, 31)};
   const W dn{__builtin_amdgcn_alignbit(a.hi, a.lo, 1), __builtin_amdgcn_alignbit(a.lo, a.hi, 1)};
   const W c0 = l3<0x96>(up, dn, a), c1 = l3<0xE8>(up, dn, a);
@@ -74,9 +92,19 @@ __global__ __launch_bounds__(256) void k_iter(const uint64_t *in, uint64_t *out,
     t0 = __builtin_amdgcn_s_memtime();
     r0 = __builtin_amdgcn_s_memrealtime();
   }
-  for (uint32_t g = 0; g < gens; ++g)
+  if constexpr (V == 4) {  // row-first, generation loop unrolled x4
+    uint32_t g = 0;
+    for (; g + 4 <= gens; g += 4)
 #pragma unroll
-    for (int k = 0; k < U; ++k) a[k] = gen<V>(a[k]);
+      for (int k = 0; k < U; ++k) a[k] = gen<V>(gen<V>(gen<V>(gen<V>(a[k]))));
+    for (; g < gens; ++g)
+#pragma unroll
+      for (int k = 0; k < U; ++k) a[k] = gen<V>(a[k]);
+  } else {
+    for (uint32_t g = 0; g < gens; ++g)
+#pragma unroll
+      for (int k = 0; k < U; ++k) a[k] = gen<V>(a[k]);
+  }
   if (STAMP && lane == 0 && (threadIdx.x >> 6) == 0) {
     const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
     clk[2 * blockIdx.x] = t1 - t0;
@@ -130,6 +158,10 @@ int main() {
   CHECK(hipMemset(a, 0x6b, n * 512));
   int rc = 0;
   for (int rep = 0; rep < 2; ++rep) {
+    rc |= run<3, 1, false>("rowfirst", a, b, n, gens, clk);
+    rc |= run<4, 1, false>("rowfirst_unroll4", a, b, n, gens, clk);
+    rc |= run<3, 2, false>("rowfirst", a, b, n, gens, clk);
+    rc |= run<4, 2, false>("rowfirst_unroll4", a, b, n, gens, clk);
     rc |= run<0, 1, false>("dpp_wave", a, b, n, gens, clk);
     rc |= run<1, 1, false>("dpp_row", a, b, n, gens, clk);
     rc |= run<2, 1, false>("no_xlane", a, b, n, gens, clk);
