@@ -224,6 +224,65 @@ inline bool LifeState::Contains(const LifeTarget &t) const {
   return d == 0;
 }
 
+// NeighbourCount.hpp:7-102 (hot-path subset): inclusive 3x3 count 0..9 as
+// four bit planes, same member order as the reference.
+struct NeighbourCount {
+  LifeState bit3, bit2, bit1, bit0;
+
+  NeighbourCount() = default;
+  explicit NeighbourCount(const LifeState &s) {
+    LifeState c0(InitializedTag::UNINITIALIZED), c1(InitializedTag::UNINITIALIZED);
+    s.CountRows(c0, c1);
+    for (int i = 0; i < N; ++i) {
+      const int u = (i + N - 1) & (N - 1), d = (i + 1) & (N - 1);
+      uint64_t fs, fc, cs, cc;
+      LifeState::FullAdd(fs, fc, c0[u], c0[i], c0[d]);
+      LifeState::FullAdd(cs, cc, c1[u], c1[i], c1[d]);
+      bit0[i] = fs;
+      bit1[i] = fc ^ cs;
+      bit2[i] = cc ^ (fc & cs);
+      bit3[i] = cc & fc & cs;
+    }
+  }
+  LifeState WithExactly(unsigned n) const {
+    LifeState r = ~LifeState();
+    r &= (n & 1) ? bit0 : ~bit0;
+    r &= (n & 2) ? bit1 : ~bit1;
+    r &= (n & 4) ? bit2 : ~bit2;
+    r &= (n & 8) ? bit3 : ~bit3;
+    return r;
+  }
+};
+
+// LifeWeld.hpp:18-186 (hot-path subset): a state plus a frozen 3-bit
+// neighbour count added when stepping.
+struct LifeWeld {
+  LifeState state, frozen2, frozen1, frozen0;
+
+  bool operator==(const LifeWeld &o) const {
+    return state == o.state && frozen2 == o.frozen2 && frozen1 == o.frozen1 && frozen0 == o.frozen0;
+  }
+  void Step() {  // LifeWeld.hpp:169-186
+    const NeighbourCount c(state);
+    for (int i = 0; i < N; ++i) {
+      uint64_t s0, k0, s1, k1, s2, k2;
+      LifeState::HalfAdd(s0, k0, c.bit0[i], frozen0[i]);
+      LifeState::FullAdd(s1, k1, c.bit1[i], frozen1[i], k0);
+      LifeState::FullAdd(s2, k2, c.bit2[i], frozen2[i], k1);
+      state[i] = (s0 ^ s2) & (s1 ^ s2) & (state[i] | s0);
+    }
+  }
+};
+
+// LifeStable.hpp:41-53: the ten planes of the stable-search state (options
+// stored as "1 = ruled out").  Propagation runs on the GPU:
+// lifeapi::PropagateStepBatch / PropagateBatch in lifeapi/batch.hpp.
+struct LifeStable {
+  LifeState state, unknown;
+  LifeState live2, live3;
+  LifeState dead0, dead1, dead2, dead4, dead5, dead6;
+};
+
 }  // namespace lifeapi
 
 #include "batch.hpp"

@@ -65,6 +65,71 @@ std::vector<uint32_t> GetPopBatch(std::span<const S> states, int device = 0) {
   return pops;
 }
 
+// ---- the other per-generation kernels, on the reference's own types ----
+//
+// Each concept pins the reference struct's byte layout: N LifeStates in
+// member order, nothing else.
+template <class T, size_t Planes>
+concept PlaneLayout = sizeof(T) == Planes * 64 * sizeof(uint64_t) && std::is_trivially_copyable_v<T> &&
+                      std::is_standard_layout_v<T>;
+// LifeWeld {state, frozen2, frozen1, frozen0}           LifeWeld.hpp:18-20
+template <class T> concept LifeWeldLayout = PlaneLayout<T, 4>;
+// LifeStable {state, unknown, live2 .. dead6}            LifeStable.hpp:41-53
+template <class T> concept LifeStableLayout = PlaneLayout<T, 10>;
+// NeighbourCount {bit3, bit2, bit1, bit0}                NeighbourCount.hpp:7-11
+template <class T> concept NeighbourCountLayout = PlaneLayout<T, 4>;
+// LifeTarget {wanted, unwanted}                          LifeTarget.hpp:5-7
+template <class T> concept LifeTargetLayout = PlaneLayout<T, 2>;
+
+// welds[i].Step() `generations` times (LifeWeld.hpp:169-186)
+template <LifeWeldLayout W>
+void WeldStepBatch(std::span<W> welds, unsigned generations = 1, int device = 0) {
+  check(lifeapi_weld_step_batch(words(welds.data()), welds.size(), generations, device));
+}
+
+// LifeStable::PropagateResult (LifeStable.hpp:123-126)
+struct PropagateResult {
+  bool consistent;
+  bool changed;
+};
+
+namespace detail {
+template <LifeStableLayout S>
+std::vector<PropagateResult> stable_pass(std::span<S> s, int pass, unsigned max_iters, int device) {
+  std::vector<uint8_t> f(s.size());
+  check(lifeapi_stable_pass_batch(words(s.data()), f.data(), s.size(), pass, max_iters, device));
+  std::vector<PropagateResult> r(s.size());
+  for (size_t i = 0; i < s.size(); ++i) r[i] = {(f[i] & 1) != 0, (f[i] & 2) != 0};
+  return r;
+}
+}  // namespace detail
+
+// s[i].PropagateStep() / s[i].Propagate() (LifeStable.hpp:695-729), in place
+template <LifeStableLayout S>
+std::vector<PropagateResult> PropagateStepBatch(std::span<S> s, int device = 0) {
+  return detail::stable_pass(s, 3, 0, device);
+}
+template <LifeStableLayout S>
+std::vector<PropagateResult> PropagateBatch(std::span<S> s, int device = 0) {
+  return detail::stable_pass(s, 4, 0, device);
+}
+
+// out[i] = NeighbourCount(in[i])  (NeighbourCount.hpp:40-70)
+template <LifeStateLayout S, NeighbourCountLayout C>
+void NeighbourCountBatch(std::span<const S> in, std::span<C> out, int device = 0) {
+  if (out.size() != in.size()) throw Error(LIFEAPI_E_INVALID, "lifeapi: size mismatch");
+  check(lifeapi_neighbour_count_batch(words(in.data()), words(out.data()), in.size(), device));
+}
+
+// r[i] = in[i].Contains(target)  (LifeTarget.hpp:44-51)
+template <LifeStateLayout S, LifeTargetLayout T>
+std::vector<uint8_t> ContainsBatch(std::span<const S> in, const T &target, int device = 0) {
+  std::vector<uint8_t> r(in.size());
+  const uint64_t *t = words(&target);
+  check(lifeapi_contains_batch(words(in.data()), t, t + 64, r.data(), in.size(), device));
+  return r;
+}
+
 inline int DeviceCount() { return lifeapi_device_count(); }
 
 }  // namespace lifeapi

@@ -148,6 +148,17 @@ int lifeapi_fill_random_dev(uint64_t *d_out, size_t n, uint64_t seed,
 int lifeapi_step_batch(const uint64_t *in, uint64_t *out, size_t n, uint32_t generations,
                        int device);
 int lifeapi_pop_batch(const uint64_t *states, uint32_t *pop, size_t n, int device);
+/* host-pointer forms of the *_dev entry points above (same layouts); each
+ * stages through `device` (-1 = device 0) in chunks of <= 1 GiB          */
+int lifeapi_weld_step_batch(uint64_t *welds, size_t n, uint32_t generations, int device);
+int lifeapi_stable_pass_batch(uint64_t *planes, uint8_t *flags, size_t n, int pass,
+                              uint32_t max_iters, int device);
+int lifeapi_neighbour_count_batch(const uint64_t *in, uint64_t *out, size_t n, int device);
+int lifeapi_interaction_counts_batch(const uint64_t *in, uint64_t *out, size_t n, int with_next,
+                                     int device);
+int lifeapi_refined_step_batch(const uint64_t *in, uint64_t *out, size_t n, int device);
+int lifeapi_contains_batch(const uint64_t *states, const uint64_t *wanted, const uint64_t *unwanted,
+                           uint8_t *out, size_t n, int device);
 
 #ifdef __cplusplus
 }

@@ -791,8 +791,8 @@ int launched(const char *what) {
 struct HostCtx {
   std::mutex mu;
   hipStream_t stream = nullptr;
-  uint64_t *buf = nullptr;
-  size_t cap = 0;  // universes
+  char *buf = nullptr;
+  size_t cap = 0;  // bytes
 };
 std::mutex g_ctx_mu;
 std::vector<HostCtx *> g_ctx;
@@ -812,9 +812,21 @@ struct DeviceGuard {
   }
 };
 
-constexpr size_t kChunk = size_t(1) << 21;  // 2M universes = 1 GiB per staging pass
+constexpr size_t kStagingBytes = size_t(1) << 30;  // device staging per pass (1 GiB)
 
-int host_step_one_device(const uint64_t *in, uint64_t *out, size_t n, uint32_t gens, int dev) {
+// One host array taking part in a host-pointer call: `bytes` per universe;
+// src -> copied in before each chunk's launch, dst -> copied out after it
+// (src == dst for in-place arrays).
+struct HostIO {
+  const void *src;
+  void *dst;
+  size_t bytes;
+};
+using ChunkFn = int (*)(void *const *dev, size_t m, hipStream_t s, const void *arg);
+
+// Stages n universes through this device's reusable buffer in chunks of at
+// most kStagingBytes: H2D, the stream-ordered *_dev entry point, D2H, sync.
+int host_chunked(int dev, size_t n, const HostIO *io, int nio, ChunkFn fn, const void *arg) {
   DeviceGuard guard;
   hipError_t e = hipSetDevice(dev);
   if (e != hipSuccess) return fail_hip(e, "hipSetDevice");
@@ -824,27 +836,62 @@ int host_step_one_device(const uint64_t *in, uint64_t *out, size_t n, uint32_t g
     e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) return fail_hip(e, "hipStreamCreate");
   }
-  const size_t want = std::min(n, kChunk);
-  if (c->cap < want) {
+  size_t per = 0;
+  for (int k = 0; k < nio; ++k) per += (io[k].bytes + 255) & ~size_t(255);
+  const size_t chunk = std::max<size_t>(1, std::min(n, kStagingBytes / per));
+  size_t need = 0;
+  for (int k = 0; k < nio; ++k) need += ((io[k].bytes * chunk + 255) & ~size_t(255));
+  if (c->cap < need) {
     if (c->buf) (void)hipFree(c->buf);
     c->buf = nullptr;
     c->cap = 0;
-    e = hipMalloc(&c->buf, want * 512);
+    e = hipMalloc(&c->buf, need);
     if (e != hipSuccess) return fail_hip(e, "hipMalloc(staging)");
-    c->cap = want;
+    c->cap = need;
   }
-  for (size_t off = 0; off < n; off += kChunk) {
-    const size_t m = std::min(kChunk, n - off);
-    e = hipMemcpyAsync(c->buf, in + off * 64, m * 512, hipMemcpyHostToDevice, c->stream);
-    if (e != hipSuccess) return fail_hip(e, "hipMemcpyAsync(H2D)");
-    int rc = lifeapi_step_batch_dev(c->buf, c->buf, m, gens, c->stream);
+  void *d[8];
+  for (size_t off = 0; off < n; off += chunk) {
+    const size_t m = std::min(chunk, n - off);
+    size_t pos = 0;
+    for (int k = 0; k < nio; ++k) {
+      d[k] = c->buf + pos;
+      pos += (io[k].bytes * chunk + 255) & ~size_t(255);
+      if (io[k].src) {
+        e = hipMemcpyAsync(d[k], (const char *)io[k].src + off * io[k].bytes, m * io[k].bytes,
+                           hipMemcpyHostToDevice, c->stream);
+        if (e != hipSuccess) return fail_hip(e, "hipMemcpyAsync(H2D)");
+      }
+    }
+    const int rc = fn(d, m, c->stream, arg);
     if (rc != LIFEAPI_OK) return rc;
-    e = hipMemcpyAsync(out + off * 64, c->buf, m * 512, hipMemcpyDeviceToHost, c->stream);
-    if (e != hipSuccess) return fail_hip(e, "hipMemcpyAsync(D2H)");
+    for (int k = 0; k < nio; ++k)
+      if (io[k].dst) {
+        e = hipMemcpyAsync((char *)io[k].dst + off * io[k].bytes, d[k], m * io[k].bytes,
+                           hipMemcpyDeviceToHost, c->stream);
+        if (e != hipSuccess) return fail_hip(e, "hipMemcpyAsync(D2H)");
+      }
     e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) return fail_hip(e, "hipStreamSynchronize");
   }
   return LIFEAPI_OK;
+}
+
+int host_device(int device) {
+  const int ndev = lifeapi_device_count();
+  if (ndev <= 0) return fail(LIFEAPI_E_NODEVICE, "no HIP device visible%s");
+  if (device < 0) device = 0;
+  if (device >= ndev) return fail(LIFEAPI_E_NODEVICE, "bad device index%s");
+  return device;
+}
+
+int host_step_one_device(const uint64_t *in, uint64_t *out, size_t n, uint32_t gens, int dev) {
+  const HostIO io[1] = {{in, out, 512}};
+  return host_chunked(dev, n, io, 1,
+                      [](void *const *d, size_t m, hipStream_t s, const void *arg) {
+                        return lifeapi_step_batch_dev((const uint64_t *)d[0], (uint64_t *)d[0], m,
+                                                      *(const uint32_t *)arg, s);
+                      },
+                      &gens);
 }
 
 }  // namespace
@@ -1095,27 +1142,119 @@ int lifeapi_step_batch(const uint64_t *in, uint64_t *out, size_t n, uint32_t gen
 int lifeapi_pop_batch(const uint64_t *states, uint32_t *pop, size_t n, int device) {
   if (n == 0) return LIFEAPI_OK;
   if (!states || !pop || !aligned8(states)) return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_pop_batch%s");
-  const int ndev = lifeapi_device_count();
-  if (ndev <= 0) return fail(LIFEAPI_E_NODEVICE, "no HIP device visible%s");
-  if (device < 0) device = 0;
-  if (device >= ndev) return fail(LIFEAPI_E_NODEVICE, "bad device index%s");
+  const int dev = host_device(device);
+  if (dev < 0) return dev;
+  const HostIO io[2] = {{states, nullptr, 512}, {nullptr, pop, 4}};
+  return host_chunked(dev, n, io, 2,
+                      [](void *const *d, size_t m, hipStream_t s, const void *) {
+                        return lifeapi_pop_batch_dev((const uint64_t *)d[0], (uint32_t *)d[1], m, s);
+                      },
+                      nullptr);
+}
+
+int lifeapi_weld_step_batch(uint64_t *welds, size_t n, uint32_t generations, int device) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!welds || !aligned8(welds)) return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_weld_step_batch%s");
+  const int dev = host_device(device);
+  if (dev < 0) return dev;
+  const HostIO io[1] = {{welds, welds, 4 * 512}};
+  return host_chunked(dev, n, io, 1,
+                      [](void *const *d, size_t m, hipStream_t s, const void *arg) {
+                        return lifeapi_weld_step_batch_dev((uint64_t *)d[0], m, *(const uint32_t *)arg, s);
+                      },
+                      &generations);
+}
+
+int lifeapi_stable_pass_batch(uint64_t *planes, uint8_t *flags, size_t n, int pass,
+                              uint32_t max_iters, int device) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!planes || !flags || !aligned8(planes) || pass < 0 || pass > 4)
+    return fail(LIFEAPI_E_INVALID, "bad argument to lifeapi_stable_pass_batch%s");
+  const int dev = host_device(device);
+  if (dev < 0) return dev;
+  const uint32_t arg[2] = {(uint32_t)pass, max_iters};
+  const HostIO io[2] = {{planes, planes, 10 * 512}, {nullptr, flags, 1}};
+  return host_chunked(dev, n, io, 2,
+                      [](void *const *d, size_t m, hipStream_t s, const void *a) {
+                        const uint32_t *p = (const uint32_t *)a;
+                        return lifeapi_stable_pass_batch_dev((uint64_t *)d[0], (uint8_t *)d[1], m,
+                                                             (int)p[0], p[1], s);
+                      },
+                      arg);
+}
+
+int lifeapi_neighbour_count_batch(const uint64_t *in, uint64_t *out, size_t n, int device) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!in || !out || !aligned8(in) || !aligned8(out))
+    return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_neighbour_count_batch%s");
+  const int dev = host_device(device);
+  if (dev < 0) return dev;
+  const HostIO io[2] = {{in, nullptr, 512}, {nullptr, out, 4 * 512}};
+  return host_chunked(dev, n, io, 2,
+                      [](void *const *d, size_t m, hipStream_t s, const void *) {
+                        return lifeapi_neighbour_count_batch_dev((const uint64_t *)d[0], (uint64_t *)d[1], m, s);
+                      },
+                      nullptr);
+}
+
+int lifeapi_interaction_counts_batch(const uint64_t *in, uint64_t *out, size_t n, int with_next,
+                                     int device) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!in || !out || !aligned8(in) || !aligned8(out))
+    return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_interaction_counts_batch%s");
+  const int dev = host_device(device);
+  if (dev < 0) return dev;
+  const HostIO io[2] = {{in, nullptr, 512}, {nullptr, out, (with_next ? 4u : 3u) * 512}};
+  return host_chunked(dev, n, io, 2,
+                      [](void *const *d, size_t m, hipStream_t s, const void *a) {
+                        return lifeapi_interaction_counts_batch_dev((const uint64_t *)d[0], (uint64_t *)d[1],
+                                                                    m, *(const int *)a, s);
+                      },
+                      &with_next);
+}
+
+int lifeapi_refined_step_batch(const uint64_t *in, uint64_t *out, size_t n, int device) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!in || !out || !aligned8(in) || !aligned8(out))
+    return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_refined_step_batch%s");
+  const int dev = host_device(device);
+  if (dev < 0) return dev;
+  const HostIO io[2] = {{in, nullptr, 11 * 512}, {nullptr, out, 3 * 512}};
+  return host_chunked(dev, n, io, 2,
+                      [](void *const *d, size_t m, hipStream_t s, const void *) {
+                        return lifeapi_refined_step_batch_dev((const uint64_t *)d[0], (uint64_t *)d[1], m, s);
+                      },
+                      nullptr);
+}
+
+int lifeapi_contains_batch(const uint64_t *states, const uint64_t *wanted, const uint64_t *unwanted,
+                           uint8_t *out, size_t n, int device) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!states || !wanted || !unwanted || !out || !aligned8(states))
+    return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_contains_batch%s");
+  const int dev = host_device(device);
+  if (dev < 0) return dev;
+  // the target rides along as a tiny device copy owned by this call
   DeviceGuard guard;
-  hipError_t e = hipSetDevice(device);
+  hipError_t e = hipSetDevice(dev);
   if (e != hipSuccess) return fail_hip(e, "hipSetDevice");
-  uint64_t *ds = nullptr;
-  uint32_t *dp = nullptr;
-  if ((e = hipMalloc(&ds, n * 512)) != hipSuccess) return fail_hip(e, "hipMalloc");
-  if ((e = hipMalloc(&dp, n * 4)) != hipSuccess) {
-    (void)hipFree(ds);
-    return fail_hip(e, "hipMalloc");
-  }
+  uint64_t *dt = nullptr;
+  if ((e = hipMalloc(&dt, 2 * 512)) != hipSuccess) return fail_hip(e, "hipMalloc(target)");
   int rc = LIFEAPI_OK;
-  if ((e = hipMemcpy(ds, states, n * 512, hipMemcpyHostToDevice)) != hipSuccess) rc = fail_hip(e, "hipMemcpy");
-  if (rc == LIFEAPI_OK) rc = lifeapi_pop_batch_dev(ds, dp, n, nullptr);
-  if (rc == LIFEAPI_OK && (e = hipMemcpy(pop, dp, n * 4, hipMemcpyDeviceToHost)) != hipSuccess)
-    rc = fail_hip(e, "hipMemcpy");
-  (void)hipFree(ds);
-  (void)hipFree(dp);
+  if ((e = hipMemcpy(dt, wanted, 512, hipMemcpyHostToDevice)) != hipSuccess ||
+      (e = hipMemcpy(dt + 64, unwanted, 512, hipMemcpyHostToDevice)) != hipSuccess)
+    rc = fail_hip(e, "hipMemcpy(target)");
+  if (rc == LIFEAPI_OK) {
+    const HostIO io[2] = {{states, nullptr, 512}, {nullptr, out, 1}};
+    rc = host_chunked(dev, n, io, 2,
+                      [](void *const *d, size_t m, hipStream_t s, const void *a) {
+                        const uint64_t *t = (const uint64_t *)a;
+                        return lifeapi_contains_batch_dev((const uint64_t *)d[0], t, t + 64,
+                                                          (uint8_t *)d[1], m, s);
+                      },
+                      dt);
+  }
+  (void)hipFree(dt);
   return rc;
 }
 

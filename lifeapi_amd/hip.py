@@ -68,6 +68,12 @@ _SIGS = {
     "lifeapi_refined_step_batch_dev_cfg": ([_vp, _vp, _sz, _vp, ctypes.POINTER(LaunchCfg)], _int),
     "lifeapi_step_batch": ([_vp, _vp, _sz, _u32, _int], _int),
     "lifeapi_pop_batch": ([_vp, _vp, _sz, _int], _int),
+    "lifeapi_weld_step_batch": ([_vp, _sz, _u32, _int], _int),
+    "lifeapi_stable_pass_batch": ([_vp, _vp, _sz, _int, _u32, _int], _int),
+    "lifeapi_neighbour_count_batch": ([_vp, _vp, _sz, _int], _int),
+    "lifeapi_interaction_counts_batch": ([_vp, _vp, _sz, _int, _int], _int),
+    "lifeapi_refined_step_batch": ([_vp, _vp, _sz, _int], _int),
+    "lifeapi_contains_batch": ([_vp, _vp, _vp, _vp, _sz, _int], _int),
 }
 for _name, (_args, _res) in _SIGS.items():
     _f = getattr(lib, _name)

@@ -102,6 +102,65 @@ static void MultiDevice_Shards() {
   for (size_t i = 0; i < a.size(); ++i) EXPECT_EQ(a[i], b[i]);
 }
 
+// LifeWeldTest.StableTest (tests/LifeWeldTest.cpp:6-17), batched: a weld of a
+// still life with nothing frozen is invariant; random welds match the CPU
+static void LifeWeld_StableAndRandom() {
+  std::vector<lifeapi::LifeWeld> w(2);
+  w[0].state = LifeState::Parse("2b2o$bobo$bo$2o!");
+  w[1].state = LifeState::Parse("2o$2o!");
+  auto copy = w;
+  lifeapi::WeldStepBatch(std::span(w), 1);
+  EXPECT_TRUE(w[0] == copy[0] && w[1] == copy[1]);
+  uint64_t seed = 4242;
+  std::vector<lifeapi::LifeWeld> r(1001);
+  for (auto &x : r) {
+    x.state = LifeState::RandomState(seed);
+    x.frozen0 = LifeState::RandomState(seed) & LifeState::RandomState(seed);
+    x.frozen1 = LifeState::RandomState(seed) & LifeState::RandomState(seed) & LifeState::RandomState(seed);
+  }
+  auto cpu = r;
+  for (auto &x : cpu) {
+    x.Step();
+    x.Step();
+  }
+  lifeapi::WeldStepBatch(std::span(r), 2);
+  for (size_t i = 0; i < r.size(); ++i) EXPECT_TRUE(r[i] == cpu[i]);
+}
+
+// NeighbourCount / Contains batches vs the CPU facade
+static void Counts_And_Contains() {
+  uint64_t seed = 777;
+  std::vector<LifeState> s(513);
+  for (auto &x : s) x = LifeState::RandomState(seed);
+  std::vector<lifeapi::NeighbourCount> nc(s.size());
+  lifeapi::NeighbourCountBatch(std::span<const LifeState>(s), std::span(nc));
+  for (size_t i = 0; i < s.size(); i += 5) {
+    const lifeapi::NeighbourCount c(s[i]);
+    EXPECT_TRUE(nc[i].bit0 == c.bit0 && nc[i].bit1 == c.bit1 && nc[i].bit2 == c.bit2 && nc[i].bit3 == c.bit3);
+    // Life == WithExactly(3) | (s & WithExactly(4)) (the NeighbourCount rule)
+    EXPECT_EQ(c.WithExactly(3) | (s[i] & c.WithExactly(4)), s[i].Stepped());
+  }
+  lifeapi::LifeTarget t(s[3], ~s[3]);
+  auto hit = lifeapi::ContainsBatch(std::span<const LifeState>(s), t);
+  for (size_t i = 0; i < s.size(); ++i) EXPECT_EQ(hit[i] != 0, s[i].Contains(t));
+  EXPECT_TRUE(hit[3] != 0);
+}
+
+// LifeStable propagation: a block field with an unknown window stays
+// consistent and fills in; an inconsistent (unstable) known region is flagged
+static void Stable_Propagate() {
+  std::vector<lifeapi::LifeStable> st(2);
+  for (int k = 0; k < 4; ++k) {
+    st[0].state |= LifeState::Parse("2o$2o!");
+    for (auto &w : st[0].state.state) w = std::rotl(w, 16);
+  }
+  for (int x = 20; x < 30; ++x) st[0].unknown[x] = 0xFFFull << 20;
+  st[1].state = LifeState::Parse("3o!");  // a blinker is not still: inconsistent
+  auto r = lifeapi::PropagateBatch(std::span(st));
+  EXPECT_TRUE(r[0].consistent);
+  EXPECT_TRUE(!r[1].consistent);
+}
+
 // errors surface as lifeapi::Error (the reference has no failure path)
 static void Errors_Throw() {
   std::vector<LifeState> a(4);
@@ -121,6 +180,9 @@ int main() {
   Interaction_BatchMatchesCpu();
   Glider_Translation();
   MultiDevice_Shards();
+  LifeWeld_StableAndRandom();
+  Counts_And_Contains();
+  Stable_Propagate();
   Errors_Throw();
   std::printf("%d checks, %d failures\n", g_checks, g_failures);
   return g_failures == 0 ? 0 : 1;

@@ -170,6 +170,39 @@ def test_host_api(hip, port):
     assert (hip.pop_host(x) == port.pop(x)).all()
 
 
+def test_host_api_other_kernels(hip, port):
+    """Host-pointer forms of the weld / stable / counts / refined / contains
+    entry points (staged through device memory in chunks)."""
+    L = hip.lib
+    w = port.fill(300 * 4, seed=31).reshape(300, 256)
+    w[:, 64:] &= port.fill(900, seed=32).reshape(300, 192)
+    hw = w.copy()
+    hip._check(L.lifeapi_weld_step_batch(hw.ctypes.data, 300, 3, 0))
+    assert (hw == port.weld_step(w, 3)).all()
+    x = port.fill(200, seed=33)
+    nc = np.zeros((200, 4, 64), np.uint64)
+    hip._check(L.lifeapi_neighbour_count_batch(x.ctypes.data, nc.ctypes.data, 200, 0))
+    assert all((nc[u] == port.neighbour_count(x[u])).all() for u in range(200))
+    ic = np.zeros((200, 3, 64), np.uint64)
+    hip._check(L.lifeapi_interaction_counts_batch(x.ctypes.data, ic.ctypes.data, 200, 0, 0))
+    assert all((ic[u] == port.interaction_counts(x[u])[:3]).all() for u in range(200))
+    r = port.fill(50 * 11, seed=34).reshape(50, 704)
+    ro = np.zeros((50, 192), np.uint64)
+    hip._check(L.lifeapi_refined_step_batch(r.ctypes.data, ro.ctypes.data, 50, 0))
+    assert (ro == port.refined_step(r)).all()
+    want, unw = x[7].copy(), np.zeros(64, np.uint64)
+    hit = np.zeros(200, np.uint8)
+    hip._check(L.lifeapi_contains_batch(x.ctypes.data, want.ctypes.data, unw.ctypes.data,
+                                        hit.ctypes.data, 200, 0))
+    assert (hit.astype(bool) == [port.contains(x[u], want, unw) for u in range(200)]).all()
+    import os
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "stable.npz"))
+    sp = np.ascontiguousarray(g["input"]).copy()
+    fl = np.zeros(len(sp), np.uint8)
+    hip._check(L.lifeapi_stable_pass_batch(sp.ctypes.data, fl.ctypes.data, len(sp), 4, 0, 0))
+    assert (sp == g["propagate"]).all() and (fl == g["propagate_flags"]).all()
+
+
 def test_full_size_config2(hip, port):
     """Config 2 at full size (1M universes x 1 gen): every word vs the oracle."""
     n = 1 << 20
