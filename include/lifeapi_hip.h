@@ -55,6 +55,14 @@ extern "C" {
 #define LIFEAPI_XCHG_DPP 0    /* DPP wave_ror:1 / wave_rol:1 (default) */
 #define LIFEAPI_XCHG_LDS 1    /* stage the column sums through LDS */
 #define LIFEAPI_XCHG_BPERM 2  /* ds_bpermute lane gather */
+#define LIFEAPI_XCHG_MIX 3    /* left neighbour by DPP, right by ds_bpermute
+                                 (moves half the exchange to the LDS pipe)  */
+#define LIFEAPI_XCHG_MIX1 4   /* 3 of 4 words by DPP, 1 by ds_bpermute      */
+#define LIFEAPI_XCHG_MIX3 5   /* 1 of 4 words by DPP, 3 by ds_bpermute      */
+#define LIFEAPI_XCHG_LDSR 6   /* left by DPP, right through LDS memory      */
+#define LIFEAPI_XCHG_LDSR3 7  /* 1 of 4 words by DPP, 3 through LDS memory  */
+#define LIFEAPI_XCHG_ASM 8    /* rule 4 only: hand-allocated generation loop
+                                 (LDS exchange, no VGPR bank conflicts)     */
 
 typedef struct lifeapi_launch_cfg {
   int xchg;                /* LIFEAPI_XCHG_*                                */
@@ -64,7 +72,11 @@ typedef struct lifeapi_launch_cfg {
   int rule;                /* 0: column-first adder network (bitop3),
                               1: the same in plain and/or/xor,
                               2: row-first adder network (bitop3, half the
-                                 DPP moves; default)                     */
+                                 DPP moves),
+                              3: row-first, 7-LUT network (one bitop3 fewer
+                                 per half),
+                              4: rule 3 on an even/odd row split of each
+                                 column (half the row rotates)            */
 } lifeapi_launch_cfg;
 
 int lifeapi_abi_version(void);

@@ -75,7 +75,18 @@ __device__ __forceinline__ W lut3(W a, W b, W c) {
 // neighbour-column exchange (lane x <- lanes x-1 and x+1, mod 64)
 // ------------------------------------------------------------------------
 
-enum Xchg { XDPP = LIFEAPI_XCHG_DPP, XLDS = LIFEAPI_XCHG_LDS, XBPERM = LIFEAPI_XCHG_BPERM };
+enum Xchg {
+  XDPP = LIFEAPI_XCHG_DPP,
+  XLDS = LIFEAPI_XCHG_LDS,
+  XBPERM = LIFEAPI_XCHG_BPERM,
+  XMIX = LIFEAPI_XCHG_MIX,
+  XMIX1 = LIFEAPI_XCHG_MIX1,
+  XMIX3 = LIFEAPI_XCHG_MIX3,
+  XLDSR = LIFEAPI_XCHG_LDSR,
+  XLDSR3 = LIFEAPI_XCHG_LDSR3,
+  XASM = LIFEAPI_XCHG_ASM
+};
+constexpr bool uses_lds(int x) { return x == XLDS || x == XLDSR || x == XLDSR3 || x == XASM; }
 
 // A full-wave rotate has no out-of-range source lane, so bound_ctrl (read 0
 // for invalid lanes) never fires; it lets the compiler skip the old-value init.
@@ -85,33 +96,32 @@ __device__ __forceinline__ uint32_t dpp_prev(uint32_t v) {  // wave_ror:1
 __device__ __forceinline__ uint32_t dpp_next(uint32_t v) {  // wave_rol:1
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x134, 0xF, 0xF, true);
 }
+// the same rotates through the LDS crossbar (ds_bpermute: no LDS memory, but
+// it issues on the LDS pipe instead of the VALU)
+__device__ __forceinline__ uint32_t bperm_prev(uint32_t v, int lane) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute(((lane + kWave - 1) & (kWave - 1)) << 2, (int)v);
+}
+__device__ __forceinline__ uint32_t bperm_next(uint32_t v, int lane) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute(((lane + 1) & (kWave - 1)) << 2, (int)v);
+}
+
+template <int X>
+__device__ __forceinline__ void neighbour_cols(W a, W &L, W &R, uint64_t *slot, int lane);
 
 // slot: 128 words of this wave's LDS scratch (only used by XLDS)
 template <int X>
 __device__ __forceinline__ void neighbours(W c0, W c1, W &L0, W &R0, W &L1, W &R1,
                                            uint64_t *slot, int lane) {
-  if constexpr (X == XDPP) {
-    L0 = W{dpp_prev(c0.lo), dpp_prev(c0.hi)};
-    R0 = W{dpp_next(c0.lo), dpp_next(c0.hi)};
-    L1 = W{dpp_prev(c1.lo), dpp_prev(c1.hi)};
-    R1 = W{dpp_next(c1.lo), dpp_next(c1.hi)};
-  } else if constexpr (X == XBPERM) {
-    const int ap = ((lane + kWave - 1) & (kWave - 1)) << 2;
-    const int an = ((lane + 1) & (kWave - 1)) << 2;
-    L0 = W{(uint32_t)__builtin_amdgcn_ds_bpermute(ap, (int)c0.lo),
-           (uint32_t)__builtin_amdgcn_ds_bpermute(ap, (int)c0.hi)};
-    R0 = W{(uint32_t)__builtin_amdgcn_ds_bpermute(an, (int)c0.lo),
-           (uint32_t)__builtin_amdgcn_ds_bpermute(an, (int)c0.hi)};
-    L1 = W{(uint32_t)__builtin_amdgcn_ds_bpermute(ap, (int)c1.lo),
-           (uint32_t)__builtin_amdgcn_ds_bpermute(ap, (int)c1.hi)};
-    R1 = W{(uint32_t)__builtin_amdgcn_ds_bpermute(an, (int)c1.lo),
-           (uint32_t)__builtin_amdgcn_ds_bpermute(an, (int)c1.hi)};
+  if constexpr (X != XLDS) {  // (the LDSR variants stage each plane in turn)
+    neighbour_cols<X>(c0, L0, R0, slot, lane);
+    neighbour_cols<X>(c1, L1, R1, slot, lane);
   } else {
     // Stage the two column-sum planes through LDS: [0,64) plane 0, [64,128)
     // plane 1, one 8-byte word per lane (ds_write_b64 / ds_read_b64, bank-
     // conflict free: consecutive lanes, consecutive 8-byte words).  DS ops of
-    // one wave complete in order, so a wave only needs compiler ordering.
-    volatile uint64_t *s = slot;
+    // one wave complete in order, so a wave only needs compiler ordering,
+    // which the possible aliasing of the store and the loads already gives.
+    uint64_t *s = slot;
     s[lane] = join(c0);
     s[kWave + lane] = join(c1);
     __builtin_amdgcn_wave_barrier();
@@ -135,14 +145,35 @@ __device__ __forceinline__ void neighbour_cols(W a, W &L, W &R, uint64_t *slot, 
     L = W{dpp_prev(a.lo), dpp_prev(a.hi)};
     R = W{dpp_next(a.lo), dpp_next(a.hi)};
   } else if constexpr (X == XBPERM) {
-    const int ap = ((lane + kWave - 1) & (kWave - 1)) << 2;
-    const int an = ((lane + 1) & (kWave - 1)) << 2;
-    L = W{(uint32_t)__builtin_amdgcn_ds_bpermute(ap, (int)a.lo),
-          (uint32_t)__builtin_amdgcn_ds_bpermute(ap, (int)a.hi)};
-    R = W{(uint32_t)__builtin_amdgcn_ds_bpermute(an, (int)a.lo),
-          (uint32_t)__builtin_amdgcn_ds_bpermute(an, (int)a.hi)};
+    L = W{bperm_prev(a.lo, lane), bperm_prev(a.hi, lane)};
+    R = W{bperm_next(a.lo, lane), bperm_next(a.hi, lane)};
+  } else if constexpr (X == XMIX) {
+    L = W{dpp_prev(a.lo), dpp_prev(a.hi)};
+    R = W{bperm_next(a.lo, lane), bperm_next(a.hi, lane)};
+  } else if constexpr (X == XMIX1) {
+    L = W{dpp_prev(a.lo), dpp_prev(a.hi)};
+    R = W{dpp_next(a.lo), bperm_next(a.hi, lane)};
+  } else if constexpr (X == XMIX3) {
+    L = W{dpp_prev(a.lo), bperm_prev(a.hi, lane)};
+    R = W{bperm_next(a.lo, lane), bperm_next(a.hi, lane)};
+  } else if constexpr (X == XLDSR || X == XLDSR3) {
+    // one ds_write_b64 of the column, then the right neighbour by one
+    // ds_read_b64 (and, for LDSR3, the left high word by one ds_read_b32).
+    // A wave's LDS operations complete in order, so the only ordering needed
+    // is the compiler's: the store and the loads may alias.
+    uint64_t *s = slot;
+    s[lane] = join(a);
+    __builtin_amdgcn_wave_barrier();
+    R = split(s[(lane + 1) & (kWave - 1)]);
+    if constexpr (X == XLDSR) {
+      L = W{dpp_prev(a.lo), dpp_prev(a.hi)};
+    } else {
+      const uint32_t *s32 = reinterpret_cast<const uint32_t *>(s);
+      L = W{dpp_prev(a.lo), s32[2 * ((lane + kWave - 1) & (kWave - 1)) + 1]};
+    }
+    __builtin_amdgcn_wave_barrier();
   } else {
-    volatile uint64_t *s = slot;
+    uint64_t *s = slot;  // (ordering as in neighbours<XLDS>)
     s[lane] = join(a);
     __builtin_amdgcn_wave_barrier();
     L = split(s[(lane + kWave - 1) & (kWave - 1)]);
@@ -151,8 +182,86 @@ __device__ __forceinline__ void neighbour_cols(W a, W &L, W &R, uint64_t *slot, 
   }
 }
 
+// Tables of the 7-LUT network (RULE 3).  Over the vertical triples of the
+// horizontal 3-sum planes h0 (A) and h1 (B), with SA, SB their 0..3 sums and
+// count = SA + 2 SB (inclusive of the centre):
+//   s0 = SA <= 1,  s1 = SA in {1,2},  s2 = SB <= 1,  s3 = SB in {0,2}
+//   next = T3(s1, s3, T2(s2, a, T1(s0, s1, a)))
+// T1..T3 were found by exhaustive search over all 3-gate tails on every pair
+// of symmetric encodings (tools/exact_tail.c) and are checked on all 512
+// 3x3 neighbourhoods by tests/test_oracle.py::test_rule3_network_truth.
+// No 3-gate tail exists for the FullAdd encoding (fs, fc, cs, cc), so this
+// saves one v_bitop3 per 32-bit half over StepAlt's tail.
+constexpr uint32_t kLe1 = (~kMaj) & 0xFF;                        // 0x17: sum <= 1
+constexpr uint32_t kNae = ((TA ^ TB) | (TB ^ TC)) & 0xFF;         // 0x7E: sum in {1,2}
+constexpr uint32_t kEven = (~kXor3) & 0xFF;                       // 0x69: sum in {0,2}
+constexpr uint32_t kT1 = 0x34, kT2 = 0x58, kT3 = 0x28;
+
+// ---- even/odd row layout (RULE 4) ----
+// A 64-bit column held as (E, O): E bit k = row 2k, O bit k = row 2k+1.  The
+// vertical neighbours of row 2k are O bits k-1 and k; those of row 2k+1 are
+// E bits k and k+1.  So a vertical triple costs one 32-bit rotate per plane
+// and parity instead of two 64-bit rotates (four v_alignbit) per plane, and a
+// v_alignbit issues at half rate on gfx950 (tools/bank_probe.hip).
+__device__ __forceinline__ uint32_t delta_swap(uint32_t x, uint32_t m, int s) {
+  const uint32_t t = ((x >> s) ^ x) & m;
+  return x ^ t ^ (t << s);
+}
+// even bits -> low half, odd bits -> high half
+__device__ __forceinline__ uint32_t unzip32(uint32_t x) {
+  x = delta_swap(x, 0x22222222u, 1);
+  x = delta_swap(x, 0x0C0C0C0Cu, 2);
+  x = delta_swap(x, 0x00F000F0u, 4);
+  return delta_swap(x, 0x0000FF00u, 8);
+}
+__device__ __forceinline__ uint32_t zip32(uint32_t x) {
+  x = delta_swap(x, 0x0000FF00u, 8);
+  x = delta_swap(x, 0x00F000F0u, 4);
+  x = delta_swap(x, 0x0C0C0C0Cu, 2);
+  return delta_swap(x, 0x22222222u, 1);
+}
+__device__ __forceinline__ W to_eo(W a) {  // (lo, hi) rows -> (E, O)
+  const uint32_t l = unzip32(a.lo), h = unzip32(a.hi);
+  return W{__builtin_amdgcn_perm(h, l, 0x05040100u), __builtin_amdgcn_perm(h, l, 0x07060302u)};
+}
+__device__ __forceinline__ W from_eo(W e) {
+  return W{zip32(__builtin_amdgcn_perm(e.hi, e.lo, 0x05040100u)),
+           zip32(__builtin_amdgcn_perm(e.hi, e.lo, 0x07060302u))};
+}
+__device__ __forceinline__ uint32_t rotl1(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 31); }
+__device__ __forceinline__ uint32_t rotr1(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 1); }
+
 template <int X, int RULE>
 __device__ __forceinline__ W life_gen(W a, uint64_t *slot, int lane) {
+  if constexpr (RULE == 4) {
+    // the RULE 3 network on the (E, O) layout: 18 v_bitop3 + 4 v_alignbit
+    // per generation plus the exchange
+    W L, R;
+    neighbour_cols<X>(a, L, R, slot, lane);
+    const W h0 = lut3<kXor3>(L, a, R), h1 = lut3<kMaj>(L, a, R);
+    const uint32_t h0u = rotl1(h0.hi), h0d = rotr1(h0.lo);  // rows 2k-1 (for E), 2k+2 (for O)
+    const uint32_t h1u = rotl1(h1.hi), h1d = rotr1(h1.lo);
+    const W s0{lut3<kLe1>(h0u, h0.lo, h0.hi), lut3<kLe1>(h0.lo, h0.hi, h0d)};
+    const W s1{lut3<kNae>(h0u, h0.lo, h0.hi), lut3<kNae>(h0.lo, h0.hi, h0d)};
+    const W s2{lut3<kLe1>(h1u, h1.lo, h1.hi), lut3<kLe1>(h1.lo, h1.hi, h1d)};
+    const W s3{lut3<kEven>(h1u, h1.lo, h1.hi), lut3<kEven>(h1.lo, h1.hi, h1d)};
+    const W t1 = lut3<kT1>(s0, s1, a);
+    const W t2 = lut3<kT2>(s2, a, t1);
+    return lut3<kT3>(s1, s3, t2);
+  }
+  if constexpr (RULE == 3) {
+    // row-first exchange and rotations as RULE 2, then the 7-LUT network:
+    // 26 VALU per generation plus the exchange
+    W L, R;
+    neighbour_cols<X>(a, L, R, slot, lane);
+    const W h0 = lut3<kXor3>(L, a, R), h1 = lut3<kMaj>(L, a, R);
+    const W h0u = rot_up(h0), h0d = rot_dn(h0), h1u = rot_up(h1), h1d = rot_dn(h1);
+    const W s0 = lut3<kLe1>(h0u, h0, h0d), s1 = lut3<kNae>(h0u, h0, h0d);
+    const W s2 = lut3<kLe1>(h1u, h1, h1d), s3 = lut3<kEven>(h1u, h1, h1d);
+    const W t1 = lut3<kT1>(s0, s1, a);
+    const W t2 = lut3<kT2>(s2, a, t1);
+    return lut3<kT3>(s1, s3, t2);
+  }
   if constexpr (RULE == 2) {
     // Row-first form of the same adder network.  A DPP move issues at half
     // the VALU rate on gfx950 (tools/valu_probe.hip: 8 DPP of 32 instructions
@@ -225,11 +334,73 @@ __device__ __forceinline__ void st(uint64_t *p, W v) {
 
 // out[u] = in[u] stepped `gens` times.  Wave w of the grid takes groups of U
 // consecutive universes, grid-strided.  All branches are wave-uniform.
+// `gens` generations of one universe in the (E, O) layout (RULE 4), as one
+// hand-allocated loop.  The compiler's allocation puts two or three sources
+// of about half of the v_bitop3 in one VGPR bank (tools/vbank.py), and such an
+// instruction issues at half rate (tools/bank_probe.hip).  Here every VALU
+// instruction reads its sources from distinct banks (bank = vN mod 4):
+//   A = (E, O) v0:v1 (banks 0,1)   R = right column v2:v3 (2,3)
+//   L = left column v5 (E, bank 1), v4 (O, bank 0)
+// The exchange goes through this wave's 512-B LDS slot (ds_write_b64 of A,
+// ds_read_b64 of the right neighbour's word, two ds_read_b32 of the left
+// one); a wave's LDS operations complete in order and each generation waits
+// for its reads before the next write.  Network: life_gen<_, 4>.
+__device__ __forceinline__ void gens_asm(W &a, uint32_t gens, uint32_t lds_self, uint32_t lds_prev,
+                                         uint32_t lds_next) {
+  asm volatile(
+      "v_mov_b32 v0, %[e]\n"
+      "v_mov_b32 v1, %[o]\n"
+      "s_cmp_eq_u32 %[g], 0\n"
+      "s_cbranch_scc1 2f\n"
+      "1:\n"
+      "ds_write_b64 %[as], v[0:1]\n"
+      "ds_read_b64 v[2:3], %[an]\n"
+      "ds_read_b32 v5, %[ap]\n"
+      "ds_read_b32 v4, %[ap] offset:4\n"
+      "s_sub_u32 %[g], %[g], 1\n"
+      "s_waitcnt lgkmcnt(0)\n"
+      "v_bitop3_b32 v8, v5, v0, v2 bitop3:0x96\n"      // h0 E = xor3(L, A, R)
+      "v_bitop3_b32 v9, v4, v1, v3 bitop3:0x96\n"      // h0 O
+      "v_bitop3_b32 v10, v5, v0, v2 bitop3:0xe8\n"     // h1 E = maj(L, A, R)
+      "v_bitop3_b32 v11, v4, v1, v3 bitop3:0xe8\n"     // h1 O
+      "v_alignbit_b32 v6, v9, v9, 31\n"                // u0 = rotl1(h0 O): row 2k-1
+      "v_alignbit_b32 v14, v8, v8, 1\n"                // d0 = rotr1(h0 E): row 2k+2
+      "v_alignbit_b32 v12, v11, v11, 31\n"             // u1
+      "v_alignbit_b32 v16, v10, v10, 1\n"              // d1
+      "v_bitop3_b32 v13, v6, v8, v9 bitop3:0x17\n"     // s0 E = SA <= 1
+      "v_bitop3_b32 v18, v6, v8, v9 bitop3:0x7e\n"     // s1 E = SA in {1,2}
+      "v_bitop3_b32 v20, v8, v9, v14 bitop3:0x17\n"    // s0 O
+      "v_bitop3_b32 v22, v8, v9, v14 bitop3:0x7e\n"    // s1 O
+      "v_bitop3_b32 v17, v12, v10, v11 bitop3:0x17\n"  // s2 E = SB <= 1
+      "v_bitop3_b32 v24, v12, v10, v11 bitop3:0x69\n"  // s3 E = SB in {0,2}
+      "v_bitop3_b32 v28, v10, v11, v16 bitop3:0x17\n"  // s2 O
+      "v_bitop3_b32 v21, v10, v11, v16 bitop3:0x69\n"  // s3 O
+      "v_bitop3_b32 v15, v13, v18, v0 bitop3:0x34\n"   // t1 E = T1(s0, s1, a)
+      "v_bitop3_b32 v19, v20, v22, v1 bitop3:0x34\n"   // t1 O
+      "v_bitop3_b32 v25, v17, v0, v15 bitop3:0x58\n"   // t2 E = T2(s2, a, t1)
+      "v_bitop3_b32 v23, v28, v1, v19 bitop3:0x58\n"   // t2 O
+      "v_bitop3_b32 v0, v18, v24, v25 bitop3:0x28\n"   // a E = T3(s1, s3, t2)
+      "v_bitop3_b32 v1, v22, v21, v23 bitop3:0x28\n"   // a O
+      "s_cmp_lg_u32 %[g], 0\n"
+      "s_cbranch_scc1 1b\n"
+      "2:\n"
+      "v_mov_b32 %[e], v0\n"
+      "v_mov_b32 %[o], v1\n"
+      : [e] "+v"(a.lo), [o] "+v"(a.hi), [g] "+s"(gens)
+      : [as] "v"(lds_self), [ap] "v"(lds_prev), [an] "v"(lds_next)
+      : "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v8", "v9", "v10", "v11", "v12", "v13", "v14",
+        "v15", "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v28", "scc",
+        "memory");
+  static_assert(kT1 == 0x34 && kT2 == 0x58 && kT3 == 0x28 && kLe1 == 0x17 && kNae == 0x7E &&
+                    kEven == 0x69 && kXor3 == 0x96 && kMaj == 0xE8,
+                "gens_asm spells out the RULE 4 tables");
+}
+
 template <int X, int U, bool NT, int RULE>
 __global__ __launch_bounds__(kBlock) void k_step(const uint64_t *__restrict__ in,
                                                  uint64_t *__restrict__ out, uint64_t n,
                                                  uint32_t gens) {
-  __shared__ uint64_t lds[X == XLDS ? kWavesPerBlock * U * 2 * kWave : 1];
+  __shared__ uint64_t lds[uses_lds(X) ? kWavesPerBlock * U * 2 * kWave : 1];
   const int lane = threadIdx.x & (kWave - 1);
   // wave index in the block, made provably wave-uniform so that the tail
   // tests below are scalar branches
@@ -240,10 +411,30 @@ __global__ __launch_bounds__(kBlock) void k_step(const uint64_t *__restrict__ in
 #pragma unroll
     for (int k = 0; k < U; ++k)
       a[k] = (u0 + k < n) ? ld<NT>(in + (u0 + k) * kWave + lane) : W{0u, 0u};
-    for (uint32_t g = 0; g < gens; ++g) {
+    if constexpr (RULE == 4) {
 #pragma unroll
-      for (int k = 0; k < U; ++k)
-        a[k] = life_gen<X, RULE>(a[k], lds + (wib * U + k) * 2 * kWave, lane);
+      for (int k = 0; k < U; ++k) a[k] = to_eo(a[k]);
+    }
+    if constexpr (X == XASM) {
+      static_assert(RULE == 4, "the hand-allocated loop is the RULE 4 network");
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        // LDS byte addresses of this wave's slot: own word, left and right neighbours
+        const uint32_t base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)(
+            lds + (wib * U + k) * 2 * kWave);
+        gens_asm(a[k], gens, base + lane * 8u, base + ((lane + kWave - 1) & (kWave - 1)) * 8u,
+                 base + ((lane + 1) & (kWave - 1)) * 8u);
+      }
+    } else {
+      for (uint32_t g = 0; g < gens; ++g) {
+#pragma unroll
+        for (int k = 0; k < U; ++k)
+          a[k] = life_gen<X, RULE>(a[k], lds + (wib * U + k) * 2 * kWave, lane);
+      }
+    }
+    if constexpr (RULE == 4) {
+#pragma unroll
+      for (int k = 0; k < U; ++k) a[k] = from_eo(a[k]);
     }
 #pragma unroll
     for (int k = 0; k < U; ++k)
@@ -766,11 +957,17 @@ template <int X, int RULE>
 StepFn pick_nt(int u, bool nt) { return nt ? pick_u<X, true, RULE>(u) : pick_u<X, false, RULE>(u); }
 template <int X>
 StepFn pick_rule(int u, bool nt, int rule) {
-  switch (rule) {
-    case 0: return pick_nt<X, 0>(u, nt);
-    case 1: return pick_nt<X, 1>(u, nt);
-    case 2: return pick_nt<X, 2>(u, nt);
-    default: return nullptr;
+  if constexpr (X == XASM) {
+    return rule == 4 ? pick_nt<X, 4>(u, nt) : nullptr;
+  } else {
+    switch (rule) {
+      case 0: return pick_nt<X, 0>(u, nt);
+      case 1: return pick_nt<X, 1>(u, nt);
+      case 2: return pick_nt<X, 2>(u, nt);
+      case 3: return pick_nt<X, 3>(u, nt);
+      case 4: return pick_nt<X, 4>(u, nt);
+      default: return nullptr;
+    }
   }
 }
 StepFn pick_step(const lifeapi_launch_cfg &c) {
@@ -778,6 +975,12 @@ StepFn pick_step(const lifeapi_launch_cfg &c) {
     case LIFEAPI_XCHG_DPP: return pick_rule<XDPP>(c.universes_per_wave, c.nontemporal != 0, c.rule);
     case LIFEAPI_XCHG_LDS: return pick_rule<XLDS>(c.universes_per_wave, c.nontemporal != 0, c.rule);
     case LIFEAPI_XCHG_BPERM: return pick_rule<XBPERM>(c.universes_per_wave, c.nontemporal != 0, c.rule);
+    case LIFEAPI_XCHG_MIX: return pick_rule<XMIX>(c.universes_per_wave, c.nontemporal != 0, c.rule);
+    case LIFEAPI_XCHG_MIX1: return pick_rule<XMIX1>(c.universes_per_wave, c.nontemporal != 0, c.rule);
+    case LIFEAPI_XCHG_MIX3: return pick_rule<XMIX3>(c.universes_per_wave, c.nontemporal != 0, c.rule);
+    case LIFEAPI_XCHG_LDSR: return pick_rule<XLDSR>(c.universes_per_wave, c.nontemporal != 0, c.rule);
+    case LIFEAPI_XCHG_LDSR3: return pick_rule<XLDSR3>(c.universes_per_wave, c.nontemporal != 0, c.rule);
+    case LIFEAPI_XCHG_ASM: return pick_rule<XASM>(c.universes_per_wave, c.nontemporal != 0, c.rule);
     default: return nullptr;
   }
 }

@@ -27,7 +27,7 @@ if not os.path.exists(LIB_PATH):
         "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950)")
 lib = ctypes.CDLL(LIB_PATH)
 
-XCHG_DPP, XCHG_LDS, XCHG_BPERM = 0, 1, 2
+XCHG_DPP, XCHG_LDS, XCHG_BPERM, XCHG_MIX, XCHG_MIX1, XCHG_MIX3, XCHG_LDSR, XCHG_LDSR3, XCHG_ASM = range(9)
 
 
 class LaunchCfg(ctypes.Structure):

@@ -76,10 +76,10 @@ def test_argument_validation_without_device():
     # n == 0 is a no-op success even with null pointers
     assert L.lifeapi_step_batch_dev(None, None, 0, 1, None) == 0
     # bad launch cfg
-    cfg = hip.LaunchCfg(7, 4, 8, 0, 0)
-    assert L.lifeapi_step_batch_dev_cfg(4096, 8192 * 4, 1, 1, None, ctypes.byref(cfg)) == -1
-    cfg = hip.LaunchCfg(0, 3, 8, 0, 0)
-    assert L.lifeapi_step_batch_dev_cfg(4096, 8192 * 4, 1, 1, None, ctypes.byref(cfg)) == -1
+    for bad in [(9, 4, 8, 0, 0), (0, 3, 8, 0, 0), (0, 1, 8, 0, 5),
+                (hip.XCHG_ASM, 1, 8, 0, 2)]:     # the hand-allocated loop is rule 4 only
+        cfg = hip.LaunchCfg(*bad)
+        assert L.lifeapi_step_batch_dev_cfg(4096, 8192 * 4, 1, 1, None, ctypes.byref(cfg)) == -1, bad
     assert L.lifeapi_fill_random_dev(4096, 1, 0, 0, 5, None) == -1
 
 

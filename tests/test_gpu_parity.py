@@ -13,7 +13,9 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-ALL_CFGS = list(itertools.product((0, 1, 2), (1, 2, 4, 8), (0, 1), (0, 1, 2)))
+ALL_CFGS = list(itertools.product(range(8), (1, 2, 4, 8), (0, 1), (0, 1, 2, 3, 4)))
+# the hand-allocated loop exists for rule 4 only
+ALL_CFGS += list(itertools.product((8,), (1, 2, 4, 8), (0, 1), (4,)))
 
 
 def to_dev(a: np.ndarray) -> torch.Tensor:

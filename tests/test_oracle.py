@@ -192,6 +192,30 @@ def test_generated_circuit_is_the_table(inc, ttfile):
     assert (np.stack(outs) == tt).all()
 
 
+def test_rule3_network_truth():
+    """The 7-LUT network of k_step RULE 3 (tables parsed from the kernel
+    source), evaluated on all 512 3x3 neighbourhoods, is B3/S23 on the
+    inclusive count (LifeAPI.hpp:1251-1252: count 3, or 4 with the centre)."""
+    import re
+    src = open(os.path.join(os.path.dirname(GOLD), "..", "lifeapi_amd", "csrc", "lifeapi_hip.hip")).read()
+    t = {k: int(v, 16) for k, v in re.findall(r"\b(kT[123]) = (?:0x)?([0-9A-Fa-f]+)", src)}
+    assert set(t) == {"kT1", "kT2", "kT3"}
+
+    def lut(tab, x, y, z):
+        return (tab >> ((x << 2) | (y << 1) | z)) & 1
+
+    for bits in range(512):
+        n = [(bits >> i) & 1 for i in range(9)]      # n[3*col + row], col 0 = left
+        a = n[4]
+        cnt = sum(n)
+        h = [n[r] + n[3 + r] + n[6 + r] for r in range(3)]
+        sa, sb = sum(x & 1 for x in h), sum(x >> 1 for x in h)
+        s0, s1, s2, s3 = int(sa <= 1), int(sa in (1, 2)), int(sb <= 1), int(sb in (0, 2))
+        t1 = lut(t["kT1"], s0, s1, a)
+        t2 = lut(t["kT2"], s2, a, t1)
+        assert lut(t["kT3"], s1, s3, t2) == int(cnt == 3 or (a == 1 and cnt == 4)), bits
+
+
 def test_stable_passes_golden(port):
     """LifeStable passes (LifeStable.hpp:526-729) vs the reference-generated
     fixture: every plane and the PropagateResult flags, all five passes."""

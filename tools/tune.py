@@ -84,7 +84,7 @@ def main():
         work.append(("c2", n, g, list(itertools.product(xs, us, bpcs, nts, rules))))
     if args.workload in ("c3", "both", "all"):
         n, g = 1 << 16, 1024
-        work.append(("c3", n, g, list(itertools.product([0], [1, 2], [8, 0], [0], [0, 2]))))
+        work.append(("c3", n, g, list(itertools.product([1, 7, 8], [1, 2], [0], [0], [4]))))
 
     for name, n, g, cfgs in work:
         a = hip.fill_random(n, seed=2)
