@@ -127,16 +127,18 @@ def secondary_config3(hip, device, stream):
         ms.append(e0.elapsed_time(e1))
     t = min(ms) / 1e3
     gps = n * gens / t
-    # VALU issue model of the generation loop (build/asm): 28
-    # full-rate VALU + 4 DPP moves, a DPP move taking two issue slots
-    # (tools/valu_probe.hip) = 36 slots per universe-generation per wave.
-    slots = 36
+    # VALU issue model of the default generation loop (rule 6, build/asm,
+    # DESIGN.md 3.1): per 4 universes 72 v_bitop3 (one slot) + 4 v_alignbit
+    # (two slots, tools/bank_probe2.hip) = 20 issue slots per universe-gen;
+    # the exchange runs on the LDS pipe (ds_write_b128 x2, ds_read_b128 x4).
+    slots = 20
     peak_slots = 1024 * 2.4e9 / 2  # 1024 SIMDs, one wave64 VALU op per 2 clk at 2.4 GHz
+    cfg = hip.default_cfg(gens).as_dict()
     return {"workload": "config3: 64K universes x 1024 generations (one launch)",
             "value": gps, "unit": "universe-gen/s", "cell_updates_per_s": gps * 4096,
-            "kernel_ms": min(ms), "kernel_ms_all": ms,
+            "kernel_ms": min(ms), "kernel_ms_all": ms, "launch_cfg": cfg,
             "roofline": {"bound": "valu", "achieved": gps * slots / 1e12, "peak": peak_slots / 1e12,
-                         "unit": "T VALU issue slots/s (36 per universe-gen)",
+                         "unit": f"T VALU issue slots/s ({slots} per universe-gen)",
                          "frac": gps * slots / peak_slots},
             "reference_op_equivalent_Tops": OPS_PER_UNIVERSE_GEN * gps / 1e12}
 

@@ -76,7 +76,11 @@ typedef struct lifeapi_launch_cfg {
                               3: row-first, 7-LUT network (one bitop3 fewer
                                  per half),
                               4: rule 3 on an even/odd row split of each
-                                 column (half the row rotates)            */
+                                 column (half the row rotates),
+                              5, 6: rule 3 on a 4- / 8-way row split with 2 /
+                                 4 universes bit-interleaved per register
+                                 (LIFEAPI_XCHG_LDS only; universes_per_wave
+                                 then counts such groups: 1 or 2)          */
 } lifeapi_launch_cfg;
 
 int lifeapi_abi_version(void);

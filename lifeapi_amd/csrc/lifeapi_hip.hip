@@ -442,6 +442,174 @@ __global__ __launch_bounds__(kBlock) void k_step(const uint64_t *__restrict__ in
   }
 }
 
+// ------------------------------------------------------------------------
+// Row-split layouts (RULE 5: S = 4, RULE 6: S = 8)
+// ------------------------------------------------------------------------
+//
+// P = S/2 universes share a lane's S registers: bit P*k + u of R_j holds
+// universe u, row S*k + j (k < 64/S).  The vertical neighbours of R_j are
+// R_{j-1} and R_{j+1} at the same bit, except at the ends of the register
+// ring: R_0's upper neighbour is R_{S-1} rotated left by P bits, R_{S-1}'s
+// lower one is R_0 rotated right by P bits.  Because the P universes are
+// interleaved bit by bit, one 32-bit rotate by P rotates all P of their
+// 64/S-row rings at once.  Per register and generation that leaves the nine
+// v_bitop3 of the RULE 3 network plus 4/S v_alignbit (two per plane per
+// ring), against 9 + 2 for the even/odd split (S = 2, RULE 4).  The
+// exchange goes through LDS (lane-major, S words per lane).
+
+// Layout change by index-bit transpositions.  Number the 8*P source words
+// X[2u + h] = universe u's column, h = high half (rows 32..63); a bit is then
+// addressed by (register index bits | 5 position bits).  Exchanging register
+// index bit a with position bit b (shift s = 2^b) is one delta swap per pair
+// of registers:  t = ((A >> s) ^ B) & m_b;  B ^= t;  A ^= t << s.  Five such
+// swaps route the row's upper bits k to the top of the word, the universe
+// bits below them and the row's low bits j into the register index; the
+// target register R_j is then a fixed renaming of X.  Each swap is its own
+// inverse, so the store path runs them backwards.  About 30 VALU per
+// universe each way (tools/split_layout.py checks the tables).
+template <int S>
+struct SplitNet;
+template <>
+struct SplitNet<2> {  // R_j: j = row bit 0;            (E, O) of RULE 4
+  static constexpr int a[5] = {0, 0, 0, 0, 0};
+  static constexpr __device__ int reg(int j) { return j; }
+};
+template <>
+struct SplitNet<4> {  // R_j: j = row bits 1..0, 2 universes
+  static constexpr int a[5] = {0, 0, 0, 0, 1};
+  static constexpr __device__ int reg(int j) { return ((j & 1) << 1) | (j >> 1); }
+};
+template <>
+struct SplitNet<8> {  // R_j: j = row bits 2..0, 4 universes
+  static constexpr int a[5] = {0, 0, 0, 2, 1};
+  static constexpr __device__ int reg(int j) { return ((j & 3) << 1) | (j >> 2); }
+};
+
+template <int S>
+__device__ __forceinline__ void split_swap(uint32_t (&x)[S], int stage) {
+  constexpr uint32_t masks[5] = {0x0000FFFFu, 0x00FF00FFu, 0x0F0F0F0Fu, 0x33333333u, 0x55555555u};
+  const int a = SplitNet<S>::a[stage], sh = 16 >> stage;
+  const uint32_t m = masks[stage];
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    if ((i >> a) & 1) continue;
+    const int k = i | (1 << a);
+    const uint32_t t = ((x[i] >> sh) ^ x[k]) & m;
+    x[k] ^= t;
+    x[i] ^= t << sh;
+  }
+}
+
+template <int S>
+struct Split {
+  static constexpr int P = S / 2;
+  static __device__ __forceinline__ void load(const W (&c)[P], uint32_t (&r)[S]) {
+    uint32_t x[S];
+#pragma unroll
+    for (int u = 0; u < P; ++u) x[2 * u] = c[u].lo, x[2 * u + 1] = c[u].hi;
+#pragma unroll
+    for (int st = 0; st < 5; ++st) split_swap<S>(x, st);
+#pragma unroll
+    for (int j = 0; j < S; ++j) r[j] = x[SplitNet<S>::reg(j)];
+  }
+  static __device__ __forceinline__ void store(const uint32_t (&r)[S], W (&c)[P]) {
+    uint32_t x[S];
+#pragma unroll
+    for (int j = 0; j < S; ++j) x[SplitNet<S>::reg(j)] = r[j];
+#pragma unroll
+    for (int st = 4; st >= 0; --st) split_swap<S>(x, st);
+#pragma unroll
+    for (int u = 0; u < P; ++u) c[u] = W{x[2 * u], x[2 * u + 1]};
+  }
+};
+
+// one generation of the P universes in r[] (RULE 3 network per register)
+template <int S>
+__device__ __forceinline__ void gen_split(uint32_t (&r)[S], uint32_t *slot, int lane) {
+  constexpr int P = S / 2;
+  // LDS planes of Q <= 4 words per lane: 16-B lane stride keeps ds_write_b128
+  // / ds_read_b128 free of bank conflicts (a 32-B stride would be 2-way)
+  constexpr int Q = S < 4 ? S : 4;
+  typedef uint32_t vec __attribute__((ext_vector_type(Q)));
+  vec *v = reinterpret_cast<vec *>(slot);
+  const int xp = (lane + kWave - 1) & (kWave - 1), xn = (lane + 1) & (kWave - 1);
+#pragma unroll
+  for (int p = 0; p < S / Q; ++p) {
+    vec mine;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) mine[q] = r[p * Q + q];
+    v[p * kWave + lane] = mine;  // a wave's LDS operations complete in order; the
+  }                              // store and the loads may alias, so the compiler
+  uint32_t lv[S], rv[S];         // keeps their order
+#pragma unroll
+  for (int p = 0; p < S / Q; ++p) {
+    const vec l = v[p * kWave + xp], rr = v[p * kWave + xn];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) lv[p * Q + q] = l[q], rv[p * Q + q] = rr[q];
+  }
+  uint32_t h0[S], h1[S];
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    h0[j] = lut3<kXor3>(lv[j], r[j], rv[j]);
+    h1[j] = lut3<kMaj>(lv[j], r[j], rv[j]);
+  }
+  const uint32_t h0u = __builtin_amdgcn_alignbit(h0[S - 1], h0[S - 1], 32 - P);  // rotl P
+  const uint32_t h1u = __builtin_amdgcn_alignbit(h1[S - 1], h1[S - 1], 32 - P);
+  const uint32_t h0d = __builtin_amdgcn_alignbit(h0[0], h0[0], P);  // rotr P
+  const uint32_t h1d = __builtin_amdgcn_alignbit(h1[0], h1[0], P);
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    const uint32_t a0 = j == 0 ? h0u : h0[j - 1], c0 = j == S - 1 ? h0d : h0[j + 1];
+    const uint32_t a1 = j == 0 ? h1u : h1[j - 1], c1 = j == S - 1 ? h1d : h1[j + 1];
+    const uint32_t s0 = lut3<kLe1>(a0, h0[j], c0), s1 = lut3<kNae>(a0, h0[j], c0);
+    const uint32_t s2 = lut3<kLe1>(a1, h1[j], c1), s3 = lut3<kEven>(a1, h1[j], c1);
+    const uint32_t t1 = lut3<kT1>(s0, s1, r[j]);
+    const uint32_t t2 = lut3<kT2>(s2, r[j], t1);
+    r[j] = lut3<kT3>(s1, s3, t2);
+  }
+}
+
+// k_step for the split layouts: wave w takes G groups of P = S/2
+// consecutive universes, grid-strided; all branches wave-uniform.
+template <int S, int G, bool NT>
+__global__ __launch_bounds__(kBlock) void k_step_split(const uint64_t *__restrict__ in,
+                                                       uint64_t *__restrict__ out, uint64_t n,
+                                                       uint32_t gens) {
+  constexpr int P = S / 2;
+  __shared__ uint32_t lds[kWavesPerBlock * G * S * kWave];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint64_t per_wave = (uint64_t)G * P;
+  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock * per_wave;
+  for (uint64_t u0 = ((uint64_t)blockIdx.x * kWavesPerBlock + wib) * per_wave; u0 < n; u0 += stride) {
+    uint32_t r[G][S];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      W c[P];
+#pragma unroll
+      for (int u = 0; u < P; ++u) {
+        const uint64_t x = u0 + g * P + u;
+        c[u] = x < n ? ld<NT>(in + x * kWave + lane) : W{0u, 0u};
+      }
+      Split<S>::load(c, r[g]);
+    }
+    for (uint32_t it = 0; it < gens; ++it) {
+#pragma unroll
+      for (int g = 0; g < G; ++g) gen_split<S>(r[g], lds + (wib * G + g) * S * kWave, lane);
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      W c[P];
+      Split<S>::store(r[g], c);
+#pragma unroll
+      for (int u = 0; u < P; ++u) {
+        const uint64_t x = u0 + g * P + u;
+        if (x < n) st<NT>(out + x * kWave + lane, c[u]);
+      }
+    }
+  }
+}
+
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
@@ -970,7 +1138,23 @@ StepFn pick_rule(int u, bool nt, int rule) {
     }
   }
 }
+template <int S>
+StepFn pick_split(int groups, bool nt) {
+  switch (groups) {
+    case 1: return nt ? k_step_split<S, 1, true> : k_step_split<S, 1, false>;
+    case 2: return nt ? k_step_split<S, 2, true> : k_step_split<S, 2, false>;
+    default: return nullptr;
+  }
+}
+// universes one wave holds per universes_per_wave unit (rules 5, 6: groups)
+int group_size(int rule) { return rule == 5 ? 2 : rule == 6 ? 4 : 1; }
+
 StepFn pick_step(const lifeapi_launch_cfg &c) {
+  if (c.rule == 5 || c.rule == 6) {  // split layouts: LDS exchange only
+    if (c.xchg != LIFEAPI_XCHG_LDS) return nullptr;
+    return c.rule == 5 ? pick_split<4>(c.universes_per_wave, c.nontemporal != 0)
+                       : pick_split<8>(c.universes_per_wave, c.nontemporal != 0);
+  }
   switch (c.xchg) {
     case LIFEAPI_XCHG_DPP: return pick_rule<XDPP>(c.universes_per_wave, c.nontemporal != 0, c.rule);
     case LIFEAPI_XCHG_LDS: return pick_rule<XLDS>(c.universes_per_wave, c.nontemporal != 0, c.rule);
@@ -1117,17 +1301,23 @@ int lifeapi_device_count(void) {
 
 void lifeapi_default_cfg(lifeapi_launch_cfg *cfg, uint32_t generations) {
   if (!cfg) return;
-  cfg->xchg = LIFEAPI_XCHG_DPP;
-  cfg->rule = 2;  // row-first network: 4 DPP moves per generation instead of 8
-  // Measured on MI355X (profiles/r01/tune.jsonl): a one-shot grid (no
-  // grid-stride cap) beats every capped grid in both regimes.
+  // Measured on MI355X (profiles/r01/tune_c3x.jsonl, tune_gsweep.jsonl): a
+  // one-shot grid (no grid-stride cap) beats every capped grid.
   cfg->blocks_per_cu = 0;
-  if (generations <= 1) {  // HBM-streaming regime: 4 x 512 B loads in flight per wave
+  if (generations <= 2) {
+    // HBM-streaming regime: 4 x 512 B loads in flight per wave, DPP exchange,
+    // the 7-LUT network on the natural layout (no layout change to pay for)
+    cfg->xchg = LIFEAPI_XCHG_DPP;
+    cfg->rule = 3;
     cfg->universes_per_wave = 4;
     cfg->nontemporal = 1;
-  } else {  // VALU regime: state resident in VGPRs for all generations
+  } else {
+    // VALU regime: 8-way row split, 4 universes per wave interleaved bit by
+    // bit, LDS exchange; state resident in VGPRs for all generations
+    cfg->xchg = LIFEAPI_XCHG_LDS;
+    cfg->rule = 6;
     cfg->universes_per_wave = 1;
-    cfg->nontemporal = 0;
+    cfg->nontemporal = generations < 32 ? 1 : 0;
   }
 }
 
@@ -1144,7 +1334,8 @@ int lifeapi_step_batch_dev_cfg(const uint64_t *d_in, uint64_t *d_out, size_t n,
   int cus = 0;
   rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
-  const uint64_t waves = (n + c.universes_per_wave - 1) / c.universes_per_wave;
+  const uint64_t per_wave = (uint64_t)c.universes_per_wave * group_size(c.rule);
+  const uint64_t waves = (n + per_wave - 1) / per_wave;
   const unsigned grid = grid_for(waves, cus, c.blocks_per_cu);
   hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, d_in, d_out,
                      (uint64_t)n, generations);

@@ -63,7 +63,7 @@ def tune_c5(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=["c2", "c3", "c5", "both", "all"], default="both")
+    ap.add_argument("--workload", choices=["c2", "c3", "c5", "gsweep", "both", "all"], default="both")
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--quick", action="store_true")
@@ -82,9 +82,14 @@ def main():
         nts = [1]
         rules = [0, 2]
         work.append(("c2", n, g, list(itertools.product(xs, us, bpcs, nts, rules))))
+    if args.workload == "gsweep":  # where the split layouts start to pay
+        cfgs = [(0, 4, 0, 1, 2), (0, 4, 0, 1, 3), (0, 1, 0, 0, 3), (1, 1, 0, 0, 6), (1, 2, 0, 0, 6),
+                (1, 2, 0, 1, 6)]
+        for g in (1, 2, 4, 8, 16, 32):
+            work.append((f"g{g}", 1 << 18, g, cfgs))
     if args.workload in ("c3", "both", "all"):
         n, g = 1 << 16, 1024
-        work.append(("c3", n, g, list(itertools.product([1, 7, 8], [1, 2], [0], [0], [4]))))
+        work.append(("c3", n, g, list(itertools.product([1], [1, 2], [0], [0], [4, 5, 6])) + [(8, 1, 0, 0, 4)]))
 
     for name, n, g, cfgs in work:
         a = hip.fill_random(n, seed=2)
