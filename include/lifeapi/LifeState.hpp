@@ -191,6 +191,42 @@ struct alignas(64) LifeState {
     return r;
   }
 
+  // LifeState::RLE() (Parsing.hpp:8-63,200-204): printed from x = y = 32 like
+  // the reference, so Parse(s.RLE()) is s moved by (32, 32)
+  std::string RLE() const {
+    std::string out;
+    auto count = [&](unsigned c) {
+      if (c > 1) out += std::to_string(c);
+    };
+    unsigned rows = 0;
+    for (int j = 0; j < N; ++j) {
+      const int y = (j + 32) & (N - 1);
+      bool last = Get(32, y);
+      unsigned run = 0;
+      for (int i = 0; i < N; ++i) {
+        const bool v = Get((i + 32) & (N - 1), y);
+        if (v && rows) {
+          count(rows);
+          out += '$';
+          rows = 0;
+        }
+        if (v != last) {
+          count(run);
+          out += last ? 'o' : 'b';
+          run = 0;
+        }
+        ++run;
+        last = v;
+      }
+      if (last) {
+        count(run);
+        out += 'o';
+      }
+      ++rows;
+    }
+    return out + '!';
+  }
+
   // Seeded counterpart of RandomState() (LifeAPI.hpp:18-23,63-69): each column
   // uniform on [2^61, 2^62) (row 61 on, rows 62-63 off), from a splitmix64
   // stream instead of the reference's random_device-seeded mt19937_64.

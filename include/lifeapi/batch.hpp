@@ -130,6 +130,40 @@ std::vector<uint8_t> ContainsBatch(std::span<const S> in, const T &target, int d
   return r;
 }
 
+// LifeState::Parse of every string (Parsing.hpp:143-198).  status (optional)
+// gets lifeapi_parse_rle_batch's per-pattern bits: 1 = a live cell off the
+// 64x64 board was dropped (the reference writes out of bounds there), 2 =
+// stopped at a "$" count of 129.
+template <LifeStateLayout S>
+std::vector<S> ParseBatch(std::span<const std::string> rles, std::vector<uint8_t> *status = nullptr,
+                          int device = 0) {
+  std::vector<uint64_t> offs(rles.size() + 1, 0);
+  std::string blob;
+  for (size_t i = 0; i < rles.size(); ++i) {
+    blob += rles[i];
+    offs[i + 1] = blob.size();
+  }
+  std::vector<S> out(rles.size());
+  std::vector<uint8_t> st(rles.size());
+  check(lifeapi_parse_rle_batch(blob.c_str(), offs.data(), rles.size(), words(out.data()), st.data(),
+                                device));
+  if (status) *status = std::move(st);
+  return out;
+}
+
+// s.RLE() for every state (Parsing.hpp:8-63,200-204)
+template <LifeStateLayout S>
+std::vector<std::string> RLEBatch(std::span<const S> states, int device = 0) {
+  std::vector<uint64_t> offs(states.size() + 1, 0);
+  check(lifeapi_rle_batch(words(states.data()), states.size(), nullptr, 0, offs.data(), device));
+  std::string text(offs.back(), '\0');
+  check(lifeapi_rle_batch(words(states.data()), states.size(), text.data(), text.size(), offs.data(),
+                          device));
+  std::vector<std::string> out(states.size());
+  for (size_t i = 0; i < states.size(); ++i) out[i] = text.substr(offs[i], offs[i + 1] - offs[i]);
+  return out;
+}
+
 inline int DeviceCount() { return lifeapi_device_count(); }
 
 }  // namespace lifeapi

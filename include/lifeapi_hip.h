@@ -15,6 +15,8 @@
  *   lifeapi_fill_random_dev      LifeState::RandomState()   LifeAPI.hpp:63-69
  *                                (seeded splitmix64; mode 1 = RandomState's
  *                                 [2^61, 2^62) column distribution)
+ *   lifeapi_parse_rle_batch[_dev] LifeState::Parse          Parsing.hpp:143-198
+ *   lifeapi_rle_*batch[_dev]     LifeState::RLE()           Parsing.hpp:8-63,200-204
  *   lifeapi_hash_batch_dev       (build-defined digest; stands in for
  *                                 LifeState::GetHash, LifeAPI.hpp:373, which
  *                                 needs the un-vendored xxHash)
@@ -77,8 +79,9 @@ typedef struct lifeapi_launch_cfg {
                                  per half),
                               4: rule 3 on an even/odd row split of each
                                  column (half the row rotates),
-                              5, 6: rule 3 on a 4- / 8-way row split with 2 /
-                                 4 universes bit-interleaved per register
+                              5, 6, 7: rule 3 on a 4- / 8- / 16-way row
+                                 split with 2 / 4 / 8 universes interleaved
+                                 bit by bit in each register
                                  (LIFEAPI_XCHG_LDS only; universes_per_wave
                                  then counts such groups: 1 or 2)          */
 } lifeapi_launch_cfg;
@@ -156,6 +159,20 @@ int lifeapi_refined_step_batch_dev_cfg(const uint64_t *d_in, uint64_t *d_out, si
  * [2^61, 2^62) like RandomState()                                         */
 int lifeapi_fill_random_dev(uint64_t *d_out, size_t n, uint64_t seed,
                             uint64_t first_universe, int mode, void *stream);
+/* RLE batch I/O.  Text is a byte blob; pattern u is bytes
+ * [offsets[u], offsets[u+1]) (n+1 offsets, no terminators).
+ * LifeState::RLE() (Parsing.hpp:8-63,200-204; rows and columns printed
+ * from 32, as the reference does): lengths first, the caller scans them
+ * into offsets, then the write.                                           */
+int lifeapi_rle_lengths_batch_dev(const uint64_t *d_states, uint32_t *d_len, size_t n, void *stream);
+int lifeapi_rle_write_batch_dev(const uint64_t *d_states, const uint64_t *d_offsets, char *d_text,
+                                size_t n, void *stream);
+/* LifeState::Parse (GenericParse, Parsing.hpp:143-198) of every pattern.
+ * d_status[u] bit 0: a live cell off the 64x64 board was dropped (the
+ * reference writes out of bounds there); bit 1: parsing stopped at a "$"
+ * count of 129 (the reference's early return, Parsing.hpp:171-173).       */
+int lifeapi_parse_rle_batch_dev(const char *d_text, const uint64_t *d_offsets, size_t n,
+                                uint64_t *d_out, uint8_t *d_status, void *stream);
 
 /* ---- host pointers, synchronous ----------------------------------------- */
 
@@ -175,6 +192,13 @@ int lifeapi_interaction_counts_batch(const uint64_t *in, uint64_t *out, size_t n
 int lifeapi_refined_step_batch(const uint64_t *in, uint64_t *out, size_t n, int device);
 int lifeapi_contains_batch(const uint64_t *states, const uint64_t *wanted, const uint64_t *unwanted,
                            uint8_t *out, size_t n, int device);
+/* RLE of every state: fills offsets[0..n] (offsets[n] = total bytes); with
+ * text == NULL only the offsets (size query), else writes the patterns to
+ * text (LIFEAPI_E_INVALID if text_cap < offsets[n])                       */
+int lifeapi_rle_batch(const uint64_t *states, size_t n, char *text, size_t text_cap, uint64_t *offsets,
+                      int device);
+int lifeapi_parse_rle_batch(const char *text, const uint64_t *offsets, size_t n, uint64_t *out,
+                            uint8_t *status, int device);
 
 #ifdef __cplusplus
 }

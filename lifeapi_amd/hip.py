@@ -74,6 +74,11 @@ _SIGS = {
     "lifeapi_interaction_counts_batch": ([_vp, _vp, _sz, _int, _int], _int),
     "lifeapi_refined_step_batch": ([_vp, _vp, _sz, _int], _int),
     "lifeapi_contains_batch": ([_vp, _vp, _vp, _vp, _sz, _int], _int),
+    "lifeapi_rle_lengths_batch_dev": ([_vp, _vp, _sz, _vp], _int),
+    "lifeapi_rle_write_batch_dev": ([_vp, _vp, _vp, _sz, _vp], _int),
+    "lifeapi_parse_rle_batch_dev": ([_vp, _vp, _sz, _vp, _vp, _vp], _int),
+    "lifeapi_rle_batch": ([_vp, _sz, _vp, _sz, _vp, _int], _int),
+    "lifeapi_parse_rle_batch": ([_vp, _vp, _sz, _vp, _vp, _int], _int),
 }
 for _name, (_args, _res) in _SIGS.items():
     _f = getattr(lib, _name)
@@ -282,3 +287,60 @@ def interaction_counts(states: torch.Tensor, with_next: bool = False, stream=Non
     _check(lib.lifeapi_interaction_counts_batch_dev(states.data_ptr(), out.data_ptr(), n,
                                                     1 if with_next else 0, _stream(stream)))
     return out
+
+
+def rle(states: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """``LifeState::RLE()`` (Parsing.hpp:8-63,200-204) of every universe on
+    the device, on torch's current stream: (text uint8 tensor, offsets int64
+    tensor of n+1; pattern u = text[offsets[u]:offsets[u+1]])."""
+    n = _universes(states)
+    s = _stream(None)
+    lens = torch.empty(n, dtype=torch.int32, device=states.device)
+    _check(lib.lifeapi_rle_lengths_batch_dev(states.data_ptr(), lens.data_ptr(), n, s))
+    offs = torch.zeros(n + 1, dtype=torch.int64, device=states.device)
+    if n:
+        torch.cumsum(lens, 0, out=offs[1:])
+    total = int(offs[-1].item()) if n else 0
+    text = torch.empty(max(total, 1), dtype=torch.uint8, device=states.device)
+    _check(lib.lifeapi_rle_write_batch_dev(states.data_ptr(), offs.data_ptr(), text.data_ptr(), n, s))
+    return text[:total], offs
+
+
+def parse_rle(text: torch.Tensor, offsets: torch.Tensor, stream=None) -> tuple[torch.Tensor, torch.Tensor]:
+    """``LifeState::Parse`` (Parsing.hpp:143-198) of every pattern of a device
+    text blob: (states (n, 64) int64, status uint8; bit 0 = cells off the
+    board dropped, bit 1 = stopped at a "$" count of 129)."""
+    if not (text.is_cuda and offsets.is_cuda) or text.dtype != torch.uint8 or offsets.dtype != torch.int64:
+        raise ValueError("text must be a device uint8 tensor, offsets a device int64 tensor")
+    n = offsets.numel() - 1
+    out = torch.empty((max(n, 0), N), dtype=torch.int64, device=text.device)
+    status = torch.empty(max(n, 0), dtype=torch.uint8, device=text.device)
+    buf = text if text.numel() else torch.zeros(1, dtype=torch.uint8, device=text.device)
+    _check(lib.lifeapi_parse_rle_batch_dev(buf.data_ptr(), offsets.data_ptr(), max(n, 0), out.data_ptr(),
+                                           status.data_ptr(), _stream(stream)))
+    return out, status
+
+
+def rle_host(states: np.ndarray, device: int = 0) -> list[str]:
+    """Host-pointer ``lifeapi_rle_batch``: size query, then the write."""
+    src = _host_u64(states)
+    n = src.size // N
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    _check(lib.lifeapi_rle_batch(src.ctypes.data, n, None, 0, offs.ctypes.data, device))
+    text = ctypes.create_string_buffer(max(int(offs[-1]), 1))
+    _check(lib.lifeapi_rle_batch(src.ctypes.data, n, text, int(offs[-1]), offs.ctypes.data, device))
+    raw = text.raw
+    return [raw[int(offs[u]):int(offs[u + 1])].decode() for u in range(n)]
+
+
+def parse_rle_host(patterns: list[str | bytes], device: int = 0) -> tuple[np.ndarray, np.ndarray]:
+    """Host-pointer ``lifeapi_parse_rle_batch``."""
+    bs = [p.encode() if isinstance(p, str) else bytes(p) for p in patterns]
+    offs = np.zeros(len(bs) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(b) for b in bs])
+    blob = b"".join(bs) or b"\0"
+    out = np.zeros((len(bs), N), dtype=np.uint64)
+    status = np.zeros(len(bs), dtype=np.uint8)
+    _check(lib.lifeapi_parse_rle_batch(blob, offs.ctypes.data, len(bs), out.ctypes.data, status.ctypes.data,
+                                       device))
+    return out, status

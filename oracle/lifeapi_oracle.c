@@ -266,6 +266,57 @@ int oracle_parse_rle(const char *rle, uint64_t out[64]) {
   return bad ? -1 : 0;
 }
 
+/* LifeState::RLE() = GenericRLE with cellchar 'o'/'b' (Parsing.hpp:8-63,
+ * 200-204): rows printed from y = 32 (torus_wrap(j + 32)), cells from
+ * x = 32 (torus_wrap(i + N/2)); per row, runs "<n>o" / "<n>b" (n omitted
+ * when 1) with a dead run at the end of a row dropped; a row's first live
+ * cell is preceded by the rows passed since the last flush as "<k>$"; no
+ * trailing "$" (flushtrailing = false); then "!".  Writes at most `cap`
+ * bytes (no NUL) and returns the full length. */
+static size_t rle_put_count(char *out, size_t n, size_t cap, unsigned count) {
+  char digits[12];
+  int k = 0;
+  if (count <= 1) return n;
+  while (count) { digits[k++] = (char)('0' + count % 10); count /= 10; }
+  while (k) { if (n < cap) out[n] = digits[--k]; else --k; ++n; }
+  return n;
+}
+
+size_t oracle_rle(const uint64_t s[64], char *out, size_t cap) {
+  size_t n = 0;
+  unsigned rows_pending = 0;
+  for (unsigned j = 0; j < 64; ++j) {
+    const unsigned y = (j + 32) & 63;
+    int last = (int)((s[32] >> y) & 1);
+    unsigned run = 0;
+    for (unsigned i = 0; i < 64; ++i) {
+      const int cell = (int)((s[(i + 32) & 63] >> y) & 1);
+      if (cell && rows_pending) {
+        n = rle_put_count(out, n, cap, rows_pending);
+        if (n < cap) out[n] = '$';
+        ++n;
+        rows_pending = 0;
+      }
+      if (cell != last) {
+        n = rle_put_count(out, n, cap, run);
+        if (n < cap) out[n] = last ? 'o' : 'b';
+        ++n;
+        run = 0;
+      }
+      ++run;
+      last = cell;
+    }
+    if (last) {
+      n = rle_put_count(out, n, cap, run);
+      if (n < cap) out[n] = 'o';
+      ++n;
+    }
+    ++rows_pending;
+  }
+  if (n < cap) out[n] = '!';
+  return n + 1;
+}
+
 /* ---- build-defined synthetic input and digests (no reference analogue) ---- */
 
 #define GOLDEN 0x9E3779B97F4A7C15ULL

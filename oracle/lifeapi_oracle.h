@@ -54,6 +54,7 @@ int oracle_contains_target(const uint64_t s[64], const uint64_t wanted[64],
                            const uint64_t unwanted[64]);
 /* returns 0 on success, -1 on a cell outside the 64x64 board */
 int oracle_parse_rle(const char *rle, uint64_t out[64]);
+size_t oracle_rle(const uint64_t s[64], char *out, size_t cap);
 
 /* build-defined synthetic input: splitmix64 stream indexed by global word */
 uint64_t oracle_splitmix64_mix(uint64_t z);

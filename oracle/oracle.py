@@ -65,6 +65,8 @@ class Port:
         L.oracle_pop_batch.argtypes = [_u64p, _u32p, ctypes.c_size_t]
         L.oracle_contains_target.argtypes = [_u64p, _u64p, _u64p]
         L.oracle_parse_rle.argtypes = [ctypes.c_char_p, _u64p]
+        L.oracle_rle.argtypes = [_u64p, ctypes.c_char_p, ctypes.c_size_t]
+        L.oracle_rle.restype = ctypes.c_size_t
         L.oracle_fill.argtypes = [_u64p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64,
                                   ctypes.c_int]
         L.oracle_hash_batch.argtypes = [_u64p, _u64p, ctypes.c_size_t]
@@ -119,6 +121,12 @@ class Port:
         if rc != 0:
             raise ValueError(f"RLE places a cell outside the 64x64 board: {rle!r}")
         return out
+
+    def rle(self, state) -> str:
+        s = np.ascontiguousarray(state, dtype=np.uint64).reshape(64)
+        buf = ctypes.create_string_buffer(8192)
+        n = self.lib.oracle_rle(_p64(s), buf, 8192)
+        return buf.raw[:n].decode()
 
     def neighbour_count(self, state) -> np.ndarray:
         s = np.ascontiguousarray(state, dtype=np.uint64).reshape(64)
@@ -193,6 +201,8 @@ class Ref:
         L.ref_pop.restype = ctypes.c_uint
         L.ref_contains_target.argtypes = [_u64p, _u64p, _u64p]
         L.ref_parse.argtypes = [ctypes.c_char_p, _u64p]
+        L.ref_rle.argtypes = [_u64p, ctypes.c_char_p, ctypes.c_size_t]
+        L.ref_rle.restype = ctypes.c_size_t
         L.ref_neighbour_count.argtypes = [_u64p] * 5
         L.ref_count_neighbourhood.argtypes = [_u64p] * 5
         L.ref_interaction_counts.argtypes = [_u64p] * 5
@@ -233,6 +243,12 @@ class Ref:
         out = np.zeros(64, dtype=np.uint64)
         self.lib.ref_parse(rle.encode(), _p64(out))
         return out
+
+    def rle(self, state) -> str:
+        s = np.ascontiguousarray(state, dtype=np.uint64).reshape(64)
+        buf = ctypes.create_string_buffer(8192)
+        n = self.lib.ref_rle(_p64(s), buf, 8192)
+        return buf.raw[:n].decode()
 
     def pop(self, state) -> int:
         s = np.ascontiguousarray(state, dtype=np.uint64).reshape(64)

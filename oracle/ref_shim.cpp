@@ -155,6 +155,12 @@ int ref_contains_target(const uint64_t *s, const uint64_t *wanted, const uint64_
 }
 // LifeState::Parse  Parsing.hpp:192-198
 void ref_parse(const char *rle, uint64_t *out) { store(LifeState::Parse(std::string(rle)), out); }
+// LifeState::RLE  Parsing.hpp:8-63,200-204: writes at most cap bytes, returns the length
+size_t ref_rle(const uint64_t *s, char *out, size_t cap) {
+  const std::string r = load(s).RLE();
+  std::memcpy(out, r.data(), r.size() < cap ? r.size() : cap);
+  return r.size();
+}
 // LifeState::RandomState  LifeAPI.hpp:63-69 (non-deterministic, random_device seeded)
 void ref_random_state(uint64_t *out) { store(LifeState::RandomState(), out); }
 

@@ -161,6 +161,32 @@ static void Stable_Propagate() {
   EXPECT_TRUE(!r[1].consistent);
 }
 
+// RLE batch I/O: RLEBatch == RLE() per state, ParseBatch(RLE) == state moved
+// by (32, 32), ParseBatch == Parse on hand-written strings
+static void Rle_Batch() {
+  uint64_t seed = 31337;
+  std::vector<LifeState> s(777);
+  for (auto &x : s) x = LifeState::RandomState(seed) & LifeState::RandomState(seed);
+  s[0] = LifeState();
+  s[1] = LifeState::Parse("bo$2bo$3o!");
+  const auto rles = lifeapi::RLEBatch(std::span<const LifeState>(s));
+  for (size_t i = 0; i < s.size(); i += 7) EXPECT_EQ(rles[i], s[i].RLE());
+  EXPECT_EQ(rles[0], std::string("!"));
+  std::vector<uint8_t> st;
+  const auto back = lifeapi::ParseBatch<LifeState>(std::span<const std::string>(rles), &st);
+  for (size_t i = 0; i < s.size(); ++i) {
+    LifeState moved;
+    for (int x = 0; x < 64; ++x)
+      for (int y = 0; y < 64; ++y)
+        if (s[i].Get(x, y)) moved.SetSafe(x + 32, y + 32, true);
+    EXPECT_TRUE(back[i] == moved && st[i] == 0);
+  }
+  const std::vector<std::string> hand{"x = 3, y = 3\nbo$2bo$3o!", "2b2o$bobo$bo$2o!", "1 2o!", "70o!"};
+  const auto p = lifeapi::ParseBatch<LifeState>(std::span<const std::string>(hand), &st);
+  for (size_t i = 0; i + 1 < hand.size(); ++i) EXPECT_TRUE(p[i] == LifeState::Parse(hand[i]) && st[i] == 0);
+  EXPECT_EQ(st[3], 1u);
+}
+
 // errors surface as lifeapi::Error (the reference has no failure path)
 static void Errors_Throw() {
   std::vector<LifeState> a(4);
@@ -183,6 +209,7 @@ int main() {
   LifeWeld_StableAndRandom();
   Counts_And_Contains();
   Stable_Propagate();
+  Rle_Batch();
   Errors_Throw();
   std::printf("%d checks, %d failures\n", g_checks, g_failures);
   return g_failures == 0 ? 0 : 1;

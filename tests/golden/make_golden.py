@@ -338,5 +338,53 @@ def main():
     print(json.dumps(meta["digests"], indent=1))
 
 
+# RLE batch I/O (Parsing.hpp:143-204): tricky inputs for LifeState::Parse
+# (all cells on the board, so the reference's behaviour is defined) and
+# states for LifeState::RLE().  Strings are stored as one uint8 text blob +
+# n+1 offsets, as the C ABI takes them.
+PARSE_CASES = [
+    "b2o$2o$bo!", "bo$2bo$3o!", "x = 3, y = 3, rule = B3/S23\nbo$2bo$3o!",
+    "x = 0, y = 0\r\nb2o$\r\n2o$\r\nbo!\r\n", "#N name\nbo$2bo$3o!", "1 2o$o!", "1\n2b2o$o!",
+    "64o!", "b63o$64b$63bo!", "o129$o!", "o3$o59$o!", "2o!3o", "3o", "", "!", "$$$o!",
+    "10$10$10$10$10$10$3o!", "obo$A.*$3o!", "o\n\nx skipped line\n2o!", "xo$oo!", "5bo\n$2o!",
+    "o0$o!", "00o$0o!", "2b3o5$o2bo$obo!", "o$" * 63 + "o!",
+]
+
+
+def rle_fixture():
+    rng = np.random.default_rng(4242)
+    states = []
+    for d in (0.0, 1.0, 0.5, 0.02, 0.1, 0.3, 0.7, 0.95):
+        for _ in range(8):
+            bits = rng.random((64, 64)) < d
+            states.append(np.array([sum(1 << y for y in range(64) if bits[x, y]) for x in range(64)],
+                                   dtype=np.uint64))
+    chk = np.array([0x5555555555555555 if x % 2 else 0xAAAAAAAAAAAAAAAA for x in range(64)], np.uint64)
+    states += [chk, R.parse("bo$2bo$3o!"), moved(R.parse("bo$2bo$3o!"), 62, 62),
+               moved(R.parse("bo$2bo$3o!"), 30, 31), rect(31, 31, 2, 2), rect(0, 0, 64, 1)]
+    for x, y in ((0, 0), (31, 31), (32, 32), (63, 63), (32, 0), (0, 32), (33, 31)):
+        st = np.zeros(64, np.uint64)
+        st[x] = np.uint64(1 << y)
+        states.append(st)
+    states = np.stack(states)
+    rles = [R.rle(st).encode() for st in states]
+    cases = [c.encode() for c in PARSE_CASES]
+
+    def blob(strs):
+        off = np.zeros(len(strs) + 1, np.uint64)
+        off[1:] = np.cumsum([len(x) for x in strs])
+        return np.frombuffer(b"".join(strs), np.uint8).copy(), off
+
+    rtext, roff = blob(rles)
+    ptext, poff = blob(cases)
+    parsed = np.stack([R.parse(c) for c in PARSE_CASES])
+    np.savez_compressed(os.path.join(HERE, "rle.npz"), states=states, rle_text=rtext, rle_offsets=roff,
+                        parse_text=ptext, parse_offsets=poff, parsed=parsed)
+
+
 if __name__ == "__main__":
-    main()
+    if "--only-rle" in sys.argv:
+        rle_fixture()
+    else:
+        main()
+        rle_fixture()

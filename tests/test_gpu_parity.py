@@ -17,7 +17,7 @@ ALL_CFGS = list(itertools.product(range(8), (1, 2, 4, 8), (0, 1), (0, 1, 2, 3, 4
 # the hand-allocated loop exists for rule 4 only
 ALL_CFGS += list(itertools.product((8,), (1, 2, 4, 8), (0, 1), (4,)))
 # the row-split layouts: LDS exchange, 1 or 2 groups of 2 / 4 universes
-ALL_CFGS += list(itertools.product((1,), (1, 2), (0, 1), (5, 6)))
+ALL_CFGS += list(itertools.product((1,), (1, 2), (0, 1), (5, 6, 7)))
 
 
 def to_dev(a: np.ndarray) -> torch.Tensor:

@@ -262,3 +262,37 @@ def test_refined_oracle_equals_reference_fragment(port, ref):
 def test_parse_equals_reference(port, ref):
     for rle in ("b2o$2o$bo!", "bo$2bo$3o!", "2b2o$bobo$bo$2o!", "x = 1\n3o$b2o3$o!", "o2$3bo!"):
         assert (port.parse(rle) == ref.parse(rle)).all(), rle
+
+
+def _blob(text, offs, u):
+    return text[int(offs[u]):int(offs[u + 1])].tobytes().decode()
+
+
+def test_rle_io_golden(port):
+    """LifeState::RLE() / Parse (Parsing.hpp:8-63,143-204) vs the reference-
+    generated fixture: every state's RLE, every tricky parse case."""
+    g = load("rle.npz")
+    for u, s in enumerate(g["states"]):
+        assert port.rle(s) == _blob(g["rle_text"], g["rle_offsets"], u), u
+    for u, want in enumerate(g["parsed"]):
+        assert (port.parse(_blob(g["parse_text"], g["parse_offsets"], u)) == want).all(), u
+
+
+def test_rle_parse_round_trip(port):
+    """Parse(RLE(s)) is s moved by (32, 32): RLE prints from x = y = 32."""
+    x = port.fill(16, seed=31)
+    x[8:] &= port.fill(8, seed=32) & port.fill(8, seed=33)
+    for s in x:
+        back = port.parse(port.rle(s))
+        want = np.roll(s, 32)
+        want = np.array([((int(w) << 32) | (int(w) >> 32)) & (2**64 - 1) for w in want], np.uint64)
+        assert (back == want).all()
+
+
+def test_rle_equals_reference(port, ref):
+    x = port.fill(24, seed=41)
+    x[8:16] &= port.fill(8, seed=42) & port.fill(8, seed=43)
+    x[16:] = 0
+    x[16:, 5] = np.uint64(1) << np.arange(8, dtype=np.uint64) * np.uint64(7)
+    for s in x:
+        assert port.rle(s) == ref.rle(s)

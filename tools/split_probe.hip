@@ -116,6 +116,7 @@ int main() {
   run<2, 3>(in, out, n, gens, "full");
   run<4, 3>(in, out, n, gens, "full");
   run<8, 3>(in, out, n, gens, "full");
+  run<16, 3>(in, out, n, gens, "full");
   run<4, 1>(in, out, n, gens, "exchange_only");
   run<8, 1>(in, out, n, gens, "exchange_only");
   run<4, 2>(in, out, n, gens, "network_only");
