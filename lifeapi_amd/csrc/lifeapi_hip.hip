@@ -700,11 +700,19 @@ __device__ uint32_t rle_row_tokens(uint64_t r, uint32_t eol, char *out) {
   return n;
 }
 
+// longest RLE() of a 64x64 board: per row at most a 3-byte "<k>$" and 64
+// bytes of runs (a run of n cells costs at most n bytes), then "!"
+constexpr uint32_t kRleMaxBytes = 64 * (3 + 64) + 1 + 63;
+
 // WRITE = false: len[u] = strlen(RLE()); WRITE = true: RLE() at text + offs[u]
 template <bool WRITE>
 __global__ __launch_bounds__(kBlock) void k_rle(const uint64_t *__restrict__ s, uint32_t *__restrict__ len,
                                                 const uint64_t *__restrict__ offs, char *__restrict__ text,
                                                 uint64_t n) {
+  // the pattern is assembled in LDS and then copied out 64 consecutive bytes
+  // per store (the rows' tokens land at scattered offsets)
+  __shared__ char stage_all[WRITE ? kWavesPerBlock : 1][WRITE ? kRleMaxBytes : 1];
+  char *stage = stage_all[WRITE ? threadIdx.x / kWave : 0];
   const int lane = threadIdx.x & (kWave - 1);
   const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock;
   for (uint64_t u = (uint64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave; u < n; u += stride) {
@@ -718,9 +726,11 @@ __global__ __launch_bounds__(kBlock) void k_rle(const uint64_t *__restrict__ s, 
       if (lane == 0) len[u] = total;
     } else {
       const uint32_t at = wave_excl_scan(mine, lane);
+      rle_row_tokens<true>(r, eol, stage + at);
+      if (lane == kWave - 1) stage[at + mine] = '!';
+      const uint32_t total = __shfl(at + mine, kWave - 1, kWave) + 1;
       char *base = text + offs[u];
-      rle_row_tokens<true>(r, eol, base + at);
-      if (lane == kWave - 1) base[at + mine] = '!';
+      for (uint32_t i = lane; i < total; i += kWave) base[i] = stage[i];
     }
   }
 }
@@ -735,22 +745,25 @@ __global__ __launch_bounds__(kBlock) void k_rle(const uint64_t *__restrict__ s, 
 //  * any other byte is a run of count cells (0 -> 1), live iff 'o' (:196).
 // Per step: ballots give the line starts, kept bytes, digit and tag masks;
 // each tag's count comes from the digit bit planes; wave scans give every
-// tag's (x, y); the 'o' runs are then OR-ed into the lanes (= columns) they
-// cover.  status[u] bit 0: a live cell fell off the 64x64 board and was
+// tag's (x, y); every 'o' run ORs its cells into its row in LDS (one
+// ds_or_b64 for all runs of the step), and the rows are turned into
+// columns at the end.  status[u] bit 0: a live cell fell off the 64x64 board and was
 // dropped (the reference writes out of bounds there); bit 1: stopped by a
 // "$" count of 129.
 __global__ __launch_bounds__(kBlock) void k_parse_rle(const char *__restrict__ text,
                                                       const uint64_t *__restrict__ offs,
                                                       uint64_t *__restrict__ out, uint8_t *__restrict__ status,
                                                       uint64_t n) {
+  __shared__ uint64_t board[kWavesPerBlock][kWave];  // row y of this wave's pattern
   const int lane = threadIdx.x & (kWave - 1);
+  uint64_t *rows = board[threadIdx.x / kWave];
   const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock;
   for (uint64_t u = (uint64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave; u < n; u += stride) {
     const uint64_t b = offs[u], e = offs[u + 1] > b ? offs[u + 1] : b;
-    uint64_t word = 0;
+    rows[lane] = 0;
     int64_t x = 0, y = 0;
     uint32_t cnt = 0, st = 0;
-    bool line_start = true, header = false, done = false;
+    bool line_start = true, header = false, done = false, off_board = false;
     for (uint64_t p0 = b; p0 < e && !done; p0 += kWave) {
       const uint64_t p = p0 + lane;
       const bool valid = p < e;
@@ -791,12 +804,14 @@ __global__ __launch_bounds__(kBlock) void k_parse_rle(const char *__restrict__ t
       const uint32_t ex_ld = __shfl(ex, ld < 0 ? 0 : ld, kWave);
       const int64_t my_y = y + ey;
       const int64_t my_x = ld < 0 ? x + ex : (int64_t)(ex - ex_ld);
-      for (uint64_t o = __ballot(cell && c == 'o'); o; o &= o - 1) {
-        const int k = __builtin_ctzll(o);
-        const int64_t cx = __shfl(my_x, k, kWave), cy = __shfl(my_y, k, kWave);
-        const int64_t cc = (int64_t)__shfl(cv, k, kWave);
-        if (cy < 0 || cy >= 64 || cx < 0 || cx + cc > 64) st |= 1u;
-        if (cy >= 0 && cy < 64 && lane >= cx && lane < cx + cc) word |= 1ull << cy;
+      if (cell && c == 'o') {  // each 'o' run ORs its cells into its row of the board
+        if (my_y < 0 || my_y >= 64 || my_x < 0 || my_x + cv > 64) off_board = true;
+        if (my_y >= 0 && my_y < 64 && my_x >= 0 && my_x < 64) {
+          const uint64_t end = my_x + cv < 64 ? my_x + cv : 64;
+          const uint64_t hi = end == 64 ? ~0ull : (1ull << end) - 1;
+          __hip_atomic_fetch_or(&rows[my_y], hi & ~((1ull << my_x) - 1), __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
       }
       // carry to the next 64 bytes
       const uint32_t ey_all = __shfl(ey + dy, kWave - 1, kWave), ex_all = __shfl(ex + dx, kWave - 1, kWave);
@@ -814,6 +829,11 @@ __global__ __launch_bounds__(kBlock) void k_parse_rle(const char *__restrict__ t
       line_start = __shfl(c, kWave - 1, kWave) == '\n';
       header = __shfl((uint32_t)hdr, kWave - 1, kWave) != 0;
     }
+    // rows -> columns: lane x collects bit x of every row
+    uint64_t word = 0;
+#pragma unroll 8
+    for (int r = 0; r < kWave; ++r) word |= ((rows[r] >> lane) & 1ull) << r;
+    if (__ballot(off_board)) st |= 1u;
     out[u * kWave + lane] = word;
     if (lane == 0) status[u] = (uint8_t)st;
   }
