@@ -48,13 +48,18 @@ def main(prof_dir: str, out_json: str, universes: int = 1 << 20):
                 "hbm_bytes_per_launch": fetch_b + write_b, "algorithmic_bytes_per_launch": algo,
                 "traffic_over_algorithmic": (fetch_b + write_b) / algo}
 
-    c2 = entry("k_step<0, 4, true, 2>", "k_step<DPP, U=4, nt, row-first> (config 2: 1M universes x 1 gen)",
+    c2 = entry("k_step<0, 4, true, 3>", "k_step<DPP, U=4, nt, rule 3> (config 2: 1M universes x 1 gen)",
                universes * 1024)
     d = dict(c2)
     d["universes"] = universes
     d["calibration"] = {"kernel": "tools/membw.hip calib: dwordx2 U=4 nt copy, 512 MiB each way",
                         "FETCH_SIZE_KiB_mean": cf, "WRITE_SIZE_KiB_mean": cw,
                         "fetch_factor": ff, "write_factor": wf, "dispatches": [ncf, ncw]}
+    try:  # config 3: 1024 generations in VGPRs, HBM touched once per universe
+        d["config3"] = entry("k_step_split<8, 1, false>",
+                             "k_step_split<S=8, G=1> (config 3: 64K universes x 1024 gens)", (1 << 16) * 1024)
+    except SystemExit:
+        pass
     try:  # config 5 (present when the bench ran its secondaries under the PMC passes)
         d["config5"] = entry("k_refined<1, 0>", "k_refined (config 5: 256K universes, 11 planes in, 3 out)",
                              (1 << 18) * 7168)
