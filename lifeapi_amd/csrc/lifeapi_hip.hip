@@ -896,11 +896,84 @@ __global__ __launch_bounds__(kBlock) void k_step_contains(const uint64_t *__rest
     W a = split(in[u * kWave + lane]);
     uint32_t hit = 0;
     for (uint32_t g = 1; g <= gens; ++g) {
-      a = life_gen<XDPP, 0>(a, nullptr, lane);
+      a = life_gen<XDPP, 3>(a, nullptr, lane);
       if (hit == 0 && wave_contains(a, w, uw)) hit = g;
     }
     if (fin) fin[u * kWave + lane] = join(a);
     if (lane == 0) first[u] = hit;
+  }
+}
+
+// The same on the 8-way split layout (k_step_split): 4 universes per wave.
+// The target is put into the same register layout once, replicated for the
+// 4 universes; after every generation (r ^ w) & (w | u) is OR-ed over the
+// registers and one ballot per universe (its bits are every P-th) tests it,
+// with no branch per universe.  The check costs about 5 VALU per
+// universe-generation on top of the 20 of the step (+25 % measured,
+// profiles/r01/contains_bench.jsonl); branching around the bookkeeping
+// when no universe is clean measured slower still.
+// Without d_final, a wave stops once all its universes have hit.
+constexpr uint32_t kDiff = ((TA ^ TB) & (TB | TC)) & 0xFF;  // (s ^ wanted) & (wanted | unwanted)
+template <int S>
+__global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *__restrict__ in,
+                                                                uint64_t *__restrict__ fin,
+                                                                const uint64_t *__restrict__ wanted,
+                                                                const uint64_t *__restrict__ unwanted,
+                                                                uint32_t *__restrict__ first, uint64_t n,
+                                                                uint32_t gens) {
+  constexpr int P = S / 2;
+  constexpr uint32_t every = P == 1 ? ~0u : P == 2 ? 0x55555555u : P == 4 ? 0x11111111u : 0x01010101u;
+  __shared__ uint32_t lds[kWavesPerBlock * S * kWave];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  uint32_t tw[S], tu[S];
+  {
+    W c[P];
+#pragma unroll
+    for (int u = 0; u < P; ++u) c[u] = split(wanted[lane]);
+    Split<S>::load(c, tw);
+#pragma unroll
+    for (int u = 0; u < P; ++u) c[u] = split(unwanted[lane]);
+    Split<S>::load(c, tu);
+  }
+
+  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock * P;
+  for (uint64_t u0 = ((uint64_t)blockIdx.x * kWavesPerBlock + wib) * P; u0 < n; u0 += stride) {
+    uint32_t r[S];
+    W c[P];
+#pragma unroll
+    for (int u = 0; u < P; ++u) c[u] = u0 + u < n ? split(in[(u0 + u) * kWave + lane]) : W{0u, 0u};
+    Split<S>::load(c, r);
+    uint32_t hit[P];
+#pragma unroll
+    for (int u = 0; u < P; ++u) hit[u] = 0;
+    uint32_t found = 0;
+    for (uint32_t g = 1; g <= gens; ++g) {
+      gen_split<S>(r, lds + wib * S * kWave, lane);
+      uint32_t d = 0;
+#pragma unroll
+      for (int j = 0; j < S; ++j) d |= lut3<kDiff>(r[j], tw[j], tu[j]);
+      // straight-line: a ballot per universe, the bookkeeping in scalar registers
+      uint32_t clean = 0;
+#pragma unroll
+      for (int u = 0; u < P; ++u) clean |= (__ballot((d & (every << u)) != 0) == 0 ? 1u : 0u) << u;
+      const uint32_t fresh = clean & ~found;
+#pragma unroll
+      for (int u = 0; u < P; ++u) hit[u] = (fresh >> u) & 1 ? g : hit[u];
+      found |= fresh;
+      if (!fin && found == (1u << P) - 1) break;
+    }
+    if (fin) {
+      Split<S>::store(r, c);
+#pragma unroll
+      for (int u = 0; u < P; ++u)
+        if (u0 + u < n) fin[(u0 + u) * kWave + lane] = join(c[u]);
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int u = 0; u < P; ++u)
+        if (u0 + u < n) first[u0 + u] = hit[u];
+    }
   }
 }
 
@@ -1611,9 +1684,15 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
   }
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
-  hipLaunchKernelGGL(k_step_contains, dim3(grid_for(n, cus, 0)), dim3(kBlock), 0,
-                     (hipStream_t)stream, d_in, d_final, d_wanted, d_unwanted, d_first_gen,
-                     (uint64_t)n, generations);
+  if (generations > 2) {  // the default layout of k_step for gens > 2 (lifeapi_default_cfg)
+    hipLaunchKernelGGL(k_step_contains_split<8>, dim3(grid_for((n + 3) / 4, cus, 0)), dim3(kBlock), 0,
+                       (hipStream_t)stream, d_in, d_final, d_wanted, d_unwanted, d_first_gen,
+                       (uint64_t)n, generations);
+  } else {
+    hipLaunchKernelGGL(k_step_contains, dim3(grid_for(n, cus, 0)), dim3(kBlock), 0,
+                       (hipStream_t)stream, d_in, d_final, d_wanted, d_unwanted, d_first_gen,
+                       (uint64_t)n, generations);
+  }
   return launched("k_step_contains launch");
 }
 

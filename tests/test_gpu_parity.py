@@ -167,6 +167,38 @@ def test_step_contains(hip, port):
     assert (to_host(final) == port.step_batch(x, 6)).all()
 
 
+@pytest.mark.parametrize("gens", [1, 2, 3, 6, 37])
+@pytest.mark.parametrize("with_final", [False, True])
+def test_step_contains_batch(hip, port, gens, with_final):
+    """First generation containing a block + its empty ring (LifeTarget.hpp:44-51)
+    over ragged batches of sparse soups and planted blinkers/blocks, every layout
+    the entry point picks (natural for gens <= 2, 8-way split above)."""
+    n = 1003
+    x = port.fill(n, seed=123) & port.fill(n, seed=124) & port.fill(n, seed=125)
+    blk = np.zeros(64, np.uint64)
+    blk[10] = blk[11] = np.uint64(0b11 << 40)
+    ring = np.zeros(64, np.uint64)
+    for c in (9, 10, 11, 12):
+        ring[c] = np.uint64(0b1111 << 39)
+    ring &= ~blk
+    x[::7] &= ~ring & ~blk                               # clear the spot ...
+    x[::14] |= blk                                       # ... and plant blocks in half of them
+    wanted, unwanted = blk, ring
+    fin = torch.empty((n, 64), dtype=torch.int64, device="cuda") if with_final else None
+    first, final = hip.step_contains(to_dev(x), to_dev(wanted[None]), to_dev(unwanted[None]), gens, final=fin)
+    got = first.cpu().numpy()
+    exp = np.zeros(n, np.int64)
+    s = x.copy()
+    for g in range(1, gens + 1):
+        s = port.step_batch(s, 1)
+        hit = (((s ^ wanted) & (wanted | unwanted)) == 0).all(axis=1)
+        exp[(exp == 0) & hit] = g
+    assert (got == exp).all(), np.nonzero(got != exp)[0][:10]
+    assert exp.any()
+    if with_final:
+        assert (to_host(final) == s).all()
+
+
 def test_host_api(hip, port):
     x = port.fill(2500, seed=8)
     assert (hip.step_host(x, 4, device=0).reshape(-1, 64) == port.step_batch(x, 4)).all()
