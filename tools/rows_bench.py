@@ -1,0 +1,91 @@
+"""Throughput and HBM roofline fraction of every SURVEY 8(f) kernel on
+1M objects (--n) (one JSON line each).  Algorithmic bytes = what the entry point
+must read and write per object; peak = 8 TB/s (MI355X_MICROARCH.md)."""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import lifeapi_amd.hip as hip  # noqa: E402
+
+PEAK = 8000.0  # GB/s
+
+
+def timed(fn, reps=9):
+    fn()
+    torch.cuda.synchronize()
+    ms = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        b.synchronize()
+        ms.append(a.elapsed_time(b))
+    return sorted(ms)[len(ms) // 2]
+
+
+def report(name, n, nbytes, ms, extra=None):
+    gbs = n * nbytes / (ms / 1e3) / 1e9
+    d = {"kernel": name, "objects": n, "algorithmic_bytes_per_object": nbytes, "ms": ms,
+         "objects_per_s": n / ms * 1e3, "GBps": gbs, "hbm_frac": gbs / PEAK}
+    d.update(extra or {})
+    print(json.dumps(d), flush=True)
+
+
+def stable_inputs(n):
+    """Block still lifes with an unknown window, tiled from 256 seeded cases
+    (the test_gpu_parity generator), as (n, 640) int64 planes."""
+    rng = np.random.default_rng(5)
+    base = np.zeros((256, 10, 64), np.uint64)
+    blk = np.zeros(64, np.uint64)
+    blk[0] = blk[1] = np.uint64(3)
+    for u in range(256):
+        st = np.zeros(64, np.uint64)
+        for _ in range(6):
+            bx, by = int(rng.integers(4)) * 16, int(rng.integers(4)) * 16
+            st |= np.roll(blk, bx) << np.uint64(by)
+        w0, h0 = int(rng.integers(4, 20)), int(rng.integers(4, 20))
+        x0, y0 = int(rng.integers(0, 64 - w0)), int(rng.integers(0, 64 - h0))
+        unk = np.zeros(64, np.uint64)
+        unk[x0:x0 + w0] = np.uint64(((1 << h0) - 1) << y0)
+        base[u, 0], base[u, 1] = st & ~unk, unk
+    x = np.tile(base.reshape(256, 640), (n // 256, 1))
+    return torch.from_numpy(x.view(np.int64)).cuda()
+
+
+def main():
+    n = int(sys.argv[sys.argv.index('--n') + 1]) if '--n' in sys.argv else 1 << 20
+    x = hip.fill_random(n, seed=7)
+    y = torch.empty_like(x)
+    report("k_step (1 gen)", n, 1024, timed(lambda: hip.step(x, out=y, generations=1)))
+    report("k_pop", n, 516, timed(lambda: hip.pop(x)))
+    report("k_hash", n, 520, timed(lambda: hip.hashes(x)))
+    w = x[:1].clone()
+    report("k_contains", n, 513, timed(lambda: hip.contains(x, w, w)))
+    report("k_fill", n, 512, timed(lambda: hip.fill_random(n, seed=9)))
+    report("k_counts NeighbourCount", n, 512 + 2048, timed(lambda: hip.neighbour_count(x)))
+    report("k_counts InteractionCounts", n, 512 + 1536, timed(lambda: hip.interaction_counts(x)))
+    report("k_counts InteractionCountsAndNext", n, 512 + 2048,
+           timed(lambda: hip.interaction_counts(x, with_next=True)))
+    welds = torch.cat([hip.fill_random(n, seed=s).view(n, 1, 64) for s in (11, 12, 13, 14)], 1).reshape(n, 256)
+    welds[:, 64:] &= hip.fill_random(3 * n, seed=15).view(n, 192)
+    report("k_weld (1 gen)", n, 2048 + 512, timed(lambda: hip.weld_step(welds, 1)))
+    st = stable_inputs(n)
+    for name in hip.STABLE_PASSES:
+        work = st.clone()
+        def run():
+            work.copy_(st)
+            hip.stable_pass(work, name)
+        t_copy = timed(lambda: work.copy_(st))
+        t = timed(run) - t_copy
+        report(f"k_stable {name}", n, 2 * 5120 + 1, t, {"note": "copy of the input subtracted"})
+    planes = hip.fill_random(11 * n, seed=21).view(n, 11 * 64)
+    report("k_refined (config 5)", n, 7168, timed(lambda: hip.refined_step(planes)))
+
+
+if __name__ == "__main__":
+    main()
