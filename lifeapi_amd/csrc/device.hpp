@@ -1,0 +1,227 @@
+// device.hpp -- lane-level building blocks shared by every kernel file.
+//
+// One 64-lane wavefront works on one universe at a time: lane x owns column x
+// (the reference's state[x], LifeAPI.hpp:39-40) as two 32-bit VGPRs.  The
+// vertical (in-column) neighbours are 1-bit rotates of the lane's own word; the
+// horizontal neighbours are the adjacent lanes' columns, fetched with DPP
+// wave_ror:1 / wave_rol:1 (64-lane rotates, so the torus wrap at columns 0/63
+// is free), ds_bpermute or LDS.  Logic is gfx950's 3-input v_bitop3_b32.  No
+// MFMA: the work is pure integer/bitwise.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "common.hpp"
+#include "lifeapi_hip.h"
+
+namespace lifeapi_impl {
+
+// ------------------------------------------------------------------------
+// lane-level primitives
+// ------------------------------------------------------------------------
+
+struct W {  // one column word, split in VGPR halves: bits 0-31 / 32-63
+  uint32_t lo, hi;
+};
+
+__device__ __forceinline__ W split(uint64_t v) { return W{(uint32_t)v, (uint32_t)(v >> 32)}; }
+__device__ __forceinline__ uint64_t join(W w) { return (uint64_t)w.lo | ((uint64_t)w.hi << 32); }
+
+// 64-bit rotates by one row: rotl(a,1) (cell y <- y-1) and rotr(a,1).
+__device__ __forceinline__ W rot_up(W a) {
+  return W{__builtin_amdgcn_alignbit(a.lo, a.hi, 31), __builtin_amdgcn_alignbit(a.hi, a.lo, 31)};
+}
+__device__ __forceinline__ W rot_dn(W a) {
+  return W{__builtin_amdgcn_alignbit(a.hi, a.lo, 1), __builtin_amdgcn_alignbit(a.lo, a.hi, 1)};
+}
+
+// v_bitop3_b32 truth tables: bit i of the table is f(bit i of 0xF0, 0xCC, 0xAA)
+// for (src0, src1, src2).
+constexpr uint32_t TA = 0xF0, TB = 0xCC, TC = 0xAA;
+constexpr uint32_t kXor3 = (TA ^ TB ^ TC) & 0xFF;                     // 0x96
+constexpr uint32_t kMaj = ((TA & TB) | (TA & TC) | (TB & TC)) & 0xFF;  // 0xE8
+constexpr uint32_t kCarry2 = (TA ^ (TB & TC)) & 0xFF;                 // a ^ (b & c)
+constexpr uint32_t kLive = ((TA ^ TB) & (TC | TA)) & 0xFF;            // (a ^ b) & (c | a)
+
+template <uint32_t TT>
+__device__ __forceinline__ uint32_t lut3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, TT);
+}
+template <uint32_t TT>
+__device__ __forceinline__ W lut3(W a, W b, W c) {
+  return W{lut3<TT>(a.lo, b.lo, c.lo), lut3<TT>(a.hi, b.hi, c.hi)};
+}
+
+// ------------------------------------------------------------------------
+// neighbour-column exchange (lane x <- lanes x-1 and x+1, mod 64)
+// ------------------------------------------------------------------------
+
+enum Xchg {
+  XDPP = LIFEAPI_XCHG_DPP,
+  XLDS = LIFEAPI_XCHG_LDS,
+  XBPERM = LIFEAPI_XCHG_BPERM,
+  XMIX = LIFEAPI_XCHG_MIX,
+  XMIX1 = LIFEAPI_XCHG_MIX1,
+  XMIX3 = LIFEAPI_XCHG_MIX3,
+  XLDSR = LIFEAPI_XCHG_LDSR,
+  XLDSR3 = LIFEAPI_XCHG_LDSR3,
+  XASM = LIFEAPI_XCHG_ASM
+};
+constexpr bool uses_lds(int x) { return x == XLDS || x == XLDSR || x == XLDSR3 || x == XASM; }
+
+// A full-wave rotate has no out-of-range source lane, so bound_ctrl (read 0
+// for invalid lanes) never fires; it lets the compiler skip the old-value init.
+__device__ __forceinline__ uint32_t dpp_prev(uint32_t v) {  // wave_ror:1
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x13C, 0xF, 0xF, true);
+}
+__device__ __forceinline__ uint32_t dpp_next(uint32_t v) {  // wave_rol:1
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x134, 0xF, 0xF, true);
+}
+// the same rotates through the LDS crossbar (ds_bpermute: no LDS memory, but
+// it issues on the LDS pipe instead of the VALU)
+__device__ __forceinline__ uint32_t bperm_prev(uint32_t v, int lane) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute(((lane + kWave - 1) & (kWave - 1)) << 2, (int)v);
+}
+__device__ __forceinline__ uint32_t bperm_next(uint32_t v, int lane) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute(((lane + 1) & (kWave - 1)) << 2, (int)v);
+}
+
+template <int X>
+__device__ __forceinline__ void neighbour_cols(W a, W &L, W &R, uint64_t *slot, int lane);
+
+// slot: 128 words of this wave's LDS scratch (only used by XLDS)
+template <int X>
+__device__ __forceinline__ void neighbours(W c0, W c1, W &L0, W &R0, W &L1, W &R1,
+                                           uint64_t *slot, int lane) {
+  if constexpr (X != XLDS) {  // (the LDSR variants stage each plane in turn)
+    neighbour_cols<X>(c0, L0, R0, slot, lane);
+    neighbour_cols<X>(c1, L1, R1, slot, lane);
+  } else {
+    // Stage the two column-sum planes through LDS: [0,64) plane 0, [64,128)
+    // plane 1, one 8-byte word per lane (ds_write_b64 / ds_read_b64, bank-
+    // conflict free: consecutive lanes, consecutive 8-byte words).  DS ops of
+    // one wave complete in order, so a wave only needs compiler ordering,
+    // which the possible aliasing of the store and the loads already gives.
+    uint64_t *s = slot;
+    s[lane] = join(c0);
+    s[kWave + lane] = join(c1);
+    __builtin_amdgcn_wave_barrier();
+    const int xp = (lane + kWave - 1) & (kWave - 1), xn = (lane + 1) & (kWave - 1);
+    L0 = split(s[xp]);
+    R0 = split(s[xn]);
+    L1 = split(s[kWave + xp]);
+    R1 = split(s[kWave + xn]);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// one 64-bit neighbour word from lanes x-1 / x+1 (used by the row-first rule)
+template <int X>
+__device__ __forceinline__ void neighbour_cols(W a, W &L, W &R, uint64_t *slot, int lane) {
+  if constexpr (X == XDPP) {
+    L = W{dpp_prev(a.lo), dpp_prev(a.hi)};
+    R = W{dpp_next(a.lo), dpp_next(a.hi)};
+  } else if constexpr (X == XBPERM) {
+    L = W{bperm_prev(a.lo, lane), bperm_prev(a.hi, lane)};
+    R = W{bperm_next(a.lo, lane), bperm_next(a.hi, lane)};
+  } else if constexpr (X == XMIX) {
+    L = W{dpp_prev(a.lo), dpp_prev(a.hi)};
+    R = W{bperm_next(a.lo, lane), bperm_next(a.hi, lane)};
+  } else if constexpr (X == XMIX1) {
+    L = W{dpp_prev(a.lo), dpp_prev(a.hi)};
+    R = W{dpp_next(a.lo), bperm_next(a.hi, lane)};
+  } else if constexpr (X == XMIX3) {
+    L = W{dpp_prev(a.lo), bperm_prev(a.hi, lane)};
+    R = W{bperm_next(a.lo, lane), bperm_next(a.hi, lane)};
+  } else if constexpr (X == XLDSR || X == XLDSR3) {
+    // one ds_write_b64 of the column, then the right neighbour by one
+    // ds_read_b64 (and, for LDSR3, the left high word by one ds_read_b32).
+    // A wave's LDS operations complete in order, so the only ordering needed
+    // is the compiler's: the store and the loads may alias.
+    uint64_t *s = slot;
+    s[lane] = join(a);
+    __builtin_amdgcn_wave_barrier();
+    R = split(s[(lane + 1) & (kWave - 1)]);
+    if constexpr (X == XLDSR) {
+      L = W{dpp_prev(a.lo), dpp_prev(a.hi)};
+    } else {
+      const uint32_t *s32 = reinterpret_cast<const uint32_t *>(s);
+      L = W{dpp_prev(a.lo), s32[2 * ((lane + kWave - 1) & (kWave - 1)) + 1]};
+    }
+    __builtin_amdgcn_wave_barrier();
+  } else {
+    uint64_t *s = slot;  // (ordering as in neighbours<XLDS>)
+    s[lane] = join(a);
+    __builtin_amdgcn_wave_barrier();
+    L = split(s[(lane + kWave - 1) & (kWave - 1)]);
+    R = split(s[(lane + 1) & (kWave - 1)]);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// Tables of the 7-LUT network (RULE 3).  Over the vertical triples of the
+// horizontal 3-sum planes h0 (A) and h1 (B), with SA, SB their 0..3 sums and
+// count = SA + 2 SB (inclusive of the centre):
+//   s0 = SA <= 1,  s1 = SA in {1,2},  s2 = SB <= 1,  s3 = SB in {0,2}
+//   next = T3(s1, s3, T2(s2, a, T1(s0, s1, a)))
+// T1..T3 were found by exhaustive search over all 3-gate tails on every pair
+// of symmetric encodings (tools/exact_tail.c) and are checked on all 512
+// 3x3 neighbourhoods by tests/test_oracle.py::test_rule3_network_truth.
+// No 3-gate tail exists for the FullAdd encoding (fs, fc, cs, cc), so this
+// saves one v_bitop3 per 32-bit half over StepAlt's tail.
+constexpr uint32_t kLe1 = (~kMaj) & 0xFF;                        // 0x17: sum <= 1
+constexpr uint32_t kNae = ((TA ^ TB) | (TB ^ TC)) & 0xFF;         // 0x7E: sum in {1,2}
+constexpr uint32_t kEven = (~kXor3) & 0xFF;                       // 0x69: sum in {0,2}
+constexpr uint32_t kT1 = 0x34, kT2 = 0x58, kT3 = 0x28;
+
+template <bool NT>
+__device__ __forceinline__ W ld(const uint64_t *p) {
+  if constexpr (NT) return split(__builtin_nontemporal_load(p));
+  else return split(*p);
+}
+template <bool NT>
+__device__ __forceinline__ void st(uint64_t *p, W v) {
+  if constexpr (NT) __builtin_nontemporal_store(join(v), p);
+  else *p = join(v);
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+  return v;
+}
+
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, int lane) {
+  uint32_t inc = v;
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) {
+    const uint32_t t = __shfl_up(inc, off, kWave);
+    if (lane >= off) inc += t;
+  }
+  return inc - v;
+}
+__device__ __forceinline__ uint64_t below_lane(int lane) { return (1ull << lane) - 1; }
+__device__ __forceinline__ int last_set(uint64_t m) { return m ? 63 - __builtin_clzll(m) : -1; }
+
+
+// Contains(LifeTarget) (LifeTarget.hpp:44-51): (s ^ w) & (w | u) == 0 on all columns
+__device__ __forceinline__ bool wave_contains(W s, W w, W u) {
+  const uint32_t dlo = (s.lo ^ w.lo) & (w.lo | u.lo), dhi = (s.hi ^ w.hi) & (w.hi | u.hi);
+  return __ballot((dlo | dhi) != 0u) == 0ull;
+}
+
+
+}  // namespace lifeapi_impl

@@ -1,0 +1,339 @@
+// host.hip -- host side of the C ABI: errors, device checks, launch
+// geometry, the staging used by every host-pointer entry point, and those
+// entry points that only stage data around a *_dev call.
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "host.hpp"
+
+namespace lifeapi_impl {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, const char *arg) {
+  char buf[512];
+  std::snprintf(buf, sizeof buf, fmt, arg ? arg : "");
+  g_err = buf;
+  return code;
+}
+int fail_hip(hipError_t e, const char *what) {
+  char buf[512];
+  std::snprintf(buf, sizeof buf, "%s: %s (hipError %d)", what, hipGetErrorString(e), (int)e);
+  g_err = buf;
+  if (e == hipErrorNoBinaryForGpu || e == hipErrorInvalidDeviceFunction ||
+      e == hipErrorInvalidImage || e == hipErrorSharedObjectInitFailed)
+    return LIFEAPI_E_NOKERNEL;
+  return (int)e;
+}
+
+struct DevInfo {
+  int cus = 0;
+  bool ok = false;
+};
+std::mutex g_info_mu;
+std::vector<DevInfo> g_info;
+
+int device_cus(int &cus) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return fail_hip(e, "hipGetDevice");
+  std::lock_guard<std::mutex> lk(g_info_mu);
+  if ((int)g_info.size() <= dev) g_info.resize(dev + 1);
+  if (!g_info[dev].ok) {
+    hipDeviceProp_t p;
+    e = hipGetDeviceProperties(&p, dev);
+    if (e != hipSuccess) return fail_hip(e, "hipGetDeviceProperties");
+    if (std::strncmp(p.gcnArchName, "gfx950", 6) != 0)
+      return fail(LIFEAPI_E_NODEVICE, "device is %s, this library is built for gfx950 only",
+                  p.gcnArchName);
+    g_info[dev].cus = p.multiProcessorCount;
+    g_info[dev].ok = true;
+  }
+  cus = g_info[dev].cus;
+  return LIFEAPI_OK;
+}
+
+bool aligned8(const void *p) { return ((uintptr_t)p & 7u) == 0; }
+
+int check_batch(const void *in, const void *out, size_t n) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!in || !out) return fail(LIFEAPI_E_INVALID, "null universe pointer%s");
+  if (!aligned8(in) || !aligned8(out)) return fail(LIFEAPI_E_INVALID, "universe pointers must be 8-byte aligned%s");
+  if (n > (SIZE_MAX / 512)) return fail(LIFEAPI_E_INVALID, "n too large%s");
+  const uintptr_t a = (uintptr_t)in, b = (uintptr_t)out, bytes = (uintptr_t)n * 512u;
+  if (a != b && a < b + bytes && b < a + bytes)
+    return fail(LIFEAPI_E_INVALID, "input and output batches overlap (only in == out is allowed)%s");
+  return LIFEAPI_OK;
+}
+
+unsigned grid_for(uint64_t waves_needed, int cus, int blocks_per_cu) {
+  uint64_t blocks = (waves_needed + kWavesPerBlock - 1) / kWavesPerBlock;
+  if (blocks_per_cu > 0) blocks = std::min<uint64_t>(blocks, (uint64_t)cus * blocks_per_cu);
+  blocks = std::min<uint64_t>(blocks, 1u << 30);
+  return (unsigned)std::max<uint64_t>(blocks, 1);
+}
+
+int launched(const char *what) {
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? LIFEAPI_OK : fail_hip(e, what);
+}
+
+// ---- host-pointer staging: one context per device ----
+struct HostCtx {
+  std::mutex mu;
+  hipStream_t stream = nullptr;
+  char *buf = nullptr;
+  size_t cap = 0;  // bytes
+};
+std::mutex g_ctx_mu;
+std::vector<HostCtx *> g_ctx;
+
+HostCtx *ctx_for(int dev) {
+  std::lock_guard<std::mutex> lk(g_ctx_mu);
+  if ((int)g_ctx.size() <= dev) g_ctx.resize(dev + 1, nullptr);
+  if (!g_ctx[dev]) g_ctx[dev] = new HostCtx();  // lives for the process
+  return g_ctx[dev];
+}
+
+constexpr size_t kStagingBytes = size_t(1) << 30;  // device staging per pass (1 GiB)
+
+// Stages n universes through this device's reusable buffer in chunks of at
+// most kStagingBytes: H2D, the stream-ordered *_dev entry point, D2H, sync.
+int host_chunked(int dev, size_t n, const HostIO *io, int nio, ChunkFn fn, const void *arg) {
+  DeviceGuard guard;
+  hipError_t e = hipSetDevice(dev);
+  if (e != hipSuccess) return fail_hip(e, "hipSetDevice");
+  HostCtx *c = ctx_for(dev);
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (!c->stream) {
+    e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) return fail_hip(e, "hipStreamCreate");
+  }
+  size_t per = 0;
+  for (int k = 0; k < nio; ++k) per += (io[k].bytes + 255) & ~size_t(255);
+  const size_t chunk = std::max<size_t>(1, std::min(n, kStagingBytes / per));
+  size_t need = 0;
+  for (int k = 0; k < nio; ++k) need += ((io[k].bytes * chunk + 255) & ~size_t(255));
+  if (c->cap < need) {
+    if (c->buf) (void)hipFree(c->buf);
+    c->buf = nullptr;
+    c->cap = 0;
+    e = hipMalloc(&c->buf, need);
+    if (e != hipSuccess) return fail_hip(e, "hipMalloc(staging)");
+    c->cap = need;
+  }
+  void *d[8];
+  for (size_t off = 0; off < n; off += chunk) {
+    const size_t m = std::min(chunk, n - off);
+    size_t pos = 0;
+    for (int k = 0; k < nio; ++k) {
+      d[k] = c->buf + pos;
+      pos += (io[k].bytes * chunk + 255) & ~size_t(255);
+      if (io[k].src) {
+        e = hipMemcpyAsync(d[k], (const char *)io[k].src + off * io[k].bytes, m * io[k].bytes,
+                           hipMemcpyHostToDevice, c->stream);
+        if (e != hipSuccess) return fail_hip(e, "hipMemcpyAsync(H2D)");
+      }
+    }
+    const int rc = fn(d, m, c->stream, arg);
+    if (rc != LIFEAPI_OK) return rc;
+    for (int k = 0; k < nio; ++k)
+      if (io[k].dst) {
+        e = hipMemcpyAsync((char *)io[k].dst + off * io[k].bytes, d[k], m * io[k].bytes,
+                           hipMemcpyDeviceToHost, c->stream);
+        if (e != hipSuccess) return fail_hip(e, "hipMemcpyAsync(D2H)");
+      }
+    e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return fail_hip(e, "hipStreamSynchronize");
+  }
+  return LIFEAPI_OK;
+}
+
+int host_device(int device) {
+  const int ndev = lifeapi_device_count();
+  if (ndev <= 0) return fail(LIFEAPI_E_NODEVICE, "no HIP device visible%s");
+  if (device < 0) device = 0;
+  if (device >= ndev) return fail(LIFEAPI_E_NODEVICE, "bad device index%s");
+  return device;
+}
+
+int host_step_one_device(const uint64_t *in, uint64_t *out, size_t n, uint32_t gens, int dev) {
+  const HostIO io[1] = {{in, out, 512}};
+  return host_chunked(dev, n, io, 1,
+                      [](void *const *d, size_t m, hipStream_t s, const void *arg) {
+                        return lifeapi_step_batch_dev((const uint64_t *)d[0], (uint64_t *)d[0], m,
+                                                      *(const uint32_t *)arg, s);
+                      },
+                      &gens);
+}
+
+}  // namespace lifeapi_impl
+
+using namespace lifeapi_impl;
+
+extern "C" {
+
+int lifeapi_abi_version(void) { return LIFEAPI_ABI_VERSION; }
+
+const char *lifeapi_last_error(void) { return g_err.c_str(); }
+
+int lifeapi_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int lifeapi_step_batch(const uint64_t *in, uint64_t *out, size_t n, uint32_t generations,
+                       int device) {
+  int rc = check_batch(in, out, n);
+  if (rc != LIFEAPI_OK || n == 0) return rc;
+  const int ndev = lifeapi_device_count();
+  if (ndev <= 0) return fail(LIFEAPI_E_NODEVICE, "no HIP device visible%s");
+  if (device >= ndev || device < -1) return fail(LIFEAPI_E_NODEVICE, "bad device index%s");
+  if (device >= 0 || ndev == 1)
+    return host_step_one_device(in, out, n, generations, device < 0 ? 0 : device);
+  // every visible device, contiguous shards, one host thread each
+  std::vector<int> rcs(ndev, LIFEAPI_OK);
+  std::vector<std::string> errs(ndev);
+  std::vector<std::thread> pool;
+  for (int d = 0; d < ndev; ++d) {
+    const size_t lo = n * d / ndev, hi = n * (d + 1) / ndev;
+    pool.emplace_back([&, d, lo, hi] {
+      if (hi > lo) rcs[d] = host_step_one_device(in + lo * 64, out + lo * 64, hi - lo, generations, d);
+      errs[d] = g_err;
+    });
+  }
+  for (auto &t : pool) t.join();
+  for (int d = 0; d < ndev; ++d)
+    if (rcs[d] != LIFEAPI_OK) {
+      g_err = errs[d];
+      return rcs[d];
+    }
+  return LIFEAPI_OK;
+}
+
+int lifeapi_pop_batch(const uint64_t *states, uint32_t *pop, size_t n, int device) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!states || !pop || !aligned8(states)) return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_pop_batch%s");
+  const int dev = host_device(device);
+  if (dev < 0) return dev;
+  const HostIO io[2] = {{states, nullptr, 512}, {nullptr, pop, 4}};
+  return host_chunked(dev, n, io, 2,
+                      [](void *const *d, size_t m, hipStream_t s, const void *) {
+                        return lifeapi_pop_batch_dev((const uint64_t *)d[0], (uint32_t *)d[1], m, s);
+                      },
+                      nullptr);
+}
+
+int lifeapi_weld_step_batch(uint64_t *welds, size_t n, uint32_t generations, int device) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!welds || !aligned8(welds)) return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_weld_step_batch%s");
+  const int dev = host_device(device);
+  if (dev < 0) return dev;
+  const HostIO io[1] = {{welds, welds, 4 * 512}};
+  return host_chunked(dev, n, io, 1,
+                      [](void *const *d, size_t m, hipStream_t s, const void *arg) {
+                        return lifeapi_weld_step_batch_dev((uint64_t *)d[0], m, *(const uint32_t *)arg, s);
+                      },
+                      &generations);
+}
+
+int lifeapi_stable_pass_batch(uint64_t *planes, uint8_t *flags, size_t n, int pass,
+                              uint32_t max_iters, int device) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!planes || !flags || !aligned8(planes) || pass < 0 || pass > 4)
+    return fail(LIFEAPI_E_INVALID, "bad argument to lifeapi_stable_pass_batch%s");
+  const int dev = host_device(device);
+  if (dev < 0) return dev;
+  const uint32_t arg[2] = {(uint32_t)pass, max_iters};
+  const HostIO io[2] = {{planes, planes, 10 * 512}, {nullptr, flags, 1}};
+  return host_chunked(dev, n, io, 2,
+                      [](void *const *d, size_t m, hipStream_t s, const void *a) {
+                        const uint32_t *p = (const uint32_t *)a;
+                        return lifeapi_stable_pass_batch_dev((uint64_t *)d[0], (uint8_t *)d[1], m,
+                                                             (int)p[0], p[1], s);
+                      },
+                      arg);
+}
+
+int lifeapi_neighbour_count_batch(const uint64_t *in, uint64_t *out, size_t n, int device) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!in || !out || !aligned8(in) || !aligned8(out))
+    return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_neighbour_count_batch%s");
+  const int dev = host_device(device);
+  if (dev < 0) return dev;
+  const HostIO io[2] = {{in, nullptr, 512}, {nullptr, out, 4 * 512}};
+  return host_chunked(dev, n, io, 2,
+                      [](void *const *d, size_t m, hipStream_t s, const void *) {
+                        return lifeapi_neighbour_count_batch_dev((const uint64_t *)d[0], (uint64_t *)d[1], m, s);
+                      },
+                      nullptr);
+}
+
+int lifeapi_interaction_counts_batch(const uint64_t *in, uint64_t *out, size_t n, int with_next,
+                                     int device) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!in || !out || !aligned8(in) || !aligned8(out))
+    return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_interaction_counts_batch%s");
+  const int dev = host_device(device);
+  if (dev < 0) return dev;
+  const HostIO io[2] = {{in, nullptr, 512}, {nullptr, out, (with_next ? 4u : 3u) * 512}};
+  return host_chunked(dev, n, io, 2,
+                      [](void *const *d, size_t m, hipStream_t s, const void *a) {
+                        return lifeapi_interaction_counts_batch_dev((const uint64_t *)d[0], (uint64_t *)d[1],
+                                                                    m, *(const int *)a, s);
+                      },
+                      &with_next);
+}
+
+int lifeapi_refined_step_batch(const uint64_t *in, uint64_t *out, size_t n, int device) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!in || !out || !aligned8(in) || !aligned8(out))
+    return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_refined_step_batch%s");
+  const int dev = host_device(device);
+  if (dev < 0) return dev;
+  const HostIO io[2] = {{in, nullptr, 11 * 512}, {nullptr, out, 3 * 512}};
+  return host_chunked(dev, n, io, 2,
+                      [](void *const *d, size_t m, hipStream_t s, const void *) {
+                        return lifeapi_refined_step_batch_dev((const uint64_t *)d[0], (uint64_t *)d[1], m, s);
+                      },
+                      nullptr);
+}
+
+int lifeapi_contains_batch(const uint64_t *states, const uint64_t *wanted, const uint64_t *unwanted,
+                           uint8_t *out, size_t n, int device) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!states || !wanted || !unwanted || !out || !aligned8(states))
+    return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_contains_batch%s");
+  const int dev = host_device(device);
+  if (dev < 0) return dev;
+  // the target rides along as a tiny device copy owned by this call
+  DeviceGuard guard;
+  hipError_t e = hipSetDevice(dev);
+  if (e != hipSuccess) return fail_hip(e, "hipSetDevice");
+  uint64_t *dt = nullptr;
+  if ((e = hipMalloc(&dt, 2 * 512)) != hipSuccess) return fail_hip(e, "hipMalloc(target)");
+  int rc = LIFEAPI_OK;
+  if ((e = hipMemcpy(dt, wanted, 512, hipMemcpyHostToDevice)) != hipSuccess ||
+      (e = hipMemcpy(dt + 64, unwanted, 512, hipMemcpyHostToDevice)) != hipSuccess)
+    rc = fail_hip(e, "hipMemcpy(target)");
+  if (rc == LIFEAPI_OK) {
+    const HostIO io[2] = {{states, nullptr, 512}, {nullptr, out, 1}};
+    rc = host_chunked(dev, n, io, 2,
+                      [](void *const *d, size_t m, hipStream_t s, const void *a) {
+                        const uint64_t *t = (const uint64_t *)a;
+                        return lifeapi_contains_batch_dev((const uint64_t *)d[0], t, t + 64,
+                                                          (uint8_t *)d[1], m, s);
+                      },
+                      dt);
+  }
+  (void)hipFree(dt);
+  return rc;
+}
+
+}  // extern "C"

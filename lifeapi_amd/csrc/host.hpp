@@ -1,0 +1,55 @@
+// host.hpp -- host-side helpers shared by the kernel files (host.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+
+#include "common.hpp"
+#include "lifeapi_hip.h"
+
+namespace lifeapi_impl {
+
+extern thread_local std::string g_err;  // lifeapi_last_error()
+
+// set g_err (fmt has one %s for arg) and return code
+int fail(int code, const char *fmt, const char *arg = nullptr);
+// set g_err from a HIP error; missing code objects map to LIFEAPI_E_NOKERNEL
+int fail_hip(hipError_t e, const char *what);
+// CUs of the current device, which must be a gfx950
+int device_cus(int &cus);
+bool aligned8(const void *p);
+// n universes in / out: non-null, 8-byte aligned, equal or disjoint
+int check_batch(const void *in, const void *out, size_t n);
+// blocks for `waves_needed` waves, capped at cus * blocks_per_cu (0 = no cap)
+unsigned grid_for(uint64_t waves_needed, int cus, int blocks_per_cu);
+// the launch's error state as a return code
+int launched(const char *what);
+
+struct DeviceGuard {  // restores the caller's current device
+  int prev = -1;
+  DeviceGuard() { (void)hipGetDevice(&prev); }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+// One host array taking part in a host-pointer call: `bytes` per universe;
+// src -> copied in before each chunk's launch, dst -> copied out after it
+// (src == dst for in-place arrays).
+struct HostIO {
+  const void *src;
+  void *dst;
+  size_t bytes;
+};
+using ChunkFn = int (*)(void *const *dev, size_t m, hipStream_t s, const void *arg);
+
+// Stages n universes through this device's reusable buffer in chunks:
+// H2D, the stream-ordered *_dev entry point, D2H, sync.
+int host_chunked(int dev, size_t n, const HostIO *io, int nio, ChunkFn fn, const void *arg);
+// the device a host-pointer call runs on (-1 = device 0), or an error code
+int host_device(int device);
+
+}  // namespace lifeapi_impl

@@ -1,0 +1,138 @@
+// reduce.hip -- per-universe reductions and synthetic input: GetPop
+// (LifeAPI.hpp:290-298), Contains(LifeTarget) (LifeTarget.hpp:44-51), the
+// build-defined hash, and the seeded RandomState()-style fill.
+#include "device.hpp"
+#include "host.hpp"
+
+using namespace lifeapi_impl;
+
+namespace {
+
+// The per-universe reductions below take kRedU universes per wave, all loads
+// issued before the first reduction (one wave per universe and a grid-stride
+// loop left them latency-bound at 36-60 % of HBM, tools/rows_bench.py).
+constexpr int kRedU = 4;
+
+// GetPop (LifeAPI.hpp:290-298): two universes' popcounts per 32-bit reduction
+__global__ __launch_bounds__(kBlock) void k_pop(const uint64_t *__restrict__ s,
+                                                uint32_t *__restrict__ pop, uint64_t n) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock * kRedU;
+  for (uint64_t u0 = ((uint64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave) * kRedU; u0 < n;
+       u0 += stride) {
+    uint32_t c[kRedU];
+#pragma unroll
+    for (int k = 0; k < kRedU; ++k) c[k] = u0 + k < n ? (uint32_t)__popcll(s[(u0 + k) * kWave + lane]) : 0u;
+#pragma unroll
+    for (int k = 0; k < kRedU; k += 2) {
+      const uint32_t t = wave_sum_u32(c[k] | c[k + 1] << 16);  // each sum <= 4096
+      if (lane == 0) {
+        if (u0 + k < n) pop[u0 + k] = t & 0xFFFF;
+        if (u0 + k + 1 < n) pop[u0 + k + 1] = t >> 16;
+      }
+    }
+  }
+}
+
+// build-defined universe hash: mix(sum_x mix(s[x] + (x+1)*G))
+__global__ __launch_bounds__(kBlock) void k_hash(const uint64_t *__restrict__ s,
+                                                 uint64_t *__restrict__ h, uint64_t n) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock * kRedU;
+  for (uint64_t u0 = ((uint64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave) * kRedU; u0 < n;
+       u0 += stride) {
+    uint64_t m[kRedU];
+#pragma unroll
+    for (int k = 0; k < kRedU; ++k) m[k] = u0 + k < n ? s[(u0 + k) * kWave + lane] : 0ull;
+#pragma unroll
+    for (int k = 0; k < kRedU; ++k) {
+      const uint64_t t = wave_sum_u64(mix64(m[k] + (uint64_t)(lane + 1) * kGolden));
+      if (lane == 0 && u0 + k < n) h[u0 + k] = mix64(t);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_contains(const uint64_t *__restrict__ s,
+                                                     const uint64_t *__restrict__ wanted,
+                                                     const uint64_t *__restrict__ unwanted,
+                                                     uint8_t *__restrict__ out, uint64_t n) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const W w = split(wanted[lane]), uw = split(unwanted[lane]);
+  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock * kRedU;
+  for (uint64_t u0 = ((uint64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave) * kRedU; u0 < n;
+       u0 += stride) {
+    W a[kRedU];
+#pragma unroll
+    for (int k = 0; k < kRedU; ++k) a[k] = u0 + k < n ? split(s[(u0 + k) * kWave + lane]) : W{0u, 0u};
+#pragma unroll
+    for (int k = 0; k < kRedU; ++k) {
+      const bool c = wave_contains(a[k], w, uw);
+      if (lane == 0 && u0 + k < n) out[u0 + k] = c ? 1 : 0;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_fill(uint64_t *__restrict__ out, uint64_t nwords,
+                                                 uint64_t seed, uint64_t first_word, int mode) {
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < nwords; i += stride) {
+    uint64_t v = mix64(seed + (first_word + i + 1) * kGolden);
+    if (mode == 1) v = (v & ((1ULL << 61) - 1)) | (1ULL << 61);
+    __builtin_nontemporal_store(v, out + i);
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int lifeapi_pop_batch_dev(const uint64_t *d_states, uint32_t *d_pop, size_t n, void *stream) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!d_states || !d_pop || !aligned8(d_states) || ((uintptr_t)d_pop & 3u))
+    return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_pop_batch_dev%s");
+  int cus = 0, rc = device_cus(cus);
+  if (rc != LIFEAPI_OK) return rc;
+  hipLaunchKernelGGL(k_pop, dim3(grid_for((n + kRedU - 1) / kRedU, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream,
+                     d_states, d_pop, (uint64_t)n);
+  return launched("k_pop launch");
+}
+
+int lifeapi_hash_batch_dev(const uint64_t *d_states, uint64_t *d_hash, size_t n, void *stream) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!d_states || !d_hash || !aligned8(d_states) || !aligned8(d_hash))
+    return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_hash_batch_dev%s");
+  int cus = 0, rc = device_cus(cus);
+  if (rc != LIFEAPI_OK) return rc;
+  hipLaunchKernelGGL(k_hash, dim3(grid_for((n + kRedU - 1) / kRedU, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream,
+                     d_states, d_hash, (uint64_t)n);
+  return launched("k_hash launch");
+}
+
+int lifeapi_contains_batch_dev(const uint64_t *d_states, const uint64_t *d_wanted,
+                               const uint64_t *d_unwanted, uint8_t *d_out, size_t n,
+                               void *stream) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!d_states || !d_wanted || !d_unwanted || !d_out || !aligned8(d_states) ||
+      !aligned8(d_wanted) || !aligned8(d_unwanted))
+    return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_contains_batch_dev%s");
+  int cus = 0, rc = device_cus(cus);
+  if (rc != LIFEAPI_OK) return rc;
+  hipLaunchKernelGGL(k_contains, dim3(grid_for((n + kRedU - 1) / kRedU, cus, 0)), dim3(kBlock), 0,
+                     (hipStream_t)stream, d_states, d_wanted, d_unwanted, d_out, (uint64_t)n);
+  return launched("k_contains launch");
+}
+
+int lifeapi_fill_random_dev(uint64_t *d_out, size_t n, uint64_t seed, uint64_t first_universe,
+                            int mode, void *stream) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!d_out || !aligned8(d_out) || (mode != 0 && mode != 1))
+    return fail(LIFEAPI_E_INVALID, "bad argument to lifeapi_fill_random_dev%s");
+  int cus = 0, rc = device_cus(cus);
+  if (rc != LIFEAPI_OK) return rc;
+  const uint64_t words = (uint64_t)n * kWave;
+  hipLaunchKernelGGL(k_fill, dim3(grid_for(words / kWave, cus, 0)), dim3(kBlock), 0,
+                     (hipStream_t)stream, d_out, words, seed, first_universe * kWave, mode);
+  return launched("k_fill launch");
+}
+
+}  // extern "C"

@@ -1,0 +1,177 @@
+// split_layout.hpp -- register layouts of the iterated Step() (RULE 4..7):
+// the even/odd row split and the S-way row splits with S/2 universes
+// interleaved bit by bit, and one generation on them.
+#pragma once
+
+#include "device.hpp"
+
+namespace lifeapi_impl {
+
+// ---- even/odd row layout (RULE 4) ----
+// A 64-bit column held as (E, O): E bit k = row 2k, O bit k = row 2k+1.  The
+// vertical neighbours of row 2k are O bits k-1 and k; those of row 2k+1 are
+// E bits k and k+1.  So a vertical triple costs one 32-bit rotate per plane
+// and parity instead of two 64-bit rotates (four v_alignbit) per plane, and a
+// v_alignbit issues at half rate on gfx950 (tools/bank_probe.hip).
+__device__ __forceinline__ uint32_t delta_swap(uint32_t x, uint32_t m, int s) {
+  const uint32_t t = ((x >> s) ^ x) & m;
+  return x ^ t ^ (t << s);
+}
+// even bits -> low half, odd bits -> high half
+__device__ __forceinline__ uint32_t unzip32(uint32_t x) {
+  x = delta_swap(x, 0x22222222u, 1);
+  x = delta_swap(x, 0x0C0C0C0Cu, 2);
+  x = delta_swap(x, 0x00F000F0u, 4);
+  return delta_swap(x, 0x0000FF00u, 8);
+}
+__device__ __forceinline__ uint32_t zip32(uint32_t x) {
+  x = delta_swap(x, 0x0000FF00u, 8);
+  x = delta_swap(x, 0x00F000F0u, 4);
+  x = delta_swap(x, 0x0C0C0C0Cu, 2);
+  return delta_swap(x, 0x22222222u, 1);
+}
+__device__ __forceinline__ W to_eo(W a) {  // (lo, hi) rows -> (E, O)
+  const uint32_t l = unzip32(a.lo), h = unzip32(a.hi);
+  return W{__builtin_amdgcn_perm(h, l, 0x05040100u), __builtin_amdgcn_perm(h, l, 0x07060302u)};
+}
+__device__ __forceinline__ W from_eo(W e) {
+  return W{zip32(__builtin_amdgcn_perm(e.hi, e.lo, 0x05040100u)),
+           zip32(__builtin_amdgcn_perm(e.hi, e.lo, 0x07060302u))};
+}
+__device__ __forceinline__ uint32_t rotl1(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 31); }
+__device__ __forceinline__ uint32_t rotr1(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 1); }
+
+// ------------------------------------------------------------------------
+// Row-split layouts (RULE 5: S = 4, RULE 6: S = 8, RULE 7: S = 16)
+// ------------------------------------------------------------------------
+//
+// P = S/2 universes share a lane's S registers: bit P*k + u of R_j holds
+// universe u, row S*k + j (k < 64/S).  The vertical neighbours of R_j are
+// R_{j-1} and R_{j+1} at the same bit, except at the ends of the register
+// ring: R_0's upper neighbour is R_{S-1} rotated left by P bits, R_{S-1}'s
+// lower one is R_0 rotated right by P bits.  Because the P universes are
+// interleaved bit by bit, one 32-bit rotate by P rotates all P of their
+// 64/S-row rings at once.  Per register and generation that leaves the nine
+// v_bitop3 of the RULE 3 network plus 4/S v_alignbit (two per plane per
+// ring), against 9 + 2 for the even/odd split (S = 2, RULE 4).  The
+// exchange goes through LDS (lane-major, S words per lane).
+
+// Layout change by index-bit transpositions.  Number the 8*P source words
+// X[2u + h] = universe u's column, h = high half (rows 32..63); a bit is then
+// addressed by (register index bits | 5 position bits).  Exchanging register
+// index bit a with position bit b (shift s = 2^b) is one delta swap per pair
+// of registers:  t = ((A >> s) ^ B) & m_b;  B ^= t;  A ^= t << s.  Five such
+// swaps route the row's upper bits k to the top of the word, the universe
+// bits below them and the row's low bits j into the register index; the
+// target register R_j is then a fixed renaming of X.  Each swap is its own
+// inverse, so the store path runs them backwards.  About 30 VALU per
+// universe each way (tools/split_layout.py checks the tables).
+template <int S>
+struct SplitNet;
+template <>
+struct SplitNet<2> {  // R_j: j = row bit 0;            (E, O) of RULE 4
+  [[maybe_unused]] static constexpr int a[5] = {0, 0, 0, 0, 0};
+  static constexpr __device__ int reg(int j) { return j; }
+};
+template <>
+struct SplitNet<4> {  // R_j: j = row bits 1..0, 2 universes
+  static constexpr int a[5] = {0, 0, 0, 0, 1};
+  static constexpr __device__ int reg(int j) { return ((j & 1) << 1) | (j >> 1); }
+};
+template <>
+struct SplitNet<8> {  // R_j: j = row bits 2..0, 4 universes
+  static constexpr int a[5] = {0, 0, 0, 2, 1};
+  static constexpr __device__ int reg(int j) { return ((j & 3) << 1) | (j >> 2); }
+};
+
+template <>
+struct SplitNet<16> {  // R_j: j = row bits 3..0, 8 universes
+  static constexpr int a[5] = {0, 0, 3, 2, 1};
+  static constexpr __device__ int reg(int j) { return ((j & 7) << 1) | (j >> 3); }
+};
+
+template <int S>
+__device__ __forceinline__ void split_swap(uint32_t (&x)[S], int stage) {
+  constexpr uint32_t masks[5] = {0x0000FFFFu, 0x00FF00FFu, 0x0F0F0F0Fu, 0x33333333u, 0x55555555u};
+  const int a = SplitNet<S>::a[stage], sh = 16 >> stage;
+  const uint32_t m = masks[stage];
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    if ((i >> a) & 1) continue;
+    const int k = i | (1 << a);
+    const uint32_t t = ((x[i] >> sh) ^ x[k]) & m;
+    x[k] ^= t;
+    x[i] ^= t << sh;
+  }
+}
+
+template <int S>
+struct Split {
+  static constexpr int P = S / 2;
+  static __device__ __forceinline__ void load(const W (&c)[P], uint32_t (&r)[S]) {
+    uint32_t x[S];
+#pragma unroll
+    for (int u = 0; u < P; ++u) x[2 * u] = c[u].lo, x[2 * u + 1] = c[u].hi;
+#pragma unroll
+    for (int st = 0; st < 5; ++st) split_swap<S>(x, st);
+#pragma unroll
+    for (int j = 0; j < S; ++j) r[j] = x[SplitNet<S>::reg(j)];
+  }
+  static __device__ __forceinline__ void store(const uint32_t (&r)[S], W (&c)[P]) {
+    uint32_t x[S];
+#pragma unroll
+    for (int j = 0; j < S; ++j) x[SplitNet<S>::reg(j)] = r[j];
+#pragma unroll
+    for (int st = 4; st >= 0; --st) split_swap<S>(x, st);
+#pragma unroll
+    for (int u = 0; u < P; ++u) c[u] = W{x[2 * u], x[2 * u + 1]};
+  }
+};
+
+// one generation of the P universes in r[] (RULE 3 network per register)
+template <int S>
+__device__ __forceinline__ void gen_split(uint32_t (&r)[S], uint32_t *slot, int lane) {
+  constexpr int P = S / 2;
+  // LDS planes of Q <= 4 words per lane: 16-B lane stride keeps ds_write_b128
+  // / ds_read_b128 free of bank conflicts (a 32-B stride would be 2-way)
+  constexpr int Q = S < 4 ? S : 4;
+  typedef uint32_t vec __attribute__((ext_vector_type(Q)));
+  vec *v = reinterpret_cast<vec *>(slot);
+  const int xp = (lane + kWave - 1) & (kWave - 1), xn = (lane + 1) & (kWave - 1);
+#pragma unroll
+  for (int p = 0; p < S / Q; ++p) {
+    vec mine;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) mine[q] = r[p * Q + q];
+    v[p * kWave + lane] = mine;  // a wave's LDS operations complete in order; the
+  }                              // store and the loads may alias, so the compiler
+  uint32_t lv[S], rv[S];         // keeps their order
+#pragma unroll
+  for (int p = 0; p < S / Q; ++p) {
+    const vec l = v[p * kWave + xp], rr = v[p * kWave + xn];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) lv[p * Q + q] = l[q], rv[p * Q + q] = rr[q];
+  }
+  uint32_t h0[S], h1[S];
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    h0[j] = lut3<kXor3>(lv[j], r[j], rv[j]);
+    h1[j] = lut3<kMaj>(lv[j], r[j], rv[j]);
+  }
+  const uint32_t h0u = __builtin_amdgcn_alignbit(h0[S - 1], h0[S - 1], 32 - P);  // rotl P
+  const uint32_t h1u = __builtin_amdgcn_alignbit(h1[S - 1], h1[S - 1], 32 - P);
+  const uint32_t h0d = __builtin_amdgcn_alignbit(h0[0], h0[0], P);  // rotr P
+  const uint32_t h1d = __builtin_amdgcn_alignbit(h1[0], h1[0], P);
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    const uint32_t a0 = j == 0 ? h0u : h0[j - 1], c0 = j == S - 1 ? h0d : h0[j + 1];
+    const uint32_t a1 = j == 0 ? h1u : h1[j - 1], c1 = j == S - 1 ? h1d : h1[j + 1];
+    const uint32_t s0 = lut3<kLe1>(a0, h0[j], c0), s1 = lut3<kNae>(a0, h0[j], c0);
+    const uint32_t s2 = lut3<kLe1>(a1, h1[j], c1), s3 = lut3<kEven>(a1, h1[j], c1);
+    const uint32_t t1 = lut3<kT1>(s0, s1, r[j]);
+    const uint32_t t2 = lut3<kT2>(s2, r[j], t1);
+    r[j] = lut3<kT3>(s1, s3, t2);
+  }
+}
+
+}  // namespace lifeapi_impl

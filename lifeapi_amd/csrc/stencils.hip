@@ -1,0 +1,439 @@
+// stencils.hip -- the other per-generation stencils of SURVEY 8(f):
+// NeighbourCount / InteractionCounts (LifeAPI.hpp:909-1040), LifeWeld::Step
+// (LifeWeld.hpp:169-186), the LifeStable propagation passes
+// (LifeStable.hpp:526-729) and the config-5 unknown_step_refined step.
+#include "device.hpp"
+#include "host.hpp"
+
+using namespace lifeapi_impl;
+
+namespace {
+
+// ---- neighbourhood counters --------------------------
+
+// Bits 2..0 of the inclusive 3x3 count of this lane's column: the
+// NeighbourCount adder chain (NeighbourCount.hpp:40-70) in the row-first
+// order of life_gen<RULE 2> (4 DPP moves): count = fs + 2(fc+cs) + 4cc.
+__device__ __forceinline__ void ncount3(W a, W &b2, W &b1, W &b0) {
+  W L, R;
+  neighbour_cols<XDPP>(a, L, R, nullptr, 0);
+  const W h0 = lut3<kXor3>(L, a, R), h1 = lut3<kMaj>(L, a, R);
+  const W h0u = rot_up(h0), h0d = rot_dn(h0), h1u = rot_up(h1), h1d = rot_dn(h1);
+  const W fs = lut3<kXor3>(h0u, h0, h0d), fc = lut3<kMaj>(h0u, h0, h0d);
+  const W cs = lut3<kXor3>(h1u, h1, h1d), cc = lut3<kMaj>(h1u, h1, h1d);
+  b0 = fs;
+  b1 = W{fc.lo ^ cs.lo, fc.hi ^ cs.hi};
+  b2 = lut3<kCarry2>(cc, fc, cs);
+}
+// Same stencil as Step(), different output planes.  The two FullAdds of the
+// vertical planes give the inclusive 3x3 count = fs + 2(fc + cs) + 4cc.
+// MODE 0: NeighbourCount / CountNeighbourhood (NeighbourCount.hpp:40-70,
+//         LifeAPI.hpp:909-952): planes bit3, bit2, bit1, bit0.
+// MODE 1: InteractionCounts (LifeAPI.hpp:956-993): out1, out2, outMore.
+// MODE 2: InteractionCountsAndNext (LifeAPI.hpp:997-1040): out1, out2,
+//         outMore, next.
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_counts(const uint64_t *__restrict__ in,
+                                                   uint64_t *__restrict__ out, uint64_t n) {
+  constexpr int P = MODE == 1 ? 3 : 4;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock;
+  for (uint64_t u = (uint64_t)blockIdx.x * kWavesPerBlock + wib; u < n; u += stride) {
+    const W a = ld<true>(in + u * kWave + lane);
+    const W up = rot_up(a), dn = rot_dn(a);
+    const W c0 = lut3<kXor3>(up, dn, a), c1 = lut3<kMaj>(up, dn, a);
+    W L0, R0, L1, R1;
+    neighbours<XDPP>(c0, c1, L0, R0, L1, R1, nullptr, lane);
+    const W fs = lut3<kXor3>(L0, c0, R0), fc = lut3<kMaj>(L0, c0, R0);
+    const W cs = lut3<kXor3>(L1, c1, R1), cc = lut3<kMaj>(L1, c1, R1);
+    uint64_t *q = out + u * P * kWave + lane;
+    const uint64_t s = join(a), vfs = join(fs), vfc = join(fc), vcs = join(cs), vcc = join(cc);
+    if constexpr (MODE == 0) {
+      const uint64_t carry = vfc & vcs;
+      st<true>(q + 0 * kWave, split(vcc & carry));          // bit3
+      st<true>(q + 1 * kWave, split(vcc ^ carry));          // bit2
+      st<true>(q + 2 * kWave, split(vfc ^ vcs));            // bit1
+      st<true>(q + 3 * kWave, fs);                          // bit0
+    } else {
+      const uint64_t o1 = ~s & ~vcc & vfs & ~vcs & ~vfc;
+      const uint64_t o2 = ~s & ~vcc & ~vfs & (vcs ^ vfc);
+      const uint64_t om = ~s & ~o2 & (vfc | vcs | vcc);
+      st<true>(q + 0 * kWave, split(o1));
+      st<true>(q + 1 * kWave, split(o2));
+      st<true>(q + 2 * kWave, split(om));
+      if constexpr (MODE == 2) {
+        const uint64_t c2 = vcc ^ (vcs & vfc);
+        st<true>(q + 3 * kWave, split((vfs ^ c2) & (vfc ^ vcs ^ c2) & (s | vfs)));
+      }
+    }
+  }
+}
+
+// ---- LifeWeld::Step ----------------------------------
+// LifeWeld.hpp:169-186: inclusive count bits 2..0 (CountNeighbourhood, bit3
+// dropped) + the frozen 3-bit count (HalfAdd, FullAdd, FullAdd), then the
+// Life rule on the sum.  The frozen planes are loop-invariant, so `gens`
+// generations run in registers.  In place on LifeWeld[] = {state, frozen2,
+// frozen1, frozen0} x 64 words; only the state plane is written back.
+__device__ __forceinline__ W weld_gen(W s, W f2, W f1, W f0) {
+  W b2, b1, b0;
+  ncount3(s, b2, b1, b0);
+  const W s0 = W{b0.lo ^ f0.lo, b0.hi ^ f0.hi}, k0 = W{b0.lo & f0.lo, b0.hi & f0.hi};
+  const W s1 = lut3<kXor3>(b1, f1, k0), k1 = lut3<kMaj>(b1, f1, k0);
+  const W s2 = lut3<kXor3>(b2, f2, k1);
+  const W p = lut3<kLive>(s0, s2, s);  // (s0 ^ s2) & (s | s0)
+  return W{p.lo & (s1.lo ^ s2.lo), p.hi & (s1.hi ^ s2.hi)};
+}
+
+__global__ __launch_bounds__(kBlock) void k_weld(uint64_t *__restrict__ welds, uint64_t n,
+                                                 uint32_t gens) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock;
+  for (uint64_t u = (uint64_t)blockIdx.x * kWavesPerBlock + wib; u < n; u += stride) {
+    uint64_t *p = welds + u * 4 * kWave + lane;
+    W s = ld<false>(p);
+    const W f2 = ld<false>(p + kWave), f1 = ld<false>(p + 2 * kWave), f0 = ld<false>(p + 3 * kWave);
+    for (uint32_t g = 0; g < gens; ++g) s = weld_gen(s, f2, f1, f0);
+    st<false>(p, s);
+  }
+}
+
+// ---- LifeStable passes --------------------------------
+// One wave per LifeStable: lane x holds column x of its 10 planes {state,
+// unknown, live2, live3, dead0, dead1, dead2, dead4, dead5, dead6}
+// (LifeStable.hpp:41-53; options "1 = ruled out").  The espresso fragments
+// the passes #include (bitslicing/stable_count.hpp, stable_signal.hpp) are
+// v_bitop3 networks generated by tools/synth_sop.py from their complete
+// truth tables.  Whole-universe tests (abort, changed) are wave ballots.
+
+__device__ __forceinline__ W operator&(W a, W b) { return W{a.lo & b.lo, a.hi & b.hi}; }
+__device__ __forceinline__ W operator|(W a, W b) { return W{a.lo | b.lo, a.hi | b.hi}; }
+__device__ __forceinline__ W operator~(W a) { return W{~a.lo, ~a.hi}; }
+__device__ __forceinline__ bool wave_any(W a) { return __ballot((a.lo | a.hi) != 0u) != 0ull; }
+
+// all four bits of the inclusive 3x3 count (NeighbourCount.hpp:40-70)
+__device__ __forceinline__ void ncount4(W a, W &b3, W &b2, W &b1, W &b0) {
+  W L, R;
+  neighbour_cols<XDPP>(a, L, R, nullptr, 0);
+  const W h0 = lut3<kXor3>(L, a, R), h1 = lut3<kMaj>(L, a, R);
+  const W h0u = rot_up(h0), h0d = rot_dn(h0), h1u = rot_up(h1), h1d = rot_dn(h1);
+  const W fs = lut3<kXor3>(h0u, h0, h0d), fc = lut3<kMaj>(h0u, h0, h0d);
+  const W cs = lut3<kXor3>(h1u, h1, h1d), cc = lut3<kMaj>(h1u, h1, h1d);
+  constexpr uint32_t kAnd3 = (TA & TB & TC) & 0xFF;
+  b0 = fs;
+  b1 = W{fc.lo ^ cs.lo, fc.hi ^ cs.hi};
+  b2 = lut3<kCarry2>(cc, fc, cs);
+  b3 = lut3<kAnd3>(cc, fc, cs);
+}
+
+// LifeState::ZOIHollow (LifeAPI.hpp:541-562): the 8 neighbours' OR
+__device__ __forceinline__ W zoi_hollow(W s) {
+  const W m = rot_up(s) | rot_dn(s);
+  const W t = s | m;
+  W L, R;
+  neighbour_cols<XDPP>(t, L, R, nullptr, 0);
+  return L | m | R;
+}
+
+template <class T>
+__device__ __forceinline__ void stable_count_circuit(const T (&x)[9], T &l2, T &l3, T &d0, T &d1,
+                                                     T &d2, T &d4, T &d5, T &d6, T &abort) {
+#include "stable_count_circuit.inc"
+}
+template <class T>
+__device__ __forceinline__ void stable_signal_circuit(const T (&x)[17], T &signaloff, T &signalon,
+                                                      T &centeroff, T &centeron) {
+#include "stable_signal_circuit.inc"
+}
+
+enum { PST, PUN, PL2, PL3, PD0, PD1, PD2, PD4, PD5, PD6 };
+
+// SynchroniseStateKnown, LifeStable.hpp:526-556
+__device__ __forceinline__ int stable_sync(W (&p)[10]) {
+  const W known_on = ~p[PUN] & p[PST];
+  const W maybe_dead = ~(p[PD0] & p[PD1] & p[PD2] & p[PD4] & p[PD5] & p[PD6]);
+  W changes = maybe_dead & known_on;
+#pragma unroll
+  for (int k = PD0; k <= PD6; ++k) p[k] = p[k] | known_on;
+  const W known_off = ~p[PUN] & ~p[PST];
+  const W maybe_live = ~(p[PL2] & p[PL3]);
+  changes = changes | (maybe_live & known_off);
+  p[PL2] = p[PL2] | known_off;
+  p[PL3] = p[PL3] | known_off;
+  if (wave_any(~maybe_live & ~maybe_dead)) return 0;
+  changes = changes | (~p[PST] & (maybe_live & ~maybe_dead));
+  p[PST] = p[PST] | (maybe_live & ~maybe_dead);
+  changes = changes | (~p[PUN] & (maybe_live & maybe_dead));
+  p[PUN] = p[PUN] & (maybe_live & maybe_dead);
+  return 1 | (wave_any(changes) ? 2 : 0);
+}
+
+// UpdateOptions, LifeStable.hpp:558-615 (stable_count.hpp at :591)
+__device__ __forceinline__ int stable_options(W (&p)[10]) {
+  const W off = ~p[PUN] & ~p[PST];
+  W s3, s2, s1, s0, o3, o2, o1, o0;
+  ncount4(p[PST], s3, s2, s1, s0);
+  ncount4(off, o3, o2, o1, o0);
+  const W x[9] = {s2, s1, s0, o3, o2, o1, o0, p[PST], off};
+  W r[8], ab;
+  stable_count_circuit(x, r[0], r[1], r[2], r[3], r[4], r[5], r[6], r[7], ab);
+  W changes = W{0u, 0u};
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    changes = changes | (r[k] & ~p[PL2 + k]);
+    p[PL2 + k] = p[PL2 + k] | r[k];
+  }
+  return (wave_any(ab) ? 0 : 1) | (wave_any(changes) ? 2 : 0);
+}
+
+// SignalNeighbours, LifeStable.hpp:617-675 (stable_signal.hpp at :654),
+// then SetOff / SetOn (:320-335)
+__device__ __forceinline__ int stable_signal(W (&p)[10]) {
+  W s3, s2, s1, s0, m3, m2, m1, m0;
+  ncount4(p[PST], s3, s2, s1, s0);
+  ncount4(p[PST] | p[PUN], m3, m2, m1, m0);
+  const W x[17] = {p[PL2], p[PL3], p[PD0], p[PD1], p[PD2], p[PD4], p[PD5], p[PD6], s2, s1, s0,
+                   m3, m2, m1, m0, p[PST], p[PUN]};
+  W soff, son, coff, con;
+  stable_signal_circuit(x, soff, son, coff, con);
+  const W off_zoi = zoi_hollow(soff) | coff, on_zoi = zoi_hollow(son) | con;
+  if (wave_any(off_zoi & on_zoi & p[PUN])) return 0;
+  const W changes = (off_zoi & p[PUN]) | (on_zoi & p[PUN]);
+  const W w_off = off_zoi & p[PUN];
+  p[PST] = p[PST] & ~w_off;
+  p[PUN] = p[PUN] & ~w_off;
+  p[PL2] = p[PL2] | w_off;
+  p[PL3] = p[PL3] | w_off;
+  const W w_on = on_zoi & p[PUN];
+  p[PST] = p[PST] | w_on;
+  p[PUN] = p[PUN] & ~w_on;
+#pragma unroll
+  for (int k = PD0; k <= PD6; ++k) p[k] = p[k] | w_on;
+  return 1 | (wave_any(changes) ? 2 : 0);
+}
+
+// PropagateStep, LifeStable.hpp:695-716
+__device__ __forceinline__ int stable_step(W (&p)[10]) {
+  const int k = stable_sync(p);
+  if (!(k & 1)) return 0;
+  const int o = stable_options(p);
+  if (!(o & 1)) return 0;
+  const int s = stable_signal(p);
+  if (!(s & 1)) return 0;
+  return 1 | ((k | o | s) & 2);
+}
+
+// PASS 0..3: one pass; 4: Propagate (LifeStable.hpp:718-729), at most
+// max_iters PropagateSteps (flag bit 2 set if that bound stopped it).
+template <int PASS>
+__global__ __launch_bounds__(kBlock) void k_stable(uint64_t *__restrict__ planes,
+                                                   uint8_t *__restrict__ flags, uint64_t n,
+                                                   uint32_t max_iters) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock;
+  for (uint64_t u = (uint64_t)blockIdx.x * kWavesPerBlock + wib; u < n; u += stride) {
+    uint64_t *q = planes + u * 10 * kWave + lane;
+    W p[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) p[k] = ld<false>(q + k * kWave);
+    int r;
+    if constexpr (PASS == 0) r = stable_sync(p);
+    else if constexpr (PASS == 1) r = stable_options(p);
+    else if constexpr (PASS == 2) r = stable_signal(p);
+    else if constexpr (PASS == 3) r = stable_step(p);
+    else {
+      int ever = 0;
+      r = -1;
+      for (uint32_t it = 0; it < max_iters; ++it) {
+        const int s = stable_step(p);
+        if (!(s & 1)) { r = 0; break; }
+        if (!(s & 2)) { r = 1 | ever; break; }
+        ever = 2;
+      }
+      if (r < 0) r = 1 | ever | 4;
+    }
+#pragma unroll
+    for (int k = 0; k < 10; ++k) st<false>(q + k * kWave, p[k]);
+    if (lane == 0) flags[u] = (uint8_t)r;
+  }
+}
+
+// ---- config 5: the unknown_step_refined ternary step --------------------
+
+// bitslicing/unknown_step_refined.hpp:1-85 as a v_bitop3 network.  The
+// network is generated (tools/synth_sop.py) from the fragment's complete
+// truth table, which tests/golden/make_golden.py extracts from the reference
+// build, and is verified against all 2^16 input combinations when generated.
+template <class T>
+__device__ __forceinline__ void refined_circuit(const T (&x)[16], T &next_on, T &next_unknown,
+                                                T &next_unknown_stable) {
+#include "refined_circuit.inc"
+}
+
+__device__ __forceinline__ void refined_load(W (&pl)[11], const uint64_t *in, uint64_t u, int lane) {
+  const uint64_t *p = in + u * 11 * kWave + lane;
+#pragma unroll
+  for (int k = 0; k < 11; ++k) pl[k] = ld<true>(p + k * kWave);
+}
+
+__device__ __forceinline__ void refined_one(const W (&pl)[11], uint64_t *out, uint64_t u, int lane) {
+  W x[16];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) x[k] = pl[3 + k];  // l2 l3 d0 d1 d2 d4 d5 d6
+  x[8] = pl[2];                                  // current_unknown
+  x[9] = pl[1];                                  // current_on
+  ncount3(pl[0], x[10], x[11], x[12]);           // s2 s1 s0
+  ncount3(pl[1], x[13], x[14], x[15]);           // on2 on1 on0
+  // Evaluate the ~500-node network on the low and then the high 32 bits of
+  // the column: the scheduling barrier keeps the two halves from being
+  // interleaved, which halves the live temporaries (VGPR pressure).
+  uint32_t xl[16], xh[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    xl[k] = x[k].lo;
+    xh[k] = x[k].hi;
+  }
+  W o0, o1, o2;
+  refined_circuit(xl, o0.lo, o1.lo, o2.lo);
+  __builtin_amdgcn_sched_barrier(0);
+  refined_circuit(xh, o0.hi, o1.hi, o2.hi);
+  uint64_t *q = out + u * 3 * kWave + lane;
+  st<true>(q, o0);
+  st<true>(q + kWave, o1);
+  st<true>(q + 2 * kWave, o2);
+}
+
+// One wave per universe at a time, grid-strided.  In: 11 planes x 64 words
+// (stable.state, current.state, current.unknown, live2, live3, dead0, dead1,
+// dead2, dead4, dead5, dead6 -- LifeStable.hpp:41-53 with options stored as
+// "1 = ruled out").  Out: 3 planes (next_on, next_unknown,
+// next_unknown_stable).  PF = 1: the next universe's 11 loads are issued
+// before this one's ~1000-instruction network runs (register double buffer),
+// so HBM traffic overlaps the VALU work of the same wave.  OCC = minimum
+// waves per SIMD requested from the register allocator (0 = no bound).
+template <int PF, int OCC>
+__global__ __launch_bounds__(kBlock, OCC > 0 ? OCC : 1) void k_refined(
+    const uint64_t *__restrict__ in, uint64_t *__restrict__ out, uint64_t n) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock;
+  uint64_t u = (uint64_t)blockIdx.x * kWavesPerBlock + wib;
+  if (u >= n) return;
+  if constexpr (PF == 0) {
+    for (; u < n; u += stride) {
+      W pl[11];
+      refined_load(pl, in, u, lane);
+      refined_one(pl, out, u, lane);
+    }
+  } else {
+    W cur[11];
+    refined_load(cur, in, u, lane);
+    for (; u < n; u += stride) {
+      const uint64_t un = u + stride;
+      W nxt[11];
+      if (un < n) refined_load(nxt, in, un, lane);
+      refined_one(cur, out, u, lane);
+      if (un < n) {
+#pragma unroll
+        for (int k = 0; k < 11; ++k) cur[k] = nxt[k];
+      }
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+static int counts_launch(const uint64_t *d_in, uint64_t *d_out, size_t n, int mode, void *stream) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!d_in || !d_out || !aligned8(d_in) || !aligned8(d_out))
+    return fail(LIFEAPI_E_INVALID, "bad pointer to a neighbourhood-count entry point%s");
+  const size_t planes = mode == 1 ? 3 : 4;
+  const uintptr_t a = (uintptr_t)d_in, b = (uintptr_t)d_out;
+  if (a < b + n * planes * 512 && b < a + n * 512)
+    return fail(LIFEAPI_E_INVALID, "count input and output overlap%s");
+  int cus = 0, rc = device_cus(cus);
+  if (rc != LIFEAPI_OK) return rc;
+  using Fn = void (*)(const uint64_t *, uint64_t *, uint64_t);
+  Fn fn = mode == 0 ? (Fn)k_counts<0> : mode == 1 ? (Fn)k_counts<1> : (Fn)k_counts<2>;
+  hipLaunchKernelGGL(fn, dim3(grid_for(n, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream, d_in,
+                     d_out, (uint64_t)n);
+  return launched("k_counts launch");
+}
+
+int lifeapi_stable_pass_batch_dev(uint64_t *d_planes, uint8_t *d_flags, size_t n, int pass,
+                                  uint32_t max_iters, void *stream) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!d_planes || !d_flags || !aligned8(d_planes) || pass < 0 || pass > 4)
+    return fail(LIFEAPI_E_INVALID, "bad argument to lifeapi_stable_pass_batch_dev%s");
+  const uintptr_t a = (uintptr_t)d_planes, b = (uintptr_t)d_flags;
+  if (b < a + n * 10 * 512 && a < b + n) return fail(LIFEAPI_E_INVALID, "flags overlap planes%s");
+  int cus = 0, rc = device_cus(cus);
+  if (rc != LIFEAPI_OK) return rc;
+  using Fn = void (*)(uint64_t *, uint8_t *, uint64_t, uint32_t);
+  const Fn fns[5] = {k_stable<0>, k_stable<1>, k_stable<2>, k_stable<3>, k_stable<4>};
+  hipLaunchKernelGGL(fns[pass], dim3(grid_for(n, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream,
+                     d_planes, d_flags, (uint64_t)n, max_iters ? max_iters : 1u << 20);
+  return launched("k_stable launch");
+}
+
+int lifeapi_weld_step_batch_dev(uint64_t *d_welds, size_t n, uint32_t generations, void *stream) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!d_welds || !aligned8(d_welds))
+    return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_weld_step_batch_dev%s");
+  int cus = 0, rc = device_cus(cus);
+  if (rc != LIFEAPI_OK) return rc;
+  hipLaunchKernelGGL(k_weld, dim3(grid_for(n, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream,
+                     d_welds, (uint64_t)n, generations);
+  return launched("k_weld launch");
+}
+
+int lifeapi_neighbour_count_batch_dev(const uint64_t *d_in, uint64_t *d_out, size_t n, void *stream) {
+  return counts_launch(d_in, d_out, n, 0, stream);
+}
+
+int lifeapi_interaction_counts_batch_dev(const uint64_t *d_in, uint64_t *d_out, size_t n,
+                                         int with_next, void *stream) {
+  return counts_launch(d_in, d_out, n, with_next ? 2 : 1, stream);
+}
+
+int lifeapi_refined_step_batch_dev_cfg(const uint64_t *d_in, uint64_t *d_out, size_t n,
+                                       void *stream, const lifeapi_launch_cfg *cfg) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!d_in || !d_out || !aligned8(d_in) || !aligned8(d_out))
+    return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_refined_step_batch_dev%s");
+  const uintptr_t a = (uintptr_t)d_in, b = (uintptr_t)d_out;
+  if (a < b + n * 3 * 512 && b < a + n * 11 * 512)
+    return fail(LIFEAPI_E_INVALID, "refined step input and output overlap%s");
+  // cfg: universes_per_wave 1 = no prefetch, 2 = prefetch next universe;
+  // blocks_per_cu = grid cap; rule = minimum waves per SIMD requested from the
+  // register allocator (0 = none, 4, 6).  Default = the measured best
+  // with the 192-op SOP network (profiles/r01/tune_c5.jsonl): prefetch the
+  // next universe, one-shot grid, no occupancy bound -> 6.3 TB/s.
+  int pf = 1, bpc = 0, occ = 0;
+  if (cfg) {
+    pf = cfg->universes_per_wave >= 2 ? 1 : 0;
+    bpc = cfg->blocks_per_cu;
+    occ = cfg->rule;
+    if (occ != 0 && occ != 4 && occ != 6)
+      return fail(LIFEAPI_E_INVALID, "unsupported refined cfg%s");
+  }
+  int cus = 0, rc = device_cus(cus);
+  if (rc != LIFEAPI_OK) return rc;
+  using Fn = void (*)(const uint64_t *, uint64_t *, uint64_t);
+  Fn fn = pf ? (occ == 4 ? (Fn)k_refined<1, 4> : occ == 6 ? (Fn)k_refined<1, 6> : (Fn)k_refined<1, 0>)
+             : (occ == 4 ? (Fn)k_refined<0, 4> : occ == 6 ? (Fn)k_refined<0, 6> : (Fn)k_refined<0, 0>);
+  hipLaunchKernelGGL(fn, dim3(grid_for(n, cus, bpc)), dim3(kBlock), 0, (hipStream_t)stream, d_in,
+                     d_out, (uint64_t)n);
+  return launched("k_refined launch");
+}
+
+int lifeapi_refined_step_batch_dev(const uint64_t *d_in, uint64_t *d_out, size_t n, void *stream) {
+  return lifeapi_refined_step_batch_dev_cfg(d_in, d_out, n, stream, nullptr);
+}
+
+}  // extern "C"

@@ -10,5 +10,5 @@ import split_layout  # noqa: E402
 
 
 def test_split_tables_route_rows():
-    src = open(os.path.join(ROOT, "lifeapi_amd", "csrc", "lifeapi_hip.hip")).read()
+    src = open(os.path.join(ROOT, "lifeapi_amd", "csrc", "split_layout.hpp")).read()
     assert split_layout.check(src) == [2, 4, 8, 16]

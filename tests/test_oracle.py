@@ -197,7 +197,7 @@ def test_rule3_network_truth():
     source), evaluated on all 512 3x3 neighbourhoods, is B3/S23 on the
     inclusive count (LifeAPI.hpp:1251-1252: count 3, or 4 with the centre)."""
     import re
-    src = open(os.path.join(os.path.dirname(GOLD), "..", "lifeapi_amd", "csrc", "lifeapi_hip.hip")).read()
+    src = open(os.path.join(os.path.dirname(GOLD), "..", "lifeapi_amd", "csrc", "device.hpp")).read()
     t = {k: int(v, 16) for k, v in re.findall(r"\b(kT[123]) = (?:0x)?([0-9A-Fa-f]+)", src)}
     assert set(t) == {"kT1", "kT2", "kT3"}
 

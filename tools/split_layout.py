@@ -1,4 +1,4 @@
-"""Check the row-split layout tables of lifeapi_hip.hip (SplitNet<S>): the
+"""Check the row-split layout tables of csrc/split_layout.hpp (SplitNet<S>): the
 five index-bit swaps map universe u, row S*k + j to register j, bit P*k + u,
 and running them backwards restores the columns.  Pure Python, no GPU."""
 import random
@@ -53,4 +53,4 @@ def check(src):
 
 
 if __name__ == "__main__":
-    print("ok", check(open(sys.argv[1] if len(sys.argv) > 1 else "lifeapi_amd/csrc/lifeapi_hip.hip").read()))
+    print("ok", check(open(sys.argv[1] if len(sys.argv) > 1 else "lifeapi_amd/csrc/split_layout.hpp").read()))

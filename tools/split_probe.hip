@@ -3,7 +3,10 @@
 // bitop3 network switched off (MODE bit 0: exchange, bit 1: network), timed
 // with HIP events on 64K universes x 1024 generations (config 3).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iinclude tools/split_probe.hip
-#include "../lifeapi_amd/csrc/lifeapi_hip.hip"
+//        -Llifeapi_amd -llifeapi_hip -Wl,-rpath,$PWD/lifeapi_amd
+#include "../lifeapi_amd/csrc/split_layout.hpp"
+
+using namespace lifeapi_impl;
 
 #include <cstdio>
 

@@ -4,11 +4,12 @@ in build/asm/*.s.  Usage: python tools/vbank.py <mangled-kernel-name>"""
 import re
 import sys
 
-ASM = "build/asm/lifeapi_hip-hip-amdgcn-amd-amdhsa-gfx950.s"
+ASM_GLOB = "build/asm/*-hip-amdgcn-amd-amdhsa-gfx950.s"
 
 
 def loop_body(name):
-    lines = open(ASM).read().split("\n")
+    import glob
+    lines = [l for f in sorted(glob.glob(ASM_GLOB)) for l in open(f).read().split("\n")]
     start = next(i for i, l in enumerate(lines) if l.startswith(name + ":"))
     end = next(i for i in range(start, len(lines)) if "s_endpgm" in lines[i])
     body = lines[start:end]
