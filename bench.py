@@ -73,6 +73,26 @@ def timed_launches(hip, bufs, steps, gens, stream):
     return (e0, e1), cur
 
 
+def copy_ceiling():
+    """Best median GB/s of the same-shape HBM copy kernel (tools/membw.hip:
+    dwordx2 lanes, 4 x 512 B in flight per wave, read + write) measured on
+    MI355X and committed under profiles/; context for the roofline."""
+    path = os.path.join(ROOT, "profiles", "r01", "membw.jsonl")
+    best = None
+    try:
+        with open(path) as f:
+            for line in f:
+                try:
+                    d = json.loads(line)
+                except ValueError:
+                    continue
+                if d.get("mode") in (0, 1, 2, 3) and "GBps_median" in d:
+                    best = max(best or 0.0, d["GBps_median"])
+    except OSError:
+        return None, None
+    return best, os.path.relpath(path, ROOT)
+
+
 def cpu_baseline(x_host: np.ndarray, seconds: float):
     """Reference CPU Step() (oracle/_ref, else the C port) on host cores."""
     from oracle.oracle import Port, Ref
@@ -279,6 +299,8 @@ def main():
         secondary = {"config3": secondary_config3(hip, device, stream),
                      "config5": secondary_config5(hip, device, stream)}
 
+    ceiling, ceiling_src = copy_ceiling()
+
     cpu = None
     if want_cpu:
         cpu = cpu_baseline(x_full, args.cpu_seconds)
@@ -308,7 +330,10 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                          "traffic": traffic, "traffic_source": tsrc,
-                         "algorithmic_bytes_per_launch": n * gens * BYTES_PER_UNIVERSE_GEN},
+                         "algorithmic_bytes_per_launch": n * gens * BYTES_PER_UNIVERSE_GEN,
+                         "read_only_GBps": achieved / 2 if achieved else None,
+                         "copy_ceiling_GBps": ceiling, "copy_ceiling_source": ceiling_src,
+                         "frac_of_copy_ceiling": (achieved / ceiling) if (achieved and ceiling) else None},
             "cpu_baseline": cpu,
             "verified": verified,
             "collect": collect,

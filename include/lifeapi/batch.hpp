@@ -113,6 +113,11 @@ template <LifeStableLayout S>
 std::vector<PropagateResult> PropagateBatch(std::span<S> s, int device = 0) {
   return detail::stable_pass(s, 4, 0, device);
 }
+// s[i].StabiliseOptions() (LifeStable.hpp:677-693), in place
+template <LifeStableLayout S>
+std::vector<PropagateResult> StabiliseOptionsBatch(std::span<S> s, int device = 0) {
+  return detail::stable_pass(s, 5, 0, device);
+}
 
 // out[i] = NeighbourCount(in[i])  (NeighbourCount.hpp:40-70)
 template <LifeStateLayout S, NeighbourCountLayout C>

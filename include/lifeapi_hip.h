@@ -131,8 +131,9 @@ int lifeapi_interaction_counts_batch_dev(const uint64_t *d_in, uint64_t *d_out, 
  * words (member order, LifeStable.hpp:41-53; option planes 1 = ruled out).
  * pass: 0 SynchroniseStateKnown (LifeStable.hpp:526-556), 1 UpdateOptions
  * (:558-615), 2 SignalNeighbours (:617-675), 3 PropagateStep (:695-716),
- * 4 Propagate (:718-729, at most max_iters steps; 0 = 2^20).
- * d_flags[u] = consistent | changed << 1 (| 4 if max_iters stopped pass 4),
+ * 4 Propagate (:718-729, at most max_iters steps; 0 = 2^20),
+ * 5 StabiliseOptions (:677-693, the same bound).
+ * d_flags[u] = consistent | changed << 1 (| 4 if max_iters stopped 4 / 5),
  * i.e. the PropagateResult; planes are left exactly as the reference leaves
  * them, including on an inconsistent early return.                        */
 int lifeapi_stable_pass_batch_dev(uint64_t *d_planes, uint8_t *d_flags, size_t n, int pass,

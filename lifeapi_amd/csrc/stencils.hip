@@ -244,7 +244,19 @@ __global__ __launch_bounds__(kBlock) void k_stable(uint64_t *__restrict__ planes
     else if constexpr (PASS == 1) r = stable_options(p);
     else if constexpr (PASS == 2) r = stable_signal(p);
     else if constexpr (PASS == 3) r = stable_step(p);
-    else {
+    else if constexpr (PASS == 5) {  // StabiliseOptions (LifeStable.hpp:677-693)
+      int ever = 0;
+      r = -1;
+      for (uint32_t it = 0; it < max_iters; ++it) {
+        const int k = stable_sync(p);
+        if (!(k & 1)) { r = 0; break; }
+        const int o = stable_options(p);
+        if (!(o & 1)) { r = 0; break; }
+        if (!((k | o) & 2)) { r = 1 | ever; break; }
+        ever = 2;
+      }
+      if (r < 0) r = 1 | ever | 4;
+    } else {
       int ever = 0;
       r = -1;
       for (uint32_t it = 0; it < max_iters; ++it) {
@@ -368,14 +380,14 @@ static int counts_launch(const uint64_t *d_in, uint64_t *d_out, size_t n, int mo
 int lifeapi_stable_pass_batch_dev(uint64_t *d_planes, uint8_t *d_flags, size_t n, int pass,
                                   uint32_t max_iters, void *stream) {
   if (n == 0) return LIFEAPI_OK;
-  if (!d_planes || !d_flags || !aligned8(d_planes) || pass < 0 || pass > 4)
+  if (!d_planes || !d_flags || !aligned8(d_planes) || pass < 0 || pass > 5)
     return fail(LIFEAPI_E_INVALID, "bad argument to lifeapi_stable_pass_batch_dev%s");
   const uintptr_t a = (uintptr_t)d_planes, b = (uintptr_t)d_flags;
   if (b < a + n * 10 * 512 && a < b + n) return fail(LIFEAPI_E_INVALID, "flags overlap planes%s");
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
   using Fn = void (*)(uint64_t *, uint8_t *, uint64_t, uint32_t);
-  const Fn fns[5] = {k_stable<0>, k_stable<1>, k_stable<2>, k_stable<3>, k_stable<4>};
+  const Fn fns[6] = {k_stable<0>, k_stable<1>, k_stable<2>, k_stable<3>, k_stable<4>, k_stable<5>};
   hipLaunchKernelGGL(fns[pass], dim3(grid_for(n, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream,
                      d_planes, d_flags, (uint64_t)n, max_iters ? max_iters : 1u << 20);
   return launched("k_stable launch");

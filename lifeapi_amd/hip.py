@@ -253,7 +253,7 @@ def weld_step(welds: torch.Tensor, generations: int = 1, stream=None) -> torch.T
     return welds
 
 
-STABLE_PASSES = ("sync", "options", "signal", "step", "propagate")
+STABLE_PASSES = ("sync", "options", "signal", "step", "propagate", "stabilise")
 
 
 def stable_pass(planes: torch.Tensor, which: str | int, max_iters: int = 0,

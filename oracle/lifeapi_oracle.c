@@ -495,6 +495,17 @@ int oracle_stable_pass(uint64_t *planes, int which, const uint8_t *tt_count,
     case 1: return stable_options(planes, tt_count);
     case 2: return stable_signal(planes, tt_signal);
     case 3: return stable_step(planes, tt_count, tt_signal);
+    case 5: { /* StabiliseOptions, LifeStable.hpp:677-693 */
+      int ever = 0;
+      for (;;) {
+        const int k = stable_sync(planes);
+        if (!(k & 1)) return 0;
+        const int o = stable_options(planes, tt_count);
+        if (!(o & 1)) return 0;
+        if (!((k | o) & 2)) return 1 | ever;
+        ever = 2;
+      }
+    }
     default: { /* LifeStable.hpp:718-729 */
       int ever = 0;
       for (;;) {

@@ -75,7 +75,8 @@ void oracle_weld_step(uint64_t w[256], unsigned gens);
 
 /* LifeStable passes, in place on 10 planes (see lifeapi_oracle.c):
  * which = 0 SynchroniseStateKnown, 1 UpdateOptions, 2 SignalNeighbours,
- * 3 PropagateStep, 4 Propagate.  Returns consistent | changed << 1. */
+ * 3 PropagateStep, 4 Propagate, 5 StabiliseOptions (LifeStable.hpp:677-693).
+ * Returns consistent | changed << 1. */
 int oracle_stable_pass(uint64_t *planes, int which, const uint8_t *tt_count,
                        const uint8_t *tt_signal);
 

@@ -149,10 +149,10 @@ class Port:
             self.lib.oracle_weld_step(_p64(out[u]), gens)
         return out
 
-    STABLE_PASSES = ("sync", "options", "signal", "step", "propagate")
+    STABLE_PASSES = ("sync", "options", "signal", "step", "propagate", "stabilise")
 
     def stable_pass(self, planes: np.ndarray, which: int):
-        """LifeStable pass `which` (0..4, see lifeapi_oracle.h) on (n, 640)
+        """LifeStable pass `which` (0..5, see lifeapi_oracle.h) on (n, 640)
         planes; returns (planes, flags: bit0 consistent, bit1 changed)."""
         gold = os.path.join(os.path.dirname(HERE), "tests", "golden")
         if not hasattr(self, "_stt"):

@@ -112,7 +112,7 @@ static void store_stable(const LifeStable &s, uint64_t *p) {
 }
 // which: 0 SynchroniseStateKnown (:526-556), 1 UpdateOptions (:558-615),
 // 2 SignalNeighbours (:617-675), 3 PropagateStep (:695-716),
-// 4 Propagate (:718-729).  Returns consistent | changed << 1.
+// 4 Propagate (:718-729), 5 StabiliseOptions (:677-693).  Returns consistent | changed << 1.
 int ref_stable_pass(uint64_t *planes, int which) {
   LifeStable s = load_stable(planes);
   LifeStable::PropagateResult r{};
@@ -121,6 +121,7 @@ int ref_stable_pass(uint64_t *planes, int which) {
     case 1: r = s.UpdateOptions(); break;
     case 2: r = s.SignalNeighbours(); break;
     case 3: r = s.PropagateStep(); break;
+    case 5: r = s.StabiliseOptions(); break;
     default: r = s.Propagate(); break;
   }
   store_stable(s, planes);

@@ -256,34 +256,7 @@ def main():
     meta["weld"] = {"n": int(len(wel)), "required_examples": len(req),
                     "layout": "state,frozen2,frozen1,frozen0"}
 
-    # 5d. LifeStable passes (SURVEY 8(f) row 3): the two espresso fragments as
-    #     complete truth tables, and seeded 10-plane LifeStables through the
-    #     reference's SynchroniseStateKnown / UpdateOptions / SignalNeighbours /
-    #     PropagateStep / Propagate
-    R.lib.ref_stable_count_frag.argtypes = [_u64p, _u64p]
-    R.lib.ref_stable_signal_frag.argtypes = [_u64p, _u64p]
-    R.lib.ref_stable_pass.argtypes = [_u64p, ctypes.c_int]
-    sc = fragment_truth_table(R.lib.ref_stable_count_frag, 9, 9)
-    np.savez_compressed(os.path.join(HERE, "stable_count_tt.npz"), tt=sc,
-                        inputs=np.array(STABLE_COUNT_INPUTS), outputs=np.array(STABLE_COUNT_OUTPUTS))
-    ss = fragment_truth_table(R.lib.ref_stable_signal_frag, 17, 4)
-    np.savez_compressed(os.path.join(HERE, "stable_signal_tt.npz"), tt=ss,
-                        inputs=np.array(STABLE_SIGNAL_INPUTS), outputs=np.array(STABLE_SIGNAL_OUTPUTS))
-    st_in = stable_inputs(48)
-    res = {}
-    for which, name in enumerate(["sync", "options", "signal", "step", "propagate"]):
-        planes = st_in.copy()
-        flags = np.array([R.lib.ref_stable_pass(_p64(planes[u]), which) for u in range(len(planes))],
-                         dtype=np.uint8)
-        res[name] = planes
-        res[name + "_flags"] = flags
-    np.savez_compressed(os.path.join(HERE, "stable.npz"), input=st_in, **res)
-    meta["stable"] = {"n": int(len(st_in)), "passes": ["sync", "options", "signal", "step", "propagate"],
-                      "flags": "bit0 consistent, bit1 changed",
-                      "step_consistent": int((res["step_flags"] & 1).sum()),
-                      "propagate_consistent": int((res["propagate_flags"] & 1).sum()),
-                      "stable_count_ones": [int(v) for v in sc.sum(axis=1)],
-                      "stable_signal_ones": [int(v) for v in ss.sum(axis=1)]}
+    stable_fixture(meta)
 
     # 5b. config 5: bitslicing/unknown_step_refined.hpp (the reference's espresso
     #     fragment) as a complete truth table over its 16 inputs, plus seeded
@@ -338,6 +311,37 @@ def main():
     print(json.dumps(meta["digests"], indent=1))
 
 
+def stable_fixture(meta):
+    # 5d. LifeStable passes (SURVEY 8(f) row 3): the two espresso fragments as
+    #     complete truth tables, and seeded 10-plane LifeStables through the
+    #     reference's SynchroniseStateKnown / UpdateOptions / SignalNeighbours /
+    #     PropagateStep / Propagate
+    R.lib.ref_stable_count_frag.argtypes = [_u64p, _u64p]
+    R.lib.ref_stable_signal_frag.argtypes = [_u64p, _u64p]
+    R.lib.ref_stable_pass.argtypes = [_u64p, ctypes.c_int]
+    sc = fragment_truth_table(R.lib.ref_stable_count_frag, 9, 9)
+    np.savez_compressed(os.path.join(HERE, "stable_count_tt.npz"), tt=sc,
+                        inputs=np.array(STABLE_COUNT_INPUTS), outputs=np.array(STABLE_COUNT_OUTPUTS))
+    ss = fragment_truth_table(R.lib.ref_stable_signal_frag, 17, 4)
+    np.savez_compressed(os.path.join(HERE, "stable_signal_tt.npz"), tt=ss,
+                        inputs=np.array(STABLE_SIGNAL_INPUTS), outputs=np.array(STABLE_SIGNAL_OUTPUTS))
+    st_in = stable_inputs(48)
+    res = {}
+    for which, name in enumerate(["sync", "options", "signal", "step", "propagate", "stabilise"]):
+        planes = st_in.copy()
+        flags = np.array([R.lib.ref_stable_pass(_p64(planes[u]), which) for u in range(len(planes))],
+                         dtype=np.uint8)
+        res[name] = planes
+        res[name + "_flags"] = flags
+    np.savez_compressed(os.path.join(HERE, "stable.npz"), input=st_in, **res)
+    meta["stable"] = {"n": int(len(st_in)), "passes": ["sync", "options", "signal", "step", "propagate", "stabilise"],
+                      "flags": "bit0 consistent, bit1 changed",
+                      "step_consistent": int((res["step_flags"] & 1).sum()),
+                      "propagate_consistent": int((res["propagate_flags"] & 1).sum()),
+                      "stable_count_ones": [int(v) for v in sc.sum(axis=1)],
+                      "stable_signal_ones": [int(v) for v in ss.sum(axis=1)]}
+
+
 # RLE batch I/O (Parsing.hpp:143-204): tricky inputs for LifeState::Parse
 # (all cells on the board, so the reference's behaviour is defined) and
 # states for LifeState::RLE().  Strings are stored as one uint8 text blob +
@@ -385,6 +389,13 @@ def rle_fixture():
 if __name__ == "__main__":
     if "--only-rle" in sys.argv:
         rle_fixture()
+    elif "--only-stable" in sys.argv:  # refresh stable*.npz and golden.json["stable"]
+        gj = os.path.join(HERE, "golden.json")
+        with open(gj) as f:
+            m = json.load(f)
+        stable_fixture(m)
+        with open(gj, "w") as f:
+            json.dump(m, f, indent=1)
     else:
         main()
         rle_fixture()
