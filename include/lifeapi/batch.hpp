@@ -119,6 +119,13 @@ std::vector<PropagateResult> StabiliseOptionsBatch(std::span<S> s, int device = 
   return detail::stable_pass(s, 5, 0, device);
 }
 
+// out[i] = s[i].Vulnerable()  (LifeStable.hpp:366-412)
+template <LifeStableLayout S, LifeStateLayout L>
+void VulnerableBatch(std::span<const S> s, std::span<L> out, int device = 0) {
+  if (out.size() != s.size()) throw Error(LIFEAPI_E_INVALID, "lifeapi: size mismatch");
+  check(lifeapi_stable_vulnerable_batch(words(s.data()), words(out.data()), s.size(), device));
+}
+
 // out[i] = NeighbourCount(in[i])  (NeighbourCount.hpp:40-70)
 template <LifeStateLayout S, NeighbourCountLayout C>
 void NeighbourCountBatch(std::span<const S> in, std::span<C> out, int device = 0) {

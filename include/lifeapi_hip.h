@@ -138,6 +138,9 @@ int lifeapi_interaction_counts_batch_dev(const uint64_t *d_in, uint64_t *d_out, 
  * them, including on an inconsistent early return.                        */
 int lifeapi_stable_pass_batch_dev(uint64_t *d_planes, uint8_t *d_flags, size_t n, int pass,
                                   uint32_t max_iters, void *stream);
+/* LifeStable::Vulnerable() (LifeStable.hpp:366-412) of every LifeStable[n]
+ * (layout as above): d_out = n LifeStates.                                */
+int lifeapi_stable_vulnerable_batch_dev(const uint64_t *d_planes, uint64_t *d_out, size_t n, void *stream);
 /* LifeWeld::Step() (LifeWeld.hpp:169-186) `generations` times, in place on
  * LifeWeld[n] = {state, frozen2, frozen1, frozen0} x 64 words (the struct's
  * member order, LifeWeld.hpp:18-20); only the state planes change.        */
@@ -187,6 +190,7 @@ int lifeapi_pop_batch(const uint64_t *states, uint32_t *pop, size_t n, int devic
 int lifeapi_weld_step_batch(uint64_t *welds, size_t n, uint32_t generations, int device);
 int lifeapi_stable_pass_batch(uint64_t *planes, uint8_t *flags, size_t n, int pass,
                               uint32_t max_iters, int device);
+int lifeapi_stable_vulnerable_batch(const uint64_t *planes, uint64_t *out, size_t n, int device);
 int lifeapi_neighbour_count_batch(const uint64_t *in, uint64_t *out, size_t n, int device);
 int lifeapi_interaction_counts_batch(const uint64_t *in, uint64_t *out, size_t n, int with_next,
                                      int device);

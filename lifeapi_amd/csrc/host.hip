@@ -261,6 +261,21 @@ int lifeapi_stable_pass_batch(uint64_t *planes, uint8_t *flags, size_t n, int pa
                       arg);
 }
 
+int lifeapi_stable_vulnerable_batch(const uint64_t *planes, uint64_t *out, size_t n, int device) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!planes || !out || !aligned8(planes) || !aligned8(out))
+    return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_stable_vulnerable_batch%s");
+  const int dev = host_device(device);
+  if (dev < 0) return dev;
+  const HostIO io[2] = {{planes, nullptr, 10 * 512}, {nullptr, out, 512}};
+  return host_chunked(dev, n, io, 2,
+                      [](void *const *d, size_t m, hipStream_t s, const void *) {
+                        return lifeapi_stable_vulnerable_batch_dev((const uint64_t *)d[0], (uint64_t *)d[1],
+                                                                   m, s);
+                      },
+                      nullptr);
+}
+
 int lifeapi_neighbour_count_batch(const uint64_t *in, uint64_t *out, size_t n, int device) {
   if (n == 0) return LIFEAPI_OK;
   if (!in || !out || !aligned8(in) || !aligned8(out))

@@ -148,6 +148,14 @@ __device__ __forceinline__ void stable_signal_circuit(const T (&x)[17], T &signa
 #include "stable_signal_circuit.inc"
 }
 
+// stable_vulnerable.hpp (LifeStable.hpp:400), 15 in / 4 out, same pipeline
+template <class T>
+__device__ __forceinline__ void stable_vulnerable_circuit(const T (&x)[15], T &vulnerable_on,
+                                                          T &vulnerable_off, T &vulnerable_center_on,
+                                                          T &vulnerable_center_off) {
+#include "stable_vulnerable_circuit.inc"
+}
+
 enum { PST, PUN, PL2, PL3, PD0, PD1, PD2, PD4, PD5, PD6 };
 
 // SynchroniseStateKnown, LifeStable.hpp:526-556
@@ -273,6 +281,30 @@ __global__ __launch_bounds__(kBlock) void k_stable(uint64_t *__restrict__ planes
   }
 }
 
+// LifeStable::Vulnerable() (LifeStable.hpp:366-412), one wave per
+// LifeStable: the cells whose neighbourhood admits both an ON and an OFF
+// stable completion.  Reads the 10 planes, writes one LifeState.
+__global__ __launch_bounds__(kBlock) void k_stable_vulnerable(const uint64_t *__restrict__ planes,
+                                                              uint64_t *__restrict__ out, uint64_t n) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock;
+  for (uint64_t u = (uint64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave; u < n; u += stride) {
+    const uint64_t *q = planes + u * 10 * kWave + lane;
+    W p[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) p[k] = ld<false>(q + k * kWave);
+    W s3, s2, s1, s0, u3, u2, u1, u0;
+    ncount4(p[PST], s3, s2, s1, s0);
+    ncount4(p[PUN], u3, u2, u1, u0);
+    const W x[15] = {p[PL2], p[PL3], p[PD0], p[PD1], p[PD2], p[PD4], p[PD5], p[PD6],
+                     s2,     s1,     s0,     u3,     u2,     u1,     u0};
+    W von, voff, vcon, vcoff;
+    stable_vulnerable_circuit(x, von, voff, vcon, vcoff);
+    const W on = zoi_hollow(von) | vcon, off = zoi_hollow(voff) | vcoff;
+    st<false>(out + u * kWave + lane, on & off);
+  }
+}
+
 // ---- config 5: the unknown_step_refined ternary step --------------------
 
 // bitslicing/unknown_step_refined.hpp:1-85 as a v_bitop3 network.  The
@@ -391,6 +423,19 @@ int lifeapi_stable_pass_batch_dev(uint64_t *d_planes, uint8_t *d_flags, size_t n
   hipLaunchKernelGGL(fns[pass], dim3(grid_for(n, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream,
                      d_planes, d_flags, (uint64_t)n, max_iters ? max_iters : 1u << 20);
   return launched("k_stable launch");
+}
+
+int lifeapi_stable_vulnerable_batch_dev(const uint64_t *d_planes, uint64_t *d_out, size_t n, void *stream) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!d_planes || !d_out || !aligned8(d_planes) || !aligned8(d_out))
+    return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_stable_vulnerable_batch_dev%s");
+  const uintptr_t a = (uintptr_t)d_planes, b = (uintptr_t)d_out;
+  if (b < a + n * 10 * 512 && a < b + n * 512) return fail(LIFEAPI_E_INVALID, "out overlaps planes%s");
+  int cus = 0, rc = device_cus(cus);
+  if (rc != LIFEAPI_OK) return rc;
+  hipLaunchKernelGGL(k_stable_vulnerable, dim3(grid_for(n, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream,
+                     d_planes, d_out, (uint64_t)n);
+  return launched("k_stable_vulnerable launch");
 }
 
 int lifeapi_weld_step_batch_dev(uint64_t *d_welds, size_t n, uint32_t generations, void *stream) {

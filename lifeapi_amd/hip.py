@@ -74,6 +74,8 @@ _SIGS = {
     "lifeapi_interaction_counts_batch": ([_vp, _vp, _sz, _int, _int], _int),
     "lifeapi_refined_step_batch": ([_vp, _vp, _sz, _int], _int),
     "lifeapi_contains_batch": ([_vp, _vp, _vp, _vp, _sz, _int], _int),
+    "lifeapi_stable_vulnerable_batch_dev": ([_vp, _vp, _sz, _vp], _int),
+    "lifeapi_stable_vulnerable_batch": ([_vp, _vp, _sz, _int], _int),
     "lifeapi_rle_lengths_batch_dev": ([_vp, _vp, _sz, _vp], _int),
     "lifeapi_rle_write_batch_dev": ([_vp, _vp, _vp, _sz, _vp], _int),
     "lifeapi_parse_rle_batch_dev": ([_vp, _vp, _sz, _vp, _vp, _vp], _int),
@@ -269,6 +271,17 @@ def stable_pass(planes: torch.Tensor, which: str | int, max_iters: int = 0,
     _check(lib.lifeapi_stable_pass_batch_dev(planes.data_ptr(), flags.data_ptr(), n, w, max_iters,
                                              _stream(stream)))
     return flags
+
+
+def stable_vulnerable(planes: torch.Tensor, stream=None) -> torch.Tensor:
+    """LifeStable::Vulnerable() (LifeStable.hpp:366-412) of (n, 10*64) planes -> (n, 64)."""
+    if not planes.is_cuda or planes.dtype not in (torch.int64, torch.uint64) or \
+            not planes.is_contiguous() or planes.numel() % (10 * N):
+        raise ValueError("planes must be a contiguous int64 device tensor of shape (n, 10*64)")
+    n = planes.numel() // (10 * N)
+    out = torch.empty((n, N), dtype=torch.int64, device=planes.device)
+    _check(lib.lifeapi_stable_vulnerable_batch_dev(planes.data_ptr(), out.data_ptr(), n, _stream(stream)))
+    return out
 
 
 def neighbour_count(states: torch.Tensor, stream=None) -> torch.Tensor:

@@ -488,6 +488,34 @@ static int stable_step(uint64_t *p, const uint8_t *ttc, const uint8_t *tts) {
   return 1 | ((k | o | s) & 2);
 }
 
+/* LifeStable::Vulnerable() (LifeStable.hpp:366-412): the cells whose
+ * neighbourhood admits both an ON and an OFF stable completion.  The
+ * stable_vulnerable.hpp fragment (15 inputs: options, NeighbourCount bits
+ * 2..0 of state, bits 3..0 of unknown) is evaluated by table lookup in tt
+ * (4 x 2^15, extracted from the reference build); then
+ * on = ZOIHollow(vulnerable_on) | vulnerable_center_on, likewise off, and
+ * the result is on & off. */
+void oracle_stable_vulnerable(const uint64_t *p, uint64_t out[64], const uint8_t *tt) {
+  uint64_t s3[64], s2[64], s1[64], s0[64], u3[64], u2[64], u1[64], u0[64];
+  uint64_t von[64], voff[64], vcon[64], vcoff[64], onz[64], offz[64];
+  oracle_neighbour_count(PL(p, ST), s3, s2, s1, s0);
+  oracle_neighbour_count(PL(p, UN), u3, u2, u1, u0);
+  for (int x = 0; x < 64; ++x) {
+    const uint64_t in[15] = {PL(p, L2)[x], PL(p, L3)[x], PL(p, D0)[x], PL(p, D1)[x], PL(p, D2)[x],
+                             PL(p, D4)[x], PL(p, D5)[x], PL(p, D6)[x], s2[x], s1[x], s0[x],
+                             u3[x], u2[x], u1[x], u0[x]};
+    uint64_t r[4] = {0};
+    for (int y = 0; y < 64; ++y) {
+      const unsigned idx = cell_index(in, 15, y);
+      for (int k = 0; k < 4; ++k) r[k] |= (uint64_t)(tt[k * 32768 + idx] & 1u) << y;
+    }
+    von[x] = r[0]; voff[x] = r[1]; vcon[x] = r[2]; vcoff[x] = r[3];
+  }
+  zoi_hollow(von, onz);
+  zoi_hollow(voff, offz);
+  for (int x = 0; x < 64; ++x) out[x] = (onz[x] | vcon[x]) & (offz[x] | vcoff[x]);
+}
+
 int oracle_stable_pass(uint64_t *planes, int which, const uint8_t *tt_count,
                        const uint8_t *tt_signal) {
   switch (which) {

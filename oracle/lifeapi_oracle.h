@@ -77,6 +77,7 @@ void oracle_weld_step(uint64_t w[256], unsigned gens);
  * which = 0 SynchroniseStateKnown, 1 UpdateOptions, 2 SignalNeighbours,
  * 3 PropagateStep, 4 Propagate, 5 StabiliseOptions (LifeStable.hpp:677-693).
  * Returns consistent | changed << 1. */
+void oracle_stable_vulnerable(const uint64_t *planes, uint64_t out[64], const uint8_t *tt);
 int oracle_stable_pass(uint64_t *planes, int which, const uint8_t *tt_count,
                        const uint8_t *tt_signal);
 

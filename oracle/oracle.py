@@ -75,6 +75,7 @@ class Port:
         L.oracle_neighbour_count.argtypes = [_u64p] * 5
         L.oracle_interaction_counts.argtypes = [_u64p] * 5
         L.oracle_weld_step.argtypes = [_u64p, ctypes.c_uint]
+        L.oracle_stable_vulnerable.argtypes = [_u64p, _u64p, ctypes.POINTER(ctypes.c_uint8)]
         L.oracle_stable_pass.argtypes = [_u64p, ctypes.c_int, ctypes.POINTER(ctypes.c_uint8),
                                          ctypes.POINTER(ctypes.c_uint8)]
         L.oracle_refined_step_batch.argtypes = [_u64p, _u64p, ctypes.c_size_t,
@@ -165,6 +166,18 @@ class Port:
             flags[u] = self.lib.oracle_stable_pass(_p64(out[u]), which, self._stt[0].ctypes.data_as(u8),
                                                    self._stt[1].ctypes.data_as(u8))
         return out, flags
+
+    def stable_vulnerable(self, planes: np.ndarray) -> np.ndarray:
+        """LifeStable::Vulnerable() (LifeStable.hpp:366-412) of (n, 640) planes."""
+        if not hasattr(self, "_vtt"):
+            gold = os.path.join(os.path.dirname(HERE), "tests", "golden", "stable_vulnerable_tt.npz")
+            self._vtt = np.ascontiguousarray(np.load(gold)["tt"].astype(np.uint8))
+        src = np.ascontiguousarray(planes, dtype=np.uint64).reshape(-1, 640)
+        out = universes(src.shape[0])
+        u8 = ctypes.POINTER(ctypes.c_uint8)
+        for u in range(src.shape[0]):
+            self.lib.oracle_stable_vulnerable(_p64(src[u]), _p64(out[u]), self._vtt.ctypes.data_as(u8))
+        return out
 
     def refined_truth_table(self) -> np.ndarray:
         if self._tt is None:

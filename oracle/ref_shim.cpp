@@ -147,6 +147,20 @@ void ref_stable_signal_frag(const uint64_t *in, uint64_t *out) {
   const uint64_t r[4] = {signaloff, signalon, centeroff, centeron};
   std::memcpy(out, r, sizeof r);
 }
+// stable_vulnerable.hpp (included at LifeStable.hpp:400): 15 inputs -> 4 outputs
+void ref_stable_vulnerable_frag(const uint64_t *in, uint64_t *out) {
+  const uint64_t l2 = in[0], l3 = in[1], d0 = in[2], d1 = in[3], d2 = in[4], d4 = in[5], d5 = in[6],
+                 d6 = in[7], s2 = in[8], s1 = in[9], s0 = in[10], unk3 = in[11], unk2 = in[12],
+                 unk1 = in[13], unk0 = in[14];
+  uint64_t vulnerable_on = 0, vulnerable_off = 0, vulnerable_center_on = 0, vulnerable_center_off = 0;
+#include "bitslicing/stable_vulnerable.hpp"
+  const uint64_t r[4] = {vulnerable_on, vulnerable_off, vulnerable_center_on, vulnerable_center_off};
+  std::memcpy(out, r, sizeof r);
+}
+// LifeStable::Vulnerable()  LifeStable.hpp:366-412
+void ref_stable_vulnerable(const uint64_t *planes, uint64_t *out) {
+  store(load_stable(planes).Vulnerable(), out);
+}
 // LifeState::GetPop  LifeAPI.hpp:290-298
 unsigned ref_pop(const uint64_t *s) { return load(s).GetPop(); }
 // LifeState::Contains(const LifeTarget&)  LifeTarget.hpp:44-51

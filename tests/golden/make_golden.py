@@ -72,6 +72,10 @@ STABLE_COUNT_OUTPUTS = ["l2", "l3", "d0", "d1", "d2", "d4", "d5", "d6", "abort"]
 STABLE_SIGNAL_INPUTS = ["l2", "l3", "d0", "d1", "d2", "d4", "d5", "d6", "s2", "s1", "s0",
                         "m3", "m2", "m1", "m0", "stateon", "stateunk"]
 STABLE_SIGNAL_OUTPUTS = ["signaloff", "signalon", "centeroff", "centeron"]
+STABLE_VULNERABLE_INPUTS = ["l2", "l3", "d0", "d1", "d2", "d4", "d5", "d6", "s2", "s1", "s0",
+                            "unk3", "unk2", "unk1", "unk0"]
+STABLE_VULNERABLE_OUTPUTS = ["vulnerable_on", "vulnerable_off", "vulnerable_center_on",
+                             "vulnerable_center_off"]
 
 
 def moved(s, dx, dy):
@@ -333,13 +337,26 @@ def stable_fixture(meta):
                          dtype=np.uint8)
         res[name] = planes
         res[name + "_flags"] = flags
+    # LifeStable::Vulnerable (LifeStable.hpp:366-412): its fragment's table and
+    # the reference's result on every input
+    R.lib.ref_stable_vulnerable_frag.argtypes = [_u64p, _u64p]
+    R.lib.ref_stable_vulnerable.argtypes = [_u64p, _u64p]
+    sv = fragment_truth_table(R.lib.ref_stable_vulnerable_frag, 15, 4)
+    np.savez_compressed(os.path.join(HERE, "stable_vulnerable_tt.npz"), tt=sv,
+                        inputs=np.array(STABLE_VULNERABLE_INPUTS), outputs=np.array(STABLE_VULNERABLE_OUTPUTS))
+    vul = np.zeros((len(st_in), 64), np.uint64)
+    for u in range(len(st_in)):
+        R.lib.ref_stable_vulnerable(_p64(st_in[u]), _p64(vul[u]))
+    res["vulnerable"] = vul
     np.savez_compressed(os.path.join(HERE, "stable.npz"), input=st_in, **res)
     meta["stable"] = {"n": int(len(st_in)), "passes": ["sync", "options", "signal", "step", "propagate", "stabilise"],
                       "flags": "bit0 consistent, bit1 changed",
                       "step_consistent": int((res["step_flags"] & 1).sum()),
                       "propagate_consistent": int((res["propagate_flags"] & 1).sum()),
                       "stable_count_ones": [int(v) for v in sc.sum(axis=1)],
-                      "stable_signal_ones": [int(v) for v in ss.sum(axis=1)]}
+                      "stable_signal_ones": [int(v) for v in ss.sum(axis=1)],
+                      "stable_vulnerable_ones": [int(v) for v in sv.sum(axis=1)],
+                      "vulnerable_nonempty": int((vul != 0).any(axis=1).sum())}
 
 
 # RLE batch I/O (Parsing.hpp:143-204): tricky inputs for LifeState::Parse

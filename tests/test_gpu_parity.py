@@ -371,13 +371,34 @@ def test_stable_passes_vs_oracle(hip, port):
             f = port.fill(10, seed=u)
             x[u, 2:] = f[2:] & port.fill(8, seed=u + 1000)
     x = x.reshape(n, 640)
+    results = {}
     for w, name in enumerate(hip.STABLE_PASSES):
         d = to_dev(x).reshape(n, 640)
         fl = hip.stable_pass(d, name).cpu().numpy()
         want, wfl = port.stable_pass(x, w)
         assert (d.cpu().numpy().view(np.uint64) == want).all(), name
         assert (fl == wfl).all(), name
+        results[name] = (want, wfl)
+    want, wfl = results["propagate"]
     assert (wfl & 1).sum() > n // 3  # the propagate loop ran to a fixpoint on many
+    # Vulnerable (LifeStable.hpp:366-412) on the raw and on the propagated planes
+    for planes in (x, want):
+        got = hip.stable_vulnerable(to_dev(planes).reshape(n, 640))
+        exp = port.stable_vulnerable(planes)
+        assert (to_host(got) == exp).all()
+    assert exp.any()
+
+
+def test_stable_vulnerable_golden_gpu(hip):
+    import os
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "stable.npz"))
+    got = hip.stable_vulnerable(to_dev(g["input"]).reshape(-1, 640))
+    assert (to_host(got) == g["vulnerable"]).all()
+    # host-pointer twin
+    out = np.zeros((g["input"].shape[0], 64), np.uint64)
+    inp = np.ascontiguousarray(g["input"], dtype=np.uint64)
+    hip._check(hip.lib.lifeapi_stable_vulnerable_batch(inp.ctypes.data, out.ctypes.data, inp.shape[0], 0))
+    assert (out == g["vulnerable"]).all()
 
 
 # ---- config 5: unknown_step_refined ternary step ----

@@ -165,7 +165,8 @@ def test_refined_truth_table_fixture(port, meta):
 
 @pytest.mark.parametrize("inc,ttfile", [("refined_circuit.inc", "unknown_step_refined_tt.npz"),
                                          ("stable_count_circuit.inc", "stable_count_tt.npz"),
-                                         ("stable_signal_circuit.inc", "stable_signal_tt.npz")])
+                                         ("stable_signal_circuit.inc", "stable_signal_tt.npz"),
+                                         ("stable_vulnerable_circuit.inc", "stable_vulnerable_tt.npz")])
 def test_generated_circuit_is_the_table(inc, ttfile):
     """A generated bitop3 network (lifeapi_amd/csrc/*.inc), simulated on every
     input combination, is exactly the reference fragment's truth table."""
@@ -214,6 +215,13 @@ def test_rule3_network_truth():
         t1 = lut(t["kT1"], s0, s1, a)
         t2 = lut(t["kT2"], s2, a, t1)
         assert lut(t["kT3"], s1, s3, t2) == int(cnt == 3 or (a == 1 and cnt == 4)), bits
+
+
+def test_stable_vulnerable_golden(port):
+    """LifeStable::Vulnerable (LifeStable.hpp:366-412) vs the reference's output."""
+    g = load("stable.npz")
+    got = port.stable_vulnerable(g["input"])
+    assert (got == g["vulnerable"]).all() and g["vulnerable"].any()
 
 
 def test_stable_passes_golden(port):

@@ -83,6 +83,7 @@ def main():
         t_copy = timed(lambda: work.copy_(st))
         t = timed(run) - t_copy
         report(f"k_stable {name}", n, 2 * 5120 + 1, t, {"note": "copy of the input subtracted"})
+    report("k_stable_vulnerable", n, 5120 + 512, timed(lambda: hip.stable_vulnerable(st)))
     planes = hip.fill_random(11 * n, seed=21).view(n, 11 * 64)
     report("k_refined (config 5)", n, 7168, timed(lambda: hip.refined_step(planes)))
 

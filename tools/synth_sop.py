@@ -294,7 +294,7 @@ def main():
         "// GENERATED by tools/synth_sop.py from " + args.tt.split("/")[-1] + " -- do not edit.",
         f"// {len(net.ops)} v_bitop3_b32 per 32-bit half: {ncubes} cubes, output phases {phases}",
         "// inputs x[i]: " + ", ".join(f"{i}={n}" for i, n in enumerate(names)),
-        "// verified against the full 2^16-entry truth table before writing.",
+        f"// verified against the full 2^{nvar}-entry truth table before writing.",
     ]
     with open(args.out, "w") as f:
         f.write("\n".join(emit(net, outs, out_names, hdr)) + "\n")
