@@ -93,10 +93,10 @@ __global__ __launch_bounds__(kBlock) void k_weld(uint64_t *__restrict__ welds, u
   const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock;
   for (uint64_t u = (uint64_t)blockIdx.x * kWavesPerBlock + wib; u < n; u += stride) {
     uint64_t *p = welds + u * 4 * kWave + lane;
-    W s = ld<false>(p);
-    const W f2 = ld<false>(p + kWave), f1 = ld<false>(p + 2 * kWave), f0 = ld<false>(p + 3 * kWave);
+    W s = ld<true>(p);
+    const W f2 = ld<true>(p + kWave), f1 = ld<true>(p + 2 * kWave), f0 = ld<true>(p + 3 * kWave);
     for (uint32_t g = 0; g < gens; ++g) s = weld_gen(s, f2, f1, f0);
-    st<false>(p, s);
+    st<true>(p, s);
   }
 }
 
@@ -246,7 +246,7 @@ __global__ __launch_bounds__(kBlock) void k_stable(uint64_t *__restrict__ planes
     uint64_t *q = planes + u * 10 * kWave + lane;
     W p[10];
 #pragma unroll
-    for (int k = 0; k < 10; ++k) p[k] = ld<false>(q + k * kWave);
+    for (int k = 0; k < 10; ++k) p[k] = ld<true>(q + k * kWave);
     int r;
     if constexpr (PASS == 0) r = stable_sync(p);
     else if constexpr (PASS == 1) r = stable_options(p);
@@ -276,7 +276,7 @@ __global__ __launch_bounds__(kBlock) void k_stable(uint64_t *__restrict__ planes
       if (r < 0) r = 1 | ever | 4;
     }
 #pragma unroll
-    for (int k = 0; k < 10; ++k) st<false>(q + k * kWave, p[k]);
+    for (int k = 0; k < 10; ++k) st<true>(q + k * kWave, p[k]);
     if (lane == 0) flags[u] = (uint8_t)r;
   }
 }
@@ -292,7 +292,7 @@ __global__ __launch_bounds__(kBlock) void k_stable_vulnerable(const uint64_t *__
     const uint64_t *q = planes + u * 10 * kWave + lane;
     W p[10];
 #pragma unroll
-    for (int k = 0; k < 10; ++k) p[k] = ld<false>(q + k * kWave);
+    for (int k = 0; k < 10; ++k) p[k] = ld<true>(q + k * kWave);
     W s3, s2, s1, s0, u3, u2, u1, u0;
     ncount4(p[PST], s3, s2, s1, s0);
     ncount4(p[PUN], u3, u2, u1, u0);
@@ -301,7 +301,7 @@ __global__ __launch_bounds__(kBlock) void k_stable_vulnerable(const uint64_t *__
     W von, voff, vcon, vcoff;
     stable_vulnerable_circuit(x, von, voff, vcon, vcoff);
     const W on = zoi_hollow(von) | vcon, off = zoi_hollow(voff) | vcoff;
-    st<false>(out + u * kWave + lane, on & off);
+    st<true>(out + u * kWave + lane, on & off);
   }
 }
 
