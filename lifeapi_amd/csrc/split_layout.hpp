@@ -174,4 +174,86 @@ __device__ __forceinline__ void gen_split(uint32_t (&r)[S], uint32_t *slot, int 
   }
 }
 
+// ------------------------------------------------------------------------
+// Tile layouts (RULE 8: C = 4, RULE 9: C = 2 adjacent columns per lane)
+// ------------------------------------------------------------------------
+//
+// The S-way row split of gen_split, but a lane owns C adjacent columns
+// (x = C*i .. C*i + C-1 of its group's P universes), so a group of 64/C lanes
+// holds P whole universes and a wave C*P of them.  Horizontal neighbours of
+// the inner columns are the lane's own registers; only the two edge columns
+// cross lanes.  Per generation a lane publishes columns 0 and C-1 and fetches
+// column C-1 of lane i-1 and column 0 of lane i+1 (mod 64/C: the torus wrap).
+// Against gen_split (C = 1) that is 2/C of the exchanged words per cell, which
+// takes the LDS pipe off the critical path; with C = 4 a group is one 16-lane
+// DPP row, so row_ror moves the edges with the wrap built in (XDPP), at 0.9
+// VALU slot per word instead of LDS traffic (XLDS).
+template <int S, int C, int X>
+__device__ __forceinline__ void gen_tile(uint32_t (&r)[C][S], uint32_t *slot, int lane) {
+  constexpr int P = S / 2;
+  uint32_t lv[S], rv[S];
+  if constexpr (X == XDPP) {
+    static_assert(C == 4, "row_ror rotates 16-lane rows: 4 columns per lane");
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      // row_ror:1 -> lane i reads lane i-1 of its row; row_ror:15 -> lane i+1
+      lv[j] = (uint32_t)__builtin_amdgcn_mov_dpp((int)r[C - 1][j], 0x121, 0xF, 0xF, true);
+      rv[j] = (uint32_t)__builtin_amdgcn_mov_dpp((int)r[0][j], 0x12F, 0xF, 0xF, true);
+    }
+  } else {
+    static_assert(S % 4 == 0, "16-B LDS planes");
+    constexpr int LPG = kWave / C;  // lanes per group
+    constexpr int Q = S / 4;        // planes per edge column
+    typedef uint32_t vec __attribute__((ext_vector_type(4)));
+    vec *v = reinterpret_cast<vec *>(slot);
+#pragma unroll
+    for (int p = 0; p < Q; ++p) {
+      v[p * kWave + lane] = vec{r[0][4 * p], r[0][4 * p + 1], r[0][4 * p + 2], r[0][4 * p + 3]};
+      v[(Q + p) * kWave + lane] =
+          vec{r[C - 1][4 * p], r[C - 1][4 * p + 1], r[C - 1][4 * p + 2], r[C - 1][4 * p + 3]};
+    }
+    // a wave's LDS operations complete in order; stores and loads may alias,
+    // so the compiler keeps their order
+    const int g0 = lane & ~(LPG - 1);
+    const int xp = g0 | ((lane + LPG - 1) & (LPG - 1)), xn = g0 | ((lane + 1) & (LPG - 1));
+#pragma unroll
+    for (int p = 0; p < Q; ++p) {
+      const vec l = v[(Q + p) * kWave + xp], rr = v[p * kWave + xn];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) lv[4 * p + q] = l[q], rv[4 * p + q] = rr[q];
+    }
+  }
+  // Order: h(0), h(1), out(0), h(2), out(1), ...  Column c's new state is
+  // produced after h(c+1) has read its old one, so it can take the old
+  // registers (no loop-carried copies).
+  uint32_t h0[C][S], h1[C][S];
+  auto hcol = [&](int c) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      const uint32_t L = c == 0 ? lv[j] : r[c - 1][j], R = c == C - 1 ? rv[j] : r[c + 1][j];
+      h0[c][j] = lut3<kXor3>(L, r[c][j], R);
+      h1[c][j] = lut3<kMaj>(L, r[c][j], R);
+    }
+  };
+  hcol(0);
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    if (c + 1 < C) hcol(c + 1);
+    const uint32_t h0u = __builtin_amdgcn_alignbit(h0[c][S - 1], h0[c][S - 1], 32 - P);  // rotl P
+    const uint32_t h1u = __builtin_amdgcn_alignbit(h1[c][S - 1], h1[c][S - 1], 32 - P);
+    const uint32_t h0d = __builtin_amdgcn_alignbit(h0[c][0], h0[c][0], P);  // rotr P
+    const uint32_t h1d = __builtin_amdgcn_alignbit(h1[c][0], h1[c][0], P);
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      const uint32_t a0 = j == 0 ? h0u : h0[c][j - 1], c0 = j == S - 1 ? h0d : h0[c][j + 1];
+      const uint32_t a1 = j == 0 ? h1u : h1[c][j - 1], c1 = j == S - 1 ? h1d : h1[c][j + 1];
+      const uint32_t s0 = lut3<kLe1>(a0, h0[c][j], c0), s1 = lut3<kNae>(a0, h0[c][j], c0);
+      const uint32_t s2 = lut3<kLe1>(a1, h1[c][j], c1), s3 = lut3<kEven>(a1, h1[c][j], c1);
+      const uint32_t t1 = lut3<kT1>(s0, s1, r[c][j]);
+      const uint32_t t2 = lut3<kT2>(s2, r[c][j], t1);
+      r[c][j] = lut3<kT3>(s1, s3, t2);
+    }
+  }
+}
+
 }  // namespace lifeapi_impl

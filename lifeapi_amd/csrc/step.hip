@@ -5,6 +5,7 @@
 
 #include "host.hpp"
 #include "split_layout.hpp"
+#include "tile_asm.inc"
 
 using namespace lifeapi_impl;
 
@@ -247,6 +248,95 @@ __global__ __launch_bounds__(kBlock) void k_step_split(const uint64_t *__restric
   }
 }
 
+// k_step for the tile layouts (gen_tile): a wave holds C groups of P = S/2
+// universes, lane i of group g columns C*i .. C*i+C-1 of each (C*8
+// contiguous bytes per universe: two dwordx4 loads for C = 4).
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+template <bool NT>
+__device__ __forceinline__ u64x2 ld2(const uint64_t *p) {
+  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(p));
+  else return *reinterpret_cast<const u64x2 *>(p);
+}
+template <bool NT>
+__device__ __forceinline__ void st2(uint64_t *p, u64x2 v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<u64x2 *>(p));
+  else *reinterpret_cast<u64x2 *>(p) = v;
+}
+
+template <int S, int C, int X, bool NT>
+__global__ __launch_bounds__(kBlock) void k_step_tile(const uint64_t *__restrict__ in,
+                                                      uint64_t *__restrict__ out, uint64_t n,
+                                                      uint32_t gens) {
+  constexpr int P = S / 2, LPG = kWave / C;
+  static_assert(C % 2 == 0, "columns are moved in pairs");
+  __shared__ uint32_t lds[X == XDPP ? 1 : kWavesPerBlock * 2 * S * kWave];  // 4 planes of 1 KiB per wave (S = 8)
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int grp = lane / LPG, col0 = (lane & (LPG - 1)) * C;
+  const uint64_t per_wave = (uint64_t)C * P;
+  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock * per_wave;
+  uint32_t *slot = lds + (X == XDPP ? 0 : wib * 2 * S * kWave);
+  // per-lane offsets stay 32-bit and the tile's base pointer wave-uniform, so
+  // little beyond the state is live across the generation loop
+  const uint32_t lane_off = (uint32_t)(grp * P * kWave + col0);
+  for (uint64_t u0 = ((uint64_t)blockIdx.x * kWavesPerBlock + wib) * per_wave; u0 < n; u0 += stride) {
+    const uint64_t left = n - u0;  // universes from u0 on (wave-uniform)
+    const uint64_t *src = in + u0 * kWave;
+    uint32_t off = lane_off, first = (uint32_t)(grp * P);
+    // opaque to the optimiser: keeps it from hoisting 64-bit copies of the
+    // lane offsets out of the loop (they would stay live across the generations)
+    asm volatile("" : "+v"(off), "+v"(first));
+    const uint32_t room = left < per_wave ? (uint32_t)left : (uint32_t)per_wave;
+    uint32_t r[C][S];
+    {
+      uint64_t w[P][C];
+#pragma unroll
+      for (int u = 0; u < P; ++u) {
+        const bool ok = first + u < room;
+#pragma unroll
+        for (int c = 0; c < C; c += 2) {
+          const u64x2 v = ok ? ld2<NT>(src + off + u * kWave + c) : u64x2{0, 0};
+          w[u][c] = v[0], w[u][c + 1] = v[1];
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        W cc[P];
+#pragma unroll
+        for (int u = 0; u < P; ++u) cc[u] = split(w[u][c]);
+        Split<S>::load(cc, r[c]);
+      }
+    }
+    if constexpr (X == XASM) {
+      static_assert(S == 8 && C == 4, "tile_asm.inc is the 8-way split, 4 columns per lane");
+      const uint32_t base =
+          (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)slot;
+      const int g0 = lane & ~(LPG - 1);
+      tile_gens_asm(r, gens, base + lane * 16u, base + (g0 | ((lane + LPG - 1) & (LPG - 1))) * 16u,
+                    base + (g0 | ((lane + 1) & (LPG - 1))) * 16u);
+    } else {
+      for (uint32_t it = 0; it < gens; ++it) gen_tile<S, C, X>(r, slot, lane);
+    }
+    asm volatile("" : "+v"(off), "+v"(first));  // (store addresses: recomputed here)
+    uint64_t w[P][C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      W cc[P];
+      Split<S>::store(r[c], cc);
+#pragma unroll
+      for (int u = 0; u < P; ++u) w[u][c] = join(cc[u]);
+    }
+    uint64_t *dst = out + u0 * kWave;
+#pragma unroll
+    for (int u = 0; u < P; ++u) {
+      if (first + u < room) {
+#pragma unroll
+        for (int c = 0; c < C; c += 2) st2<NT>(dst + off + u * kWave + c, u64x2{w[u][c], w[u][c + 1]});
+      }
+    }
+  }
+}
+
 // Step + Contains fused: first generation in 1..gens whose state contains the
 // target (0 = never); the state keeps stepping to `gens` for d_final.
 __global__ __launch_bounds__(kBlock) void k_step_contains(const uint64_t *__restrict__ in,
@@ -383,10 +473,24 @@ StepFn pick_split(int groups, bool nt) {
     default: return nullptr;
   }
 }
-// universes one wave holds per universes_per_wave unit (rules 5, 6: groups)
-int group_size(int rule) { return rule == 5 ? 2 : rule == 6 ? 4 : rule == 7 ? 8 : 1; }
+// universes one wave holds per universes_per_wave unit (rules 5-7: groups;
+// rules 8, 9: one tile of C groups)
+int group_size(int rule) {
+  return rule == 5 ? 2 : rule == 6 ? 4 : rule == 7 ? 8 : rule == 8 ? 16 : rule == 9 ? 8 : 1;
+}
 
 StepFn pick_step(const lifeapi_launch_cfg &c) {
+  if (c.rule == 8 || c.rule == 9) {  // tile layouts: one tile per wave
+    if (c.universes_per_wave != 1) return nullptr;
+    const bool nt = c.nontemporal != 0;
+    if (c.rule == 9)
+      return c.xchg == LIFEAPI_XCHG_LDS ? (nt ? k_step_tile<8, 2, XLDS, true> : k_step_tile<8, 2, XLDS, false>)
+                                        : nullptr;
+    if (c.xchg == LIFEAPI_XCHG_LDS) return nt ? k_step_tile<8, 4, XLDS, true> : k_step_tile<8, 4, XLDS, false>;
+    if (c.xchg == LIFEAPI_XCHG_DPP) return nt ? k_step_tile<8, 4, XDPP, true> : k_step_tile<8, 4, XDPP, false>;
+    if (c.xchg == LIFEAPI_XCHG_ASM) return nt ? k_step_tile<8, 4, XASM, true> : k_step_tile<8, 4, XASM, false>;
+    return nullptr;
+  }
   if (c.rule >= 5 && c.rule <= 7) {  // split layouts: LDS exchange only
     if (c.xchg != LIFEAPI_XCHG_LDS) return nullptr;
     const bool nt = c.nontemporal != 0;

@@ -18,6 +18,8 @@ ALL_CFGS = list(itertools.product(range(8), (1, 2, 4, 8), (0, 1), (0, 1, 2, 3, 4
 ALL_CFGS += list(itertools.product((8,), (1, 2, 4, 8), (0, 1), (4,)))
 # the row-split layouts: LDS exchange, 1 or 2 groups of 2 / 4 universes
 ALL_CFGS += list(itertools.product((1,), (1, 2), (0, 1), (5, 6, 7)))
+# the tile layouts (4 / 2 columns per lane): one tile per wave
+ALL_CFGS += [(x, 1, nt, r) for r, xs in ((8, (0, 1, 8)), (9, (1,))) for x in xs for nt in (0, 1)]
 
 
 def to_dev(a: np.ndarray) -> torch.Tensor:

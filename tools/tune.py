@@ -89,7 +89,8 @@ def main():
             work.append((f"g{g}", 1 << 18, g, cfgs))
     if args.workload in ("c3", "both", "all"):
         n, g = 1 << 16, 1024
-        work.append(("c3", n, g, list(itertools.product([1], [1, 2], [0], [0], [6, 7]))))
+        work.append(("c3", n, g, [(1, 1, 0, 0, 6), (1, 2, 0, 0, 6), (1, 1, 0, 0, 7), (1, 1, 0, 0, 8),
+                                  (0, 1, 0, 0, 8), (1, 1, 0, 0, 9), (8, 1, 0, 0, 8), (8, 1, 0, 1, 8)]))
 
     for name, n, g, cfgs in work:
         a = hip.fill_random(n, seed=2)

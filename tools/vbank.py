@@ -20,7 +20,8 @@ def loop_body(name):
         m = re.search(r"s_cbranch_\w+\s+(\.LBB\w+)", l)
         if m and m[1] in labels and labels[m[1]] < i:
             k = sum("v_bitop3" in x for x in body[labels[m[1]]:i])
-            if best is None or k > best[2]:
+            # the innermost loop that holds a generation (>= 32 v_bitop3)
+            if k >= 32 and (best is None or i - labels[m[1]] < best[1] - best[0]):
                 best = (labels[m[1]], i, k)
     return body[best[0]:best[1] + 1]
 
