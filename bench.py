@@ -52,7 +52,8 @@ def parse_args():
     p.add_argument("--gens-per-step", type=int, default=1)
     p.add_argument("--seed", type=int, default=2)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-seconds", type=float, default=2.0, help="wall budget of the CPU baseline")
+    p.add_argument("--cpu-seconds", type=float, default=12.0,
+                   help="wall budget of the CPU baseline (half at 1 thread, half at 16)")
     p.add_argument("--no-secondary", action="store_true", help="skip the config-3 side measurement")
     p.add_argument("--no-verify", action="store_true")
     return p.parse_args()

@@ -77,7 +77,7 @@ def test_argument_validation_without_device():
     assert L.lifeapi_step_batch_dev(None, None, 0, 1, None) == 0
     # bad launch cfg
     for bad in [(9, 4, 8, 0, 0), (0, 3, 8, 0, 0), (0, 1, 8, 0, 5),
-                (hip.XCHG_ASM, 1, 8, 0, 2)]:     # the hand-allocated loop is rule 4 only
+                (hip.XCHG_ASM, 1, 8, 0, 2)]:     # the hand-allocated loops are rules 4 and 8 only
         cfg = hip.LaunchCfg(*bad)
         assert L.lifeapi_step_batch_dev_cfg(4096, 8192 * 4, 1, 1, None, ctypes.byref(cfg)) == -1, bad
     assert L.lifeapi_fill_random_dev(4096, 1, 0, 0, 5, None) == -1

@@ -23,3 +23,17 @@ def test_step_batch_cpp():
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     print(r.stdout, r.stderr)
     assert r.returncode == 0, r.stderr[-4000:]
+
+
+@pytest.mark.gpu
+def test_step_batch_cpp_asan():
+    """The same facade tests with the library's host code (every csrc/*.hip,
+    host side only) and the test under ASan + UBSan."""
+    exe = os.path.join(ROOT, "build", "step_batch_test_asan")
+    if not os.path.exists(exe):
+        pytest.skip("build/step_batch_test_asan not built (__graft_entry__.build())")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:protect_shadow_gap=0",
+               UBSAN_OPTIONS="print_stacktrace=1")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
+    print(r.stdout, r.stderr[-4000:])
+    assert r.returncode == 0, r.stderr[-4000:]
