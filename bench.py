@@ -148,19 +148,25 @@ def secondary_config3(hip, device, stream):
         ms.append(e0.elapsed_time(e1))
     t = min(ms) / 1e3
     gps = n * gens / t
-    # VALU issue model of the default generation loop (rule 6, build/asm,
-    # DESIGN.md 3.1): per 4 universes 72 v_bitop3 (one slot) + 4 v_alignbit
-    # (two slots, tools/bank_probe2.hip) = 20 issue slots per universe-gen;
-    # the exchange runs on the LDS pipe (ds_write_b128 x2, ds_read_b128 x4).
-    slots = 20
-    peak_slots = 1024 * 2.4e9 / 2  # 1024 SIMDs, one wave64 VALU op per 2 clk at 2.4 GHz
+    # VALU issue model of the default generation loop (rule 11, build/asm,
+    # DESIGN.md 3.1): per 4 universes 64 v_bitop3 (one slot; the 6-LUT tail)
+    # + 4 v_alignbit (two slots, tools/bank_probe2.hip) = 18 issue slots per
+    # universe-gen; the exchange runs on the LDS pipe (ds_write_b128 x2,
+    # ds_read_b128 x4).  peak: one wave64 VALU op per 2 clk per SIMD at
+    # 2.4 GHz; the best rate measured for independent v_bitop3 is 0.978 ns
+    # per instruction per SIMD (profiles/r01/bank_probe.jsonl), reported too.
+    slots = 18
+    peak_slots = 1024 * 2.4e9 / 2  # 1024 SIMDs
+    measured_slots = 1024 / 0.978e-9
     cfg = hip.default_cfg(gens).as_dict()
     return {"workload": "config3: 64K universes x 1024 generations (one launch)",
             "value": gps, "unit": "universe-gen/s", "cell_updates_per_s": gps * 4096,
             "kernel_ms": min(ms), "kernel_ms_all": ms, "launch_cfg": cfg,
             "roofline": {"bound": "valu", "achieved": gps * slots / 1e12, "peak": peak_slots / 1e12,
                          "unit": f"T VALU issue slots/s ({slots} per universe-gen)",
-                         "frac": gps * slots / peak_slots},
+                         "frac": gps * slots / peak_slots,
+                         "measured_issue_peak": measured_slots / 1e12,
+                         "frac_of_measured_issue_peak": gps * slots / measured_slots},
             "reference_op_equivalent_Tops": OPS_PER_UNIVERSE_GEN * gps / 1e12}
 
 

@@ -176,6 +176,46 @@ constexpr uint32_t kNae = ((TA ^ TB) | (TB ^ TC)) & 0xFF;         // 0x7E: sum i
 constexpr uint32_t kEven = (~kXor3) & 0xFF;                       // 0x69: sum in {0,2}
 constexpr uint32_t kT1 = 0x34, kT2 = 0x58, kT3 = 0x28;
 
+// The 6-LUT tail (NET 6): the same inputs as the 7-LUT network, one v_bitop3
+// fewer per 32-bit word (8 with the two h-layer LUTs, against 9).  Found by
+// stochastic search over arbitrary 6-gate DAGs (tools/cgp_search.c) using the
+// don't-cares of the centre row: its sum contains a, so (a = 1, sum 0) and
+// (a = 0, sum 3) never occur.  No 5-gate network turned up, nor a 7-gate one
+// with row- or row-pair-shared gates (tools/cgp_rows.c).
+//   g1 = SB in {0,2,3}            = N1(h1, h1u, h1d)
+//   g2 = maj(h1d, h1u, h0d)
+//   g3 = SA in {1,2}              = Nae(h0d, h0u, h0)
+//   g4 = N4(g3, g2, g1)
+//   g5 = SA odd                   = xor3(h0, h0d, h0u)
+//   next = g4 & (g5 | a)          = N6(g4, g5, a)
+// Checked on all 512 neighbourhoods by tests/test_oracle.py::test_net6_truth.
+constexpr uint32_t kN1 = 0xE9, kN4 = 0x52, kN6 = 0xE0;
+__device__ __forceinline__ uint32_t life_tail6(uint32_t h0u, uint32_t h0, uint32_t h0d, uint32_t h1u,
+                                               uint32_t h1, uint32_t h1d, uint32_t a) {
+  const uint32_t g1 = lut3<kN1>(h1, h1u, h1d);
+  const uint32_t g2 = lut3<kMaj>(h1d, h1u, h0d);
+  const uint32_t g3 = lut3<kNae>(h0d, h0u, h0);
+  const uint32_t g4 = lut3<kN4>(g3, g2, g1);
+  const uint32_t g5 = lut3<kXor3>(h0, h0d, h0u);
+  return lut3<kN6>(g4, g5, a);
+}
+// the 7-LUT tail above, per 32-bit word
+__device__ __forceinline__ uint32_t life_tail7(uint32_t h0u, uint32_t h0, uint32_t h0d, uint32_t h1u,
+                                               uint32_t h1, uint32_t h1d, uint32_t a) {
+  const uint32_t s0 = lut3<kLe1>(h0u, h0, h0d), s1 = lut3<kNae>(h0u, h0, h0d);
+  const uint32_t s2 = lut3<kLe1>(h1u, h1, h1d), s3 = lut3<kEven>(h1u, h1, h1d);
+  const uint32_t t1 = lut3<kT1>(s0, s1, a);
+  const uint32_t t2 = lut3<kT2>(s2, a, t1);
+  return lut3<kT3>(s1, s3, t2);
+}
+template <int NET>
+__device__ __forceinline__ uint32_t life_tail(uint32_t h0u, uint32_t h0, uint32_t h0d, uint32_t h1u,
+                                              uint32_t h1, uint32_t h1d, uint32_t a) {
+  static_assert(NET == 6 || NET == 7, "tails: 6 or 7 LUTs");
+  if constexpr (NET == 6) return life_tail6(h0u, h0, h0d, h1u, h1, h1d, a);
+  else return life_tail7(h0u, h0, h0d, h1u, h1, h1d, a);
+}
+
 template <bool NT>
 __device__ __forceinline__ W ld(const uint64_t *p) {
   if constexpr (NT) return split(__builtin_nontemporal_load(p));

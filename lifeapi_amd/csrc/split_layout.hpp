@@ -128,8 +128,9 @@ struct Split {
   }
 };
 
-// one generation of the P universes in r[] (RULE 3 network per register)
-template <int S>
+// one generation of the P universes in r[] (the h-layer and a NET-LUT tail
+// per register: NET 7 = the RULE 3 network, NET 6 = life_tail6)
+template <int S, int NET = 7>
 __device__ __forceinline__ void gen_split(uint32_t (&r)[S], uint32_t *slot, int lane) {
   constexpr int P = S / 2;
   // LDS planes of Q <= 4 words per lane: 16-B lane stride keeps ds_write_b128
@@ -166,11 +167,7 @@ __device__ __forceinline__ void gen_split(uint32_t (&r)[S], uint32_t *slot, int 
   for (int j = 0; j < S; ++j) {
     const uint32_t a0 = j == 0 ? h0u : h0[j - 1], c0 = j == S - 1 ? h0d : h0[j + 1];
     const uint32_t a1 = j == 0 ? h1u : h1[j - 1], c1 = j == S - 1 ? h1d : h1[j + 1];
-    const uint32_t s0 = lut3<kLe1>(a0, h0[j], c0), s1 = lut3<kNae>(a0, h0[j], c0);
-    const uint32_t s2 = lut3<kLe1>(a1, h1[j], c1), s3 = lut3<kEven>(a1, h1[j], c1);
-    const uint32_t t1 = lut3<kT1>(s0, s1, r[j]);
-    const uint32_t t2 = lut3<kT2>(s2, r[j], t1);
-    r[j] = lut3<kT3>(s1, s3, t2);
+    r[j] = life_tail<NET>(a0, h0[j], c0, a1, h1[j], c1, r[j]);
   }
 }
 
@@ -188,7 +185,7 @@ __device__ __forceinline__ void gen_split(uint32_t (&r)[S], uint32_t *slot, int 
 // takes the LDS pipe off the critical path; with C = 4 a group is one 16-lane
 // DPP row, so row_ror moves the edges with the wrap built in (XDPP), at 0.9
 // VALU slot per word instead of LDS traffic (XLDS).
-template <int S, int C, int X>
+template <int S, int C, int X, int NET = 7>
 __device__ __forceinline__ void gen_tile(uint32_t (&r)[C][S], uint32_t *slot, int lane) {
   constexpr int P = S / 2;
   uint32_t lv[S], rv[S];
@@ -247,11 +244,7 @@ __device__ __forceinline__ void gen_tile(uint32_t (&r)[C][S], uint32_t *slot, in
     for (int j = 0; j < S; ++j) {
       const uint32_t a0 = j == 0 ? h0u : h0[c][j - 1], c0 = j == S - 1 ? h0d : h0[c][j + 1];
       const uint32_t a1 = j == 0 ? h1u : h1[c][j - 1], c1 = j == S - 1 ? h1d : h1[c][j + 1];
-      const uint32_t s0 = lut3<kLe1>(a0, h0[c][j], c0), s1 = lut3<kNae>(a0, h0[c][j], c0);
-      const uint32_t s2 = lut3<kLe1>(a1, h1[c][j], c1), s3 = lut3<kEven>(a1, h1[c][j], c1);
-      const uint32_t t1 = lut3<kT1>(s0, s1, r[c][j]);
-      const uint32_t t2 = lut3<kT2>(s2, r[c][j], t1);
-      r[c][j] = lut3<kT3>(s1, s3, t2);
+      r[c][j] = life_tail<NET>(a0, h0[c][j], c0, a1, h1[c][j], c1, r[c][j]);
     }
   }
 }

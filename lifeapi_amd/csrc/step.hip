@@ -208,8 +208,9 @@ __global__ __launch_bounds__(kBlock) void k_step(const uint64_t *__restrict__ in
 }
 
 // k_step for the split layouts: wave w takes G groups of P = S/2
-// consecutive universes, grid-strided; all branches wave-uniform.
-template <int S, int G, bool NT>
+// consecutive universes, grid-strided; all branches wave-uniform.  NET: the
+// tail network (7 = RULE 3's, 6 = life_tail6).
+template <int S, int G, bool NT, int NET>
 __global__ __launch_bounds__(kBlock) void k_step_split(const uint64_t *__restrict__ in,
                                                        uint64_t *__restrict__ out, uint64_t n,
                                                        uint32_t gens) {
@@ -233,7 +234,7 @@ __global__ __launch_bounds__(kBlock) void k_step_split(const uint64_t *__restric
     }
     for (uint32_t it = 0; it < gens; ++it) {
 #pragma unroll
-      for (int g = 0; g < G; ++g) gen_split<S>(r[g], lds + (wib * G + g) * S * kWave, lane);
+      for (int g = 0; g < G; ++g) gen_split<S, NET>(r[g], lds + (wib * G + g) * S * kWave, lane);
     }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
@@ -263,7 +264,7 @@ __device__ __forceinline__ void st2(uint64_t *p, u64x2 v) {
   else *reinterpret_cast<u64x2 *>(p) = v;
 }
 
-template <int S, int C, int X, bool NT>
+template <int S, int C, int X, bool NT, int NET>
 __global__ __launch_bounds__(kBlock) void k_step_tile(const uint64_t *__restrict__ in,
                                                       uint64_t *__restrict__ out, uint64_t n,
                                                       uint32_t gens) {
@@ -315,7 +316,7 @@ __global__ __launch_bounds__(kBlock) void k_step_tile(const uint64_t *__restrict
       tile_gens_asm(r, gens, base + lane * 16u, base + (g0 | ((lane + LPG - 1) & (LPG - 1))) * 16u,
                     base + (g0 | ((lane + 1) & (LPG - 1))) * 16u);
     } else {
-      for (uint32_t it = 0; it < gens; ++it) gen_tile<S, C, X>(r, slot, lane);
+      for (uint32_t it = 0; it < gens; ++it) gen_tile<S, C, X, NET>(r, slot, lane);
     }
     asm volatile("" : "+v"(off), "+v"(first));  // (store addresses: recomputed here)
     uint64_t w[P][C];
@@ -370,7 +371,8 @@ __global__ __launch_bounds__(kBlock) void k_step_contains(const uint64_t *__rest
 // when no universe is clean measured slower still.
 // Without d_final, a wave stops once all its universes have hit.
 constexpr uint32_t kDiff = ((TA ^ TB) & (TB | TC)) & 0xFF;  // (s ^ wanted) & (wanted | unwanted)
-template <int S>
+constexpr int kContainsNet = 6;  // tail network of the fused kernel (as k_step's default, rule 11)
+template <int S, int NET>
 __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *__restrict__ in,
                                                                 uint64_t *__restrict__ fin,
                                                                 const uint64_t *__restrict__ wanted,
@@ -405,7 +407,7 @@ __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *
     for (int u = 0; u < P; ++u) hit[u] = 0;
     uint32_t found = 0;
     for (uint32_t g = 1; g <= gens; ++g) {
-      gen_split<S>(r, lds + wib * S * kWave, lane);
+      gen_split<S, NET>(r, lds + wib * S * kWave, lane);
       uint32_t d = 0;
 #pragma unroll
       for (int j = 0; j < S; ++j) d |= lut3<kDiff>(r[j], tw[j], tu[j]);
@@ -465,38 +467,56 @@ StepFn pick_rule(int u, bool nt, int rule) {
     }
   }
 }
-template <int S>
+template <int S, int NET>
 StepFn pick_split(int groups, bool nt) {
   switch (groups) {
-    case 1: return nt ? k_step_split<S, 1, true> : k_step_split<S, 1, false>;
-    case 2: return nt ? k_step_split<S, 2, true> : k_step_split<S, 2, false>;
+    case 1: return nt ? k_step_split<S, 1, true, NET> : k_step_split<S, 1, false, NET>;
+    case 2: return nt ? k_step_split<S, 2, true, NET> : k_step_split<S, 2, false, NET>;
     default: return nullptr;
   }
 }
-// universes one wave holds per universes_per_wave unit (rules 5-7: groups;
-// rules 8, 9: one tile of C groups)
+// universes one wave holds per universes_per_wave unit (rules 5-7, 10-12:
+// groups; rules 8, 9, 13: one tile of C groups)
 int group_size(int rule) {
-  return rule == 5 ? 2 : rule == 6 ? 4 : rule == 7 ? 8 : rule == 8 ? 16 : rule == 9 ? 8 : 1;
+  switch (rule) {
+    case 5: case 10: return 2;
+    case 6: case 11: return 4;
+    case 7: case 12: return 8;
+    case 8: case 13: return 16;
+    case 9: return 8;
+    default: return 1;
+  }
+}
+
+template <int NET>
+StepFn pick_tile4(int xchg, bool nt) {
+  if (xchg == LIFEAPI_XCHG_LDS) return nt ? k_step_tile<8, 4, XLDS, true, NET> : k_step_tile<8, 4, XLDS, false, NET>;
+  if (xchg == LIFEAPI_XCHG_DPP) return nt ? k_step_tile<8, 4, XDPP, true, NET> : k_step_tile<8, 4, XDPP, false, NET>;
+  return nullptr;
 }
 
 StepFn pick_step(const lifeapi_launch_cfg &c) {
-  if (c.rule == 8 || c.rule == 9) {  // tile layouts: one tile per wave
+  if (c.rule == 8 || c.rule == 9 || c.rule == 13) {  // tile layouts: one tile per wave
     if (c.universes_per_wave != 1) return nullptr;
     const bool nt = c.nontemporal != 0;
     if (c.rule == 9)
-      return c.xchg == LIFEAPI_XCHG_LDS ? (nt ? k_step_tile<8, 2, XLDS, true> : k_step_tile<8, 2, XLDS, false>)
+      return c.xchg == LIFEAPI_XCHG_LDS ? (nt ? k_step_tile<8, 2, XLDS, true, 7> : k_step_tile<8, 2, XLDS, false, 7>)
                                         : nullptr;
-    if (c.xchg == LIFEAPI_XCHG_LDS) return nt ? k_step_tile<8, 4, XLDS, true> : k_step_tile<8, 4, XLDS, false>;
-    if (c.xchg == LIFEAPI_XCHG_DPP) return nt ? k_step_tile<8, 4, XDPP, true> : k_step_tile<8, 4, XDPP, false>;
-    if (c.xchg == LIFEAPI_XCHG_ASM) return nt ? k_step_tile<8, 4, XASM, true> : k_step_tile<8, 4, XASM, false>;
-    return nullptr;
+    if (c.rule == 13) return pick_tile4<6>(c.xchg, nt);
+    if (c.xchg == LIFEAPI_XCHG_ASM) return nt ? k_step_tile<8, 4, XASM, true, 7> : k_step_tile<8, 4, XASM, false, 7>;
+    return pick_tile4<7>(c.xchg, nt);
   }
-  if (c.rule >= 5 && c.rule <= 7) {  // split layouts: LDS exchange only
+  if ((c.rule >= 5 && c.rule <= 7) || (c.rule >= 10 && c.rule <= 12)) {  // split layouts: LDS exchange only
     if (c.xchg != LIFEAPI_XCHG_LDS) return nullptr;
     const bool nt = c.nontemporal != 0;
-    return c.rule == 5 ? pick_split<4>(c.universes_per_wave, nt)
-         : c.rule == 6 ? pick_split<8>(c.universes_per_wave, nt)
-                       : pick_split<16>(c.universes_per_wave, nt);
+    switch (c.rule) {
+      case 5: return pick_split<4, 7>(c.universes_per_wave, nt);
+      case 6: return pick_split<8, 7>(c.universes_per_wave, nt);
+      case 7: return pick_split<16, 7>(c.universes_per_wave, nt);
+      case 10: return pick_split<4, 6>(c.universes_per_wave, nt);
+      case 11: return pick_split<8, 6>(c.universes_per_wave, nt);
+      default: return pick_split<16, 6>(c.universes_per_wave, nt);
+    }
   }
   switch (c.xchg) {
     case LIFEAPI_XCHG_DPP: return pick_rule<XDPP>(c.universes_per_wave, c.nontemporal != 0, c.rule);
@@ -530,9 +550,11 @@ void lifeapi_default_cfg(lifeapi_launch_cfg *cfg, uint32_t generations) {
     cfg->nontemporal = 1;
   } else {
     // VALU regime: 8-way row split, 4 universes per wave interleaved bit by
-    // bit, LDS exchange; state resident in VGPRs for all generations
+    // bit, LDS exchange, the 6-LUT tail; state resident in VGPRs for all
+    // generations (rule 11 over rule 6: 1.47 vs 1.61 ms on config 3,
+    // profiles/r01/tune_c3net.jsonl)
     cfg->xchg = LIFEAPI_XCHG_LDS;
-    cfg->rule = 6;
+    cfg->rule = 11;
     cfg->universes_per_wave = 1;
     cfg->nontemporal = generations < 32 ? 1 : 0;
   }
@@ -579,7 +601,7 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
   if (generations > 2) {  // the default layout of k_step for gens > 2 (lifeapi_default_cfg)
-    hipLaunchKernelGGL(k_step_contains_split<8>, dim3(grid_for((n + 3) / 4, cus, 0)), dim3(kBlock), 0,
+    hipLaunchKernelGGL((k_step_contains_split<8, kContainsNet>), dim3(grid_for((n + 3) / 4, cus, 0)), dim3(kBlock), 0,
                        (hipStream_t)stream, d_in, d_final, d_wanted, d_unwanted, d_first_gen,
                        (uint64_t)n, generations);
   } else {

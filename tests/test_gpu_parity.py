@@ -20,6 +20,9 @@ ALL_CFGS += list(itertools.product((8,), (1, 2, 4, 8), (0, 1), (4,)))
 ALL_CFGS += list(itertools.product((1,), (1, 2), (0, 1), (5, 6, 7)))
 # the tile layouts (4 / 2 columns per lane): one tile per wave
 ALL_CFGS += [(x, 1, nt, r) for r, xs in ((8, (0, 1, 8)), (9, (1,))) for x in xs for nt in (0, 1)]
+# the 6-LUT tail: split layouts (rules 10-12) and the 4-column tile (rule 13)
+ALL_CFGS += list(itertools.product((1,), (1, 2), (0, 1), (10, 11, 12)))
+ALL_CFGS += [(x, 1, nt, 13) for x in (0, 1) for nt in (0, 1)]
 
 
 def to_dev(a: np.ndarray) -> torch.Tensor:

@@ -217,6 +217,38 @@ def test_rule3_network_truth():
         assert lut(t["kT3"], s1, s3, t2) == int(cnt == 3 or (a == 1 and cnt == 4)), bits
 
 
+def test_net6_truth():
+    """The 6-LUT tail life_tail6 (gates and tables parsed from device.hpp)
+    behind the h-layer h0 = xor3, h1 = maj of each row, on all 512 3x3
+    neighbourhoods: B3/S23 on the inclusive count (LifeAPI.hpp:1196-1216)."""
+    import re
+    src = open(os.path.join(os.path.dirname(GOLD), "..", "lifeapi_amd", "csrc", "device.hpp")).read()
+    tabs = {"kMaj": 0xE8, "kNae": 0x7E, "kXor3": 0x96}
+    tabs.update({k: int(v, 16) for k, v in re.findall(r"\b(kN[146]) = 0x([0-9A-Fa-f]+)", src)})
+    assert set(tabs) == {"kMaj", "kNae", "kXor3", "kN1", "kN4", "kN6"}
+    body = src[src.index("uint32_t life_tail6("):]
+    body = body[:body.index("\n}\n")]
+    gates = re.findall(r"const uint32_t (g\d) = lut3<(\w+)>\((\w+), (\w+), (\w+)\);", body)
+    ret = re.search(r"return lut3<(\w+)>\((\w+), (\w+), (\w+)\);", body)
+    assert len(gates) == 5 and ret
+
+    def lut(tab, x, y, z):
+        return (tab >> ((x << 2) | (y << 1) | z)) & 1
+
+    for bits in range(512):
+        n = [(bits >> i) & 1 for i in range(9)]      # n[3*col + row], col 0 = left
+        a, cnt = n[4], sum(n)
+        rows = [(n[r], n[3 + r], n[6 + r]) for r in range(3)]
+        v = {"a": a}
+        for nm, r in (("u", 0), ("", 1), ("d", 2)):
+            v["h0" + nm] = lut(0x96, *rows[r])
+            v["h1" + nm] = lut(0xE8, *rows[r])
+        for g, tab, x, y, z in gates:
+            v[g] = lut(tabs[tab], v[x], v[y], v[z])
+        got = lut(tabs[ret[1]], v[ret[2]], v[ret[3]], v[ret[4]])
+        assert got == int(cnt == 3 or (a == 1 and cnt == 4)), bits
+
+
 def test_stable_vulnerable_golden(port):
     """LifeStable::Vulnerable (LifeStable.hpp:366-412) vs the reference's output."""
     g = load("stable.npz")

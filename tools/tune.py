@@ -63,7 +63,7 @@ def tune_c5(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=["c2", "c3", "c5", "gsweep", "both", "all"], default="both")
+    ap.add_argument("--workload", choices=["c2", "c3", "c3net", "c5", "gsweep", "both", "all"], default="both")
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--quick", action="store_true")
@@ -91,6 +91,14 @@ def main():
         n, g = 1 << 16, 1024
         work.append(("c3", n, g, [(1, 1, 0, 0, 6), (1, 2, 0, 0, 6), (1, 1, 0, 0, 7), (1, 1, 0, 0, 8),
                                   (0, 1, 0, 0, 8), (1, 1, 0, 0, 9), (8, 1, 0, 0, 8), (8, 1, 0, 1, 8)]))
+    if args.workload == "c3net":  # 6-LUT tail (rules 10-13) against the 7-LUT one
+        n, g = 1 << 16, 1024
+        work.append(("c3", n, g, [(1, 1, 0, 0, 6), (1, 1, 0, 0, 11), (1, 2, 0, 0, 6), (1, 2, 0, 0, 11),
+                                  (1, 1, 0, 0, 7), (1, 1, 0, 0, 12), (1, 1, 0, 0, 10),
+                                  (1, 1, 0, 0, 8), (1, 1, 0, 0, 13), (0, 1, 0, 0, 8), (0, 1, 0, 0, 13)]))
+        for gg in (4, 16, 64):
+            work.append((f"g{gg}", 1 << 18, gg, [(1, 1, 0, 1, 6), (1, 1, 0, 1, 11), (1, 1, 0, 0, 6),
+                                                  (1, 1, 0, 0, 11)]))
 
     for name, n, g, cfgs in work:
         a = hip.fill_random(n, seed=2)
