@@ -128,31 +128,76 @@ struct Split {
   }
 };
 
-// one generation of the P universes in r[] (the h-layer and a NET-LUT tail
-// per register: NET 7 = the RULE 3 network, NET 6 = life_tail6)
-template <int S, int NET = 7>
-__device__ __forceinline__ void gen_split(uint32_t (&r)[S], uint32_t *slot, int lane) {
-  constexpr int P = S / 2;
-  // LDS planes of Q <= 4 words per lane: 16-B lane stride keeps ds_write_b128
-  // / ds_read_b128 free of bank conflicts (a 32-B stride would be 2-way)
-  constexpr int Q = S < 4 ? S : 4;
-  typedef uint32_t vec __attribute__((ext_vector_type(Q)));
-  vec *v = reinterpret_cast<vec *>(slot);
+// LDS exchange of m registers (m = 4a + 2b + c): planes of 4, then 2, then
+// 1 words per lane, each at its natural lane stride (16 / 8 / 4 B), which
+// keeps every ds_write / ds_read free of bank conflicts (a 32-B stride would
+// be 2-way).  All writes first, then the reads of lanes x-1 and x+1: a wave's
+// LDS operations complete in order, and the store and the loads may alias,
+// so the compiler keeps their order.
+template <int Q>
+struct LdsVec {
+  typedef uint32_t type __attribute__((ext_vector_type(Q)));
+};
+template <>
+struct LdsVec<1> {
+  typedef uint32_t type;
+};
+template <int Q>
+__device__ __forceinline__ void lds_put(uint32_t *plane, const uint32_t *r, int lane) {
+  typename LdsVec<Q>::type v;
+  if constexpr (Q == 1) v = r[0];
+  else {
+#pragma unroll
+    for (int q = 0; q < Q; ++q) v[q] = r[q];
+  }
+  reinterpret_cast<typename LdsVec<Q>::type *>(plane)[lane] = v;
+}
+template <int Q>
+__device__ __forceinline__ void lds_get(const uint32_t *plane, uint32_t *out, int src) {
+  const typename LdsVec<Q>::type v = reinterpret_cast<const typename LdsVec<Q>::type *>(plane)[src];
+  if constexpr (Q == 1) out[0] = v;
+  else {
+#pragma unroll
+    for (int q = 0; q < Q; ++q) out[q] = v[q];
+  }
+}
+template <int M>
+__device__ __forceinline__ void lds_exchange(const uint32_t *r, uint32_t *lv, uint32_t *rv, uint32_t *slot,
+                                             int lane) {
+  constexpr int A = M / 4, B = (M % 4) / 2, C = M % 2;
   const int xp = (lane + kWave - 1) & (kWave - 1), xn = (lane + 1) & (kWave - 1);
 #pragma unroll
-  for (int p = 0; p < S / Q; ++p) {
-    vec mine;
+  for (int p = 0; p < A; ++p) lds_put<4>(slot + 4 * p * kWave, r + 4 * p, lane);
+  if constexpr (B) lds_put<2>(slot + 4 * A * kWave, r + 4 * A, lane);
+  if constexpr (C) lds_put<1>(slot + (4 * A + 2 * B) * kWave, r + 4 * A + 2 * B, lane);
 #pragma unroll
-    for (int q = 0; q < Q; ++q) mine[q] = r[p * Q + q];
-    v[p * kWave + lane] = mine;  // a wave's LDS operations complete in order; the
-  }                              // store and the loads may alias, so the compiler
-  uint32_t lv[S], rv[S];         // keeps their order
-#pragma unroll
-  for (int p = 0; p < S / Q; ++p) {
-    const vec l = v[p * kWave + xp], rr = v[p * kWave + xn];
-#pragma unroll
-    for (int q = 0; q < Q; ++q) lv[p * Q + q] = l[q], rv[p * Q + q] = rr[q];
+  for (int p = 0; p < A; ++p) {
+    lds_get<4>(slot + 4 * p * kWave, lv + 4 * p, xp);
+    lds_get<4>(slot + 4 * p * kWave, rv + 4 * p, xn);
   }
+  if constexpr (B) {
+    lds_get<2>(slot + 4 * A * kWave, lv + 4 * A, xp);
+    lds_get<2>(slot + 4 * A * kWave, rv + 4 * A, xn);
+  }
+  if constexpr (C) {
+    lds_get<1>(slot + (4 * A + 2 * B) * kWave, lv + 4 * A + 2 * B, xp);
+    lds_get<1>(slot + (4 * A + 2 * B) * kWave, rv + 4 * A + 2 * B, xn);
+  }
+}
+
+// one generation of the P universes in r[] (the h-layer and a NET-LUT tail
+// per register: NET 7 = the RULE 3 network, NET 6 = life_tail6).  The
+// neighbour columns of registers 0..S-D-1 go through LDS, those of the last
+// D registers by DPP wave_ror / wave_rol (VALU slots instead of LDS
+// bandwidth: the two pipes balance the load).
+template <int S, int NET = 7, int D = 0>
+__device__ __forceinline__ void gen_split(uint32_t (&r)[S], uint32_t *slot, int lane) {
+  constexpr int P = S / 2;
+  static_assert(D >= 0 && D <= S, "DPP registers");
+  uint32_t lv[S], rv[S];
+  if constexpr (D < S) lds_exchange<S - D>(r, lv, rv, slot, lane);
+#pragma unroll
+  for (int j = S - D; j < S; ++j) lv[j] = dpp_prev(r[j]), rv[j] = dpp_next(r[j]);
   uint32_t h0[S], h1[S];
 #pragma unroll
   for (int j = 0; j < S; ++j) {
@@ -168,6 +213,59 @@ __device__ __forceinline__ void gen_split(uint32_t (&r)[S], uint32_t *slot, int 
     const uint32_t a0 = j == 0 ? h0u : h0[j - 1], c0 = j == S - 1 ? h0d : h0[j + 1];
     const uint32_t a1 = j == 0 ? h1u : h1[j - 1], c1 = j == S - 1 ? h1d : h1[j + 1];
     r[j] = life_tail<NET>(a0, h0[j], c0, a1, h1[j], c1, r[j]);
+  }
+}
+
+// `gens` generations of gen_split<S, NET> (S % 4 == 0), software-pipelined
+// across the LDS planes: a plane's four new registers are published, and the
+// next generation's reads of that plane issued, as soon as its rows' tail is
+// done, so those LDS round trips overlap the remaining planes' tails instead
+// of stalling the wave at the top of each generation.  The reads for the
+// generation after the last are issued too and simply dropped.
+template <int S, int NET>
+__device__ __forceinline__ void gens_split_pipe(uint32_t (&r)[S], uint32_t *slot, int lane, uint32_t gens) {
+  constexpr int P = S / 2, NPL = S / 4;
+  static_assert(S % 4 == 0, "planes of 4 registers");
+  typedef uint32_t vec __attribute__((ext_vector_type(4)));
+  vec *v = reinterpret_cast<vec *>(slot);
+  const int xp = (lane + kWave - 1) & (kWave - 1), xn = (lane + 1) & (kWave - 1);
+  vec L[NPL], R[NPL];
+#pragma unroll
+  for (int p = 0; p < NPL; ++p) {
+    v[p * kWave + lane] = vec{r[4 * p], r[4 * p + 1], r[4 * p + 2], r[4 * p + 3]};
+    L[p] = v[p * kWave + xp];
+    R[p] = v[p * kWave + xn];
+  }
+  for (uint32_t it = 0; it < gens; ++it) {
+    uint32_t h0[S], h1[S];
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      const uint32_t l = L[j / 4][j % 4], rr = R[j / 4][j % 4];
+      h0[j] = lut3<kXor3>(l, r[j], rr);
+      h1[j] = lut3<kMaj>(l, r[j], rr);
+    }
+    const uint32_t h0u = __builtin_amdgcn_alignbit(h0[S - 1], h0[S - 1], 32 - P);  // rotl P
+    const uint32_t h1u = __builtin_amdgcn_alignbit(h1[S - 1], h1[S - 1], 32 - P);
+    const uint32_t h0d = __builtin_amdgcn_alignbit(h0[0], h0[0], P);  // rotr P
+    const uint32_t h1d = __builtin_amdgcn_alignbit(h1[0], h1[0], P);
+#pragma unroll
+    for (int p = 0; p < NPL; ++p) {
+#pragma unroll
+      for (int j = 4 * p; j < 4 * p + 4; ++j) {
+        const uint32_t a0 = j == 0 ? h0u : h0[j - 1], c0 = j == S - 1 ? h0d : h0[j + 1];
+        const uint32_t a1 = j == 0 ? h1u : h1[j - 1], c1 = j == S - 1 ? h1d : h1[j + 1];
+        r[j] = life_tail<NET>(a0, h0[j], c0, a1, h1[j], c1, r[j]);
+      }
+      // a wave's LDS operations complete in order: this generation's reads
+      // of plane p are done (consumed above), and the new reads see the new
+      // words; the compiler keeps the order (the store and loads may alias)
+      v[p * kWave + lane] = vec{r[4 * p], r[4 * p + 1], r[4 * p + 2], r[4 * p + 3]};
+      L[p] = v[p * kWave + xp];
+      R[p] = v[p * kWave + xn];
+      // keep the machine scheduler from sinking these LDS operations below
+      // the next plane's tail (it otherwise groups all of them at the end)
+      if (p + 1 < NPL) __builtin_amdgcn_sched_barrier(0);
+    }
   }
 }
 

@@ -209,8 +209,11 @@ __global__ __launch_bounds__(kBlock) void k_step(const uint64_t *__restrict__ in
 
 // k_step for the split layouts: wave w takes G groups of P = S/2
 // consecutive universes, grid-strided; all branches wave-uniform.  NET: the
-// tail network (7 = RULE 3's, 6 = life_tail6).
-template <int S, int G, bool NT, int NET>
+// tail network (7 = RULE 3's, 6 = life_tail6); D: registers exchanged by DPP
+// instead of LDS (gen_split), or kPipe: the software-pipelined LDS loop
+// (gens_split_pipe).
+constexpr int kPipe = -1;
+template <int S, int G, bool NT, int NET, int D = 0>
 __global__ __launch_bounds__(kBlock) void k_step_split(const uint64_t *__restrict__ in,
                                                        uint64_t *__restrict__ out, uint64_t n,
                                                        uint32_t gens) {
@@ -232,9 +235,14 @@ __global__ __launch_bounds__(kBlock) void k_step_split(const uint64_t *__restric
       }
       Split<S>::load(c, r[g]);
     }
-    for (uint32_t it = 0; it < gens; ++it) {
+    if constexpr (D == kPipe) {
 #pragma unroll
-      for (int g = 0; g < G; ++g) gen_split<S, NET>(r[g], lds + (wib * G + g) * S * kWave, lane);
+      for (int g = 0; g < G; ++g) gens_split_pipe<S, NET>(r[g], lds + (wib * G + g) * S * kWave, lane, gens);
+    } else {
+      for (uint32_t it = 0; it < gens; ++it) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) gen_split<S, NET, D>(r[g], lds + (wib * G + g) * S * kWave, lane);
+      }
     }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
@@ -467,11 +475,11 @@ StepFn pick_rule(int u, bool nt, int rule) {
     }
   }
 }
-template <int S, int NET>
+template <int S, int NET, int D = 0>
 StepFn pick_split(int groups, bool nt) {
   switch (groups) {
-    case 1: return nt ? k_step_split<S, 1, true, NET> : k_step_split<S, 1, false, NET>;
-    case 2: return nt ? k_step_split<S, 2, true, NET> : k_step_split<S, 2, false, NET>;
+    case 1: return nt ? k_step_split<S, 1, true, NET, D> : k_step_split<S, 1, false, NET, D>;
+    case 2: return nt ? k_step_split<S, 2, true, NET, D> : k_step_split<S, 2, false, NET, D>;
     default: return nullptr;
   }
 }
@@ -506,9 +514,35 @@ StepFn pick_step(const lifeapi_launch_cfg &c) {
     if (c.xchg == LIFEAPI_XCHG_ASM) return nt ? k_step_tile<8, 4, XASM, true, 7> : k_step_tile<8, 4, XASM, false, 7>;
     return pick_tile4<7>(c.xchg, nt);
   }
-  if ((c.rule >= 5 && c.rule <= 7) || (c.rule >= 10 && c.rule <= 12)) {  // split layouts: LDS exchange only
-    if (c.xchg != LIFEAPI_XCHG_LDS) return nullptr;
+  if ((c.rule >= 5 && c.rule <= 7) || (c.rule >= 10 && c.rule <= 12)) {  // split layouts
     const bool nt = c.nontemporal != 0;
+    if (c.xchg == LIFEAPI_XCHG_LDS_PIPE) {
+      switch (c.rule) {
+        case 6: return pick_split<8, 7, kPipe>(c.universes_per_wave, nt);
+        case 11: return pick_split<8, 6, kPipe>(c.universes_per_wave, nt);
+        case 12: return pick_split<16, 6, kPipe>(c.universes_per_wave, nt);
+        default: return nullptr;
+      }
+    }
+    if (c.xchg > LIFEAPI_XCHG_LDS_DPP(0) && (c.rule == 11 || c.rule == 12)) {
+      // LDS for most registers, DPP for D of them
+      const int d = c.xchg - LIFEAPI_XCHG_LDS_DPP(0);
+      if (c.rule == 11) {
+        switch (d) {
+          case 1: return pick_split<8, 6, 1>(c.universes_per_wave, nt);
+          case 2: return pick_split<8, 6, 2>(c.universes_per_wave, nt);
+          case 3: return pick_split<8, 6, 3>(c.universes_per_wave, nt);
+          case 4: return pick_split<8, 6, 4>(c.universes_per_wave, nt);
+          default: return nullptr;
+        }
+      }
+      switch (d) {
+        case 2: return pick_split<16, 6, 2>(c.universes_per_wave, nt);
+        case 4: return pick_split<16, 6, 4>(c.universes_per_wave, nt);
+        default: return nullptr;
+      }
+    }
+    if (c.xchg != LIFEAPI_XCHG_LDS) return nullptr;
     switch (c.rule) {
       case 5: return pick_split<4, 7>(c.universes_per_wave, nt);
       case 6: return pick_split<8, 7>(c.universes_per_wave, nt);

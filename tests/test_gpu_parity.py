@@ -23,6 +23,11 @@ ALL_CFGS += [(x, 1, nt, r) for r, xs in ((8, (0, 1, 8)), (9, (1,))) for x in xs 
 # the 6-LUT tail: split layouts (rules 10-12) and the 4-column tile (rule 13)
 ALL_CFGS += list(itertools.product((1,), (1, 2), (0, 1), (10, 11, 12)))
 ALL_CFGS += [(x, 1, nt, 13) for x in (0, 1) for nt in (0, 1)]
+# split layouts with part of the exchange by DPP (LIFEAPI_XCHG_LDS_DPP(d) = 16 + d)
+ALL_CFGS += [(16 + d, u, nt, 11) for d in (1, 2, 3, 4) for u in (1, 2) for nt in (0, 1)]
+ALL_CFGS += [(16 + d, 1, nt, 12) for d in (2, 4) for nt in (0, 1)]
+# the software-pipelined LDS loop (LIFEAPI_XCHG_LDS_PIPE = 9)
+ALL_CFGS += [(9, u, nt, r) for r in (6, 11, 12) for u in (1, 2) for nt in (0, 1)]
 
 
 def to_dev(a: np.ndarray) -> torch.Tensor:
