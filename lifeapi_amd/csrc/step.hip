@@ -374,7 +374,7 @@ __global__ __launch_bounds__(kBlock) void k_step_contains(const uint64_t *__rest
 // 4 universes; after every generation (r ^ w) & (w | u) is OR-ed over the
 // registers and one ballot per universe (its bits are every P-th) tests it,
 // with no branch per universe.  The check costs about 5 VALU per
-// universe-generation on top of the 20 of the step (+25 % measured,
+// universe-generation on top of the 18 of the step (+20-25 % measured,
 // profiles/r01/contains_bench.jsonl); branching around the bookkeeping
 // when no universe is clean measured slower still.
 // Without d_final, a wave stops once all its universes have hit.
