@@ -132,7 +132,27 @@ def cpu_baseline(x_host: np.ndarray, seconds: float):
     }
 
 
-def secondary_config3(hip, device, stream):
+def cpu_baseline_config3(x_host: np.ndarray, seconds: float):
+    """The reference's Step(gens) (oracle/_ref, else the C port) on the
+    config-3 shape: a bounded sample of the same universes, 1024 generations
+    each, on the host cores (`seconds` of work)."""
+    from oracle.oracle import Port, Ref
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    threads = max(1, min(threads, 16))
+    o, kind = (Ref(), "reference") if Ref.available() else (Port(), "port")
+    sample = x_host[: 64 * threads]
+    o.step_batch(sample[:threads], 1024, nthreads=threads)  # warm
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        o.step_batch(sample, 1024, nthreads=threads)
+        done += sample.shape[0]
+    el = time.perf_counter() - t0
+    return {"value": done * 1024 / el, "unit": "universe-gen/s", "cores": threads, "kind": kind,
+            "sample": f"{sample.shape[0]} of the config-3 universes x 1024 gens, {done // sample.shape[0]} "
+                      f"passes in {el:.2f}s, {threads} threads"}
+
+
+def secondary_config3(hip, device, stream, cpu_seconds=0.0):
     """Config 3: 64K universes x 1024 generations, state resident in VGPRs."""
     n, gens = 1 << 16, 1024
     a = hip.fill_random(n, seed=3, device=device, stream=stream)
@@ -160,6 +180,9 @@ def secondary_config3(hip, device, stream):
     peak_slots = 1024 * 2.4e9 / 2  # 1024 SIMDs
     measured_slots = 1024 / 0.978e-9
     cfg = hip.default_cfg(gens).as_dict()
+    cpu = None
+    if cpu_seconds > 0:
+        cpu = cpu_baseline_config3(a.cpu().numpy().view(np.uint64), cpu_seconds)
     return {"workload": "config3: 64K universes x 1024 generations (one launch)",
             "value": gps, "unit": "universe-gen/s", "cell_updates_per_s": gps * 4096,
             "kernel_ms": t * 1e3, "kernel_ms_min": min(ms), "kernel_ms_all": ms, "launch_cfg": cfg,
@@ -168,7 +191,8 @@ def secondary_config3(hip, device, stream):
                          "frac": gps * slots / peak_slots,
                          "measured_issue_peak": measured_slots / 1e12,
                          "frac_of_measured_issue_peak": gps * slots / measured_slots},
-            "reference_op_equivalent_Tops": OPS_PER_UNIVERSE_GEN * gps / 1e12}
+            "reference_op_equivalent_Tops": OPS_PER_UNIVERSE_GEN * gps / 1e12,
+            "cpu_baseline": cpu}
 
 
 def verify_first_launch(hip, out, first, n, gens, seed, stream, world, device):
@@ -304,7 +328,8 @@ def main():
 
     secondary = None
     if rank == 0 and world == 1 and not args.no_secondary:
-        secondary = {"config3": secondary_config3(hip, device, stream),
+        secondary = {"config3": secondary_config3(hip, device, stream,
+                                                  0.0 if args.no_cpu_baseline else args.cpu_seconds / 3),
                      "config5": secondary_config5(hip, device, stream)}
 
     ceiling, ceiling_src = copy_ceiling()

@@ -178,4 +178,19 @@ std::vector<std::string> RLEBatch(std::span<const S> states, int device = 0) {
 
 inline int DeviceCount() { return lifeapi_device_count(); }
 
+// Page-locks a caller-owned array for its lifetime (lifeapi_host_register):
+// keep one around a LifeState batch that a search loop steps repeatedly.
+class HostPin {
+ public:
+  HostPin(void *p, size_t bytes) : p_(p) { check(lifeapi_host_register(p, bytes)); }
+  template <class T>
+  explicit HostPin(std::span<T> s) : HostPin(static_cast<void *>(s.data()), s.size_bytes()) {}
+  HostPin(const HostPin &) = delete;
+  HostPin &operator=(const HostPin &) = delete;
+  ~HostPin() { (void)lifeapi_host_unregister(p_); }
+
+ private:
+  void *p_;
+};
+
 }  // namespace lifeapi

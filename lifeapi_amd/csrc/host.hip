@@ -22,6 +22,9 @@ int fail(int code, const char *fmt, const char *arg) {
   return code;
 }
 int fail_hip(hipError_t e, const char *what) {
+  // the error is reported through our return code: consume HIP's sticky
+  // per-thread copy, or the next launch's hipGetLastError() would return it
+  (void)hipGetLastError();
   char buf[512];
   std::snprintf(buf, sizeof buf, "%s: %s (hipError %d)", what, hipGetErrorString(e), (int)e);
   g_err = buf;
@@ -84,11 +87,24 @@ int launched(const char *what) {
 }
 
 // ---- host-pointer staging: one context per device ----
+// Chunks alternate between two streams, each with its own staging buffer,
+// and everything is issued asynchronously before one final sync per call.
+// Stream order alone protects a buffer's reuse (chunk k + 2 waits for chunk
+// k's D2H on the same stream).  Chunk k's H2D also waits (event) for chunk
+// k-1's H2D, so the two streams run one chunk apart and chunk k's D2H
+// overlaps chunk k+1's H2D; without that they start in phase and both
+// directions stay serialised.  That pays only for
+// page-locked host arrays (lifeapi_host_register): the runtime serialises
+// pageable copies in both directions (profiles/r01/host_bench.jsonl).
+constexpr int kLanes = 2;  // (the event chain below assumes two)
+constexpr size_t kChunkBytes = size_t(64) << 20;  // staging per stream and pass
+
 struct HostCtx {
   std::mutex mu;
-  hipStream_t stream = nullptr;
-  char *buf = nullptr;
-  size_t cap = 0;  // bytes
+  hipStream_t stream[kLanes] = {};
+  hipEvent_t h2d_done[kLanes] = {};
+  char *buf[kLanes] = {};
+  size_t cap = 0;  // bytes per stream
 };
 std::mutex g_ctx_mu;
 std::vector<HostCtx *> g_ctx;
@@ -100,58 +116,75 @@ HostCtx *ctx_for(int dev) {
   return g_ctx[dev];
 }
 
-constexpr size_t kStagingBytes = size_t(1) << 30;  // device staging per pass (1 GiB)
-
-// Stages n universes through this device's reusable buffer in chunks of at
-// most kStagingBytes: H2D, the stream-ordered *_dev entry point, D2H, sync.
+// Chunks are disjoint ranges of every array, so in-place arrays (src == dst)
+// are safe.
 int host_chunked(int dev, size_t n, const HostIO *io, int nio, ChunkFn fn, const void *arg) {
+  if (nio > 8) return fail(LIFEAPI_E_INVALID, "too many arrays%s");
   DeviceGuard guard;
   hipError_t e = hipSetDevice(dev);
   if (e != hipSuccess) return fail_hip(e, "hipSetDevice");
   HostCtx *c = ctx_for(dev);
   std::lock_guard<std::mutex> lk(c->mu);
-  if (!c->stream) {
-    e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-    if (e != hipSuccess) return fail_hip(e, "hipStreamCreate");
-  }
+  for (int l = 0; l < kLanes; ++l)
+    if (!c->stream[l]) {
+      e = hipStreamCreateWithFlags(&c->stream[l], hipStreamNonBlocking);
+      if (e != hipSuccess) return fail_hip(e, "hipStreamCreate");
+      e = hipEventCreateWithFlags(&c->h2d_done[l], hipEventDisableTiming);
+      if (e != hipSuccess) return fail_hip(e, "hipEventCreate");
+    }
   size_t per = 0;
   for (int k = 0; k < nio; ++k) per += (io[k].bytes + 255) & ~size_t(255);
-  const size_t chunk = std::max<size_t>(1, std::min(n, kStagingBytes / per));
+  const size_t half = (n + kLanes - 1) / kLanes;
+  const size_t chunk = std::max<size_t>(1, std::min(half, kChunkBytes / per));
   size_t need = 0;
   for (int k = 0; k < nio; ++k) need += ((io[k].bytes * chunk + 255) & ~size_t(255));
   if (c->cap < need) {
-    if (c->buf) (void)hipFree(c->buf);
-    c->buf = nullptr;
+    for (int l = 0; l < kLanes; ++l) {
+      if (c->buf[l]) (void)hipFree(c->buf[l]);
+      c->buf[l] = nullptr;
+    }
     c->cap = 0;
-    e = hipMalloc(&c->buf, need);
-    if (e != hipSuccess) return fail_hip(e, "hipMalloc(staging)");
+    for (int l = 0; l < kLanes; ++l) {
+      e = hipMalloc(&c->buf[l], need);
+      if (e != hipSuccess) return fail_hip(e, "hipMalloc(staging)");
+    }
     c->cap = need;
   }
+  int rc = LIFEAPI_OK;
   void *d[8];
-  for (size_t off = 0; off < n; off += chunk) {
-    const size_t m = std::min(chunk, n - off);
-    size_t pos = 0;
-    for (int k = 0; k < nio; ++k) {
-      d[k] = c->buf + pos;
-      pos += (io[k].bytes * chunk + 255) & ~size_t(255);
-      if (io[k].src) {
-        e = hipMemcpyAsync(d[k], (const char *)io[k].src + off * io[k].bytes, m * io[k].bytes,
-                           hipMemcpyHostToDevice, c->stream);
-        if (e != hipSuccess) return fail_hip(e, "hipMemcpyAsync(H2D)");
-      }
+  for (size_t k = 0; k * chunk < n && rc == LIFEAPI_OK; ++k) {
+    const int l = (int)(k % kLanes);
+    hipStream_t st = c->stream[l];
+    const size_t off = k * chunk, m = std::min(chunk, n - off);
+    if (k > 0 && (e = hipStreamWaitEvent(st, c->h2d_done[1 - l], 0)) != hipSuccess) {
+      rc = fail_hip(e, "hipStreamWaitEvent");
+      break;
     }
-    const int rc = fn(d, m, c->stream, arg);
-    if (rc != LIFEAPI_OK) return rc;
-    for (int k = 0; k < nio; ++k)
-      if (io[k].dst) {
-        e = hipMemcpyAsync((char *)io[k].dst + off * io[k].bytes, d[k], m * io[k].bytes,
-                           hipMemcpyDeviceToHost, c->stream);
-        if (e != hipSuccess) return fail_hip(e, "hipMemcpyAsync(D2H)");
-      }
-    e = hipStreamSynchronize(c->stream);
-    if (e != hipSuccess) return fail_hip(e, "hipStreamSynchronize");
+    size_t pos = 0;
+    for (int q = 0; q < nio && rc == LIFEAPI_OK; ++q) {
+      d[q] = c->buf[l] + pos;
+      pos += (io[q].bytes * chunk + 255) & ~size_t(255);
+      if (io[q].src &&
+          (e = hipMemcpyAsync(d[q], (const char *)io[q].src + off * io[q].bytes, m * io[q].bytes,
+                              hipMemcpyHostToDevice, st)) != hipSuccess)
+        rc = fail_hip(e, "hipMemcpyAsync(H2D)");
+    }
+    if (rc == LIFEAPI_OK && (e = hipEventRecord(c->h2d_done[l], st)) != hipSuccess)
+      rc = fail_hip(e, "hipEventRecord");
+    if (rc == LIFEAPI_OK) rc = fn(d, m, st, arg);
+    for (int q = 0; q < nio && rc == LIFEAPI_OK; ++q)
+      if (io[q].dst &&
+          (e = hipMemcpyAsync((char *)io[q].dst + off * io[q].bytes, d[q], m * io[q].bytes,
+                              hipMemcpyDeviceToHost, st)) != hipSuccess)
+        rc = fail_hip(e, "hipMemcpyAsync(D2H)");
   }
-  return LIFEAPI_OK;
+  // drain both streams even after an error: nothing may still read or write
+  // the caller's arrays once we return
+  for (int l = 0; l < kLanes; ++l) {
+    e = hipStreamSynchronize(c->stream[l]);
+    if (e != hipSuccess && rc == LIFEAPI_OK) rc = fail_hip(e, "hipStreamSynchronize");
+  }
+  return rc;
 }
 
 int host_device(int device) {
@@ -215,6 +248,20 @@ int lifeapi_step_batch(const uint64_t *in, uint64_t *out, size_t n, uint32_t gen
       return rcs[d];
     }
   return LIFEAPI_OK;
+}
+
+int lifeapi_host_register(void *p, size_t bytes) {
+  if (!p || bytes == 0) return fail(LIFEAPI_E_INVALID, "null or empty range to lifeapi_host_register%s");
+  if (lifeapi_device_count() <= 0) return fail(LIFEAPI_E_NODEVICE, "no HIP device visible%s");
+  const hipError_t e = hipHostRegister(p, bytes, hipHostRegisterPortable);
+  return e == hipSuccess ? LIFEAPI_OK : fail_hip(e, "hipHostRegister");
+}
+
+int lifeapi_host_unregister(void *p) {
+  if (!p) return fail(LIFEAPI_E_INVALID, "null pointer to lifeapi_host_unregister%s");
+  if (lifeapi_device_count() <= 0) return fail(LIFEAPI_E_NODEVICE, "no HIP device visible%s");
+  const hipError_t e = hipHostUnregister(p);
+  return e == hipSuccess ? LIFEAPI_OK : fail_hip(e, "hipHostUnregister");
 }
 
 int lifeapi_pop_batch(const uint64_t *states, uint32_t *pop, size_t n, int device) {

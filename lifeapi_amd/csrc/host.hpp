@@ -46,8 +46,9 @@ struct HostIO {
 };
 using ChunkFn = int (*)(void *const *dev, size_t m, hipStream_t s, const void *arg);
 
-// Stages n universes through this device's reusable buffer in chunks:
-// H2D, the stream-ordered *_dev entry point, D2H, sync.
+// Stages n universes through this device's reusable buffers in chunks that
+// alternate between two streams: H2D, the stream-ordered *_dev entry point,
+// D2H, all asynchronous, then one sync of both streams.
 int host_chunked(int dev, size_t n, const HostIO *io, int nio, ChunkFn fn, const void *arg);
 // the device a host-pointer call runs on (-1 = device 0), or an error code
 int host_device(int device);

@@ -67,6 +67,8 @@ _SIGS = {
     "lifeapi_refined_step_batch_dev": ([_vp, _vp, _sz, _vp], _int),
     "lifeapi_refined_step_batch_dev_cfg": ([_vp, _vp, _sz, _vp, ctypes.POINTER(LaunchCfg)], _int),
     "lifeapi_step_batch": ([_vp, _vp, _sz, _u32, _int], _int),
+    "lifeapi_host_register": ([_vp, _sz], _int),
+    "lifeapi_host_unregister": ([_vp], _int),
     "lifeapi_pop_batch": ([_vp, _vp, _sz, _int], _int),
     "lifeapi_weld_step_batch": ([_vp, _sz, _u32, _int], _int),
     "lifeapi_stable_pass_batch": ([_vp, _vp, _sz, _int, _u32, _int], _int),
@@ -211,6 +213,31 @@ def step_host(states: np.ndarray, generations: int = 1, device: int = 0,
     dst = np.empty_like(src) if out is None else out
     _check(lib.lifeapi_step_batch(src.ctypes.data, dst.ctypes.data, src.size // N, generations, device))
     return dst
+
+
+class host_pinned:
+    """Context manager: page-lock numpy arrays (lifeapi_host_register) for
+    the host-pointer calls inside the block."""
+
+    def __init__(self, *arrays: np.ndarray):
+        self.arrays = arrays
+
+    def __enter__(self):
+        done = []
+        try:
+            for a in self.arrays:
+                _check(lib.lifeapi_host_register(a.ctypes.data, a.nbytes))
+                done.append(a)
+        except Exception:
+            for a in done:
+                lib.lifeapi_host_unregister(a.ctypes.data)
+            raise
+        return self
+
+    def __exit__(self, *exc):
+        for a in self.arrays:
+            _check(lib.lifeapi_host_unregister(a.ctypes.data))
+        return False
 
 
 def pop_host(states: np.ndarray, device: int = 0) -> np.ndarray:

@@ -102,6 +102,23 @@ static void MultiDevice_Shards() {
   for (size_t i = 0; i < a.size(); ++i) EXPECT_EQ(a[i], b[i]);
 }
 
+// a page-locked batch (lifeapi::HostPin) stepped many chunks at a time gives
+// the CPU's answer, as the pageable batch does
+static void HostPin_ManyChunks() {
+  uint64_t seed = 7;
+  std::vector<LifeState> a(300000), want;
+  for (auto &s : a) s = LifeState::RandomState(seed);
+  want = a;
+  for (size_t i = 0; i < 2000; ++i) want[i].Step(2);
+  {
+    lifeapi::HostPin pin{std::span(a)};
+    lifeapi::StepBatch(std::span(a), 2);
+  }
+  for (size_t i = 0; i < 2000; ++i) EXPECT_EQ(a[i], want[i]);
+  lifeapi::StepBatch(std::span(want).subspan(2000), 2);
+  for (size_t i = 2000; i < a.size(); ++i) EXPECT_EQ(a[i], want[i]);
+}
+
 // LifeWeldTest.StableTest (tests/LifeWeldTest.cpp:6-17), batched: a weld of a
 // still life with nothing frozen is invariant; random welds match the CPU
 static void LifeWeld_StableAndRandom() {
@@ -206,6 +223,7 @@ int main() {
   Interaction_BatchMatchesCpu();
   Glider_Translation();
   MultiDevice_Shards();
+  HostPin_ManyChunks();
   LifeWeld_StableAndRandom();
   Counts_And_Contains();
   Stable_Propagate();

@@ -216,6 +216,24 @@ def test_host_api(hip, port):
     assert (hip.pop_host(x) == port.pop(x)).all()
 
 
+def test_host_api_many_chunks_pinned(hip, port):
+    """More chunks than lanes (64 MiB chunks, two lanes: 300K universes is
+    three chunks, the last ragged), in place and out of place, pageable and
+    page-locked (lifeapi_host_register)."""
+    n = 300_000
+    x = port.fill(n, seed=9)
+    want = port.step_batch(x, 2)
+    out = np.zeros_like(x)
+    assert (hip.step_host(x, 2, out=out).reshape(-1, 64) == want).all()
+    y = x.copy()
+    with hip.host_pinned(y, out):
+        out[:] = 0
+        assert (hip.step_host(y, 2, out=out).reshape(-1, 64) == want).all()
+        hip.step_host(y, 2, out=y)  # in place, pinned
+        assert (y == want).all()
+    assert hip.lib.lifeapi_host_unregister(y.ctypes.data) != 0  # no longer registered
+
+
 def test_host_api_other_kernels(hip, port):
     """Host-pointer forms of the weld / stable / counts / refined / contains
     entry points (staged through device memory in chunks)."""
