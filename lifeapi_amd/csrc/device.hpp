@@ -233,6 +233,38 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   return z ^ (z >> 31);
 }
 
+// Wave sums without the LDS crossbar (__shfl_xor is one ds_bpermute per
+// step: a chain of six LDS round trips): four DPP adds sum each 16-lane row
+// (quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror, row_mirror),
+// then v_readlane of lanes 0/16/32/48 and scalar adds.  Wave-uniform result.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t wave_sum_u32_dpp(uint32_t v) {
+  v += dpp_mov<0xB1>(v);
+  v += dpp_mov<0x4E>(v);
+  v += dpp_mov<0x141>(v);
+  v += dpp_mov<0x140>(v);
+  return (uint32_t)__builtin_amdgcn_readlane(v, 0) + (uint32_t)__builtin_amdgcn_readlane(v, 16) +
+         (uint32_t)__builtin_amdgcn_readlane(v, 32) + (uint32_t)__builtin_amdgcn_readlane(v, 48);
+}
+__device__ __forceinline__ uint64_t wave_sum_u64_dpp(uint64_t v) {
+  auto step = [&](auto mov) __attribute__((always_inline)) {
+    v += (uint64_t)mov((uint32_t)v) | ((uint64_t)mov((uint32_t)(v >> 32)) << 32);
+  };
+  step(dpp_mov<0xB1>);
+  step(dpp_mov<0x4E>);
+  step(dpp_mov<0x141>);
+  step(dpp_mov<0x140>);
+  uint64_t t = 0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    t += (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)v, 16 * r) |  // (readlane
+         ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), 16 * r) << 32);  // is int)
+  return t;
+}
+
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);

@@ -10,7 +10,8 @@ namespace {
 
 // The per-universe reductions below take kRedU universes per wave, all loads
 // issued before the first reduction (one wave per universe and a grid-stride
-// loop left them latency-bound at 36-60 % of HBM, tools/rows_bench.py).
+// loop left them latency-bound at 36-60 % of HBM, tools/rows_bench.py), and
+// sum over the wave by DPP (wave_sum_*_dpp), not through ds_bpermute.
 constexpr int kRedU = 4;
 
 // GetPop (LifeAPI.hpp:290-298): two universes' popcounts per 32-bit reduction
@@ -25,7 +26,7 @@ __global__ __launch_bounds__(kBlock) void k_pop(const uint64_t *__restrict__ s,
     for (int k = 0; k < kRedU; ++k) c[k] = u0 + k < n ? (uint32_t)__popcll(s[(u0 + k) * kWave + lane]) : 0u;
 #pragma unroll
     for (int k = 0; k < kRedU; k += 2) {
-      const uint32_t t = wave_sum_u32(c[k] | c[k + 1] << 16);  // each sum <= 4096
+      const uint32_t t = wave_sum_u32_dpp(c[k] | c[k + 1] << 16);  // each sum <= 4096
       if (lane == 0) {
         if (u0 + k < n) pop[u0 + k] = t & 0xFFFF;
         if (u0 + k + 1 < n) pop[u0 + k + 1] = t >> 16;
@@ -46,7 +47,7 @@ __global__ __launch_bounds__(kBlock) void k_hash(const uint64_t *__restrict__ s,
     for (int k = 0; k < kRedU; ++k) m[k] = u0 + k < n ? s[(u0 + k) * kWave + lane] : 0ull;
 #pragma unroll
     for (int k = 0; k < kRedU; ++k) {
-      const uint64_t t = wave_sum_u64(mix64(m[k] + (uint64_t)(lane + 1) * kGolden));
+      const uint64_t t = wave_sum_u64_dpp(mix64(m[k] + (uint64_t)(lane + 1) * kGolden));
       if (lane == 0 && u0 + k < n) h[u0 + k] = mix64(t);
     }
   }
