@@ -1,0 +1,173 @@
+// ref_dropin_test.cpp -- the drop-in claim, checked with the REFERENCE's own
+// types: a search loop keeps #include "LifeAPI.hpp" (and friends) and adds
+// <lifeapi/batch.hpp>; the batched GPU calls on ::LifeState, ::LifeTarget,
+// ::LifeWeld, ::NeighbourCount and ::LifeStable must give exactly what the
+// reference's own member functions give.
+//
+// Built by oracle/Makefile (target ref, into oracle/_ref/) only where
+// /root/reference exists (this container): the reference headers are compiled
+// in, from where they lie, with oracle/ref_prelude.hpp (see oracle/Makefile
+// for the two image gaps it bridges).  The binary travels to the GPU box with
+// oracle/_ref/; nothing reads /root/reference at run time.  Run by
+// tests/test_cpp_facade.py.  Exit status = number of failed checks.
+#include <lifeapi/batch.hpp>  // first: ref_prelude.hpp defines `constexpr` away
+
+#include "ref_prelude.hpp"
+
+#include "LifeAPI.hpp"
+#include "LifeStable.hpp"
+#include "LifeTarget.hpp"
+#include "LifeWeld.hpp"
+#include "NeighbourCount.hpp"
+#include "Parsing.hpp"
+
+#include <cstdio>
+#include <span>
+#include <vector>
+
+static int g_failures = 0, g_checks = 0;
+#define EXPECT_TRUE(c)                                                                  \
+  do {                                                                                  \
+    ++g_checks;                                                                         \
+    if (!(c)) {                                                                         \
+      ++g_failures;                                                                     \
+      if (g_failures < 20) std::fprintf(stderr, "%s:%d: %s failed\n", __FILE__, __LINE__, #c); \
+    }                                                                                   \
+  } while (0)
+
+// tests/StepAltTest.cpp:5-13 on the reference's own RandomState(), batched:
+// StepBatch == Step() == StepAlt() for every state
+static void StepAltTest_Random() {
+  std::vector<LifeState> batch(10000), cpu, alt;
+  for (auto &s : batch) s = LifeState::RandomState();
+  cpu = alt = batch;
+  for (size_t i = 0; i < batch.size(); ++i) {
+    cpu[i].Step();
+    alt[i].StepAlt();
+  }
+  lifeapi::StepBatch(std::span(batch), 1);
+  for (size_t i = 0; i < batch.size(); ++i) {
+    EXPECT_TRUE(batch[i] == cpu[i]);
+    EXPECT_TRUE(cpu[i] == alt[i]);
+  }
+}
+
+// Stepped(n) (LifeAPI.hpp:882-886) into a second span, and GetPop()
+static void Stepped_And_Pop() {
+  std::vector<LifeState> in(3000), out(3000);
+  for (auto &s : in) s = LifeState::RandomState();
+  lifeapi::SteppedBatch(std::span<const LifeState>(in), std::span(out), 37);
+  const std::vector<uint32_t> pops = lifeapi::GetPopBatch(std::span<const LifeState>(out));
+  for (size_t i = 0; i < in.size(); ++i) {
+    EXPECT_TRUE(out[i] == in[i].Stepped(37));
+    EXPECT_TRUE(pops[i] == (uint32_t)out[i].GetPop());
+  }
+}
+
+// R-pentomino (BASELINE config 1) to generation 1103
+static void RPentomino() {
+  std::vector<LifeState> one{LifeState::Parse("b2o$2o$bo!")};
+  LifeState cpu = one[0];
+  cpu.Step(1103);
+  lifeapi::StepBatch(std::span(one), 1103);
+  EXPECT_TRUE(one[0] == cpu);
+  EXPECT_TRUE(one[0].GetPop() == 113);
+}
+
+// LifeState::Contains(const LifeTarget&) (LifeTarget.hpp:44-51)
+static void Contains_Target() {
+  const LifeState block = LifeState::Parse("2o$2o!");
+  const LifeTarget target(block, block.ZOI() & ~block);
+  std::vector<LifeState> s(2000);
+  for (size_t i = 0; i < s.size(); ++i) {
+    s[i] = LifeState::RandomState();
+    if (i % 3 == 0) s[i] = (s[i] & ~block.ZOI()) | block;
+  }
+  const std::vector<uint8_t> hit = lifeapi::ContainsBatch(std::span<const LifeState>(s), target);
+  int hits = 0;
+  for (size_t i = 0; i < s.size(); ++i) {
+    EXPECT_TRUE((hit[i] != 0) == s[i].Contains(target));
+    hits += hit[i] != 0;
+  }
+  EXPECT_TRUE(hits >= 600);
+}
+
+// NeighbourCount(state) (NeighbourCount.hpp:40-70)
+static void NeighbourCount_Planes() {
+  std::vector<LifeState> s(1000);
+  for (auto &x : s) x = LifeState::RandomState();
+  std::vector<NeighbourCount> nc(s.size(), NeighbourCount(LifeState()));
+  lifeapi::NeighbourCountBatch(std::span<const LifeState>(s), std::span(nc));
+  for (size_t i = 0; i < s.size(); ++i) {
+    const NeighbourCount want(s[i]);
+    EXPECT_TRUE(nc[i].bit3 == want.bit3 && nc[i].bit2 == want.bit2 && nc[i].bit1 == want.bit1 &&
+                nc[i].bit0 == want.bit0);
+  }
+}
+
+// LifeWeld::Step() (LifeWeld.hpp:169-186) on welds from FromRequired
+// (tests/LifeWeldTest.cpp:19-33 shape, Parse for the `$`-safe patterns)
+static void LifeWeld_Step() {
+  const LifeState eater = LifeState::Parse("2o$obo$2bo$2b2o!");
+  std::vector<LifeWeld> w;
+  for (int k = 0; k < 300; ++k) {
+    const LifeState junk = LifeState::RandomState() & LifeState::Parse("8o$8o$8o$8o!").Moved(20, 20);
+    w.push_back(LifeWeld::FromRequired(eater | junk, eater));
+  }
+  std::vector<LifeWeld> cpu = w;
+  for (auto &x : cpu) {
+    x.Step();
+    x.Step();
+  }
+  lifeapi::WeldStepBatch(std::span(w), 2);
+  for (size_t i = 0; i < w.size(); ++i) EXPECT_TRUE(w[i].state == cpu[i].state);
+}
+
+// LifeStable::Propagate() (LifeStable.hpp:718-729) on partially unknown still
+// lifes: every plane and the PropagateResult
+static void LifeStable_Propagate() {
+  std::vector<LifeStable> s;
+  const LifeState block = LifeState::Parse("2o$2o!");
+  for (int k = 0; k < 200; ++k) {
+    LifeStable c;
+    LifeState st;
+    for (int b = 0; b < 5; ++b) st |= block.Moved(13 * ((k + 3 * b) % 5), 11 * ((k * 7 + b) % 5));
+    LifeState unk = LifeState::Parse("6o$6o$6o$6o$6o$6o!").Moved((k * 5) % 50, (k * 3) % 50);
+    c.state = st & ~unk;
+    c.unknown = unk;
+    s.push_back(c);
+  }
+  std::vector<LifeStable> cpu = s;
+  std::vector<LifeStable::PropagateResult> want;
+  for (auto &x : cpu) want.push_back(x.Propagate());
+  const std::vector<lifeapi::PropagateResult> got = lifeapi::PropagateBatch(std::span(s));
+  for (size_t i = 0; i < s.size(); ++i) {
+    EXPECT_TRUE(got[i].consistent == want[i].consistent && got[i].changed == want[i].changed);
+    EXPECT_TRUE(s[i] == cpu[i]);  // every plane (LifeStable::operator==, LifeStable.hpp:55)
+  }
+}
+
+// LifeState::Parse / RLE() (Parsing.hpp:143-204), batched
+static void Rle_RoundTrip() {
+  std::vector<LifeState> s(500);
+  for (auto &x : s) x = LifeState::RandomState() & LifeState::RandomState();
+  const std::vector<std::string> rle = lifeapi::RLEBatch(std::span<const LifeState>(s));
+  const std::vector<LifeState> back = lifeapi::ParseBatch<LifeState>(std::span<const std::string>(rle));
+  for (size_t i = 0; i < s.size(); ++i) {
+    EXPECT_TRUE(rle[i] == s[i].RLE());
+    EXPECT_TRUE(back[i] == LifeState::Parse(rle[i]));
+  }
+}
+
+int main() {
+  StepAltTest_Random();
+  Stepped_And_Pop();
+  RPentomino();
+  Contains_Target();
+  NeighbourCount_Planes();
+  LifeWeld_Step();
+  LifeStable_Propagate();
+  Rle_RoundTrip();
+  std::printf("%d checks, %d failures\n", g_checks, g_failures);
+  return g_failures == 0 ? 0 : 1;
+}

@@ -37,3 +37,18 @@ def test_step_batch_cpp_asan():
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
     print(r.stdout, r.stderr[-4000:])
     assert r.returncode == 0, r.stderr[-4000:]
+
+
+@pytest.mark.gpu
+def test_reference_types_dropin():
+    """The batch header on the REFERENCE's own ::LifeState / ::LifeTarget /
+    ::LifeWeld / ::NeighbourCount / ::LifeStable (tests/cpp/ref_dropin_test.cpp,
+    compiled against the reference headers in the build container by
+    oracle/Makefile, target ref) gives
+    exactly what their member functions give."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "ref_dropin_test")  # oracle/Makefile, target ref
+    if not os.path.exists(exe):
+        pytest.skip("oracle/_ref/ref_dropin_test needs the reference headers at build time")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    print(r.stdout, r.stderr[-4000:])
+    assert r.returncode == 0, r.stderr[-4000:]
