@@ -4,6 +4,7 @@
 // (LifeStable.hpp:526-729) and the config-5 unknown_step_refined step.
 #include "device.hpp"
 #include "host.hpp"
+#include "split_layout.hpp"
 
 using namespace lifeapi_impl;
 
@@ -97,6 +98,95 @@ __global__ __launch_bounds__(kBlock) void k_weld(uint64_t *__restrict__ welds, u
     const W f2 = ld<true>(p + kWave), f1 = ld<true>(p + 2 * kWave), f0 = ld<true>(p + 3 * kWave);
     for (uint32_t g = 0; g < gens; ++g) s = weld_gen(s, f2, f1, f0);
     st<true>(p, s);
+  }
+}
+
+// LifeWeld::Step iterated on the 8-way row split (split_layout.hpp): a wave
+// holds 4 welds, state and the three frozen planes each in 8 VGPRs per lane,
+// the state exchanged through LDS as in gen_split.
+//
+// The tail: the reference adds the inclusive count's bits 2..0 to the frozen
+// count (HalfAdd, FullAdd, FullAdd, mod 8) and applies the Life rule to the
+// sum (LifeWeld.hpp:169-186): 13 v_bitop3 after the h-layer when written as
+// that adder chain.  tools/cgp_weld.c (the network search of
+// tools/cgp_search.c with f2, f1, f0 as three more inputs) found this 10-gate
+// network for the same function on all 4096 combinations of neighbourhood
+// and frozen count, using the centre-row don't-cares; checked by
+// tests/test_oracle.py::test_weld_tail_truth, and every GPU result is
+// compared with the reference's own LifeWeld::Step.  Per 32-bit word and
+// generation: 12 v_bitop3 with the h-layer, against about 25 slots on the
+// natural layout (k_weld).  Its layout change of four planes costs more than
+// the plain step's, so it pays from about 12 generations up: 256K welds x 16
+// gens 0.24 vs 0.29 ms, x 256 gens 2.30 vs 3.31 ms, x 3 gens 0.14 vs 0.11 ms
+// (profiles/r01/weld_ab.jsonl).
+constexpr uint32_t kW0 = 0x69, kW2 = 0x52, kW5 = 0x95, kW6 = 0xA5, kW8 = 0x31, kW9 = 0x28;
+__device__ __forceinline__ uint32_t weld_tail(uint32_t h0u, uint32_t h0, uint32_t h0d, uint32_t h1u,
+                                              uint32_t h1, uint32_t h1d, uint32_t a, uint32_t f2,
+                                              uint32_t f1, uint32_t f0) {
+  const uint32_t w0 = lut3<kW0>(h0u, h0d, f0);
+  const uint32_t w1 = lut3<kXor3>(f1, h1u, h1d);
+  const uint32_t w2 = lut3<kW2>(w0, a, h0);
+  const uint32_t w3 = lut3<kMaj>(h0d, f0, w0);
+  const uint32_t w4 = lut3<kMaj>(h1d, f1, h1u);
+  const uint32_t w5 = lut3<kW5>(w1, w3, f2);
+  const uint32_t w6 = lut3<kW6>(w5, h1d, w4);
+  const uint32_t w7 = lut3<kXor3>(w1, w2, w3);
+  const uint32_t w8 = lut3<kW8>(a, w6, w2);
+  return lut3<kW9>(h1, w7, w8);
+}
+
+__device__ __forceinline__ void gen_weld_split(uint32_t (&r)[8], const uint32_t (&f2)[8],
+                                               const uint32_t (&f1)[8], const uint32_t (&f0)[8],
+                                               uint32_t *slot, int lane) {
+  constexpr int S = 8, P = 4;
+  uint32_t lv[S], rv[S];
+  lds_exchange<S>(r, lv, rv, slot, lane);
+  uint32_t h0[S], h1[S];
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    h0[j] = lut3<kXor3>(lv[j], r[j], rv[j]);
+    h1[j] = lut3<kMaj>(lv[j], r[j], rv[j]);
+  }
+  const uint32_t h0u = __builtin_amdgcn_alignbit(h0[S - 1], h0[S - 1], 32 - P);  // rotl P
+  const uint32_t h1u = __builtin_amdgcn_alignbit(h1[S - 1], h1[S - 1], 32 - P);
+  const uint32_t h0d = __builtin_amdgcn_alignbit(h0[0], h0[0], P);  // rotr P
+  const uint32_t h1d = __builtin_amdgcn_alignbit(h1[0], h1[0], P);
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    const uint32_t a0 = j == 0 ? h0u : h0[j - 1], c0 = j == S - 1 ? h0d : h0[j + 1];
+    const uint32_t a1 = j == 0 ? h1u : h1[j - 1], c1 = j == S - 1 ? h1d : h1[j + 1];
+    r[j] = weld_tail(a0, h0[j], c0, a1, h1[j], c1, r[j], f2[j], f1[j], f0[j]);
+  }
+}
+
+template <bool NT>
+__global__ __launch_bounds__(kBlock) void k_weld_split(uint64_t *__restrict__ welds, uint64_t n,
+                                                       uint32_t gens) {
+  constexpr int S = 8, P = 4;
+  __shared__ uint32_t lds[kWavesPerBlock * S * kWave];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock * P;
+  for (uint64_t u0 = ((uint64_t)blockIdx.x * kWavesPerBlock + wib) * P; u0 < n; u0 += stride) {
+    uint32_t r[S], f2[S], f1[S], f0[S];
+    {
+      W c[4][P];  // [plane][weld]: state, frozen2, frozen1, frozen0 (LifeWeld.hpp:18-20)
+#pragma unroll
+      for (int u = 0; u < P; ++u)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          c[q][u] = u0 + u < n ? ld<NT>(welds + ((u0 + u) * 4 + q) * kWave + lane) : W{0u, 0u};
+      Split<S>::load(c[0], r);
+      Split<S>::load(c[1], f2);
+      Split<S>::load(c[2], f1);
+      Split<S>::load(c[3], f0);
+    }
+    for (uint32_t g = 0; g < gens; ++g) gen_weld_split(r, f2, f1, f0, lds + wib * S * kWave, lane);
+    W c[P];
+    Split<S>::store(r, c);
+#pragma unroll
+    for (int u = 0; u < P; ++u)
+      if (u0 + u < n) st<NT>(welds + (u0 + u) * 4 * kWave + lane, c[u]);
   }
 }
 
@@ -444,8 +534,13 @@ int lifeapi_weld_step_batch_dev(uint64_t *d_welds, size_t n, uint32_t generation
     return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_weld_step_batch_dev%s");
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
-  hipLaunchKernelGGL(k_weld, dim3(grid_for(n, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream,
-                     d_welds, (uint64_t)n, generations);
+  if (generations >= 12)  // state resident in VGPRs on the split layout (k_weld_split)
+    hipLaunchKernelGGL(generations < 32 ? k_weld_split<true> : k_weld_split<false>,
+                       dim3(grid_for((n + 3) / 4, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream,
+                       d_welds, (uint64_t)n, generations);
+  else
+    hipLaunchKernelGGL(k_weld, dim3(grid_for(n, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream,
+                       d_welds, (uint64_t)n, generations);
   return launched("k_weld launch");
 }
 

@@ -355,14 +355,17 @@ def test_weld_golden_gpu(hip):
         assert (d.cpu().numpy().view(np.uint64) == g[key]).all()
 
 
-def test_weld_vs_oracle_ragged(hip, port):
-    n = 3003
-    w = port.fill(n * 4, seed=9191).reshape(n, 256)
-    w[:, 64:] &= port.fill(n * 3, seed=9192).reshape(n, 192)
+@pytest.mark.parametrize("n,gens", [(3003, 1), (3003, 2), (3003, 4), (3003, 12), (3003, 31), (5, 33), (1, 13), (1026, 100)])
+def test_weld_vs_oracle_ragged(hip, port, n, gens):
+    """Natural layout (gens < 12) and the split-layout kernel (k_weld_split,
+    4 welds per wave: ragged n; nontemporal below 32 gens) against the
+    oracle's LifeWeld::Step."""
+    w = port.fill(n * 4, seed=9191 + gens).reshape(n, 256)
+    w[:, 64:] &= port.fill(n * 3, seed=9192 + gens).reshape(n, 192)
     d = to_dev(w).reshape(n, 256)
-    hip.weld_step(d, 4)
+    hip.weld_step(d, gens)
     torch.cuda.synchronize()
-    assert (d.cpu().numpy().view(np.uint64) == port.weld_step(w, 4)).all()
+    assert (d.cpu().numpy().view(np.uint64) == port.weld_step(w, gens)).all()
 
 
 # ---- LifeStable passes (SURVEY 8(f) row 3) ----

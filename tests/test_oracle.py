@@ -249,6 +249,41 @@ def test_net6_truth():
         assert got == int(cnt == 3 or (a == 1 and cnt == 4)), bits
 
 
+def test_weld_tail_truth():
+    """The 10-gate LifeWeld tail of k_weld_split (weld_tail, stencils.hip:
+    gates and tables parsed from the source) behind the h-layer, on all 512
+    neighbourhoods x 8 frozen counts, against LifeWeld::Step's adder chain and
+    rule (LifeWeld.hpp:169-186: count bits 2..0 + frozen, mod 8)."""
+    import re
+    src = open(os.path.join(os.path.dirname(GOLD), "..", "lifeapi_amd", "csrc", "stencils.hip")).read()
+    tabs = {"kMaj": 0xE8, "kXor3": 0x96}
+    tabs.update({k: int(v, 16) for k, v in re.findall(r"\b(kW\d) = 0x([0-9A-Fa-f]+)", src)})
+    body = src[src.index("uint32_t weld_tail("):]
+    body = body[:body.index("\n}\n")]
+    gates = re.findall(r"const uint32_t (w\d) = lut3<(\w+)>\((\w+), (\w+), (\w+)\);", body)
+    ret = re.search(r"return lut3<(\w+)>\((\w+), (\w+), (\w+)\);", body)
+    assert len(gates) == 9 and ret
+
+    def lut(tab, x, y, z):
+        return (tab >> ((x << 2) | (y << 1) | z)) & 1
+
+    for bits in range(512):
+        n = [(bits >> i) & 1 for i in range(9)]      # n[3*col + row], col 0 = left
+        a, cnt = n[4], sum(n)
+        rows = [(n[r], n[3 + r], n[6 + r]) for r in range(3)]
+        for fz in range(8):
+            v = {"a": a, "f0": fz & 1, "f1": (fz >> 1) & 1, "f2": fz >> 2}
+            for nm, r in (("u", 0), ("", 1), ("d", 2)):
+                v["h0" + nm] = lut(0x96, *rows[r])
+                v["h1" + nm] = lut(0xE8, *rows[r])
+            for g, tab, x, y, z in gates:
+                v[g] = lut(tabs[tab], v[x], v[y], v[z])
+            got = lut(tabs[ret[1]], v[ret[2]], v[ret[3]], v[ret[4]])
+            t = ((cnt & 7) + fz) & 7
+            s0, s1, s2 = t & 1, (t >> 1) & 1, t >> 2
+            assert got == (s0 ^ s2) & (s1 ^ s2) & (a | s0), (bits, fz)
+
+
 def test_stable_vulnerable_golden(port):
     """LifeStable::Vulnerable (LifeStable.hpp:366-412) vs the reference's output."""
     g = load("stable.npz")

@@ -74,6 +74,11 @@ def main():
     welds = torch.cat([hip.fill_random(n, seed=s).view(n, 1, 64) for s in (11, 12, 13, 14)], 1).reshape(n, 256)
     welds[:, 64:] &= hip.fill_random(3 * n, seed=15).view(n, 192)
     report("k_weld (1 gen)", n, 2048 + 512, timed(lambda: hip.weld_step(welds, 1)))
+    # iterated welds (k_weld_split, VALU-bound): weld-generations per second
+    nw, gw = 1 << 18, 256
+    ms = timed(lambda: hip.weld_step(welds[:nw], gw))
+    print(json.dumps({"kernel": "k_weld_split (256 gens)", "objects": nw, "gens": gw, "ms": ms,
+                      "weld_gen_per_s": nw * gw / ms * 1e3}), flush=True)
     st = stable_inputs(n)
     for name in hip.STABLE_PASSES:
         work = st.clone()
