@@ -142,6 +142,19 @@ std::vector<uint8_t> ContainsBatch(std::span<const S> in, const T &target, int d
   return r;
 }
 
+// The search-loop idiom over a batch, in place (LifeAPI.hpp:1196-1216,
+// LifeTarget.hpp:44-51):
+//     for (unsigned g = 1; g <= gens; ++g) { s.Step(); if (!first && s.Contains(target)) first = g; }
+// returns first (0 = never) per state; the states end Stepped(gens).
+template <LifeStateLayout S, LifeTargetLayout T>
+std::vector<uint32_t> StepContainsBatch(std::span<S> states, const T &target, unsigned gens, int device = 0) {
+  std::vector<uint32_t> first(states.size());
+  const uint64_t *t = words(&target);
+  check(lifeapi_step_contains_batch(words(states.data()), words(states.data()), t, t + 64, first.data(),
+                                    states.size(), gens, device));
+  return first;
+}
+
 // LifeState::Parse of every string (Parsing.hpp:143-198).  status (optional)
 // gets lifeapi_parse_rle_batch's per-pattern bits: 1 = a live cell off the
 // 64x64 board was dropped (the reference writes out of bounds there), 2 =

@@ -398,4 +398,47 @@ int lifeapi_contains_batch(const uint64_t *states, const uint64_t *wanted, const
   return rc;
 }
 
+int lifeapi_step_contains_batch(const uint64_t *in, uint64_t *final_states, const uint64_t *wanted,
+                                const uint64_t *unwanted, uint32_t *first_gen, size_t n,
+                                uint32_t generations, int device) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!in || !wanted || !unwanted || !first_gen || !aligned8(in))
+    return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_step_contains_batch%s");
+  if (final_states) {
+    const int rc = check_batch(in, final_states, n);
+    if (rc != LIFEAPI_OK) return rc;
+  }
+  const int dev = host_device(device);
+  if (dev < 0) return dev;
+  DeviceGuard guard;
+  hipError_t e = hipSetDevice(dev);
+  if (e != hipSuccess) return fail_hip(e, "hipSetDevice");
+  uint64_t *dt = nullptr;  // the target, a tiny device copy owned by this call
+  if ((e = hipMalloc(&dt, 2 * 512)) != hipSuccess) return fail_hip(e, "hipMalloc(target)");
+  int rc = LIFEAPI_OK;
+  if ((e = hipMemcpy(dt, wanted, 512, hipMemcpyHostToDevice)) != hipSuccess ||
+      (e = hipMemcpy(dt + 64, unwanted, 512, hipMemcpyHostToDevice)) != hipSuccess)
+    rc = fail_hip(e, "hipMemcpy(target)");
+  if (rc == LIFEAPI_OK) {
+    struct Arg {
+      const uint64_t *t;
+      uint32_t gens;
+      bool keep;
+    } arg{dt, generations, final_states != nullptr};
+    // the states' staging slot doubles as the device final buffer (in place)
+    const HostIO io[2] = {{in, final_states, 512}, {nullptr, first_gen, 4}};
+    rc = host_chunked(dev, n, io, 2,
+                      [](void *const *d, size_t m, hipStream_t s, const void *a) {
+                        const Arg *g = (const Arg *)a;
+                        return lifeapi_step_contains_batch_dev((const uint64_t *)d[0],
+                                                               g->keep ? (uint64_t *)d[0] : nullptr,
+                                                               g->t, g->t + 64, (uint32_t *)d[1], m,
+                                                               g->gens, s);
+                      },
+                      &arg);
+  }
+  (void)hipFree(dt);
+  return rc;
+}
+
 }  // extern "C"

@@ -68,6 +68,7 @@ _SIGS = {
     "lifeapi_refined_step_batch_dev_cfg": ([_vp, _vp, _sz, _vp, ctypes.POINTER(LaunchCfg)], _int),
     "lifeapi_step_batch": ([_vp, _vp, _sz, _u32, _int], _int),
     "lifeapi_host_register": ([_vp, _sz], _int),
+    "lifeapi_step_contains_batch": ([_vp, _vp, _vp, _vp, _vp, _sz, _u32, _int], _int),
     "lifeapi_host_unregister": ([_vp], _int),
     "lifeapi_pop_batch": ([_vp, _vp, _sz, _int], _int),
     "lifeapi_weld_step_batch": ([_vp, _sz, _u32, _int], _int),
@@ -213,6 +214,20 @@ def step_host(states: np.ndarray, generations: int = 1, device: int = 0,
     dst = np.empty_like(src) if out is None else out
     _check(lib.lifeapi_step_batch(src.ctypes.data, dst.ctypes.data, src.size // N, generations, device))
     return dst
+
+
+def step_contains_host(states: np.ndarray, wanted: np.ndarray, unwanted: np.ndarray, generations: int,
+                       final: np.ndarray | None = None, device: int = 0) -> np.ndarray:
+    """Host-pointer ``lifeapi_step_contains_batch``: first generation (1..gens,
+    0 = never) containing the target; ``final`` (may be ``states``) gets
+    Stepped(gens)."""
+    src = _host_u64(states)
+    w, u = _host_u64(wanted), _host_u64(unwanted)
+    first = np.empty(src.size // N, dtype=np.uint32)
+    fptr = None if final is None else final.ctypes.data
+    _check(lib.lifeapi_step_contains_batch(src.ctypes.data, fptr, w.ctypes.data, u.ctypes.data,
+                                           first.ctypes.data, src.size // N, generations, device))
+    return first
 
 
 class host_pinned:

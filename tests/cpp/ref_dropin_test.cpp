@@ -92,6 +92,32 @@ static void Contains_Target() {
   EXPECT_TRUE(hits >= 600);
 }
 
+// the search-loop idiom: step, then Contains(target), first hit per state
+static void StepContains_SearchLoop() {
+  const LifeState block = LifeState::Parse("2o$2o!").Moved(30, 30);
+  const LifeTarget target(block, block.ZOI() & ~block);
+  std::vector<LifeState> s(3000);
+  for (size_t i = 0; i < s.size(); ++i) {
+    s[i] = LifeState::RandomState() & LifeState::RandomState();
+    if (i % 4 == 0) s[i] = (s[i] & ~block.ZOI()) | block;
+  }
+  std::vector<LifeState> cpu = s;
+  std::vector<uint32_t> want(s.size(), 0);
+  for (size_t i = 0; i < s.size(); ++i)
+    for (unsigned g = 1; g <= 20; ++g) {
+      cpu[i].Step();
+      if (!want[i] && cpu[i].Contains(target)) want[i] = g;
+    }
+  const std::vector<uint32_t> got = lifeapi::StepContainsBatch(std::span(s), target, 20);
+  int hits = 0;
+  for (size_t i = 0; i < s.size(); ++i) {
+    EXPECT_TRUE(got[i] == want[i]);
+    EXPECT_TRUE(s[i] == cpu[i]);
+    hits += want[i] != 0;
+  }
+  EXPECT_TRUE(hits > 0);
+}
+
 // NeighbourCount(state) (NeighbourCount.hpp:40-70)
 static void NeighbourCount_Planes() {
   std::vector<LifeState> s(1000);
@@ -164,6 +190,7 @@ int main() {
   Stepped_And_Pop();
   RPentomino();
   Contains_Target();
+  StepContains_SearchLoop();
   NeighbourCount_Planes();
   LifeWeld_Step();
   LifeStable_Propagate();

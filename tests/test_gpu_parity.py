@@ -234,6 +234,33 @@ def test_host_api_many_chunks_pinned(hip, port):
     assert hip.lib.lifeapi_host_unregister(y.ctypes.data) != 0  # no longer registered
 
 
+@pytest.mark.parametrize("gens", [2, 40])
+def test_host_step_contains(hip, port, gens):
+    """lifeapi_step_contains_batch on host arrays (natural layout for gens <= 2,
+    the split layout above), in place and without final states, vs the oracle."""
+    n = 2001
+    x = port.fill(n, seed=51) & port.fill(n, seed=52) & port.fill(n, seed=53)
+    blk = np.zeros(64, np.uint64)
+    blk[20] = blk[21] = np.uint64(0b11 << 30)
+    ring = np.zeros(64, np.uint64)
+    for c in (19, 20, 21, 22):
+        ring[c] = np.uint64(0b1111 << 29)
+    ring &= ~blk
+    x[::5] &= ~ring & ~blk
+    x[::10] |= blk
+    exp = np.zeros(n, np.uint32)
+    s = x.copy()
+    for g in range(1, gens + 1):
+        s = port.step_batch(s, 1)
+        hit = (((s ^ blk) & (blk | ring)) == 0).all(axis=1)
+        exp[(exp == 0) & hit] = g
+    assert exp.any()
+    assert (hip.step_contains_host(x, blk, ring, gens) == exp).all()
+    y = x.copy()
+    assert (hip.step_contains_host(y, blk, ring, gens, final=y) == exp).all()
+    assert (y == s).all()
+
+
 def test_host_api_other_kernels(hip, port):
     """Host-pointer forms of the weld / stable / counts / refined / contains
     entry points (staged through device memory in chunks)."""
