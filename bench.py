@@ -169,8 +169,9 @@ def secondary_config3(hip, device, stream, cpu_seconds=0.0):
         ms.append(e0.elapsed_time(e1))
     t = sorted(ms)[len(ms) // 2] / 1e3  # median launch
     gps = n * gens / t
-    # VALU issue model of the default generation loop (rule 11, build/asm,
-    # DESIGN.md 3.1): per 4 universes 64 v_bitop3 (one slot; the 6-LUT tail)
+    # VALU issue model of the default generation loop (rule 11, the
+    # hand-allocated loop of split_asm.inc): per 4 universes
+    # 64 v_bitop3 (one slot; the 6-LUT tail)
     # + 4 v_alignbit (two slots, tools/bank_probe2.hip) = 18 issue slots per
     # universe-gen; the exchange runs on the LDS pipe (ds_write_b128 x2,
     # ds_read_b128 x4).  peak: one wave64 VALU op per 2 clk per SIMD at

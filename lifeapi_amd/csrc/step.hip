@@ -6,6 +6,7 @@
 #include "host.hpp"
 #include "split_layout.hpp"
 #include "tile_asm.inc"
+#include "split_asm.inc"
 
 using namespace lifeapi_impl;
 
@@ -213,6 +214,7 @@ __global__ __launch_bounds__(kBlock) void k_step(const uint64_t *__restrict__ in
 // instead of LDS (gen_split), or kPipe: the software-pipelined LDS loop
 // (gens_split_pipe).
 constexpr int kPipe = -1;
+constexpr int kAsmLoop = -3;  // the hand-allocated rule-11 loop (split_asm.inc)
 template <int S, int G, bool NT, int NET, int D = 0>
 __global__ __launch_bounds__(kBlock) void k_step_split(const uint64_t *__restrict__ in,
                                                        uint64_t *__restrict__ out, uint64_t n,
@@ -238,6 +240,15 @@ __global__ __launch_bounds__(kBlock) void k_step_split(const uint64_t *__restric
     if constexpr (D == kPipe) {
 #pragma unroll
       for (int g = 0; g < G; ++g) gens_split_pipe<S, NET>(r[g], lds + (wib * G + g) * S * kWave, lane, gens);
+    } else if constexpr (D == kAsmLoop) {
+      static_assert(S == 8 && NET == 6, "split_asm.inc is rule 11");
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const uint32_t base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)(
+            lds + (wib * G + g) * S * kWave);
+        split_gens_asm(r[g], gens, base + lane * 16u, base + ((lane + kWave - 1) & (kWave - 1)) * 16u,
+                       base + ((lane + 1) & (kWave - 1)) * 16u);
+      }
     } else {
       for (uint32_t it = 0; it < gens; ++it) {
 #pragma unroll
@@ -516,6 +527,9 @@ StepFn pick_step(const lifeapi_launch_cfg &c) {
   }
   if ((c.rule >= 5 && c.rule <= 7) || (c.rule >= 10 && c.rule <= 12)) {  // split layouts
     const bool nt = c.nontemporal != 0;
+    if (c.xchg == LIFEAPI_XCHG_ASM) {
+      return c.rule == 11 ? pick_split<8, 6, kAsmLoop>(c.universes_per_wave, nt) : nullptr;
+    }
     if (c.xchg == LIFEAPI_XCHG_LDS_PIPE) {
       switch (c.rule) {
         case 6: return pick_split<8, 7, kPipe>(c.universes_per_wave, nt);
@@ -586,8 +600,9 @@ void lifeapi_default_cfg(lifeapi_launch_cfg *cfg, uint32_t generations) {
     // VALU regime: 8-way row split, 4 universes per wave interleaved bit by
     // bit, LDS exchange, the 6-LUT tail; state resident in VGPRs for all
     // generations (rule 11 over rule 6: 1.47 vs 1.61 ms on config 3,
-    // profiles/r01/tune_c3net.jsonl)
-    cfg->xchg = LIFEAPI_XCHG_LDS;
+    // profiles/r01/tune_c3net.jsonl), as the hand-allocated loop of
+    // split_asm.inc (2-2.5 % over the compiled one, tune_c3asm.jsonl)
+    cfg->xchg = LIFEAPI_XCHG_ASM;
     cfg->rule = 11;
     cfg->universes_per_wave = 1;
     cfg->nontemporal = generations < 32 ? 1 : 0;

@@ -1,0 +1,41 @@
+"""CPU: the generated rule-11 assembly loop (tools/gen_split_asm.py ->
+lifeapi_amd/csrc/split_asm.inc) is up to date, keeps its bank rules, and -- run
+on numpy lanes -- computes gen_split's network (the oracle's Step() on the
+8-way split layout)."""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import gen_split_asm as g  # noqa: E402
+
+
+def test_inc_is_generated():
+    assert open(g.OUT).read() == g.emit()
+
+
+def test_bank_rules():
+    n, bad = g.check_banks(g.body())
+    assert n == 68 and len(bad) == 16
+    assert all(l.split()[-1] in ("bitop3:0x96", "bitop3:0xe8") for l in bad)  # the h-layer only
+
+
+def _to_split(states):
+    """4 universes (4 x 64 uint64) -> r[8][64] of the 8-way split: bit 4k + u of
+    R_j = universe u, row 8k + j (split_layout.hpp)."""
+    r = np.zeros((8, 64), np.uint32)
+    for u in range(4):
+        for j in range(8):
+            for k in range(8):
+                bit = (states[u] >> np.uint64(8 * k + j)) & np.uint64(1)
+                r[j] |= (bit.astype(np.uint32) << np.uint32(4 * k + u))
+    return r
+
+
+def test_simulated_loop_is_step(port):
+    x = port.fill(4, seed=77)
+    for gens in (1, 3):
+        got = g.simulate(_to_split(x), gens)
+        assert (got == _to_split(port.step_batch(x, gens))).all(), gens

@@ -1,0 +1,234 @@
+#!/usr/bin/env python3
+"""Generate the hand-allocated generation loop of rule 11 (8-way row split, 4
+universes per wave interleaved bit by bit, LDS exchange, the 6-LUT tail of
+device.hpp's life_tail6) as inline gfx950 assembly:
+lifeapi_amd/csrc/split_asm.inc, used by k_step_split with LIFEAPI_XCHG_ASM.
+
+Why: the compiler's allocation of the rule-11 loop puts 30 of its 68 VALU on
+two sources in one VGPR bank (bank = vN mod 4, tools/vbank.py), and such a
+v_bitop3 issues at about half rate (tools/bank_probe.hip).  16 of them are the
+h-layer xor3 / maj(L, r, R), which cannot avoid it: r, L and R all live in
+even-aligned b128 tuples (ds_write_b128 / ds_read_b128), so word j sits at the
+same position parity in each and only two banks are left for three operands.
+The other 52 (the tails and the ring rotates) are conflict-free here:
+
+  r[j]  bank j        (v0..v7, the ds_write_b128 tuples)
+  L[j]  bank j + 2    (ds_read_b128 at v[10:13], v[14:17])
+  R[j]  bank j        (ds_read_b128 at v[20:23], v[24:27]); h1[j] overwrites R[j]
+                      (h1[3] in v55: see H1)
+  h0[j] bank j + 1,  h1[j] bank j  (vertical triples j-1, j, j+1 span 3 banks;
+        maj(h1[j+1], h1[j-1], h0[j+1]) needs h0's offset odd against h1's)
+  tail temps by bank: g1/g4 j+1, g2 j+2, g3 j+3, g5 j+2 (g4, g5 and r[j]
+        distinct for the last LUT)
+
+`simulate()` runs the generated text on numpy lanes (LDS exchange = lane
+rotate); tests/test_split_asm.py checks it against gen_split's network on
+random states and that the bank rules hold.
+
+Usage: python tools/gen_split_asm.py [--check]
+"""
+from __future__ import annotations
+
+import os
+import re
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "lifeapi_amd", "csrc", "split_asm.inc")
+
+S, P = 8, 4
+XOR3, MAJ, N1, NAE, N4, N6 = 0x96, 0xE8, 0xE9, 0x7E, 0x52, 0xE0
+
+R = [j for j in range(8)]                       # r[j]: v0..v7
+L = [10 + j for j in range(4)] + [14 + j - 4 for j in range(4, 8)]
+RR = [20 + j for j in range(4)] + [24 + j - 4 for j in range(4, 8)]
+# h1[j] overwrites R[j], except h1[3]: rows 4..7's tails still read it after
+# the next generation's plane-0 reads have refilled v[20:23] (PIPE)
+H1 = RR[:3] + [55] + RR[4:]
+H0 = [29 + j for j in range(8)]                 # bank j + 1
+H0U, H0D, H1U, H1D = 40, 41, 39, 44              # banks 0, 1, 3, 0 (as h0[-1], h0[8], h1[-1], h1[8])
+TEMPS = [8, 9, 18, 19, 28, 37, 38, 42, 43, 45, 46, 47, 48, 49, 50, 51]
+A_SELF, A_PREV, A_NEXT = 52, 53, 54
+N_VGPR = 56
+
+
+class Alloc:
+    def __init__(self):
+        self.free = {b: [r for r in TEMPS if r % 4 == b] for b in range(4)}
+
+    def get(self, bank):
+        return self.free[bank % 4].pop(0)
+
+    def put(self, r):
+        self.free[r % 4].append(r)
+
+
+def op(dst, a, b, c, tt):
+    return f"v_bitop3_b32 v{dst}, v{a}, v{b}, v{c} bitop3:0x{tt:02x}"
+
+
+def tail_ops(j, al: Alloc):
+    a0 = H0U if j == 0 else H0[j - 1]
+    c0 = H0D if j == S - 1 else H0[j + 1]
+    a1 = H1U if j == 0 else H1[j - 1]
+    c1 = H1D if j == S - 1 else H1[j + 1]
+    g1, g2, g3, g5 = al.get(j + 1), al.get(j + 2), al.get(j + 3), al.get(j + 2)
+    ops = [
+        op(g1, H1[j], a1, c1, N1),        # SB in {0,2,3}
+        op(g2, c1, a1, c0, MAJ),
+        op(g3, c0, a0, H0[j], NAE),       # SA in {1,2}
+        op(g5, H0[j], c0, a0, XOR3),      # SA odd
+        op(g1, g3, g2, g1, N4),           # g4 (in g1's register)
+        op(R[j], g1, g5, R[j], N6),       # next = g4 & (g5 | a)
+    ]
+    return ops, (g1, g2, g3, g5)
+
+
+PIPE = True  # publish plane 0 (and issue its reads) before rows 4..7's tails
+
+
+def exchange(plane):
+    off = " offset:1024" if plane else ""
+    lo = 4 * plane
+    return [f"ds_write_b128 v{A_SELF}, v[{lo}:{lo + 3}]{off}",
+            f"ds_read_b128 v[{L[lo]}:{L[lo] + 3}], v{A_PREV}{off}",
+            f"ds_read_b128 v[{RR[lo]}:{RR[lo] + 3}], v{A_NEXT}{off}"]
+
+
+def prologue():
+    return exchange(0) + exchange(1) if PIPE else []
+
+
+def body():
+    # plane by plane (write, then its two reads), and the h-layer of plane 0
+    # starts once its reads are back (lgkmcnt(3): plane 1's write and reads
+    # may still be in flight), as the compiler orders the compiled loop.
+    # PIPE: the exchange of the NEXT generation is issued inside this one --
+    # plane 0 right after rows 0..3's tails, plane 1 at the end -- so plane
+    # 0's round trip overlaps rows 4..7's tails.
+    lines = [] if PIPE else exchange(0) + exchange(1)
+    lines += ["s_sub_u32 %[g], %[g], 1", "s_waitcnt lgkmcnt(3)"]
+    for j in range(S):
+        if j == 4:
+            lines.append("s_waitcnt lgkmcnt(0)")
+        lines.append(op(H0[j], L[j], R[j], RR[j], XOR3))
+        lines.append(op(H1[j], L[j], R[j], RR[j], MAJ))
+    lines += [
+        f"v_alignbit_b32 v{H0U}, v{H0[S - 1]}, v{H0[S - 1]}, {32 - P}",   # rotl P
+        f"v_alignbit_b32 v{H1U}, v{H1[S - 1]}, v{H1[S - 1]}, {32 - P}",
+        f"v_alignbit_b32 v{H0D}, v{H0[0]}, v{H0[0]}, {P}",                 # rotr P
+        f"v_alignbit_b32 v{H1D}, v{H1[0]}, v{H1[0]}, {P}",
+    ]
+    al = Alloc()
+    # two rows at a time, interleaved, so each dependent pair sits apart
+    for j in range(0, S, 2):
+        (a, ra), (b, rb) = tail_ops(j, al), tail_ops(j + 1, al)
+        for x, y in zip(a, b):
+            lines += [x, y]
+        for r in ra + rb:  # free only after both interleaved rows are emitted
+            al.put(r)
+        if PIPE and j == 2:
+            lines += exchange(0)   # rows 0..3 are final: publish plane 0
+    if PIPE:
+        lines += exchange(1)
+    return lines
+
+
+def asm_text():
+    lines = ["s_cmp_eq_u32 %[g], 0", "s_cbranch_scc1 2f"] + prologue() + ["1:"] + body() + \
+        ["s_cmp_lg_u32 %[g], 0", "s_cbranch_scc1 1b", "s_waitcnt lgkmcnt(0)", "2:"]
+    return lines
+
+
+def check_banks(lines):
+    """(VALU instructions, those with two sources in one bank)"""
+    n, bad = 0, []
+    for l in lines:
+        if not l.startswith("v_"):
+            continue
+        n += 1
+        srcs = {int(x) for x in re.findall(r"v(\d+)", l.split(",", 1)[1])}
+        banks = [s % 4 for s in srcs]
+        if len(banks) != len(set(banks)):
+            bad.append(l)
+    return n, bad
+
+
+def simulate(r, gens):
+    """Run the generated loop on numpy: r = uint32 [8, 64] (register j, lane)."""
+    v = np.zeros((N_VGPR, 64), np.uint32)
+    v[:8] = r
+    lds_plane = {}
+    seq = prologue() + body() * gens if gens else []
+    for _ in range(1):
+        for l in seq:
+            if l.startswith("ds_write_b128"):
+                off = int(re.search(r"offset:(\d+)", l)[1]) if "offset" in l else 0
+                base = int(re.search(r"v\[(\d+):", l)[1])
+                lds_plane[off] = v[base:base + 4].copy()
+            elif l.startswith("ds_read_b128"):
+                off = int(re.search(r"offset:(\d+)", l)[1]) if "offset" in l else 0
+                base = int(re.search(r"v\[(\d+):", l)[1])
+                src = int(re.search(r"v(\d+)(?: offset|$)", l.split(",", 1)[1].strip())[1])
+                shift = 1 if src == A_PREV else -1          # lane i reads lane i-1 / i+1
+                v[base:base + 4] = np.roll(lds_plane[off], shift, axis=1)
+            elif l.startswith("v_bitop3_b32"):
+                d, a, b, c = (int(x) for x in re.findall(r"v(\d+)", l))
+                tt = int(l.rsplit(":", 1)[1], 16)
+                out = np.zeros(64, np.uint32)
+                for k in range(8):
+                    if tt >> k & 1:
+                        out |= ((v[a] if k & 4 else ~v[a]) & (v[b] if k & 2 else ~v[b]) &
+                                (v[c] if k & 1 else ~v[c]))
+                v[d] = out
+            elif l.startswith("v_alignbit_b32"):
+                d, a, b = (int(x) for x in re.findall(r"v(\d+)", l)[:3])
+                sh = int(l.rsplit(",", 1)[1])
+                x = (v[a].astype(np.uint64) << np.uint64(32)) | v[b].astype(np.uint64)
+                v[d] = ((x >> np.uint64(sh)) & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    return v[:8].copy()
+
+
+def emit():
+    lines = asm_text()
+    n, bad = check_banks(body())
+    asm = "\n".join(f'      "{l}\\n"' for l in lines)
+    outs = ",\n".join(f'        "+{{v{R[j]}}}"(r[{j}])' for j in range(S))
+    pinned = sorted({x for x in L + RR + H1 + H0 + [H0U, H0D, H1U, H1D] + TEMPS})
+    clob = ", ".join(f'"v{x}"' for x in pinned)
+    return f"""// split_asm.inc -- GENERATED by tools/gen_split_asm.py; do not edit.
+// The generation loop of rule 11 (8-way row split, 4 universes per wave,
+// LDS exchange, the 6-LUT tail) with hand-allocated VGPRs: of its {n} VALU
+// per generation only the {len(bad)} h-layer ones read two sources from one
+// bank (see the generator).  {N_VGPR} VGPRs pinned.
+#pragma once
+
+namespace lifeapi_impl {{
+
+// r: gen_split's r[j] for S = 8; a_self / a_prev / a_next: LDS byte addresses
+// of this lane's / lane i-1's / lane i+1's 16-B slot in the wave's two 1-KiB
+// planes
+__device__ __forceinline__ void split_gens_asm(uint32_t (&r)[8], uint32_t gens, uint32_t a_self,
+                                               uint32_t a_prev, uint32_t a_next) {{
+  asm volatile(
+{asm}
+      : {outs.strip()},
+        [g] "+s"(gens)
+      : "{{v{A_SELF}}}"(a_self), "{{v{A_PREV}}}"(a_prev), "{{v{A_NEXT}}}"(a_next)
+      : {clob}, "scc", "memory");
+}}
+
+}}  // namespace lifeapi_impl
+"""
+
+
+if __name__ == "__main__":
+    text = emit()
+    if "--check" in sys.argv:
+        sys.exit(0 if open(OUT).read() == text else 1)
+    with open(OUT, "w") as f:
+        f.write(text)
+    n, bad = check_banks(body())
+    print(f"{OUT}: {n} VALU, {len(bad)} with a bank conflict")

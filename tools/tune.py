@@ -63,7 +63,7 @@ def tune_c5(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=["c2", "c3", "c3net", "c3mix", "c3pipe", "c5", "gsweep", "both", "all"], default="both")
+    ap.add_argument("--workload", choices=["c2", "c3", "c3net", "c3mix", "c3pipe", "c3asm", "c5", "gsweep", "both", "all"], default="both")
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--quick", action="store_true")
@@ -91,6 +91,11 @@ def main():
         n, g = 1 << 16, 1024
         work.append(("c3", n, g, [(1, 1, 0, 0, 6), (1, 2, 0, 0, 6), (1, 1, 0, 0, 7), (1, 1, 0, 0, 8),
                                   (0, 1, 0, 0, 8), (1, 1, 0, 0, 9), (8, 1, 0, 0, 8), (8, 1, 0, 1, 8)]))
+    if args.workload == "c3asm":  # the hand-allocated rule-11 loop against the compiled one
+        n, g = 1 << 16, 1024
+        work.append(("c3", n, g, [(1, 1, 0, 0, 11), (8, 1, 0, 0, 11), (8, 2, 0, 0, 11)]))
+        for gg in (4, 16, 64):
+            work.append((f"g{gg}", 1 << 18, gg, [(1, 1, 0, 1, 11), (8, 1, 0, 1, 11)]))
     if args.workload == "c3pipe":  # software-pipelined LDS loop against the plain one
         n, g = 1 << 16, 1024
         work.append(("c3", n, g, [(1, 1, 0, 0, 11), (9, 1, 0, 0, 11), (9, 2, 0, 0, 11), (1, 1, 0, 0, 6),
