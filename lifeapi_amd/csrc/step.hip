@@ -241,14 +241,13 @@ __global__ __launch_bounds__(kBlock) void k_step_split(const uint64_t *__restric
 #pragma unroll
       for (int g = 0; g < G; ++g) gens_split_pipe<S, NET>(r[g], lds + (wib * G + g) * S * kWave, lane, gens);
     } else if constexpr (D == kAsmLoop) {
-      static_assert(S == 8 && NET == 6, "split_asm.inc is rule 11");
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
-        const uint32_t base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)(
-            lds + (wib * G + g) * S * kWave);
-        split_gens_asm(r[g], gens, base + lane * 16u, base + ((lane + kWave - 1) & (kWave - 1)) * 16u,
-                       base + ((lane + 1) & (kWave - 1)) * 16u);
-      }
+      static_assert(S == 8 && NET == 6 && G <= 2, "split_asm.inc is rule 11, one or two groups");
+      const uint32_t base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)(
+          lds + wib * G * S * kWave);  // group g's planes at base + 2 KiB * g
+      const uint32_t self = base + lane * 16u, prev = base + ((lane + kWave - 1) & (kWave - 1)) * 16u,
+                     next = base + ((lane + 1) & (kWave - 1)) * 16u;
+      if constexpr (G == 2) split_gens_asm2(r[0], r[1], gens, self, prev, next);
+      else split_gens_asm(r[0], gens, self, prev, next);
     } else {
       for (uint32_t it = 0; it < gens; ++it) {
 #pragma unroll

@@ -39,3 +39,13 @@ def test_simulated_loop_is_step(port):
     for gens in (1, 3):
         got = g.simulate(_to_split(x), gens)
         assert (got == _to_split(port.step_batch(x, gens))).all(), gens
+
+
+def test_simulated_two_group_loop_is_step(port):
+    """split_gens_asm2: two groups per wave, each one's exchange in flight
+    behind the other's generation."""
+    x, y = port.fill(4, seed=78), port.fill(4, seed=79)
+    for gens in (1, 2, 5):
+        ga, gb = g.simulate(_to_split(x), gens, two=_to_split(y))
+        assert (ga == _to_split(port.step_batch(x, gens))).all(), gens
+        assert (gb == _to_split(port.step_batch(y, gens))).all(), gens

@@ -136,6 +136,99 @@ def body():
     return lines
 
 
+# ---- two groups per wave (G = 2): each group's exchange hides behind the
+# other group's h-layer and tails; 8 more universes per wave in flight.
+RB_REGS = list(range(56, 64))                    # group B's r[j]: bank j
+LB2 = [66 + j for j in range(4)] + [70 + j - 4 for j in range(4, 8)]    # bank j + 2
+RRB2 = [76 + j for j in range(4)] + [80 + j - 4 for j in range(4, 8)]   # bank j
+N_VGPR2 = 84
+
+
+def exchange2(grp, plane):
+    off = 2048 * grp + 1024 * plane
+    o = f" offset:{off}" if off else ""
+    r = R if grp == 0 else RB_REGS
+    l = L if grp == 0 else LB2
+    rr = RR if grp == 0 else RRB2
+    lo = 4 * plane
+    return [f"ds_write_b128 v{A_SELF}, v[{r[lo]}:{r[lo] + 3}]{o}",
+            f"ds_read_b128 v[{l[lo]}:{l[lo] + 3}], v{A_PREV}{o}",
+            f"ds_read_b128 v[{rr[lo]}:{rr[lo] + 3}], v{A_NEXT}{o}"]
+
+
+def group_gen(grp):
+    """one generation of group grp (its exchange already landed)"""
+    r = R if grp == 0 else RB_REGS
+    l = L if grp == 0 else LB2
+    rr = RR if grp == 0 else RRB2
+    h1 = rr                                      # h1[j] overwrites R[j]
+    lines = []
+    for j in range(S):
+        lines.append(op(H0[j], l[j], r[j], rr[j], XOR3))
+        lines.append(op(h1[j], l[j], r[j], rr[j], MAJ))
+    lines += [
+        f"v_alignbit_b32 v{H0U}, v{H0[S - 1]}, v{H0[S - 1]}, {32 - P}",
+        f"v_alignbit_b32 v{H1U}, v{h1[S - 1]}, v{h1[S - 1]}, {32 - P}",
+        f"v_alignbit_b32 v{H0D}, v{H0[0]}, v{H0[0]}, {P}",
+        f"v_alignbit_b32 v{H1D}, v{h1[0]}, v{h1[0]}, {P}",
+    ]
+    al = Alloc()
+
+    def tail(j):
+        a0 = H0U if j == 0 else H0[j - 1]
+        c0 = H0D if j == S - 1 else H0[j + 1]
+        a1 = H1U if j == 0 else h1[j - 1]
+        c1 = H1D if j == S - 1 else h1[j + 1]
+        g1, g2, g3, g5 = al.get(j + 1), al.get(j + 2), al.get(j + 3), al.get(j + 2)
+        return [op(g1, h1[j], a1, c1, N1), op(g2, c1, a1, c0, MAJ), op(g3, c0, a0, H0[j], NAE),
+                op(g5, H0[j], c0, a0, XOR3), op(g1, g3, g2, g1, N4), op(r[j], g1, g5, r[j], N6)], \
+            (g1, g2, g3, g5)
+
+    for j in range(0, S, 2):
+        (a, ra), (b, rb) = tail(j), tail(j + 1)
+        for x, y in zip(a, b):
+            lines += [x, y]
+        for x in ra + rb:
+            al.put(x)
+    return lines
+
+
+def prologue2():
+    return exchange2(0, 0) + exchange2(0, 1) + exchange2(1, 0) + exchange2(1, 1)
+
+
+def body2():
+    # in order: A's 6 LDS ops, then B's 6 are outstanding at the top
+    lines = ["s_sub_u32 %[g], %[g], 1", "s_waitcnt lgkmcnt(6)"] + group_gen(0) + \
+        exchange2(0, 0) + exchange2(0, 1) + ["s_waitcnt lgkmcnt(6)"] + group_gen(1) + \
+        exchange2(1, 0) + exchange2(1, 1)
+    return lines
+
+
+def emit2():
+    lines = ["s_cmp_eq_u32 %[g], 0", "s_cbranch_scc1 2f"] + prologue2() + ["1:"] + body2() + \
+        ["s_cmp_lg_u32 %[g], 0", "s_cbranch_scc1 1b", "s_waitcnt lgkmcnt(0)", "2:"]
+    asm = "\n".join(f'      "{l}\\n"' for l in lines)
+    outs = ",\n".join([f'        "+{{v{R[j]}}}"(a[{j}])' for j in range(S)] +
+                      [f'        "+{{v{RB_REGS[j]}}}"(b[{j}])' for j in range(S)])
+    pinned = sorted({x for x in L + RR + LB2 + RRB2 + H0 + [H0U, H0D, H1U, H1D] + TEMPS})
+    clob = ", ".join(f'"v{x}"' for x in pinned)
+    return f"""
+// Two groups per wave (G = 2): a / b are the groups' r[j]; group b's planes
+// sit 2 KiB after group a's.  Each group's exchange is in flight while the
+// other group's generation runs.  {N_VGPR2} VGPRs pinned.
+__device__ __forceinline__ void split_gens_asm2(uint32_t (&a)[8], uint32_t (&b)[8], uint32_t gens,
+                                                uint32_t a_self, uint32_t a_prev, uint32_t a_next) {{
+  asm volatile(
+{asm}
+      : {outs.strip()},
+        [g] "+s"(gens)
+      : "{{v{A_SELF}}}"(a_self), "{{v{A_PREV}}}"(a_prev), "{{v{A_NEXT}}}"(a_next)
+      : {clob}, "scc", "memory");
+}}
+"""
+
+
 def asm_text():
     lines = ["s_cmp_eq_u32 %[g], 0", "s_cbranch_scc1 2f"] + prologue() + ["1:"] + body() + \
         ["s_cmp_lg_u32 %[g], 0", "s_cbranch_scc1 1b", "s_waitcnt lgkmcnt(0)", "2:"]
@@ -156,12 +249,17 @@ def check_banks(lines):
     return n, bad
 
 
-def simulate(r, gens):
-    """Run the generated loop on numpy: r = uint32 [8, 64] (register j, lane)."""
-    v = np.zeros((N_VGPR, 64), np.uint32)
+def simulate(r, gens, two=None):
+    """Run the generated loop on numpy: r = uint32 [8, 64] (register j, lane);
+    with `two` (a second group), the two-group loop; returns r (and two)."""
+    v = np.zeros((max(N_VGPR, N_VGPR2), 64), np.uint32)
     v[:8] = r
+    if two is not None:
+        v[RB_REGS] = two
+        seq = prologue2() + body2() * gens if gens else []
+    else:
+        seq = prologue() + body() * gens if gens else []
     lds_plane = {}
-    seq = prologue() + body() * gens if gens else []
     for _ in range(1):
         for l in seq:
             if l.startswith("ds_write_b128"):
@@ -188,6 +286,8 @@ def simulate(r, gens):
                 sh = int(l.rsplit(",", 1)[1])
                 x = (v[a].astype(np.uint64) << np.uint64(32)) | v[b].astype(np.uint64)
                 v[d] = ((x >> np.uint64(sh)) & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    if two is not None:
+        return v[:8].copy(), v[RB_REGS].copy()
     return v[:8].copy()
 
 
@@ -219,7 +319,7 @@ __device__ __forceinline__ void split_gens_asm(uint32_t (&r)[8], uint32_t gens, 
       : "{{v{A_SELF}}}"(a_self), "{{v{A_PREV}}}"(a_prev), "{{v{A_NEXT}}}"(a_next)
       : {clob}, "scc", "memory");
 }}
-
+{emit2()}
 }}  // namespace lifeapi_impl
 """
 
