@@ -215,7 +215,7 @@ __global__ __launch_bounds__(kBlock) void k_step(const uint64_t *__restrict__ in
 // (gens_split_pipe).
 constexpr int kPipe = -1;
 constexpr int kAsmLoop = -3;  // the hand-allocated rule-11 loop (split_asm.inc)
-template <int S, int G, bool NT, int NET, int D = 0>
+template <int S, int G, bool NT, int NET, int D = 0, int V = 0>
 __global__ __launch_bounds__(kBlock) void k_step_split(const uint64_t *__restrict__ in,
                                                        uint64_t *__restrict__ out, uint64_t n,
                                                        uint32_t gens) {
@@ -247,7 +247,10 @@ __global__ __launch_bounds__(kBlock) void k_step_split(const uint64_t *__restric
       const uint32_t self = base + lane * 16u, prev = base + ((lane + kWave - 1) & (kWave - 1)) * 16u,
                      next = base + ((lane + 1) & (kWave - 1)) * 16u;
       if constexpr (G == 2) split_gens_asm2(r[0], r[1], gens, self, prev, next);
-      else split_gens_asm(r[0], gens, self, prev, next);
+      else if constexpr (V == 1) split_gens_asm_v1(r[0], gens, self, prev, next);
+      else if constexpr (V == 2) split_gens_asm_v2(r[0], gens, self, prev, next);
+      else if constexpr (V == 3) split_gens_asm_v3(r[0], gens, self, prev, next);
+      else split_gens_asm_v0(r[0], gens, self, prev, next);
     } else {
       for (uint32_t it = 0; it < gens; ++it) {
 #pragma unroll
@@ -485,11 +488,11 @@ StepFn pick_rule(int u, bool nt, int rule) {
     }
   }
 }
-template <int S, int NET, int D = 0>
+template <int S, int NET, int D = 0, int V = 0>
 StepFn pick_split(int groups, bool nt) {
   switch (groups) {
-    case 1: return nt ? k_step_split<S, 1, true, NET, D> : k_step_split<S, 1, false, NET, D>;
-    case 2: return nt ? k_step_split<S, 2, true, NET, D> : k_step_split<S, 2, false, NET, D>;
+    case 1: return nt ? k_step_split<S, 1, true, NET, D, V> : k_step_split<S, 1, false, NET, D, V>;
+    case 2: return nt ? k_step_split<S, 2, true, NET, D, V> : k_step_split<S, 2, false, NET, D, V>;
     default: return nullptr;
   }
 }
@@ -528,6 +531,14 @@ StepFn pick_step(const lifeapi_launch_cfg &c) {
     const bool nt = c.nontemporal != 0;
     if (c.xchg == LIFEAPI_XCHG_ASM) {
       return c.rule == 11 ? pick_split<8, 6, kAsmLoop>(c.universes_per_wave, nt) : nullptr;
+    }
+    if (c.xchg > LIFEAPI_XCHG_ASM_V(0) && c.xchg <= LIFEAPI_XCHG_ASM_V(3) && c.rule == 11 &&
+        c.universes_per_wave == 1) {  // the other schedules of the assembly loop
+      switch (c.xchg - LIFEAPI_XCHG_ASM_V(0)) {
+        case 1: return pick_split<8, 6, kAsmLoop, 1>(1, nt);
+        case 2: return pick_split<8, 6, kAsmLoop, 2>(1, nt);
+        default: return pick_split<8, 6, kAsmLoop, 3>(1, nt);
+      }
     }
     if (c.xchg == LIFEAPI_XCHG_LDS_PIPE) {
       switch (c.rule) {

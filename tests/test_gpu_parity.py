@@ -28,6 +28,7 @@ ALL_CFGS += [(16 + d, u, nt, 11) for d in (1, 2, 3, 4) for u in (1, 2) for nt in
 ALL_CFGS += [(16 + d, 1, nt, 12) for d in (2, 4) for nt in (0, 1)]
 # the hand-allocated rule-11 loop (LIFEAPI_XCHG_ASM = 8)
 ALL_CFGS += [(8, u, nt, 11) for u in (1, 2) for nt in (0, 1)]
+ALL_CFGS += [(24 + k, 1, nt, 11) for k in (1, 2, 3) for nt in (0, 1)]  # its other schedules
 # the software-pipelined LDS loop (LIFEAPI_XCHG_LDS_PIPE = 9)
 ALL_CFGS += [(9, u, nt, r) for r in (6, 11, 12) for u in (1, 2) for nt in (0, 1)]
 

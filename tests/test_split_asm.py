@@ -36,9 +36,12 @@ def _to_split(states):
 
 def test_simulated_loop_is_step(port):
     x = port.fill(4, seed=77)
-    for gens in (1, 3):
-        got = g.simulate(_to_split(x), gens)
-        assert (got == _to_split(port.step_batch(x, gens))).all(), gens
+    for v in g.VARIANTS:
+        n, bad = g.check_banks(g.body(v))
+        assert n == 68 and len(bad) == 16, v
+        for gens in (1, 3):
+            got = g.simulate(_to_split(x), gens, variant=v)
+            assert (got == _to_split(port.step_batch(x, gens))).all(), (v, gens)
 
 
 def test_simulated_two_group_loop_is_step(port):

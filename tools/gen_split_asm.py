@@ -86,7 +86,17 @@ def tail_ops(j, al: Alloc):
     return ops, (g1, g2, g3, g5)
 
 
-PIPE = True  # publish plane 0 (and issue its reads) before rows 4..7's tails
+# Variants of the loop's schedule (same instructions, different order):
+#   "plain"      plane by plane (write, then its two reads) at the top of each
+#                generation; lgkmcnt(3) before plane 0's h-layer, as the
+#                compiler orders the compiled loop
+#   "pipe"       the NEXT generation's exchange is issued inside this one:
+#                plane 0 right after rows 0..3's tails, plane 1 at the end
+#   "early"      "plain", and rows 1 and 2 (which read only plane-0 h values)
+#                run their tails before waiting for plane 1
+#   "pipe_early" both
+VARIANTS = ("pipe", "plain", "early", "pipe_early")
+DEFAULT = "pipe"
 
 
 def exchange(plane):
@@ -97,41 +107,44 @@ def exchange(plane):
             f"ds_read_b128 v[{RR[lo]}:{RR[lo] + 3}], v{A_NEXT}{off}"]
 
 
-def prologue():
-    return exchange(0) + exchange(1) if PIPE else []
+def prologue(variant=DEFAULT):
+    return exchange(0) + exchange(1) if variant.startswith("pipe") else []
 
 
-def body():
-    # plane by plane (write, then its two reads), and the h-layer of plane 0
-    # starts once its reads are back (lgkmcnt(3): plane 1's write and reads
-    # may still be in flight), as the compiler orders the compiled loop.
-    # PIPE: the exchange of the NEXT generation is issued inside this one --
-    # plane 0 right after rows 0..3's tails, plane 1 at the end -- so plane
-    # 0's round trip overlaps rows 4..7's tails.
-    lines = [] if PIPE else exchange(0) + exchange(1)
+def body(variant=DEFAULT):
+    pipe, early = variant.startswith("pipe"), variant.endswith("early")
+    lines = [] if pipe else exchange(0) + exchange(1)
     lines += ["s_sub_u32 %[g], %[g], 1", "s_waitcnt lgkmcnt(3)"]
-    for j in range(S):
-        if j == 4:
-            lines.append("s_waitcnt lgkmcnt(0)")
-        lines.append(op(H0[j], L[j], R[j], RR[j], XOR3))
-        lines.append(op(H1[j], L[j], R[j], RR[j], MAJ))
-    lines += [
-        f"v_alignbit_b32 v{H0U}, v{H0[S - 1]}, v{H0[S - 1]}, {32 - P}",   # rotl P
-        f"v_alignbit_b32 v{H1U}, v{H1[S - 1]}, v{H1[S - 1]}, {32 - P}",
-        f"v_alignbit_b32 v{H0D}, v{H0[0]}, v{H0[0]}, {P}",                 # rotr P
-        f"v_alignbit_b32 v{H1D}, v{H1[0]}, v{H1[0]}, {P}",
-    ]
+
+    def hlayer(js):
+        out = []
+        for j in js:
+            out.append(op(H0[j], L[j], R[j], RR[j], XOR3))
+            out.append(op(H1[j], L[j], R[j], RR[j], MAJ))
+        return out
+
+    rot_d = [f"v_alignbit_b32 v{H0D}, v{H0[0]}, v{H0[0]}, {P}",                 # rotr P
+             f"v_alignbit_b32 v{H1D}, v{H1[0]}, v{H1[0]}, {P}"]
+    rot_u = [f"v_alignbit_b32 v{H0U}, v{H0[S - 1]}, v{H0[S - 1]}, {32 - P}",   # rotl P
+             f"v_alignbit_b32 v{H1U}, v{H1[S - 1]}, v{H1[S - 1]}, {32 - P}"]
     al = Alloc()
-    # two rows at a time, interleaved, so each dependent pair sits apart
-    for j in range(0, S, 2):
-        (a, ra), (b, rb) = tail_ops(j, al), tail_ops(j + 1, al)
-        for x, y in zip(a, b):
-            lines += [x, y]
+
+    def pair(j, k):
+        (a, ra), (b, rb) = tail_ops(j, al), tail_ops(k, al)
+        out = [x for xy in zip(a, b) for x in xy]
         for r in ra + rb:  # free only after both interleaved rows are emitted
             al.put(r)
-        if PIPE and j == 2:
-            lines += exchange(0)   # rows 0..3 are final: publish plane 0
-    if PIPE:
+        return out
+
+    lines += hlayer(range(4))
+    if early:
+        lines += rot_d + pair(1, 2) + ["s_waitcnt lgkmcnt(0)"] + hlayer(range(4, 8)) + rot_u + pair(0, 3)
+    else:
+        lines += ["s_waitcnt lgkmcnt(0)"] + hlayer(range(4, 8)) + rot_u + rot_d + pair(0, 1) + pair(2, 3)
+    if pipe:
+        lines += exchange(0)   # rows 0..3 are final: publish plane 0
+    lines += pair(4, 5) + pair(6, 7)
+    if pipe:
         lines += exchange(1)
     return lines
 
@@ -229,10 +242,9 @@ __device__ __forceinline__ void split_gens_asm2(uint32_t (&a)[8], uint32_t (&b)[
 """
 
 
-def asm_text():
-    lines = ["s_cmp_eq_u32 %[g], 0", "s_cbranch_scc1 2f"] + prologue() + ["1:"] + body() + \
+def asm_text(variant=DEFAULT):
+    return ["s_cmp_eq_u32 %[g], 0", "s_cbranch_scc1 2f"] + prologue(variant) + ["1:"] + body(variant) + \
         ["s_cmp_lg_u32 %[g], 0", "s_cbranch_scc1 1b", "s_waitcnt lgkmcnt(0)", "2:"]
-    return lines
 
 
 def check_banks(lines):
@@ -249,7 +261,7 @@ def check_banks(lines):
     return n, bad
 
 
-def simulate(r, gens, two=None):
+def simulate(r, gens, two=None, variant=DEFAULT):
     """Run the generated loop on numpy: r = uint32 [8, 64] (register j, lane);
     with `two` (a second group), the two-group loop; returns r (and two)."""
     v = np.zeros((max(N_VGPR, N_VGPR2), 64), np.uint32)
@@ -258,7 +270,7 @@ def simulate(r, gens, two=None):
         v[RB_REGS] = two
         seq = prologue2() + body2() * gens if gens else []
     else:
-        seq = prologue() + body() * gens if gens else []
+        seq = prologue(variant) + body(variant) * gens if gens else []
     lds_plane = {}
     for _ in range(1):
         for l in seq:
@@ -291,27 +303,15 @@ def simulate(r, gens, two=None):
     return v[:8].copy()
 
 
-def emit():
-    lines = asm_text()
-    n, bad = check_banks(body())
-    asm = "\n".join(f'      "{l}\\n"' for l in lines)
+def fn_text(name, variant):
+    asm = "\n".join(f'      "{l}\\n"' for l in asm_text(variant))
     outs = ",\n".join(f'        "+{{v{R[j]}}}"(r[{j}])' for j in range(S))
     pinned = sorted({x for x in L + RR + H1 + H0 + [H0U, H0D, H1U, H1D] + TEMPS})
     clob = ", ".join(f'"v{x}"' for x in pinned)
-    return f"""// split_asm.inc -- GENERATED by tools/gen_split_asm.py; do not edit.
-// The generation loop of rule 11 (8-way row split, 4 universes per wave,
-// LDS exchange, the 6-LUT tail) with hand-allocated VGPRs: of its {n} VALU
-// per generation only the {len(bad)} h-layer ones read two sources from one
-// bank (see the generator).  {N_VGPR} VGPRs pinned.
-#pragma once
-
-namespace lifeapi_impl {{
-
-// r: gen_split's r[j] for S = 8; a_self / a_prev / a_next: LDS byte addresses
-// of this lane's / lane i-1's / lane i+1's 16-B slot in the wave's two 1-KiB
-// planes
-__device__ __forceinline__ void split_gens_asm(uint32_t (&r)[8], uint32_t gens, uint32_t a_self,
-                                               uint32_t a_prev, uint32_t a_next) {{
+    return f"""
+// schedule "{variant}" (see tools/gen_split_asm.py)
+__device__ __forceinline__ void {name}(uint32_t (&r)[8], uint32_t gens, uint32_t a_self, uint32_t a_prev,
+{" " * (len(name) + 32)}uint32_t a_next) {{
   asm volatile(
 {asm}
       : {outs.strip()},
@@ -319,7 +319,26 @@ __device__ __forceinline__ void split_gens_asm(uint32_t (&r)[8], uint32_t gens, 
       : "{{v{A_SELF}}}"(a_self), "{{v{A_PREV}}}"(a_prev), "{{v{A_NEXT}}}"(a_next)
       : {clob}, "scc", "memory");
 }}
-{emit2()}
+"""
+
+
+def emit():
+    n, bad = check_banks(body())
+    fns = "".join(fn_text(f"split_gens_asm_v{k}", v) for k, v in enumerate(VARIANTS))
+    return f"""// split_asm.inc -- GENERATED by tools/gen_split_asm.py; do not edit.
+// The generation loop of rule 11 (8-way row split, 4 universes per wave,
+// LDS exchange, the 6-LUT tail) with hand-allocated VGPRs: of its {n} VALU
+// per generation only the {len(bad)} h-layer ones read two sources from one
+// bank (see the generator).  {N_VGPR} VGPRs pinned.
+//
+// split_gens_asm_v<k>(r, gens, a_self, a_prev, a_next): r is gen_split's r[j]
+// for S = 8; a_self / a_prev / a_next are the LDS byte addresses of this
+// lane's / lane i-1's / lane i+1's 16-B slot in the wave's two 1-KiB planes.
+// The variants differ only in schedule: {", ".join(f"v{k} = {v}" for k, v in enumerate(VARIANTS))}.
+#pragma once
+
+namespace lifeapi_impl {{
+{fns}{emit2()}
 }}  // namespace lifeapi_impl
 """
 

@@ -93,7 +93,8 @@ def main():
                                   (0, 1, 0, 0, 8), (1, 1, 0, 0, 9), (8, 1, 0, 0, 8), (8, 1, 0, 1, 8)]))
     if args.workload == "c3asm":  # the hand-allocated rule-11 loop against the compiled one
         n, g = 1 << 16, 1024
-        work.append(("c3", n, g, [(1, 1, 0, 0, 11), (8, 1, 0, 0, 11), (8, 2, 0, 0, 11)]))
+        work.append(("c3", n, g, [(1, 1, 0, 0, 11), (8, 1, 0, 0, 11), (25, 1, 0, 0, 11), (26, 1, 0, 0, 11),
+                                  (27, 1, 0, 0, 11), (8, 2, 0, 0, 11)]))
         for gg in (4, 16, 64):
             work.append((f"g{gg}", 1 << 18, gg, [(1, 1, 0, 1, 11), (8, 1, 0, 1, 11)]))
     if args.workload == "c3pipe":  # software-pipelined LDS loop against the plain one
