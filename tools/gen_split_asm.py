@@ -94,9 +94,21 @@ def tail_ops(j, al: Alloc):
 #                plane 0 right after rows 0..3's tails, plane 1 at the end
 #   "early"      "plain", and rows 1 and 2 (which read only plane-0 h values)
 #                run their tails before waiting for plane 1
-#   "pipe_early" both
-VARIANTS = ("pipe", "plain", "early", "pipe_early")
-DEFAULT = "pipe"
+#   "pipe_prio"  "pipe", with the wave's priority raised (s_setprio 2) from
+#                the arrival of its exchange until it has published the next
+#                generation's plane 0, so that a wave with data in hand keeps
+#                the LDS pipe fed before the others' tails
+#   "pipe_prio_e"  "pipe_prio", and raised again for rows 6..7 and the
+#                  plane-1 exchange (low only during rows 4..5)
+#   "pipe_prio_m"  priority dropped after rows 0..1's tails
+#   "pipe_prio1"   "pipe_prio" with s_setprio 1
+# v0 (LIFEAPI_XCHG_ASM) is VARIANTS[0]; the others are LIFEAPI_XCHG_ASM_V(k).
+# Measured on config 3 (profiles/r01/tune_c3asm_*.jsonl): "plain" 1.349 ms,
+# "early" 1.363, "pipe" 1.330-1.373, the compiled loop 1.370-1.392;
+# "pipe_prio" 1.287-1.307, dropping the priority right after the h-layer
+# 1.361, s_setprio 3 instead of 2 1.320.
+VARIANTS = ("pipe_prio", "pipe_prio_e", "pipe_prio_m", "pipe_prio1")
+DEFAULT = VARIANTS[0]
 
 
 def exchange(plane):
@@ -113,8 +125,13 @@ def prologue(variant=DEFAULT):
 
 def body(variant=DEFAULT):
     pipe, early = variant.startswith("pipe"), variant.endswith("early")
+    prio = 3 if variant.endswith("prio3") else 1 if variant.endswith("prio1") else 2 if "prio" in variant else 0
+    drop_after_h = variant.endswith("prio_h")
+    again, mid = variant.endswith("prio_e"), variant.endswith("prio_m")
     lines = [] if pipe else exchange(0) + exchange(1)
     lines += ["s_sub_u32 %[g], %[g], 1", "s_waitcnt lgkmcnt(3)"]
+    if prio:
+        lines.append(f"s_setprio {prio}")
 
     def hlayer(js):
         out = []
@@ -140,10 +157,21 @@ def body(variant=DEFAULT):
     if early:
         lines += rot_d + pair(1, 2) + ["s_waitcnt lgkmcnt(0)"] + hlayer(range(4, 8)) + rot_u + pair(0, 3)
     else:
-        lines += ["s_waitcnt lgkmcnt(0)"] + hlayer(range(4, 8)) + rot_u + rot_d + pair(0, 1) + pair(2, 3)
+        lines += ["s_waitcnt lgkmcnt(0)"] + hlayer(range(4, 8)) + rot_u + rot_d
+        if drop_after_h:
+            lines.append("s_setprio 0")
+        lines += pair(0, 1)
+        if mid:
+            lines.append("s_setprio 0")
+        lines += pair(2, 3)
     if pipe:
         lines += exchange(0)   # rows 0..3 are final: publish plane 0
-    lines += pair(4, 5) + pair(6, 7)
+    if prio and not (drop_after_h or mid):
+        lines.append("s_setprio 0")
+    lines += pair(4, 5)
+    if again:
+        lines.append(f"s_setprio {prio}")
+    lines += pair(6, 7)
     if pipe:
         lines += exchange(1)
     return lines
