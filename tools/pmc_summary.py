@@ -56,7 +56,7 @@ def main(prof_dir: str, out_json: str, universes: int = 1 << 20):
                         "FETCH_SIZE_KiB_mean": cf, "WRITE_SIZE_KiB_mean": cw,
                         "fetch_factor": ff, "write_factor": wf, "dispatches": [ncf, ncw]}
     try:  # config 3: 1024 generations in VGPRs, HBM touched once per universe
-        d["config3"] = entry("k_step_split<8, 1, false, 6, -3>",
+        d["config3"] = entry("k_step_split<8, 1, false, 6, -3,",
                              "k_step_split<S=8, G=1, NET 6, asm loop> (rule 11; config 3: 64K universes x 1024 gens)", (1 << 16) * 1024)
     except SystemExit:
         pass
