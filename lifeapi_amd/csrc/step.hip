@@ -393,7 +393,10 @@ __global__ __launch_bounds__(kBlock) void k_step_contains(const uint64_t *__rest
 // Without d_final, a wave stops once all its universes have hit.
 constexpr uint32_t kDiff = ((TA ^ TB) & (TB | TC)) & 0xFF;  // (s ^ wanted) & (wanted | unwanted)
 constexpr int kContainsNet = 6;  // tail network of the fused kernel (as k_step's default, rule 11)
-template <int S, int NET>
+// the fused kernel runs the assembly loop of split_asm.inc (split_contains_asm)
+// for gens > 2; the compiled loop above stays for comparison
+constexpr bool kContainsAsm = true;
+template <int S, int NET, bool ASM = false>
 __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *__restrict__ in,
                                                                 uint64_t *__restrict__ fin,
                                                                 const uint64_t *__restrict__ wanted,
@@ -415,6 +418,9 @@ __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *
     for (int u = 0; u < P; ++u) c[u] = split(unwanted[lane]);
     Split<S>::load(c, tu);
   }
+  uint32_t tm[S];  // wanted | unwanted (the assembly loop's second target plane)
+#pragma unroll
+  for (int j = 0; j < S; ++j) tm[j] = tw[j] | tu[j];
 
   const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock * P;
   for (uint64_t u0 = ((uint64_t)blockIdx.x * kWavesPerBlock + wib) * P; u0 < n; u0 += stride) {
@@ -427,7 +433,13 @@ __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *
 #pragma unroll
     for (int u = 0; u < P; ++u) hit[u] = 0;
     uint32_t found = 0;
-    for (uint32_t g = 1; g <= gens; ++g) {
+    if constexpr (ASM) {  // split_asm.inc: the default generation loop with the test fused in
+      static_assert(S == 8 && NET == 6, "split_contains_asm is rule 11");
+      const uint32_t base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)(
+          lds + wib * S * kWave);
+      split_contains_asm(r, tw, tm, gens, base + lane * 16u, base + ((lane + kWave - 1) & (kWave - 1)) * 16u,
+                         base + ((lane + 1) & (kWave - 1)) * 16u, hit);
+    } else for (uint32_t g = 1; g <= gens; ++g) {
       gen_split<S, NET>(r, lds + wib * S * kWave, lane);
       uint32_t d = 0;
 #pragma unroll
@@ -660,7 +672,7 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
   if (generations > 2) {  // the default layout of k_step for gens > 2 (lifeapi_default_cfg)
-    hipLaunchKernelGGL((k_step_contains_split<8, kContainsNet>), dim3(grid_for((n + 3) / 4, cus, 0)), dim3(kBlock), 0,
+    hipLaunchKernelGGL((k_step_contains_split<8, kContainsNet, kContainsAsm>), dim3(grid_for((n + 3) / 4, cus, 0)), dim3(kBlock), 0,
                        (hipStream_t)stream, d_in, d_final, d_wanted, d_unwanted, d_first_gen,
                        (uint64_t)n, generations);
   } else {

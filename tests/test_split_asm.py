@@ -52,3 +52,29 @@ def test_simulated_two_group_loop_is_step(port):
         ga, gb = g.simulate(_to_split(x), gens, two=_to_split(y))
         assert (ga == _to_split(port.step_batch(x, gens))).all(), gens
         assert (gb == _to_split(port.step_batch(y, gens))).all(), gens
+
+
+def test_simulated_contains_loop(port):
+    """split_contains_asm: the same generations plus, after each, the first
+    generation at which each universe contains the target (LifeTarget.hpp:44-51)."""
+    x = port.fill(4, seed=80) & port.fill(4, seed=81)
+    blk = np.zeros(64, np.uint64)
+    blk[20] = blk[21] = np.uint64(0b11 << 30)
+    ring = np.zeros(64, np.uint64)
+    for c in (19, 20, 21, 22):
+        ring[c] = np.uint64(0b1111 << 29)
+    ring &= ~blk
+    x[0] = (x[0] & ~ring & ~blk) | blk               # contained at once (still life)
+    x[2] = np.zeros(64, np.uint64)
+    x[2][20] = np.uint64(0b111 << 30)                 # no block
+    w = _to_split(np.stack([blk] * 4))
+    m = _to_split(np.stack([blk | ring] * 4))
+    for gens in (1, 4):
+        got, hits = g.simulate_contains(_to_split(x), w, m, gens)
+        s, exp = x.copy(), [0] * 4
+        for k in range(1, gens + 1):
+            s = port.step_batch(s, 1)
+            for u in range(4):
+                if not exp[u] and (((s[u] ^ blk) & (blk | ring)) == 0).all():
+                    exp[u] = k
+        assert (got == _to_split(s)).all() and hits == exp, (gens, hits, exp)

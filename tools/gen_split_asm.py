@@ -270,6 +270,144 @@ __device__ __forceinline__ void split_gens_asm2(uint32_t (&a)[8], uint32_t (&b)[
 """
 
 
+# ---- fused Step + Contains(LifeTarget) on the same loop (k_step_contains_split):
+# after each generation, d = OR_j (r_j ^ w_j) & m_j (m = wanted | unwanted,
+# LifeTarget.hpp:44-51), one ballot per universe (its bits are every 4th),
+# and the first generation with an empty ballot is kept per universe in SGPRs.
+W_REGS = [57, 58, 59, 60, 61, 62, 63, 64]        # w_j: bank j + 1
+M_REGS = [66, 67, 56, 65, 70, 71, 68, 69]        # m_j: bank j + 2
+N_VGPR_C = 72
+DIFF = 0x28        # (r ^ w) & m
+OR3 = 0xFE         # a | b | c
+ORAND = 0xA8       # (a | b) & c
+
+
+def contains_check():
+    al = Alloc()
+    d = []
+    for j in range(S):
+        t = al.get(j)
+        d.append(t)
+    lines = [op(d[j], R[j], W_REGS[j], M_REGS[j], DIFF) for j in range(S)]
+    x, y = al.get(1), al.get(2)
+    z = al.get(3)
+    lines += [op(x, d[0], d[1], d[2], OR3), op(y, d[3], d[4], d[5], OR3), op(z, d[6], d[7], x, OR3)]
+    t = al.get(0)
+    lines.append("s_add_u32 %[gc], %[gc], 1")
+    for u in range(P):
+        lines += [f"v_bitop3_b32 v{t}, v{y}, v{z}, %[m{u}] bitop3:0x{ORAND:02x}",
+                  f"v_cmp_ne_u32_e64 %[cmp], 0, v{t}",
+                  "s_cmp_eq_u64 %[cmp], 0",                 # SCC = universe u clean
+                  f"s_cselect_b32 %[c], {1 << u}, 0",
+                  "s_andn2_b32 %[c], %[c], %[found]",      # fresh hit
+                  "s_cmp_lg_u32 %[c], 0",
+                  f"s_cselect_b32 %[h{u}], %[gc], %[h{u}]",
+                  "s_or_b32 %[found], %[found], %[c]"]
+    return lines
+
+
+def contains_body():
+    """the default schedule's body with the check after rows 6..7 (all eight
+    rows final), before the plane-1 exchange"""
+    b = body(DEFAULT)
+    k = b.index(exchange(1)[0])
+    return b[:k] + contains_check() + b[k:]
+
+
+def emit_contains():
+    lines = ["s_cmp_eq_u32 %[g], 0", "s_cbranch_scc1 2f"] + prologue(DEFAULT) + ["1:"] + contains_body() + \
+        ["s_cmp_lg_u32 %[g], 0", "s_cbranch_scc1 1b", "s_waitcnt lgkmcnt(0)", "2:"]
+    asm = "\n".join(f'      "{l}\\n"' for l in lines)
+    outs = ",\n".join([f'        "+{{v{R[j]}}}"(r[{j}])' for j in range(S)] +
+                      [f'        [h{u}] "+s"(hit[{u}])' for u in range(P)])
+    ins = ", ".join([f'"{{v{W_REGS[j]}}}"(w[{j}])' for j in range(S)] +
+                    [f'"{{v{M_REGS[j]}}}"(m[{j}])' for j in range(S)] +
+                    [f'[m{u}] "s"(0x11111111u << {u})' for u in range(P)])
+    pinned = sorted({x for x in L + RR + H1 + H0 + [H0U, H0D, H1U, H1D] + TEMPS})
+    clob = ", ".join(f'"v{x}"' for x in pinned)
+    return f"""
+// Fused Step + Contains on the default schedule: after every generation the
+// containment test of all four universes (hit[u] = first generation whose
+// state contains the target, 0 = none yet).  w / m: the target's wanted and
+// wanted | unwanted planes in the same register layout.  {N_VGPR_C} VGPRs pinned.
+__device__ __forceinline__ void split_contains_asm(uint32_t (&r)[8], const uint32_t (&w)[8],
+                                                   const uint32_t (&m)[8], uint32_t gens, uint32_t a_self,
+                                                   uint32_t a_prev, uint32_t a_next, uint32_t (&hit)[4]) {{
+  uint32_t gc = 0, found = 0, c;
+  uint64_t cmp;
+  asm volatile(
+{asm}
+      : {outs.strip()},
+        [g] "+s"(gens), [gc] "+s"(gc), [found] "+s"(found), [c] "=&s"(c), [cmp] "=&s"(cmp)
+      : "{{v{A_SELF}}}"(a_self), "{{v{A_PREV}}}"(a_prev), "{{v{A_NEXT}}}"(a_next),
+        {ins}
+      : {clob}, "scc", "memory");
+}}
+"""
+
+
+def simulate_contains(r, w, m, gens):
+    """numpy run of split_contains_asm: returns (r, hits[4])"""
+    v = np.zeros((N_VGPR_C, 64), np.uint32)
+    v[:8] = r
+    v[W_REGS] = w
+    v[M_REGS] = m
+    hits, found = [0] * P, 0
+    lds_plane = {}
+    seq = prologue(DEFAULT) + (contains_body() * gens if gens else [])
+    gc = 0
+    cmp = 0
+    for l in seq:
+        if l.startswith("s_add_u32 %[gc]"):
+            gc += 1
+        elif l.startswith("v_bitop3_b32") and "%[m" in l:
+            d, a, b = (int(x) for x in re.findall(r"v(\d+)", l)[:3])
+            u = int(re.search(r"%\[m(\d)\]", l)[1])
+            v[d] = (v[a] | v[b]) & np.uint32(0x11111111 << u)
+        elif l.startswith("v_cmp_ne_u32_e64"):
+            t = int(re.findall(r"v(\d+)", l)[-1])
+            cmp = int((v[t] != 0).any())
+        elif l.startswith("s_cselect_b32 %[c]"):
+            bit = int(l.split(",")[1])
+            c = bit if cmp == 0 else 0
+        elif l.startswith("s_andn2_b32 %[c]"):
+            c &= ~found
+        elif l.startswith("s_cselect_b32 %[h"):
+            u = int(re.search(r"%\[h(\d)\]", l)[1])
+            if c:
+                hits[u] = gc
+        elif l.startswith("s_or_b32 %[found]"):
+            found |= c
+        else:
+            _exec(v, l, lds_plane)
+    return v[:8].copy(), hits
+
+
+def _exec(v, l, lds_plane):
+    if l.startswith("ds_write_b128"):
+        off = int(re.search(r"offset:(\d+)", l)[1]) if "offset" in l else 0
+        base = int(re.search(r"v\[(\d+):", l)[1])
+        lds_plane[off] = v[base:base + 4].copy()
+    elif l.startswith("ds_read_b128"):
+        off = int(re.search(r"offset:(\d+)", l)[1]) if "offset" in l else 0
+        base = int(re.search(r"v\[(\d+):", l)[1])
+        src = int(re.search(r"v(\d+)(?: offset|$)", l.split(",", 1)[1].strip())[1])
+        v[base:base + 4] = np.roll(lds_plane[off], 1 if src == A_PREV else -1, axis=1)
+    elif l.startswith("v_bitop3_b32"):
+        d, a, b, c = (int(x) for x in re.findall(r"v(\d+)", l))
+        tt = int(l.rsplit(":", 1)[1], 16)
+        out = np.zeros(64, np.uint32)
+        for k in range(8):
+            if tt >> k & 1:
+                out |= (v[a] if k & 4 else ~v[a]) & (v[b] if k & 2 else ~v[b]) & (v[c] if k & 1 else ~v[c])
+        v[d] = out
+    elif l.startswith("v_alignbit_b32"):
+        d, a, b = (int(x) for x in re.findall(r"v(\d+)", l)[:3])
+        sh = int(l.rsplit(",", 1)[1])
+        x = (v[a].astype(np.uint64) << np.uint64(32)) | v[b].astype(np.uint64)
+        v[d] = ((x >> np.uint64(sh)) & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+
+
 def asm_text(variant=DEFAULT):
     return ["s_cmp_eq_u32 %[g], 0", "s_cbranch_scc1 2f"] + prologue(variant) + ["1:"] + body(variant) + \
         ["s_cmp_lg_u32 %[g], 0", "s_cbranch_scc1 1b", "s_waitcnt lgkmcnt(0)", "2:"]
@@ -366,7 +504,7 @@ def emit():
 #pragma once
 
 namespace lifeapi_impl {{
-{fns}{emit2()}
+{fns}{emit2()}{emit_contains()}
 }}  // namespace lifeapi_impl
 """
 
