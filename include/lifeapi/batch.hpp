@@ -191,8 +191,9 @@ std::vector<std::string> RLEBatch(std::span<const S> states, int device = 0) {
 
 inline int DeviceCount() { return lifeapi_device_count(); }
 
-// Page-locks a caller-owned array for its lifetime (lifeapi_host_register):
-// keep one around a LifeState batch that a search loop steps repeatedly.
+// Page-locks a caller-owned array for its lifetime (lifeapi_host_register).
+// Calls moving 8 MiB or more pin pageable arrays themselves; a HostPin holds
+// the pin across the calls of a search loop and covers smaller batches.
 class HostPin {
  public:
   HostPin(void *p, size_t bytes) : p_(p) { check(lifeapi_host_register(p, bytes)); }

@@ -93,11 +93,16 @@ int launched(const char *what) {
 // k's D2H on the same stream).  Chunk k's H2D also waits (event) for chunk
 // k-1's H2D, so the two streams run one chunk apart and chunk k's D2H
 // overlaps chunk k+1's H2D; without that they start in phase and both
-// directions stay serialised.  That pays only for
-// page-locked host arrays (lifeapi_host_register): the runtime serialises
-// pageable copies in both directions (profiles/r01/host_bench.jsonl).
+// directions stay serialised.  That pays only for page-locked host arrays:
+// the runtime serialises pageable copies in both directions.  So every call
+// moving at least kPinMinBytes page-locks the caller's arrays itself for its
+// duration (hipHostRegister, then hipHostUnregister): on MI355X that costs
+// nothing measurable and takes 1M universes from 19.4 to 12.2 ms
+// (profiles/r01/host_bench.jsonl).  Arrays the caller pinned already
+// (lifeapi_host_register) or that cannot be pinned are used as they are.
 constexpr int kLanes = 2;  // (the event chain below assumes two)
 constexpr size_t kChunkBytes = size_t(64) << 20;  // staging per stream and pass
+constexpr size_t kPinMinBytes = size_t(8) << 20;  // smaller calls stay pageable
 
 struct HostCtx {
   std::mutex mu;
@@ -150,6 +155,31 @@ int host_chunked(int dev, size_t n, const HostIO *io, int nio, ChunkFn fn, const
     }
     c->cap = need;
   }
+  // page-lock the caller's arrays for this call (see above)
+  std::vector<void *> pinned;
+  auto try_pin = [&](const void *p, size_t bytes) {
+    if (!p || bytes < kPinMinBytes) return;
+    for (void *q : pinned)
+      if (q == p) return;
+    // Leave ranges the caller pinned alone: the runtime accepts a second
+    // registration without counting it, so our unregister would undo theirs
+    // (tools/pin_probe.cpp; hipHostGetFlags fails on registered memory, the
+    // pointer attributes report it as host memory).
+    for (const char *q : {(const char *)p, (const char *)p + bytes - 1}) {
+      hipPointerAttribute_t a{};
+      const hipError_t e = hipPointerGetAttributes(&a, q);
+      (void)hipGetLastError();
+      if (e != hipSuccess || a.type != hipMemoryTypeUnregistered) return;
+    }
+    if (hipHostRegister(const_cast<void *>(p), bytes, hipHostRegisterPortable) == hipSuccess)
+      pinned.push_back(const_cast<void *>(p));
+    else
+      (void)hipGetLastError();  // already registered, or not pinnable: copy it as it is
+  };
+  for (int q = 0; q < nio; ++q) {
+    try_pin(io[q].src, n * io[q].bytes);
+    try_pin(io[q].dst, n * io[q].bytes);
+  }
   int rc = LIFEAPI_OK;
   void *d[8];
   for (size_t k = 0; k * chunk < n && rc == LIFEAPI_OK; ++k) {
@@ -184,6 +214,8 @@ int host_chunked(int dev, size_t n, const HostIO *io, int nio, ChunkFn fn, const
     e = hipStreamSynchronize(c->stream[l]);
     if (e != hipSuccess && rc == LIFEAPI_OK) rc = fail_hip(e, "hipStreamSynchronize");
   }
+  for (void *p : pinned)
+    if (hipHostUnregister(p) != hipSuccess) (void)hipGetLastError();
   return rc;
 }
 

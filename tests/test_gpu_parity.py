@@ -228,8 +228,11 @@ def test_host_api_many_chunks_pinned(hip, port):
     want = port.step_batch(x, 2)
     out = np.zeros_like(x)
     assert (hip.step_host(x, 2, out=out).reshape(-1, 64) == want).all()
+    # the call pinned the pageable arrays for its duration only (unpinned again)
+    assert hip.lib.lifeapi_host_unregister(x.ctypes.data) != 0
+    assert hip.lib.lifeapi_host_unregister(out.ctypes.data) != 0
     y = x.copy()
-    with hip.host_pinned(y, out):
+    with hip.host_pinned(y, out):  # the call must leave the caller's pins in place
         out[:] = 0
         assert (hip.step_host(y, 2, out=out).reshape(-1, 64) == want).all()
         hip.step_host(y, 2, out=y)  # in place, pinned

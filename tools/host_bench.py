@@ -42,6 +42,12 @@ def main():
             print(json.dumps({"case": case, "universes": n, "gens": gens, "s": t,
                               "universe_gen_per_s": n * gens / t,
                               "GBps_round_trip": 2 * nbytes / t / 1e9}), flush=True)
+        def pin_each_call():  # registration inside the timed call, as a library-side pin would
+            with hip.host_pinned(x, out):
+                hip.step_host(x, generations=gens, out=out)
+        t = wall(pin_each_call)
+        print(json.dumps({"case": "step_host_register_per_call", "universes": n, "gens": gens, "s": t,
+                          "universe_gen_per_s": n * gens / t}), flush=True)
         with hip.host_pinned(x, out):  # page-locked once (lifeapi_host_register)
             for case, o in (("step_host_pinned", out), ("step_host_pinned_inplace", x)):
                 t = wall(lambda: hip.step_host(x, generations=gens, out=o))
