@@ -14,6 +14,13 @@ namespace {
 // sum over the wave by DPP (wave_sum_*_dpp), not through ds_bpermute.
 constexpr int kRedU = 4;
 
+// The states are read once: nontemporal loads, and a grid of at most 32
+// blocks per CU looping over the batch (full grids and plain loads were 6-20 %
+// slower, profiles/r01/red_ab.jsonl).
+constexpr int kRedBlocksPerCU = 32;
+
+__device__ __forceinline__ uint64_t ld_state(const uint64_t *p) { return __builtin_nontemporal_load(p); }
+
 // GetPop (LifeAPI.hpp:290-298): two universes' popcounts per 32-bit reduction
 __global__ __launch_bounds__(kBlock) void k_pop(const uint64_t *__restrict__ s,
                                                 uint32_t *__restrict__ pop, uint64_t n) {
@@ -23,7 +30,7 @@ __global__ __launch_bounds__(kBlock) void k_pop(const uint64_t *__restrict__ s,
        u0 += stride) {
     uint32_t c[kRedU];
 #pragma unroll
-    for (int k = 0; k < kRedU; ++k) c[k] = u0 + k < n ? (uint32_t)__popcll(s[(u0 + k) * kWave + lane]) : 0u;
+    for (int k = 0; k < kRedU; ++k) c[k] = u0 + k < n ? (uint32_t)__popcll(ld_state(s + (u0 + k) * kWave + lane)) : 0u;
 #pragma unroll
     for (int k = 0; k < kRedU; k += 2) {
       const uint32_t t = wave_sum_u32_dpp(c[k] | c[k + 1] << 16);  // each sum <= 4096
@@ -44,7 +51,7 @@ __global__ __launch_bounds__(kBlock) void k_hash(const uint64_t *__restrict__ s,
        u0 += stride) {
     uint64_t m[kRedU];
 #pragma unroll
-    for (int k = 0; k < kRedU; ++k) m[k] = u0 + k < n ? s[(u0 + k) * kWave + lane] : 0ull;
+    for (int k = 0; k < kRedU; ++k) m[k] = u0 + k < n ? ld_state(s + (u0 + k) * kWave + lane) : 0ull;
 #pragma unroll
     for (int k = 0; k < kRedU; ++k) {
       const uint64_t t = wave_sum_u64_dpp(mix64(m[k] + (uint64_t)(lane + 1) * kGolden));
@@ -64,7 +71,7 @@ __global__ __launch_bounds__(kBlock) void k_contains(const uint64_t *__restrict_
        u0 += stride) {
     W a[kRedU];
 #pragma unroll
-    for (int k = 0; k < kRedU; ++k) a[k] = u0 + k < n ? split(s[(u0 + k) * kWave + lane]) : W{0u, 0u};
+    for (int k = 0; k < kRedU; ++k) a[k] = u0 + k < n ? split(ld_state(s + (u0 + k) * kWave + lane)) : W{0u, 0u};
 #pragma unroll
     for (int k = 0; k < kRedU; ++k) {
       const bool c = wave_contains(a[k], w, uw);
@@ -93,8 +100,8 @@ int lifeapi_pop_batch_dev(const uint64_t *d_states, uint32_t *d_pop, size_t n, v
     return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_pop_batch_dev%s");
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
-  hipLaunchKernelGGL(k_pop, dim3(grid_for((n + kRedU - 1) / kRedU, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream,
-                     d_states, d_pop, (uint64_t)n);
+  hipLaunchKernelGGL(k_pop, dim3(grid_for((n + kRedU - 1) / kRedU, cus, kRedBlocksPerCU)), dim3(kBlock), 0,
+                     (hipStream_t)stream, d_states, d_pop, (uint64_t)n);
   return launched("k_pop launch");
 }
 
@@ -104,8 +111,8 @@ int lifeapi_hash_batch_dev(const uint64_t *d_states, uint64_t *d_hash, size_t n,
     return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_hash_batch_dev%s");
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
-  hipLaunchKernelGGL(k_hash, dim3(grid_for((n + kRedU - 1) / kRedU, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream,
-                     d_states, d_hash, (uint64_t)n);
+  hipLaunchKernelGGL(k_hash, dim3(grid_for((n + kRedU - 1) / kRedU, cus, kRedBlocksPerCU)), dim3(kBlock), 0,
+                     (hipStream_t)stream, d_states, d_hash, (uint64_t)n);
   return launched("k_hash launch");
 }
 
@@ -118,7 +125,7 @@ int lifeapi_contains_batch_dev(const uint64_t *d_states, const uint64_t *d_wante
     return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_contains_batch_dev%s");
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
-  hipLaunchKernelGGL(k_contains, dim3(grid_for((n + kRedU - 1) / kRedU, cus, 0)), dim3(kBlock), 0,
+  hipLaunchKernelGGL(k_contains, dim3(grid_for((n + kRedU - 1) / kRedU, cus, kRedBlocksPerCU)), dim3(kBlock), 0,
                      (hipStream_t)stream, d_states, d_wanted, d_unwanted, d_out, (uint64_t)n);
   return launched("k_contains launch");
 }
