@@ -97,12 +97,80 @@ int launched(const char *what) {
 // the runtime serialises pageable copies in both directions.  So every call
 // moving at least kPinMinBytes page-locks the caller's arrays itself for its
 // duration (hipHostRegister, then hipHostUnregister): on MI355X that costs
-// nothing measurable and takes 1M universes from 19.4 to 12.2 ms
+// under 1 ms and takes 1M universes from 19.4 to 12.2-13.1 ms
 // (profiles/r01/host_bench.jsonl).  Arrays the caller pinned already
 // (lifeapi_host_register) or that cannot be pinned are used as they are.
 constexpr int kLanes = 2;  // (the event chain below assumes two)
 constexpr size_t kChunkBytes = size_t(64) << 20;  // staging per stream and pass
 constexpr size_t kPinMinBytes = size_t(8) << 20;  // smaller calls stay pageable
+
+// Ranges this library pinned, shared by every call in the process: a call
+// whose array lies inside one takes a reference instead of registering again,
+// so concurrent calls (other threads, the per-device shards of
+// lifeapi_step_batch) never unpin memory another call is still copying.
+struct PinRec {
+  uintptr_t lo, hi;
+  int refs;
+};
+std::mutex g_pin_mu;
+std::vector<PinRec> g_pins;
+
+// Returns the start of the range referenced (to pass to pin_release), or 0
+// when the array is used as it is: too small, pinned by the caller, partly
+// overlapping another call's pin, or not pinnable.
+uintptr_t pin_acquire(const void *p, size_t bytes) {
+  if (!p || bytes < kPinMinBytes) return 0;
+  const uintptr_t lo = (uintptr_t)p, hi = lo + bytes;
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  for (PinRec &r : g_pins)
+    if (lo < r.hi && r.lo < hi) {
+      if (r.lo <= lo && hi <= r.hi) {
+        ++r.refs;
+        return r.lo;
+      }
+      return 0;
+    }
+  // Leave ranges the caller pinned alone: the runtime accepts a second
+  // registration without counting it, so our unregister would undo theirs
+  // (tools/pin_probe.cpp; hipHostGetFlags fails on registered memory, the
+  // pointer attributes report it as host memory).
+  for (uintptr_t q : {lo, hi - 1}) {
+    hipPointerAttribute_t a{};
+    const hipError_t e = hipPointerGetAttributes(&a, (const void *)q);
+    (void)hipGetLastError();
+    if (e != hipSuccess || a.type != hipMemoryTypeUnregistered) return 0;
+  }
+  if (hipHostRegister((void *)lo, bytes, hipHostRegisterPortable) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  g_pins.push_back({lo, hi, 1});
+  return lo;
+}
+
+void pin_release(uintptr_t key) {
+  if (!key) return;
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  for (size_t k = 0; k < g_pins.size(); ++k)
+    if (g_pins[k].lo == key) {
+      if (--g_pins[k].refs == 0) {
+        if (hipHostUnregister((void *)key) != hipSuccess) (void)hipGetLastError();
+        g_pins.erase(g_pins.begin() + k);
+      }
+      return;
+    }
+}
+
+// Holds pin_acquire references for one call.
+struct CallPins {
+  std::vector<uintptr_t> keys;
+  void add(const void *p, size_t bytes) {
+    if (const uintptr_t k = pin_acquire(p, bytes)) keys.push_back(k);
+  }
+  ~CallPins() {
+    for (uintptr_t k : keys) pin_release(k);
+  }
+};
 
 struct HostCtx {
   std::mutex mu;
@@ -156,29 +224,10 @@ int host_chunked(int dev, size_t n, const HostIO *io, int nio, ChunkFn fn, const
     c->cap = need;
   }
   // page-lock the caller's arrays for this call (see above)
-  std::vector<void *> pinned;
-  auto try_pin = [&](const void *p, size_t bytes) {
-    if (!p || bytes < kPinMinBytes) return;
-    for (void *q : pinned)
-      if (q == p) return;
-    // Leave ranges the caller pinned alone: the runtime accepts a second
-    // registration without counting it, so our unregister would undo theirs
-    // (tools/pin_probe.cpp; hipHostGetFlags fails on registered memory, the
-    // pointer attributes report it as host memory).
-    for (const char *q : {(const char *)p, (const char *)p + bytes - 1}) {
-      hipPointerAttribute_t a{};
-      const hipError_t e = hipPointerGetAttributes(&a, q);
-      (void)hipGetLastError();
-      if (e != hipSuccess || a.type != hipMemoryTypeUnregistered) return;
-    }
-    if (hipHostRegister(const_cast<void *>(p), bytes, hipHostRegisterPortable) == hipSuccess)
-      pinned.push_back(const_cast<void *>(p));
-    else
-      (void)hipGetLastError();  // already registered, or not pinnable: copy it as it is
-  };
+  CallPins pins;
   for (int q = 0; q < nio; ++q) {
-    try_pin(io[q].src, n * io[q].bytes);
-    try_pin(io[q].dst, n * io[q].bytes);
+    pins.add(io[q].src, n * io[q].bytes);
+    if (io[q].dst != io[q].src) pins.add(io[q].dst, n * io[q].bytes);
   }
   int rc = LIFEAPI_OK;
   void *d[8];
@@ -214,9 +263,7 @@ int host_chunked(int dev, size_t n, const HostIO *io, int nio, ChunkFn fn, const
     e = hipStreamSynchronize(c->stream[l]);
     if (e != hipSuccess && rc == LIFEAPI_OK) rc = fail_hip(e, "hipStreamSynchronize");
   }
-  for (void *p : pinned)
-    if (hipHostUnregister(p) != hipSuccess) (void)hipGetLastError();
-  return rc;
+  return rc;  // (both streams synchronised: the pins can go)
 }
 
 int host_device(int device) {
@@ -262,7 +309,11 @@ int lifeapi_step_batch(const uint64_t *in, uint64_t *out, size_t n, uint32_t gen
   if (device >= ndev || device < -1) return fail(LIFEAPI_E_NODEVICE, "bad device index%s");
   if (device >= 0 || ndev == 1)
     return host_step_one_device(in, out, n, generations, device < 0 ? 0 : device);
-  // every visible device, contiguous shards, one host thread each
+  // every visible device, contiguous shards, one host thread each; the whole
+  // arrays are pinned once here (shard boundaries share pages)
+  CallPins pins;
+  pins.add(in, n * 512);
+  if (out != in) pins.add(out, n * 512);
   std::vector<int> rcs(ndev, LIFEAPI_OK);
   std::vector<std::string> errs(ndev);
   std::vector<std::thread> pool;

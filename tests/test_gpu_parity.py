@@ -240,6 +240,36 @@ def test_host_api_many_chunks_pinned(hip, port):
     assert hip.lib.lifeapi_host_unregister(y.ctypes.data) != 0  # no longer registered
 
 
+def test_host_api_concurrent_shared_input(hip, port):
+    """Calls from several threads on one shared (pageable) input: each call
+    pins it for its duration (a shared, counted pin), and none may unpin it
+    under another's copies; afterwards it is no longer registered."""
+    import threading
+    n = 40_000  # 20 MiB: above the per-call pinning threshold
+    x = port.fill(n, seed=21)
+    want = port.step_batch(x, 3)
+    outs = [np.zeros_like(x) for _ in range(4)]
+    errs = []
+
+    def run(o):
+        try:
+            for _ in range(3):
+                o[:] = 0
+                hip.step_host(x, 3, out=o)
+                if not (o.reshape(-1, 64) == want).all():
+                    errs.append("mismatch")
+        except Exception as e:  # noqa: BLE001 - reported below
+            errs.append(repr(e))
+
+    ts = [threading.Thread(target=run, args=(o,)) for o in outs]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs, errs
+    assert hip.lib.lifeapi_host_unregister(x.ctypes.data) != 0
+
+
 @pytest.mark.parametrize("gens", [2, 40])
 def test_host_step_contains(hip, port, gens):
     """lifeapi_step_contains_batch on host arrays (natural layout for gens <= 2,
