@@ -1,22 +1,38 @@
 #!/usr/bin/env python3
-"""bench.py -- batched 64x64-torus LifeState::Step() on MI355X.
+"""bench.py -- batched 64x64-torus LifeState::Step() on MI355X, 1..8 GPUs.
 
-Headline workload (BASELINE.json configs[1], "config 2"): 1M random-fill
-64x64 universes x 1 generation per step, per GPU.  A step is one launch of
-the HIP step kernel over the rank's whole shard (device-resident, ping-pong
-buffers, so the state keeps evolving).  With N GPUs (one process per GPU,
-launched by torch.distributed.run) every rank steps its own contiguous shard
-of the global universe array -- no collective on the data path ("weak"
-scaling: per-GPU work fixed).  After the timed region the per-universe hashes
-are all-gathered over RCCL (result collection, timed and reported separately).
+Workloads (BASELINE.json configs; the per-universe independence that lets them
+shard with no collective is LifeAPI.hpp:1196-1216 -- Step() reads one object):
 
-Prints ONE JSON line on rank 0 (contract in the task brief / DESIGN.md).
+* config 2 (the N=1 default): 1M random-fill universes x 1 generation per step
+  on each GPU ("weak": per-GPU work fixed; rank r owns universes
+  [r*1M, (r+1)*1M) of the seed-2 array).
+* config 4 (the N>1 default): ONE fixed problem of 16M universes x 1
+  generation, split into N contiguous shards ("strong"; 8 GiB in + 8 GiB out
+  over all ranks).  `--config 4 --gpus 1` runs the same 16M on one GPU, and
+  the N=1 line carries that run as `secondary.config4`, so the 8-vs-1 ratio is
+  the same problem.
+
+A step is one launch of the HIP step kernel over the rank's whole shard
+(device-resident ping-pong buffers, so the state keeps evolving).  With
+`--gpus N` and no torch.distributed environment, this process starts N ranks
+through `torch.distributed.run` as a child process (before touching the GPU)
+and exits with its status; each rank drives one GPU.  The only collectives
+are outside the timed region: the barrier/MAX of the timing contract, the
+per-rank digest exchange of the first-launch check and the result
+collection (an all-gather of per-universe 64-bit hashes over RCCL/xGMI),
+timed and reported separately.
+
+Prints ONE JSON line on rank 0 (contract: task brief).
 """
 from __future__ import annotations
 
 import argparse
+import importlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -27,14 +43,27 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from lifeapi_amd.digest import batch_digest  # noqa: E402
-from lifeapi_amd.shard import gather_hashes, weak_shard  # noqa: E402
+from lifeapi_amd.digest import batch_digest, combine  # noqa: E402
+from lifeapi_amd.shard import gather_hashes, strong_shard, weak_shard  # noqa: E402
 
 METRIC = "64x64 universe-generations/sec (+ cell-updates/sec) at 1/2/4/8 MI355X"
-HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
 BYTES_PER_UNIVERSE_GEN = 1024  # 512 B read + 512 B write
 OPS_PER_UNIVERSE_GEN = 2688    # reference's ~21 u64 ops/column = 42 int32 x 64
+# Config 3's fixed algorithmic bound: 8 three-input LUTs per
+# 32 cell-updates (the 2-LUT horizontal layer + the 6-LUT tail, the smallest
+# network the exhaustive/CGP searches found) = 1024 lane-LUTs = 16 wave64
+# VALU issue slots per universe-generation; peak = 1024 SIMDs x one wave64
+# VALU op per 2 clk at 2.4 GHz.
+C3_SLOTS_PER_UNIVERSE_GEN = 16
+VALU_PEAK_SLOTS = 1024 * 2.4e9 / 2
 
+CONFIGS = {
+    2: {"name": "config2", "seed": 2, "universes": 1 << 20, "scaling": "weak",
+        "golden": ("weak_shards_seed2", "weak_shards_seed2_small")},
+    4: {"name": "config4", "seed": 4, "universes": 1 << 24, "scaling": "strong",
+        "golden": ("config4", "config4_small")},
+}
 
 COLL_DEV = None  # device the collectives' tensors live on (set in main)
 
@@ -43,41 +72,114 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def parse_args():
+def parse_args(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=10)
-    p.add_argument("--universes", type=int, default=1 << 20, help="universes per rank (config 2: 1M)")
+    p.add_argument("--config", default="auto", choices=("auto", "2", "4"),
+                   help="auto: config 2 at N=1, config 4 (16M strong-split) at N>1")
+    p.add_argument("--universes", type=int, default=0,
+                   help="override: per-rank universes (config 2) or the global total (config 4)")
     p.add_argument("--gens-per-step", type=int, default=1)
-    p.add_argument("--seed", type=int, default=2)
+    p.add_argument("--seed", type=int, default=-1, help="override the config's seed")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0,
-                   help="wall budget of the CPU baseline (half at 1 thread, half at 16)")
-    p.add_argument("--no-secondary", action="store_true", help="skip the config-3 side measurement")
+                   help="wall budget of the config-2 CPU baseline (half at 1 thread, half on all host cores)")
+    p.add_argument("--no-secondary", action="store_true", help="skip the config-3/4/5 side measurements")
     p.add_argument("--no-verify", action="store_true")
-    return p.parse_args()
+    return p.parse_args(argv)
 
 
-def timed_launches(hip, bufs, steps, gens, stream):
-    """Run `steps` back-to-back ping-pong launches on `stream`, bracketed by one
-    pair of HIP events on that same stream (no events between launches, so
-    none of their cost lands between kernels).  Returns ((start, end), index
+# ----------------------------------------------------------------------------
+# process launch: one rank per GPU
+# ----------------------------------------------------------------------------
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv: list[str]) -> int:
+    """Start `n` ranks of this script under torch.distributed.run as a CHILD
+    process (this process has not touched the GPU and never execs) and
+    return its exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+    log("+ " + " ".join(cmd))
+    return subprocess.call(cmd)
+
+
+class HipRuntime:
+    """Device, launch stream and timing events of one rank (one GPU)."""
+    kind = "hip"
+
+    def __init__(self, local_rank: int, world: int, backend: str):
+        ndev = torch.cuda.device_count()
+        if ndev == 0:
+            raise RuntimeError("bench.py needs a GPU (no HIP device visible)")
+        if world > ndev and backend == "nccl":
+            raise RuntimeError(f"{world} ranks but only {ndev} visible GPUs")
+        # the modulo only matters for a gloo rehearsal with more ranks than GPUs
+        self.device = torch.device("cuda", local_rank % ndev)
+        torch.cuda.set_device(self.device)
+        self.stream = torch.cuda.current_stream(self.device)
+
+    def sync(self):
+        torch.cuda.synchronize(self.device)
+
+    @staticmethod
+    def event():
+        return torch.cuda.Event(enable_timing=True)
+
+
+def load_kernels(backend: str, local_rank: int, world: int):
+    """The HIP library (lifeapi_amd.hip) and its runtime.  LIFEAPI_BENCH_STUB
+    names a CPU stand-in module used ONLY by tests/test_bench_ranks.py to
+    rehearse this rank logic without a GPU; it is refused when a GPU is
+    visible, and the line it prints says so."""
+    stub = os.environ.get("LIFEAPI_BENCH_STUB")
+    if stub:
+        if torch.cuda.is_available():
+            raise RuntimeError("LIFEAPI_BENCH_STUB is for GPU-less rank rehearsals only")
+        mod = importlib.import_module(stub)
+        return mod, mod.Runtime(local_rank)
+    import lifeapi_amd.hip as hip
+    return hip, HipRuntime(local_rank, world, backend)
+
+
+# ----------------------------------------------------------------------------
+# timing
+# ----------------------------------------------------------------------------
+def timed_launches(hip, rt, bufs, steps, gens):
+    """`steps` back-to-back ping-pong launches on the rank's stream, bracketed
+    by one pair of events on that same stream.  Returns ((start, end), index
     of the buffer holding the latest state)."""
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0, e1 = rt.event(), rt.event()
     cur = 0
-    e0.record(stream)
+    e0.record(rt.stream)
     for _ in range(steps):
-        hip.step(bufs[cur], out=bufs[1 - cur], generations=gens, stream=stream)
+        hip.step(bufs[cur], out=bufs[1 - cur], generations=gens, stream=rt.stream)
         cur = 1 - cur
-    e1.record(stream)
+    e1.record(rt.stream)
     return (e0, e1), cur
 
 
+def median_launch_ms(hip, rt, a, b, gens, reps=10):
+    ms = []
+    for _ in range(reps):
+        e0, e1 = rt.event(), rt.event()
+        e0.record(rt.stream)
+        hip.step(a, out=b, generations=gens, stream=rt.stream)
+        e1.record(rt.stream)
+        e1.synchronize()
+        ms.append(e0.elapsed_time(e1))
+    return sorted(ms)[len(ms) // 2], ms
+
+
 def copy_ceiling():
-    """Best median GB/s of the same-shape HBM copy kernel (tools/membw.hip:
-    dwordx2 lanes, 4 x 512 B in flight per wave, read + write) measured on
-    MI355X and committed under profiles/; context for the roofline."""
+    """Best median GB/s of the same-shape HBM copy kernel (tools/membw.hip)
+    measured on MI355X and committed under profiles/; context for the roofline."""
     path = os.path.join(ROOT, "profiles", "r01", "membw.jsonl")
     best = None
     try:
@@ -94,154 +196,6 @@ def copy_ceiling():
     return best, os.path.relpath(path, ROOT)
 
 
-def cpu_baseline(x_host: np.ndarray, seconds: float):
-    """Reference CPU Step() (oracle/_ref, else the C port) on host cores."""
-    from oracle.oracle import Port, Ref
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    threads = max(1, min(threads, 16))
-    if Ref.available():
-        o, kind = Ref(), "reference"
-        run = lambda a, t: o.step_batch(a, 1, nthreads=t)  # noqa: E731
-    else:
-        o, kind = Port(), "port"
-        run = lambda a, t: o.step_batch(a, 1, nthreads=t)  # noqa: E731
-    n = x_host.shape[0]
-    out = {}
-    for t in sorted({1, threads}):
-        run(x_host[: min(n, 4096)], t)  # warm
-        passes, t0 = 0, time.perf_counter()
-        while True:
-            run(x_host, t)
-            passes += 1
-            el = time.perf_counter() - t0
-            if el >= seconds / 2:
-                break
-        out[t] = (n * passes / el, passes, el)
-    v, passes, el = out[threads]
-    cpu = ""
-    try:
-        with open("/proc/cpuinfo") as f:
-            cpu = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), "")
-    except OSError:
-        pass
-    return {
-        "value": v, "unit": "universe-gen/s", "cores": threads, "kind": kind,
-        "sample": f"config-2 input ({n} universes) x 1 gen, {passes} passes in {el:.2f}s, "
-                  f"{threads} threads, contiguous slices; CPU: {cpu}",
-        "value_1thread": out[1][0],
-    }
-
-
-def cpu_baseline_config3(x_host: np.ndarray, seconds: float):
-    """The reference's Step(gens) (oracle/_ref, else the C port) on the
-    config-3 shape: a bounded sample of the same universes, 1024 generations
-    each, on the host cores (`seconds` of work)."""
-    from oracle.oracle import Port, Ref
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    threads = max(1, min(threads, 16))
-    o, kind = (Ref(), "reference") if Ref.available() else (Port(), "port")
-    sample = x_host[: 64 * threads]
-    o.step_batch(sample[:threads], 1024, nthreads=threads)  # warm
-    done, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        o.step_batch(sample, 1024, nthreads=threads)
-        done += sample.shape[0]
-    el = time.perf_counter() - t0
-    return {"value": done * 1024 / el, "unit": "universe-gen/s", "cores": threads, "kind": kind,
-            "sample": f"{sample.shape[0]} of the config-3 universes x 1024 gens, {done // sample.shape[0]} "
-                      f"passes in {el:.2f}s, {threads} threads"}
-
-
-def secondary_config3(hip, device, stream, cpu_seconds=0.0):
-    """Config 3: 64K universes x 1024 generations, state resident in VGPRs."""
-    n, gens = 1 << 16, 1024
-    a = hip.fill_random(n, seed=3, device=device, stream=stream)
-    b = torch.empty_like(a)
-    for _ in range(20):  # warm: ~30 ms of back-to-back launches (clocks settle)
-        hip.step(a, out=b, generations=gens, stream=stream)
-    reps, ms = 10, []
-    for _ in range(reps):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        hip.step(a, out=b, generations=gens, stream=stream)
-        e1.record(stream)
-        e1.synchronize()
-        ms.append(e0.elapsed_time(e1))
-    t = sorted(ms)[len(ms) // 2] / 1e3  # median launch
-    gps = n * gens / t
-    # VALU issue model of the default generation loop (rule 11, the
-    # hand-allocated loop of split_asm.inc, DESIGN.md 3.1): per 4 universes
-    # 64 v_bitop3 (one slot; the 6-LUT tail)
-    # + 4 v_alignbit (two slots, tools/bank_probe2.hip) = 18 issue slots per
-    # universe-gen; the exchange runs on the LDS pipe (ds_write_b128 x2,
-    # ds_read_b128 x4).  peak: one wave64 VALU op per 2 clk per SIMD at
-    # 2.4 GHz; the best rate measured for independent v_bitop3 is 0.978 ns
-    # per instruction per SIMD (profiles/r01/bank_probe.jsonl), reported too.
-    slots = 18
-    peak_slots = 1024 * 2.4e9 / 2  # 1024 SIMDs
-    measured_slots = 1024 / 0.978e-9
-    cfg = hip.default_cfg(gens).as_dict()
-    cpu = None
-    if cpu_seconds > 0:
-        cpu = cpu_baseline_config3(a.cpu().numpy().view(np.uint64), cpu_seconds)
-    return {"workload": "config3: 64K universes x 1024 generations (one launch)",
-            "value": gps, "unit": "universe-gen/s", "cell_updates_per_s": gps * 4096,
-            "kernel_ms": t * 1e3, "kernel_ms_min": min(ms), "kernel_ms_all": ms, "launch_cfg": cfg,
-            "roofline": {"bound": "valu", "achieved": gps * slots / 1e12, "peak": peak_slots / 1e12,
-                         "unit": f"T VALU issue slots/s ({slots} per universe-gen)",
-                         "frac": gps * slots / peak_slots,
-                         "measured_issue_peak": measured_slots / 1e12,
-                         "frac_of_measured_issue_peak": gps * slots / measured_slots},
-            "reference_op_equivalent_Tops": OPS_PER_UNIVERSE_GEN * gps / 1e12,
-            "cpu_baseline": cpu}
-
-
-def verify_first_launch(hip, out, first, n, gens, seed, stream, world, device):
-    """Digest of the first launch's output vs the reference's (golden.json)."""
-    gold = os.path.join(ROOT, "tests", "golden", "golden.json")
-    want = None
-    try:
-        with open(gold) as f:
-            d = json.load(f)["digests"]["weak_shards_seed2"]
-        k = first // n
-        if (gens == 1 and seed == d["seed"] and n == d["universes_per_rank"]
-                and k < len(d["shard_output_digests"])):
-            want = d["shard_output_digests"][k]
-    except (OSError, ValueError, KeyError):
-        pass
-    got = f"{batch_digest(hip.hashes(out, stream=stream).cpu().numpy(), first):016x}"
-    ok = None if want is None else got == want
-    if world > 1 and ok is not None:
-        f = torch.tensor([0 if ok else 1], device=COLL_DEV)
-        dist.all_reduce(f)
-        ok = int(f.item()) == 0
-    return {"ok": ok, "first_launch_digest_rank0": got, "expected": want,
-            "against": "tests/golden/golden.json weak_shards_seed2 (reference Step(), all ranks)"}
-
-
-def secondary_config5(hip, device, stream):
-    """Config 5: unknown_step_refined ternary step, 256K universes, one launch."""
-    n = 1 << 18
-    planes = hip.fill_random(n * 11, seed=6, device=device, stream=stream).reshape(n, 11 * 64)
-    out = torch.empty((n, 3 * 64), dtype=torch.int64, device=device)
-    hip.refined_step(planes, out=out, stream=stream)  # warm
-    ms = []
-    for _ in range(10):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        hip.refined_step(planes, out=out, stream=stream)
-        e1.record(stream)
-        e1.synchronize()
-        ms.append(e0.elapsed_time(e1))
-    t = sorted(ms)[len(ms) // 2] / 1e3
-    ups = n / t
-    return {"workload": "config5: 256K universes, unknown_step_refined (11 planes in, 3 out)",
-            "value": ups, "unit": "universe-steps/s", "kernel_ms_median": t * 1e3,
-            "roofline": {"bound": "hbm", "achieved": n * 7168 / t / 1e9, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": n * 7168 / t / 1e9 / HBM_PEAK_GBS,
-                         "algorithmic_bytes_per_universe": 7168}}
-
-
 def load_pmc_traffic(n: int):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, if it matches."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -255,116 +209,397 @@ def load_pmc_traffic(n: int):
     return None, None
 
 
-def main():
-    args = parse_args()
+# ----------------------------------------------------------------------------
+# CPU baseline (the reference's own Step(), oracle/_ref; else the C port)
+# ----------------------------------------------------------------------------
+def host_cores():
+    """Threads for the CPU baseline: every core in this process's affinity
+    set, limited by a cgroup CPU quota when one is set (more threads than the
+    quota would only be throttled).  Returns (threads, evidence)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            with open(path) as f:
+                q, per = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(per)
+        except (OSError, ValueError):
+            pass
+    if quota is None:
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                per = int(f.read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    threads = aff if quota is None else max(1, min(aff, int(quota)))
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
+    except OSError:
+        pass
+    return threads, {"affinity_cpus": aff, "cgroup_quota_cpus": quota, "os_cpu_count": os.cpu_count(),
+                     "cpu_model": model}
+
+
+def _cpu_stepper():
+    from oracle.oracle import Port, Ref
+    if Ref.available():
+        return Ref(), "reference"
+    return Port(), "port"
+
+
+def cpu_baseline(x_host: np.ndarray, seconds: float):
+    """The reference's Step() on the config-2 input (a bounded sample: at most
+    the first 1M universes), 1 thread and all host cores."""
+    o, kind = _cpu_stepper()
+    threads, ev = host_cores()
+    x = x_host[: 1 << 20]
+    n = x.shape[0]
+    out = {}
+    for t in sorted({1, threads}):
+        o.step_batch(x[: min(n, 4096)], 1, nthreads=t)  # warm
+        passes, t0 = 0, time.perf_counter()
+        while True:
+            o.step_batch(x, 1, nthreads=t)
+            passes += 1
+            el = time.perf_counter() - t0
+            if el >= seconds / 2:
+                break
+        out[t] = (n * passes / el, passes, el)
+    v, passes, el = out[threads]
+    return {
+        "value": v, "unit": "universe-gen/s", "cores": threads, "kind": kind,
+        "sample": f"config-2 input ({n} universes) x 1 gen, {passes} passes in {el:.2f}s, "
+                  f"{threads} threads (contiguous slices); CPU: {ev['cpu_model']}",
+        "value_1thread": out[1][0], "host": ev,
+    }
+
+
+def cpu_baseline_config3(x_host: np.ndarray, seconds: float):
+    """The reference's Step(1024) on a bounded sample of the config-3
+    universes, on all host cores (`seconds` of work)."""
+    o, kind = _cpu_stepper()
+    threads, ev = host_cores()
+    sample = x_host[: 64 * threads]
+    o.step_batch(sample[:threads], 1024, nthreads=threads)  # warm
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        o.step_batch(sample, 1024, nthreads=threads)
+        done += sample.shape[0]
+    el = time.perf_counter() - t0
+    return {"value": done * 1024 / el, "unit": "universe-gen/s", "cores": threads, "kind": kind,
+            "sample": f"{sample.shape[0]} of the config-3 universes x 1024 gens, {done // sample.shape[0]} "
+                      f"passes in {el:.2f}s, {threads} threads"}
+
+
+def cpu_baseline_config1():
+    """Config 1 (BASELINE.json configs[0]): R-pentomino x 1103 single-universe
+    Step() on the CPU, 1 thread -- the drop-in facade's Step()
+    (include/lifeapi/LifeState.hpp) next to the reference's own, same
+    compiler and flags, one binary (oracle/_ref/config1_bench, built from
+    tests/cpp/config1_bench.cpp)."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "config1_bench")
+    if not os.path.exists(exe):
+        return None
+    try:
+        r = subprocess.run([exe, "200", "5"], capture_output=True, text=True, timeout=120)
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        d["exit_status"] = r.returncode
+        return d
+    except (OSError, ValueError, IndexError, subprocess.TimeoutExpired) as e:
+        return {"error": str(e)}
+
+
+# ----------------------------------------------------------------------------
+# verification: first-launch digests vs the reference's (tests/golden/golden.json)
+# ----------------------------------------------------------------------------
+def expected_digests(cfg: int, seed: int, gens: int, world: int, n_rank: int, n_total: int, shards):
+    """(per-rank expected digests or None, expected global digest or None, source)."""
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "golden.json")) as f:
+            gold = json.load(f)["digests"]
+    except (OSError, ValueError, KeyError):
+        return [None] * world, None, None
+    for key in CONFIGS[cfg]["golden"]:
+        d = gold.get(key)
+        if not d or d.get("seed") != seed or d.get("generations") != gens:
+            continue
+        if cfg == 2 and d["universes_per_rank"] == n_rank:
+            ds = d["shard_output_digests"]
+            per = [ds[r] if r < len(ds) else None for r in range(world)]
+            glob = f"{combine(int(x, 16) for x in per):016x}" if None not in per else None
+            return per, glob, key
+        if cfg == 4 and d["universes"] == n_total:
+            chunk = d["universes"] // d["shards"]
+            chunks = [int(x, 16) for x in d["shard_output_digests"]]
+            per = []
+            for lo, cnt in shards:
+                hi = lo + cnt
+                per.append(f"{combine(chunks[lo // chunk: hi // chunk]):016x}"
+                           if lo % chunk == 0 and hi % chunk == 0 else None)
+            return per, d["output_digest"], key
+    return [None] * world, None, None
+
+
+def _i64(u: int) -> int:
+    return u - (1 << 64) if u >= 1 << 63 else u
+
+
+def all_gather_ints(vals, world):
+    """All-gather a short list of int64 bit patterns from every rank (rank order)."""
+    t = torch.tensor([_i64(v) for v in vals], dtype=torch.int64, device=COLL_DEV)
+    if world == 1:
+        return [[int(x) % (1 << 64) for x in t.tolist()]]
+    parts = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    return [[int(x) % (1 << 64) for x in p.tolist()] for p in parts]
+
+
+def verify_first_launch(hip, rt, out, first, cfg, seed, gens, world, n_rank, n_total, shards):
+    """Each rank digests its shard of the first launch's output; rank 0 gets
+    every shard's digest and checks each one, and their sum, against the
+    reference-generated digests (tests/golden/make_golden.py from oracle/_ref)."""
+    got = batch_digest(hip.hashes(out, stream=rt.stream).cpu().numpy(), first)
+    all_d = [v[0] for v in all_gather_ints([got], world)]
+    per, glob, src = expected_digests(cfg, seed, gens, world, n_rank, n_total, shards)
+    per_ok = [None if w is None else f"{g:016x}" == w for g, w in zip(all_d, per)]
+    total = f"{combine(all_d):016x}"
+    glob_ok = None if glob is None else total == glob
+    known = [x for x in per_ok + [glob_ok] if x is not None]
+    return {"ok": (all(known) if known else None), "per_rank_ok": per_ok, "global_ok": glob_ok,
+            "rank_digests": [f"{g:016x}" for g in all_d], "global_digest": total, "expected_global": glob,
+            "against": f"tests/golden/golden.json digests.{src} (reference Step() via oracle/_ref)"
+            if src else "no golden digest for this size/seed"}
+
+
+# ----------------------------------------------------------------------------
+# side measurements at N=1
+# ----------------------------------------------------------------------------
+def secondary_config3(hip, rt, cpu_seconds=0.0):
+    """Config 3: 64K universes x 1024 generations (state resident in VGPRs)."""
+    n, gens = 1 << 16, 1024
+    a = hip.fill_random(n, seed=3, device=rt.device, stream=rt.stream)
+    b = torch.empty_like(a)
+    for _ in range(20):  # warm: ~30 ms of back-to-back launches (clocks settle)
+        hip.step(a, out=b, generations=gens, stream=rt.stream)
+    med, ms = median_launch_ms(hip, rt, a, b, gens)
+    t = med / 1e3
+    gps = n * gens / t
+    digest = f"{batch_digest(hip.hashes(b, stream=rt.stream).cpu().numpy()):016x}"
+    cpu = None
+    if cpu_seconds > 0:
+        cpu = cpu_baseline_config3(a.cpu().numpy().view(np.uint64), cpu_seconds)
+    achieved = gps * C3_SLOTS_PER_UNIVERSE_GEN
+    return {"workload": "config3: 64K universes x 1024 generations (one launch)",
+            "value": gps, "unit": "universe-gen/s", "cell_updates_per_s": gps * 4096,
+            "kernel_ms": med, "kernel_ms_min": min(ms), "kernel_ms_all": ms,
+            "kernel": hip.step_kernel_name(gens),
+            "output_digest": digest, "output_digest_expected": "76acdc1ac3d9fbc7",
+            "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_SLOTS / 1e12,
+                         "unit": "T wave64-VALU slots/s", "frac": achieved / VALU_PEAK_SLOTS,
+                         "algorithmic_slots_per_universe_gen": C3_SLOTS_PER_UNIVERSE_GEN,
+                         "definition": "8 LUT3 per 32 cell-updates (2-LUT h-layer + 6-LUT tail) = 16 wave64 "
+                                       "VALU slots per universe-gen; peak 1024 SIMDs x 1 op / 2 clk x 2.4 GHz "
+                                       "(DESIGN.md 5.2)"},
+            "reference_op_equivalent_Tops": OPS_PER_UNIVERSE_GEN * gps / 1e12,
+            "cpu_baseline": cpu}
+
+
+def secondary_config4_1gpu(hip, rt, steps=10):
+    """Config 4's fixed 16M-universe problem on ONE GPU: the same-problem
+    denominator of the 8-vs-1 strong-scaling ratio."""
+    n = 1 << 24
+    a = hip.fill_random(n, seed=4, device=rt.device, stream=rt.stream)
+    b = torch.empty_like(a)
+    hip.step(a, out=b, generations=1, stream=rt.stream)
+    digest = f"{batch_digest(hip.hashes(b, stream=rt.stream).cpu().numpy()):016x}"
+    med, ms = median_launch_ms(hip, rt, a, b, 1, reps=steps)
+    gps = n / (med / 1e3)
+    achieved = n * BYTES_PER_UNIVERSE_GEN / (med / 1e3) / 1e9
+    del a, b
+    torch.cuda.empty_cache()
+    return {"workload": "config4 on 1 GPU: 16777216 universes x 1 generation per launch",
+            "value": gps, "unit": "universe-gen/s", "kernel_ms_median": med, "kernel_ms_all": ms,
+            "output_digest": digest, "output_digest_expected": "3f1b0a5bcd971521",
+            "verified": digest == "3f1b0a5bcd971521",
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS}}
+
+
+def secondary_config5(hip, rt):
+    """Config 5: unknown_step_refined ternary step, 256K universes, one launch."""
+    n = 1 << 18
+    planes = hip.fill_random(n * 11, seed=6, device=rt.device, stream=rt.stream).reshape(n, 11 * 64)
+    out = torch.empty((n, 3 * 64), dtype=torch.int64, device=rt.device)
+    hip.refined_step(planes, out=out, stream=rt.stream)  # warm
+    ms = []
+    for _ in range(10):
+        e0, e1 = rt.event(), rt.event()
+        e0.record(rt.stream)
+        hip.refined_step(planes, out=out, stream=rt.stream)
+        e1.record(rt.stream)
+        e1.synchronize()
+        ms.append(e0.elapsed_time(e1))
+    t = sorted(ms)[len(ms) // 2] / 1e3
+    ups = n / t
+    return {"workload": "config5: 256K universes, unknown_step_refined (11 planes in, 3 out)",
+            "value": ups, "unit": "universe-steps/s", "kernel_ms_median": t * 1e3,
+            "roofline": {"bound": "hbm", "achieved": n * 7168 / t / 1e9, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": n * 7168 / t / 1e9 / HBM_PEAK_GBS,
+                         "algorithmic_bytes_per_universe": 7168}}
+
+
+# ----------------------------------------------------------------------------
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus, argv))  # before any GPU call in this process
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # one process per GPU; the modulo only matters for a rehearsal with more
-    # ranks than GPUs (LIFEAPI_BENCH_BACKEND=gloo), never for the real run
-    ndev = torch.cuda.device_count()
-    device = torch.device("cuda", local % max(ndev, 1))
-    torch.cuda.set_device(device)
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; running {world} ranks")
     backend = os.environ.get("LIFEAPI_BENCH_BACKEND", "nccl")  # nccl == RCCL on ROCm
+    hip, rt = load_kernels(backend, local, world)
     global COLL_DEV
-    COLL_DEV = device if backend == "nccl" else torch.device("cpu")
+    COLL_DEV = rt.device if backend == "nccl" else torch.device("cpu")
     if world > 1:
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=device)
+            dist.init_process_group("nccl", device_id=rt.device)
         else:
             dist.init_process_group(backend)
-    import lifeapi_amd.hip as hip
+        coll_world = dist.get_world_size()
+    else:
+        coll_world = 1
 
-    n, gens = args.universes, args.gens_per_step
-    first, _ = weak_shard(rank, n)           # contiguous shard of the global array
-    stream = torch.cuda.current_stream(device)
-    a = hip.fill_random(n, seed=args.seed, first_universe=first, device=device, stream=stream)
+    cfg = (2 if world == 1 else 4) if args.config == "auto" else int(args.config)
+    spec = CONFIGS[cfg]
+    seed = spec["seed"] if args.seed < 0 else args.seed
+    gens = args.gens_per_step
+    if cfg == 2:
+        n_rank = args.universes or spec["universes"]
+        n_total = n_rank * world
+        shards = [weak_shard(r, n_rank) for r in range(world)]
+    else:
+        n_total = args.universes or spec["universes"]
+        shards = [strong_shard(r, world, n_total) for r in range(world)]
+        n_rank = shards[rank][1]
+    first, n = shards[rank]
+
+    a = hip.fill_random(n, seed=seed, first_universe=first, device=rt.device, stream=rt.stream)
     b = torch.empty_like(a)
     want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
-    x_full = a.cpu().numpy().view(np.uint64).copy() if want_cpu else None
+    x_cpu = a[: 1 << 20].cpu().numpy().view(np.uint64).copy() if want_cpu else None
     bufs = [a, b]
 
-    # warmup (untimed); the first launch's output is checked against the
-    # reference-generated digest of this shard (tests/golden/golden.json)
-    hip.step(bufs[0], out=bufs[1], generations=gens, stream=stream)
+    # warmup (untimed); the first launch's output is checked shard by shard
+    hip.step(bufs[0], out=bufs[1], generations=gens, stream=rt.stream)
     verified = None
     if not args.no_verify:
-        verified = verify_first_launch(hip, bufs[1], first, n, gens, args.seed, stream, world, device)
-    _, cur = timed_launches(hip, [bufs[1], bufs[0]], max(args.warmup - 1, 0), gens, stream)
+        verified = verify_first_launch(hip, rt, bufs[1], first, cfg, seed, gens, world, n_rank, n_total,
+                                       shards)
+    _, cur = timed_launches(hip, rt, [bufs[1], bufs[0]], max(args.warmup - 1, 0), gens)
     bufs = [bufs[1], bufs[0]] if cur == 0 else [bufs[0], bufs[1]]
-    torch.cuda.synchronize(device)
+    rt.sync()
 
     # timed region: barrier + sync on both sides, max over ranks
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(device)
+    rt.sync()
     t0 = time.perf_counter()
-    evs, cur = timed_launches(hip, bufs, args.steps, gens, stream)
-    torch.cuda.synchronize(device)
+    evs, cur = timed_launches(hip, rt, bufs, args.steps, gens)
+    rt.sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    span_ms = evs[0].elapsed_time(evs[1])   # GPU time of the K launches on their stream
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=COLL_DEV)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    span_ms = evs[0].elapsed_time(evs[1])   # GPU time of the K launches on their stream
+        per = torch.tensor([span_ms / args.steps, float(n)], dtype=torch.float64, device=COLL_DEV)
+        parts = [torch.empty_like(per) for _ in range(world)]
+        dist.all_gather(parts, per)
+        per_rank = [(float(p[0]), int(p[1])) for p in parts]
+    else:
+        per_rank = [(span_ms / args.steps, n)]
     final = bufs[cur]
 
     # result collection (not in the timed region): all-gather per-universe hashes
-    h = hip.hashes(final, stream=stream)
-    torch.cuda.synchronize(device)
+    h = hip.hashes(final, stream=rt.stream)
+    rt.sync()
     collect = None
     if world > 1:
         dist.barrier()
         c0 = time.perf_counter()
-        gathered = gather_hashes(h.to(COLL_DEV), world)
-        torch.cuda.synchronize(device)
+        gathered = gather_hashes(h.to(COLL_DEV), world, [c for _, c in shards])
+        rt.sync()
         cms = (time.perf_counter() - c0) * 1e3
-        collect = {"op": f"all_gather(per-universe hash, {'RCCL' if backend == 'nccl' else backend})",
-                   "bytes_per_rank": n * 8,
-                   "ms": cms}
+        collect = {"op": f"all_gather(per-universe 64-bit hash, {'RCCL' if backend == 'nccl' else backend})",
+                   "bytes_per_rank": n * 8, "ms": cms}
         if rank == 0:
             collect["final_digest"] = f"{batch_digest(gathered.cpu().numpy()):016x}"
+            collect["universes_gathered"] = int(gathered.numel())
 
     secondary = None
-    if rank == 0 and world == 1 and not args.no_secondary:
-        secondary = {"config3": secondary_config3(hip, device, stream,
-                                                  0.0 if args.no_cpu_baseline else args.cpu_seconds / 3),
-                     "config5": secondary_config5(hip, device, stream)}
+    if rank == 0 and world == 1 and not args.no_secondary and rt.kind == "hip":
+        csec = 0.0 if args.no_cpu_baseline else args.cpu_seconds / 3
+        secondary = {"config3": secondary_config3(hip, rt, csec),
+                     "config5": secondary_config5(hip, rt)}
+        if cfg == 2:
+            del a, b, bufs, final
+            torch.cuda.empty_cache()
+            secondary["config4"] = secondary_config4_1gpu(hip, rt)
 
     ceiling, ceiling_src = copy_ceiling()
-
     cpu = None
     if want_cpu:
-        cpu = cpu_baseline(x_full, args.cpu_seconds)
+        cpu = cpu_baseline(x_cpu, args.cpu_seconds)
+        cpu["config1"] = cpu_baseline_config1()
 
     if world > 1:
         dist.barrier()
     if rank == 0:
-        total = n * world * gens * args.steps
+        total = n_total * gens * args.steps
         value = total / elapsed
-        avg_launch = span_ms / args.steps  # includes the ~1-2 us launch gaps: conservative
-        achieved = n * gens * BYTES_PER_UNIVERSE_GEN / (avg_launch / 1e3) / 1e9 if gens == 1 else None
+        avg_launch = per_rank[0][0]  # includes the ~1-2 us launch gaps: conservative
+        bpl = n * gens * BYTES_PER_UNIVERSE_GEN
+        achieved = bpl / (avg_launch / 1e3) / 1e9 if gens == 1 else None
+        agg = sum(c * gens * BYTES_PER_UNIVERSE_GEN / (ms / 1e3) / 1e9 for ms, c in per_rank) if gens == 1 else None
         traffic, tsrc = load_pmc_traffic(n)
-        cfg = hip.default_cfg(gens).as_dict()
         line = {
             "metric": METRIC, "value": value, "unit": "universe-gen/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
-            "data": f"synthetic: splitmix64 uniform-fill universes (seed {args.seed}), generated on device",
-            "config": {"workload": f"config2: {n} random-fill 64x64 universes x {gens} generation "
-                                   f"per step per GPU", "universes_per_gpu": n,
-                       "global_universes": n * world, "gens_per_step": gens,
-                       "parallelism": f"dp{world} (contiguous universe shards, no collective)",
-                       "launch_cfg": cfg},
+            "higher_is_better": True, "scaling": spec["scaling"], "vs_baseline": None, "dtype": "u64",
+            "data": f"synthetic: splitmix64 uniform-fill universes (seed {seed}), generated on device",
+            "config": {"workload": (f"{spec['name']}: {n_rank} random-fill 64x64 universes x {gens} generation "
+                                    f"per step per GPU" if cfg == 2 else
+                                    f"{spec['name']}: {n_total} random-fill 64x64 universes x {gens} generation "
+                                    f"per step, split into {world} contiguous shards"),
+                       "universes_per_gpu": n_rank, "global_universes": n_total, "gens_per_step": gens,
+                       "parallelism": f"dp{world} (contiguous universe shards, no data-path collective)",
+                       "kernel": hip.step_kernel_name(gens)},
             "cell_updates_per_s": value * 4096,
             "kernel_ms_avg": avg_launch,
             "kernel_timing": "HIP events on the launch stream around the K timed launches / K",
+            "per_rank": [{"rank": r, "universes": c, "kernel_ms_avg": ms,
+                          "GBps": c * gens * BYTES_PER_UNIVERSE_GEN / (ms / 1e3) / 1e9 if gens == 1 else None}
+                         for r, (ms, c) in enumerate(per_rank)],
+            "collective_world_size": coll_world,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                          "traffic": traffic, "traffic_source": tsrc,
-                         "algorithmic_bytes_per_launch": n * gens * BYTES_PER_UNIVERSE_GEN,
+                         "algorithmic_bytes_per_launch": bpl,
+                         "aggregate_GBps": agg,
+                         "aggregate_frac": (agg / (world * HBM_PEAK_GBS)) if agg else None,
                          "read_only_GBps": achieved / 2 if achieved else None,
                          "copy_ceiling_GBps": ceiling, "copy_ceiling_source": ceiling_src,
                          "frac_of_copy_ceiling": (achieved / ceiling) if (achieved and ceiling) else None},
@@ -373,6 +608,8 @@ def main():
             "collect": collect,
             "secondary": secondary,
         }
+        if rt.kind != "hip":
+            line["kernel_backend"] = f"STUB {os.environ.get('LIFEAPI_BENCH_STUB')} (CPU rank rehearsal, not a measurement)"
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

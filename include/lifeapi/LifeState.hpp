@@ -107,25 +107,38 @@ struct alignas(64) LifeState {
   }
 
   // ---- stepping (LifeAPI.hpp:866-907,1196-1254), CPU, single universe
-  void CountRows(LifeState &bit0, LifeState &bit1) const {
+  void CountRows(LifeState &__restrict__ bit0, LifeState &__restrict__ bit1) const {
     for (int i = 0; i < N; ++i) {
       const uint64_t a = state[i], l = std::rotl(a, 1), r = std::rotr(a, 1);
       bit0.state[i] = l ^ r ^ a;
       bit1.state[i] = ((l ^ r) & a) | (l & r);
     }
   }
+  // Rokicki form of the B3/S23 rule (LifeAPI.hpp:837-848): the centre column
+  // plus the 2-bit vertical sums of the columns above (u) and below (b)
+  static uint64_t Rokicki(uint64_t a, uint64_t u0, uint64_t u1, uint64_t b0, uint64_t b1) {
+    const uint64_t aw = std::rotl(a, 1), ae = std::rotr(a, 1);
+    const uint64_t s0 = aw ^ ae, s1 = aw & ae;
+    const uint64_t ts0 = b0 ^ u0;
+    const uint64_t ts1 = (b0 & u0) | (ts0 & s0);
+    return (b1 ^ u1 ^ ts1 ^ s1) & ((b1 | u1) ^ (ts1 | s1)) & ((ts0 ^ s0) | a);
+  }
+  // Step() (LifeAPI.hpp:1196-1216).  The torus wrap is peeled out of the
+  // loop (columns 0 and 63), so the 62 interior columns are straight-line
+  // code the compiler unrolls and vectorises like the reference's
+  // `unroll(full)` loop.
   void Step() {
     LifeState c0(InitializedTag::UNINITIALIZED), c1(InitializedTag::UNINITIALIZED);
     CountRows(c0, c1);
-    for (int i = 0; i < N; ++i) {
-      const int u = (i + N - 1) & (N - 1), b = (i + 1) & (N - 1);
-      // Rokicki form (LifeAPI.hpp:837-848)
-      const uint64_t a = state[i], aw = std::rotl(a, 1), ae = std::rotr(a, 1);
-      const uint64_t s0 = aw ^ ae, s1 = aw & ae;
-      const uint64_t ts0 = c0[b] ^ c0[u];
-      const uint64_t ts1 = (c0[b] & c0[u]) | (ts0 & s0);
-      state[i] = (c1[b] ^ c1[u] ^ ts1 ^ s1) & ((c1[b] | c1[u]) ^ (ts1 | s1)) & ((ts0 ^ s0) | a);
-    }
+    state[0] = Rokicki(state[0], c0.state[N - 1], c1.state[N - 1], c0.state[1], c1.state[1]);
+#if defined(__clang__)
+#pragma clang loop unroll(full)
+#elif defined(__GNUC__)
+#pragma GCC unroll 64
+#endif
+    for (int i = 1; i < N - 1; ++i)
+      state[i] = Rokicki(state[i], c0.state[i - 1], c1.state[i - 1], c0.state[i + 1], c1.state[i + 1]);
+    state[N - 1] = Rokicki(state[N - 1], c0.state[N - 2], c1.state[N - 2], c0.state[0], c1.state[0]);
   }
   void StepAlt() {
     LifeState c0(InitializedTag::UNINITIALIZED), c1(InitializedTag::UNINITIALIZED);

@@ -46,79 +46,25 @@
 extern "C" {
 #endif
 
-#define LIFEAPI_ABI_VERSION 1
+#define LIFEAPI_ABI_VERSION 2
 
 #define LIFEAPI_OK 0
-#define LIFEAPI_E_INVALID (-1)   /* null/misaligned pointer, overlap, bad cfg */
+#define LIFEAPI_E_INVALID (-1)   /* null/misaligned pointer, overlap, bad argument */
 #define LIFEAPI_E_NODEVICE (-2)  /* no gfx950 device / bad device index */
 #define LIFEAPI_E_NOKERNEL (-3)  /* code object for this GPU missing */
-
-/* neighbour-column exchange used inside a wavefront */
-#define LIFEAPI_XCHG_DPP 0    /* DPP wave_ror:1 / wave_rol:1 (default) */
-#define LIFEAPI_XCHG_LDS 1    /* stage the column sums through LDS */
-#define LIFEAPI_XCHG_BPERM 2  /* ds_bpermute lane gather */
-#define LIFEAPI_XCHG_MIX 3    /* left neighbour by DPP, right by ds_bpermute
-                                 (moves half the exchange to the LDS pipe)  */
-#define LIFEAPI_XCHG_MIX1 4   /* 3 of 4 words by DPP, 1 by ds_bpermute      */
-#define LIFEAPI_XCHG_MIX3 5   /* 1 of 4 words by DPP, 3 by ds_bpermute      */
-#define LIFEAPI_XCHG_LDSR 6   /* left by DPP, right through LDS memory      */
-#define LIFEAPI_XCHG_LDSR3 7  /* 1 of 4 words by DPP, 3 through LDS memory  */
-#define LIFEAPI_XCHG_ASM 8    /* rules 4, 8 and 11: hand-allocated
-                                 generation loop (LDS exchange, VGPR banks
-                                 chosen per instruction; rules 8 and 11 are
-                                 generated by tools/gen_tile_asm.py and
-                                 tools/gen_split_asm.py)                    */
-#define LIFEAPI_XCHG_LDS_PIPE 9 /* rules 6, 11, 12: LDS exchange, software-
-                                 pipelined per plane of 4 registers         */
-#define LIFEAPI_XCHG_ASM_V(k) (24 + (k)) /* rule 11, upw 1: schedule k = 1..3
-                                 of the assembly loop (tools/gen_split_asm.py
-                                 VARIANTS; LIFEAPI_XCHG_ASM runs schedule 0) */
-#define LIFEAPI_XCHG_LDS_DPP(d) (16 + (d)) /* rules 11 (d = 1..4) and 12
-                                 (d = 2, 4): d of the S registers exchanged by
-                                 DPP wave_ror / wave_rol, the rest through LDS
-                                 (balances the VALU and LDS pipes)          */
-
-typedef struct lifeapi_launch_cfg {
-  int xchg;                /* LIFEAPI_XCHG_*                                */
-  int universes_per_wave;  /* 1, 2, 4 or 8 universes in flight per wave     */
-  int blocks_per_cu;       /* grid = min(needed, CUs * blocks_per_cu); 0=auto */
-  int nontemporal;         /* 1: nt loads/stores (streaming, 1 generation)  */
-  int rule;                /* 0: column-first adder network (bitop3),
-                              1: the same in plain and/or/xor,
-                              2: row-first adder network (bitop3, half the
-                                 DPP moves),
-                              3: row-first, 7-LUT network (one bitop3 fewer
-                                 per half),
-                              4: rule 3 on an even/odd row split of each
-                                 column (half the row rotates),
-                              5, 6, 7: rule 3 on a 4- / 8- / 16-way row
-                                 split with 2 / 4 / 8 universes interleaved
-                                 bit by bit in each register
-                                 (LIFEAPI_XCHG_LDS only; universes_per_wave
-                                 then counts such groups: 1 or 2),
-                              8, 9: rule 6 with 4 / 2 adjacent columns per
-                                 lane (16 / 8 universes per wave; only the
-                                 edge columns cross lanes; 8: LDS, DPP
-                                 row_ror or ASM, 9: LDS; universes_per_wave 1),
-                              10, 11, 12: rules 5, 6, 7 with the 6-LUT tail
-                                 (8 bitop3 per word instead of 9),
-                              13: rule 8 with the 6-LUT tail (LDS or DPP)   */
-} lifeapi_launch_cfg;
 
 int lifeapi_abi_version(void);
 const char *lifeapi_last_error(void);
 int lifeapi_device_count(void);
-/* fills the default launch configuration (what a NULL cfg means) */
-void lifeapi_default_cfg(lifeapi_launch_cfg *cfg, uint32_t generations);
+/* which shipped kernel configuration lifeapi_step_batch[_dev] runs for this
+ * many generations (a static string, for logs and benchmark records)       */
+const char *lifeapi_step_kernel_name(uint32_t generations);
 
 /* ---- device-resident, stream-ordered (the hot path) -------------------- */
 
 /* out[u] = in[u] stepped `generations` times (0 = copy), for u < n.       */
 int lifeapi_step_batch_dev(const uint64_t *d_in, uint64_t *d_out, size_t n,
                            uint32_t generations, void *stream);
-int lifeapi_step_batch_dev_cfg(const uint64_t *d_in, uint64_t *d_out, size_t n,
-                               uint32_t generations, void *stream,
-                               const lifeapi_launch_cfg *cfg);
 /* d_pop[u] = population of universe u                                     */
 int lifeapi_pop_batch_dev(const uint64_t *d_states, uint32_t *d_pop, size_t n, void *stream);
 /* d_hash[u] = build-defined 64-bit hash of universe u     */
@@ -172,11 +118,6 @@ int lifeapi_weld_step_batch_dev(uint64_t *d_welds, size_t n, uint32_t generation
  * option planes 1 = ruled out, LifeStable.hpp:41-53).  d_out: n x 3 planes
  * (next_on, next_unknown, next_unknown_stable).  No overlap allowed.      */
 int lifeapi_refined_step_batch_dev(const uint64_t *d_in, uint64_t *d_out, size_t n, void *stream);
-/* tuning form: cfg->universes_per_wave 1 = no prefetch / 2 = prefetch the
- * next universe; cfg->blocks_per_cu = grid cap (0 = one wave per universe);
- * cfg->rule = 0 or 4 (request >= 4 waves per SIMD from the allocator)     */
-int lifeapi_refined_step_batch_dev_cfg(const uint64_t *d_in, uint64_t *d_out, size_t n,
-                                       void *stream, const lifeapi_launch_cfg *cfg);
 /* synthetic universes: word w = u*64+x (u counted from first_universe) is
  * splitmix64(seed + (w+1)*0x9E3779B97F4A7C15); mode 1 maps each column to
  * [2^61, 2^62) like RandomState()                                         */

@@ -14,7 +14,6 @@
 #include <cstdint>
 
 #include "common.hpp"
-#include "lifeapi_hip.h"
 
 namespace lifeapi_impl {
 
@@ -58,17 +57,9 @@ __device__ __forceinline__ W lut3(W a, W b, W c) {
 // neighbour-column exchange (lane x <- lanes x-1 and x+1, mod 64)
 // ------------------------------------------------------------------------
 
-enum Xchg {
-  XDPP = LIFEAPI_XCHG_DPP,
-  XLDS = LIFEAPI_XCHG_LDS,
-  XBPERM = LIFEAPI_XCHG_BPERM,
-  XMIX = LIFEAPI_XCHG_MIX,
-  XMIX1 = LIFEAPI_XCHG_MIX1,
-  XMIX3 = LIFEAPI_XCHG_MIX3,
-  XLDSR = LIFEAPI_XCHG_LDSR,
-  XLDSR3 = LIFEAPI_XCHG_LDSR3,
-  XASM = LIFEAPI_XCHG_ASM
-};
+// (the numbering is the tuning build's LIFEAPI_XCHG_*, tools/tune/lifeapi_tune.h;
+// the shipped kernels use XDPP and, in the assembly loop, LDS)
+enum Xchg { XDPP = 0, XLDS = 1, XBPERM = 2, XMIX = 3, XMIX1 = 4, XMIX3 = 5, XLDSR = 6, XLDSR3 = 7, XASM = 8 };
 constexpr bool uses_lds(int x) { return x == XLDS || x == XLDSR || x == XLDSR3 || x == XASM; }
 
 // A full-wave rotate has no out-of-range source lane, so bound_ctrl (read 0

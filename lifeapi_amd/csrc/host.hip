@@ -115,21 +115,25 @@ struct PinRec {
 std::mutex g_pin_mu;
 std::vector<PinRec> g_pins;
 
-// Returns the start of the range referenced (to pass to pin_release), or 0
-// when the array is used as it is: too small, pinned by the caller, partly
-// overlapping another call's pin, or not pinnable.
-uintptr_t pin_acquire(const void *p, size_t bytes) {
-  if (!p || bytes < kPinMinBytes) return 0;
+// Adds to `keys` a reference on every range this library pinned that
+// overlaps [p, p + bytes) -- whatever the call's size, so no other call can
+// unpin memory this call's copies may DMA from, even where the ranges only
+// partly overlap.  With no overlap, a call of at least kPinMinBytes pins the
+// array itself (and references that); smaller calls, arrays the caller
+// pinned and unpinnable memory are used as they are.  Each key goes back
+// through pin_release.
+void pin_acquire(const void *p, size_t bytes, std::vector<uintptr_t> &keys) {
+  if (!p || !bytes) return;
   const uintptr_t lo = (uintptr_t)p, hi = lo + bytes;
   std::lock_guard<std::mutex> lk(g_pin_mu);
+  bool overlap = false;
   for (PinRec &r : g_pins)
     if (lo < r.hi && r.lo < hi) {
-      if (r.lo <= lo && hi <= r.hi) {
-        ++r.refs;
-        return r.lo;
-      }
-      return 0;
+      ++r.refs;
+      keys.push_back(r.lo);
+      overlap = true;
     }
+  if (overlap || bytes < kPinMinBytes) return;
   // Leave ranges the caller pinned alone: the runtime accepts a second
   // registration without counting it, so our unregister would undo theirs
   // (tools/pin_probe.cpp; hipHostGetFlags fails on registered memory, the
@@ -138,14 +142,14 @@ uintptr_t pin_acquire(const void *p, size_t bytes) {
     hipPointerAttribute_t a{};
     const hipError_t e = hipPointerGetAttributes(&a, (const void *)q);
     (void)hipGetLastError();
-    if (e != hipSuccess || a.type != hipMemoryTypeUnregistered) return 0;
+    if (e != hipSuccess || a.type != hipMemoryTypeUnregistered) return;
   }
   if (hipHostRegister((void *)lo, bytes, hipHostRegisterPortable) != hipSuccess) {
     (void)hipGetLastError();
-    return 0;
+    return;
   }
   g_pins.push_back({lo, hi, 1});
-  return lo;
+  keys.push_back(lo);
 }
 
 void pin_release(uintptr_t key) {
@@ -164,9 +168,7 @@ void pin_release(uintptr_t key) {
 // Holds pin_acquire references for one call.
 struct CallPins {
   std::vector<uintptr_t> keys;
-  void add(const void *p, size_t bytes) {
-    if (const uintptr_t k = pin_acquire(p, bytes)) keys.push_back(k);
-  }
+  void add(const void *p, size_t bytes) { pin_acquire(p, bytes, keys); }
   ~CallPins() {
     for (uintptr_t k : keys) pin_release(k);
   }
@@ -376,7 +378,7 @@ int lifeapi_weld_step_batch(uint64_t *welds, size_t n, uint32_t generations, int
 int lifeapi_stable_pass_batch(uint64_t *planes, uint8_t *flags, size_t n, int pass,
                               uint32_t max_iters, int device) {
   if (n == 0) return LIFEAPI_OK;
-  if (!planes || !flags || !aligned8(planes) || pass < 0 || pass > 4)
+  if (!planes || !flags || !aligned8(planes) || pass < 0 || pass > 5)
     return fail(LIFEAPI_E_INVALID, "bad argument to lifeapi_stable_pass_batch%s");
   const int dev = host_device(device);
   if (dev < 0) return dev;

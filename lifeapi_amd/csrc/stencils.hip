@@ -556,39 +556,20 @@ int lifeapi_interaction_counts_batch_dev(const uint64_t *d_in, uint64_t *d_out, 
   return counts_launch(d_in, d_out, n, with_next ? 2 : 1, stream);
 }
 
-int lifeapi_refined_step_batch_dev_cfg(const uint64_t *d_in, uint64_t *d_out, size_t n,
-                                       void *stream, const lifeapi_launch_cfg *cfg) {
+int lifeapi_refined_step_batch_dev(const uint64_t *d_in, uint64_t *d_out, size_t n, void *stream) {
   if (n == 0) return LIFEAPI_OK;
   if (!d_in || !d_out || !aligned8(d_in) || !aligned8(d_out))
     return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_refined_step_batch_dev%s");
   const uintptr_t a = (uintptr_t)d_in, b = (uintptr_t)d_out;
   if (a < b + n * 3 * 512 && b < a + n * 11 * 512)
     return fail(LIFEAPI_E_INVALID, "refined step input and output overlap%s");
-  // cfg: universes_per_wave 1 = no prefetch, 2 = prefetch next universe;
-  // blocks_per_cu = grid cap; rule = minimum waves per SIMD requested from the
-  // register allocator (0 = none, 4, 6).  Default = the measured best
-  // with the 192-op SOP network (profiles/r01/tune_c5.jsonl): prefetch the
-  // next universe, one-shot grid, no occupancy bound -> 6.3 TB/s.
-  int pf = 1, bpc = 0, occ = 0;
-  if (cfg) {
-    pf = cfg->universes_per_wave >= 2 ? 1 : 0;
-    bpc = cfg->blocks_per_cu;
-    occ = cfg->rule;
-    if (occ != 0 && occ != 4 && occ != 6)
-      return fail(LIFEAPI_E_INVALID, "unsupported refined cfg%s");
-  }
+  // the measured best with the 192-op SOP network (profiles/r01/tune_c5.jsonl):
+  // prefetch the next universe, one-shot grid, no occupancy bound -> 6.3 TB/s
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
-  using Fn = void (*)(const uint64_t *, uint64_t *, uint64_t);
-  Fn fn = pf ? (occ == 4 ? (Fn)k_refined<1, 4> : occ == 6 ? (Fn)k_refined<1, 6> : (Fn)k_refined<1, 0>)
-             : (occ == 4 ? (Fn)k_refined<0, 4> : occ == 6 ? (Fn)k_refined<0, 6> : (Fn)k_refined<0, 0>);
-  hipLaunchKernelGGL(fn, dim3(grid_for(n, cus, bpc)), dim3(kBlock), 0, (hipStream_t)stream, d_in,
+  hipLaunchKernelGGL((k_refined<1, 0>), dim3(grid_for(n, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream, d_in,
                      d_out, (uint64_t)n);
   return launched("k_refined launch");
-}
-
-int lifeapi_refined_step_batch_dev(const uint64_t *d_in, uint64_t *d_out, size_t n, void *stream) {
-  return lifeapi_refined_step_batch_dev_cfg(d_in, d_out, n, stream, nullptr);
 }
 
 }  // extern "C"

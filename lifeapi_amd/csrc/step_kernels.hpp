@@ -1,0 +1,204 @@
+// step_kernels.hpp -- the generation networks and the two step kernels of
+// batched LifeState::Step() (LifeAPI.hpp:1196-1216, Stepped(n) :877-886):
+// k_step (natural layout, one column per lane) and k_step_split (8-way row
+// split, state resident in VGPRs across generations).  step.hip instantiates
+// the shipped configurations; the tuning build (tools/tune/tune_step.hip)
+// instantiates the measured alternatives.
+#pragma once
+
+#include "host.hpp"
+#include "split_layout.hpp"
+#include "split_asm.inc"
+
+namespace lifeapi_impl {
+// internal linkage: every library that includes this header gets its own
+// kernels (the product and the tuning build never share instantiations)
+namespace {
+
+template <int X, int RULE>
+__device__ __forceinline__ W life_gen(W a, uint64_t *slot, int lane) {
+  if constexpr (RULE == 4) {
+    // the RULE 3 network on the (E, O) layout: 18 v_bitop3 + 4 v_alignbit
+    // per generation plus the exchange
+    W L, R;
+    neighbour_cols<X>(a, L, R, slot, lane);
+    const W h0 = lut3<kXor3>(L, a, R), h1 = lut3<kMaj>(L, a, R);
+    const uint32_t h0u = rotl1(h0.hi), h0d = rotr1(h0.lo);  // rows 2k-1 (for E), 2k+2 (for O)
+    const uint32_t h1u = rotl1(h1.hi), h1d = rotr1(h1.lo);
+    const W s0{lut3<kLe1>(h0u, h0.lo, h0.hi), lut3<kLe1>(h0.lo, h0.hi, h0d)};
+    const W s1{lut3<kNae>(h0u, h0.lo, h0.hi), lut3<kNae>(h0.lo, h0.hi, h0d)};
+    const W s2{lut3<kLe1>(h1u, h1.lo, h1.hi), lut3<kLe1>(h1.lo, h1.hi, h1d)};
+    const W s3{lut3<kEven>(h1u, h1.lo, h1.hi), lut3<kEven>(h1.lo, h1.hi, h1d)};
+    const W t1 = lut3<kT1>(s0, s1, a);
+    const W t2 = lut3<kT2>(s2, a, t1);
+    return lut3<kT3>(s1, s3, t2);
+  }
+  if constexpr (RULE == 3) {
+    // row-first exchange and rotations as RULE 2, then the 7-LUT network:
+    // 26 VALU per generation plus the exchange
+    W L, R;
+    neighbour_cols<X>(a, L, R, slot, lane);
+    const W h0 = lut3<kXor3>(L, a, R), h1 = lut3<kMaj>(L, a, R);
+    const W h0u = rot_up(h0), h0d = rot_dn(h0), h1u = rot_up(h1), h1d = rot_dn(h1);
+    const W s0 = lut3<kLe1>(h0u, h0, h0d), s1 = lut3<kNae>(h0u, h0, h0d);
+    const W s2 = lut3<kLe1>(h1u, h1, h1d), s3 = lut3<kEven>(h1u, h1, h1d);
+    const W t1 = lut3<kT1>(s0, s1, a);
+    const W t2 = lut3<kT2>(s2, a, t1);
+    return lut3<kT3>(s1, s3, t2);
+  }
+  if constexpr (RULE == 2) {
+    // Row-first form of the same adder network.  A DPP move issues at half
+    // the VALU rate on gfx950 (tools/valu_probe.hip: 8 DPP of 32 instructions
+    // cost 25 % of the loop), so exchange the raw column (4 DPP) instead of
+    // its two vertical-sum planes (8 DPP):
+    //   horizontal 3-sums  H0 = xor3(L,a,R), H1 = maj(L,a,R)   (2-bit, 0..3)
+    //   vertical    FullAdd(H0 up, H0, H0 down) -> fs, fc
+    //               FullAdd(H1 up, H1, H1 down) -> cs, cc
+    // and the 3x3 count is again fs + 2(fc + cs) + 4cc, so the rule tail is
+    // StepAlt's (LifeAPI.hpp:1251-1252).  Addition is commutative, so this is
+    // bit-identical to CountRows-then-columns (LifeAPI.hpp:897-907,1218-1254).
+    W L, R;
+    neighbour_cols<X>(a, L, R, slot, lane);
+    const W h0 = lut3<kXor3>(L, a, R), h1 = lut3<kMaj>(L, a, R);
+    const W h0u = rot_up(h0), h0d = rot_dn(h0), h1u = rot_up(h1), h1d = rot_dn(h1);
+    const W fs = lut3<kXor3>(h0u, h0, h0d), fc = lut3<kMaj>(h0u, h0, h0d);
+    const W cs = lut3<kXor3>(h1u, h1, h1d), cc = lut3<kMaj>(h1u, h1, h1d);
+    const W b2 = lut3<kCarry2>(cc, fc, cs);
+    const W p = lut3<kLive>(fs, b2, a);
+    const W q = lut3<kXor3>(fc, cs, b2);
+    return W{p.lo & q.lo, p.hi & q.hi};
+  }
+  const W up = rot_up(a), dn = rot_dn(a);
+  if constexpr (RULE == 0) {
+    // CountRows (LifeAPI.hpp:897-907): vertical 3-sum as two planes
+    const W c0 = lut3<kXor3>(up, dn, a);
+    const W c1 = lut3<kMaj>(up, dn, a);
+    W L0, R0, L1, R1;
+    neighbours<X>(c0, c1, L0, R0, L1, R1, slot, lane);
+    // FullAdd x2 (LifeAPI.hpp:826-833, StepAlt :1246-1249): 3x3 inclusive
+    // count = fs + 2(fc + cs) + 4cc
+    const W fs = lut3<kXor3>(L0, c0, R0), fc = lut3<kMaj>(L0, c0, R0);
+    const W cs = lut3<kXor3>(L1, c1, R1), cc = lut3<kMaj>(L1, c1, R1);
+    // StepAlt :1251-1252: cc ^= fc & cs;  next = (fs^cc) & (fc^cs^cc) & (a|fs)
+    const W b2 = lut3<kCarry2>(cc, fc, cs);
+    const W p = lut3<kLive>(fs, b2, a);
+    const W q = lut3<kXor3>(fc, cs, b2);
+    return W{p.lo & q.lo, p.hi & q.hi};
+  } else {
+    // the same network in plain and/or/xor (the compiler folds the DPP moves
+    // into v_*_dpp consumers); kept as an ablation of the bitop3 form
+    const uint64_t av = join(a), u = join(up), d = join(dn);
+    const uint64_t c0v = u ^ d ^ av, c1v = (u & d) | ((u ^ d) & av);
+    W L0, R0, L1, R1;
+    neighbours<X>(split(c0v), split(c1v), L0, R0, L1, R1, slot, lane);
+    const uint64_t l0 = join(L0), r0 = join(R0), l1 = join(L1), r1 = join(R1);
+    const uint64_t h0 = l0 ^ c0v, h1 = l1 ^ c1v;
+    const uint64_t fs = h0 ^ r0, fc = (l0 & c0v) | (r0 & h0);
+    const uint64_t cs = h1 ^ r1;
+    uint64_t cc = (l1 & c1v) | (r1 & h1);
+    cc ^= fc & cs;
+    return split((fs ^ cc) & (fc ^ cs ^ cc) & (av | fs));
+  }
+}
+
+// out[u] = in[u] stepped `gens` times.  Wave w of the grid takes groups of U
+// consecutive universes, grid-strided.  All branches are wave-uniform.
+// in == out is allowed (Step() in place), so neither pointer is
+// __restrict__: each wave loads its universes before it stores them and no
+// wave touches another's (the same holds for k_step_split).
+template <int X, int U, bool NT, int RULE>
+__global__ __launch_bounds__(kBlock) void k_step(const uint64_t *in, uint64_t *out, uint64_t n,
+                                                 uint32_t gens) {
+  __shared__ uint64_t lds[uses_lds(X) ? kWavesPerBlock * U * 2 * kWave : 1];
+  const int lane = threadIdx.x & (kWave - 1);
+  // wave index in the block, made provably wave-uniform so that the tail
+  // tests below are scalar branches
+  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock * U;
+  for (uint64_t u0 = ((uint64_t)blockIdx.x * kWavesPerBlock + wib) * U; u0 < n; u0 += stride) {
+    W a[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k)
+      a[k] = (u0 + k < n) ? ld<NT>(in + (u0 + k) * kWave + lane) : W{0u, 0u};
+    if constexpr (RULE == 4) {
+#pragma unroll
+      for (int k = 0; k < U; ++k) a[k] = to_eo(a[k]);
+    }
+    for (uint32_t g = 0; g < gens; ++g) {
+#pragma unroll
+      for (int k = 0; k < U; ++k)
+        a[k] = life_gen<X, RULE>(a[k], lds + (wib * U + k) * 2 * kWave, lane);
+    }
+    if constexpr (RULE == 4) {
+#pragma unroll
+      for (int k = 0; k < U; ++k) a[k] = from_eo(a[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k)
+      if (u0 + k < n) st<NT>(out + (u0 + k) * kWave + lane, a[k]);
+  }
+}
+
+// k_step for the split layouts: wave w takes G groups of P = S/2
+// consecutive universes, grid-strided; all branches wave-uniform.  NET: the
+// tail network (7 = RULE 3's, 6 = life_tail6); D: registers exchanged by DPP
+// instead of LDS (gen_split), or kPipe: the software-pipelined LDS loop
+// (gens_split_pipe).
+constexpr int kPipe = -1;
+constexpr int kAsmLoop = -3;  // the hand-allocated rule-11 loop (split_asm.inc)
+template <int S, int G, bool NT, int NET, int D = 0, int V = 0>
+__global__ __launch_bounds__(kBlock) void k_step_split(const uint64_t *in, uint64_t *out, uint64_t n,
+                                                       uint32_t gens) {
+  constexpr int P = S / 2;
+  __shared__ uint32_t lds[kWavesPerBlock * G * S * kWave];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint64_t per_wave = (uint64_t)G * P;
+  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock * per_wave;
+  for (uint64_t u0 = ((uint64_t)blockIdx.x * kWavesPerBlock + wib) * per_wave; u0 < n; u0 += stride) {
+    uint32_t r[G][S];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      W c[P];
+#pragma unroll
+      for (int u = 0; u < P; ++u) {
+        const uint64_t x = u0 + g * P + u;
+        c[u] = x < n ? ld<NT>(in + x * kWave + lane) : W{0u, 0u};
+      }
+      Split<S>::load(c, r[g]);
+    }
+    if constexpr (D == kPipe) {
+#pragma unroll
+      for (int g = 0; g < G; ++g) gens_split_pipe<S, NET>(r[g], lds + (wib * G + g) * S * kWave, lane, gens);
+    } else if constexpr (D == kAsmLoop) {
+      static_assert(S == 8 && NET == 6 && G <= 2, "split_asm.inc is rule 11, one or two groups");
+      const uint32_t base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)(
+          lds + wib * G * S * kWave);  // group g's planes at base + 2 KiB * g
+      const uint32_t self = base + lane * 16u, prev = base + ((lane + kWave - 1) & (kWave - 1)) * 16u,
+                     next = base + ((lane + 1) & (kWave - 1)) * 16u;
+      if constexpr (G == 2) split_gens_asm2(r[0], r[1], gens, self, prev, next);
+      else if constexpr (V == 1) split_gens_asm_v1(r[0], gens, self, prev, next);
+      else if constexpr (V == 2) split_gens_asm_v2(r[0], gens, self, prev, next);
+      else if constexpr (V == 3) split_gens_asm_v3(r[0], gens, self, prev, next);
+      else split_gens_asm_v0(r[0], gens, self, prev, next);
+    } else {
+      for (uint32_t it = 0; it < gens; ++it) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) gen_split<S, NET, D>(r[g], lds + (wib * G + g) * S * kWave, lane);
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      W c[P];
+      Split<S>::store(r[g], c);
+#pragma unroll
+      for (int u = 0; u < P; ++u) {
+        const uint64_t x = u0 + g * P + u;
+        if (x < n) st<NT>(out + x * kWave + lane, c[u]);
+      }
+    }
+  }
+}
+
+}  // namespace
+}  // namespace lifeapi_impl

@@ -27,20 +27,6 @@ if not os.path.exists(LIB_PATH):
         "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950)")
 lib = ctypes.CDLL(LIB_PATH)
 
-XCHG_DPP, XCHG_LDS, XCHG_BPERM, XCHG_MIX, XCHG_MIX1, XCHG_MIX3, XCHG_LDSR, XCHG_LDSR3, XCHG_ASM = range(9)
-
-
-class LaunchCfg(ctypes.Structure):
-    """lifeapi_launch_cfg (include/lifeapi_hip.h)."""
-
-    _fields_ = [("xchg", ctypes.c_int), ("universes_per_wave", ctypes.c_int),
-                ("blocks_per_cu", ctypes.c_int), ("nontemporal", ctypes.c_int),
-                ("rule", ctypes.c_int)]
-
-    def as_dict(self) -> dict:
-        return {k: getattr(self, k) for k, _ in self._fields_}
-
-
 class LifeApiError(RuntimeError):
     def __init__(self, code: int, msg: str):
         super().__init__(f"lifeapi error {code}: {msg}")
@@ -52,9 +38,8 @@ _SIGS = {
     "lifeapi_abi_version": ([], _int),
     "lifeapi_last_error": ([], ctypes.c_char_p),
     "lifeapi_device_count": ([], _int),
-    "lifeapi_default_cfg": ([ctypes.POINTER(LaunchCfg), _u32], None),
+    "lifeapi_step_kernel_name": ([_u32], ctypes.c_char_p),
     "lifeapi_step_batch_dev": ([_vp, _vp, _sz, _u32, _vp], _int),
-    "lifeapi_step_batch_dev_cfg": ([_vp, _vp, _sz, _u32, _vp, ctypes.POINTER(LaunchCfg)], _int),
     "lifeapi_pop_batch_dev": ([_vp, _vp, _sz, _vp], _int),
     "lifeapi_hash_batch_dev": ([_vp, _vp, _sz, _vp], _int),
     "lifeapi_contains_batch_dev": ([_vp, _vp, _vp, _vp, _sz, _vp], _int),
@@ -65,7 +50,6 @@ _SIGS = {
     "lifeapi_neighbour_count_batch_dev": ([_vp, _vp, _sz, _vp], _int),
     "lifeapi_interaction_counts_batch_dev": ([_vp, _vp, _sz, _int, _vp], _int),
     "lifeapi_refined_step_batch_dev": ([_vp, _vp, _sz, _vp], _int),
-    "lifeapi_refined_step_batch_dev_cfg": ([_vp, _vp, _sz, _vp, ctypes.POINTER(LaunchCfg)], _int),
     "lifeapi_step_batch": ([_vp, _vp, _sz, _u32, _int], _int),
     "lifeapi_host_register": ([_vp, _sz], _int),
     "lifeapi_step_contains_batch": ([_vp, _vp, _vp, _vp, _vp, _sz, _u32, _int], _int),
@@ -106,10 +90,9 @@ def device_count() -> int:
     return lib.lifeapi_device_count()
 
 
-def default_cfg(generations: int = 1) -> LaunchCfg:
-    c = LaunchCfg()
-    lib.lifeapi_default_cfg(ctypes.byref(c), generations)
-    return c
+def step_kernel_name(generations: int = 1) -> str:
+    """The shipped kernel configuration a step of `generations` runs."""
+    return lib.lifeapi_step_kernel_name(generations).decode()
 
 
 def _stream(stream) -> int:
@@ -131,19 +114,14 @@ def empty_universes(n: int, device=None) -> torch.Tensor:
 
 
 def step(states: torch.Tensor, out: torch.Tensor | None = None, generations: int = 1,
-         cfg: LaunchCfg | None = None, stream=None) -> torch.Tensor:
+         stream=None) -> torch.Tensor:
     """Batched ``Stepped(generations)`` (LifeAPI.hpp:882-886); ``out`` may be ``states``."""
     n = _universes(states)
     if out is None:
         out = torch.empty_like(states)
     if _universes(out, "out") != n:
         raise ValueError("out has a different number of universes")
-    s = _stream(stream)
-    if cfg is None:
-        _check(lib.lifeapi_step_batch_dev(states.data_ptr(), out.data_ptr(), n, generations, s))
-    else:
-        _check(lib.lifeapi_step_batch_dev_cfg(states.data_ptr(), out.data_ptr(), n, generations, s,
-                                              ctypes.byref(cfg)))
+    _check(lib.lifeapi_step_batch_dev(states.data_ptr(), out.data_ptr(), n, generations, _stream(stream)))
     return out
 
 

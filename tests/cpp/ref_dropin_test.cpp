@@ -151,7 +151,7 @@ static void LifeWeld_Step() {
 
 // LifeStable::Propagate() (LifeStable.hpp:718-729) on partially unknown still
 // lifes: every plane and the PropagateResult
-static void LifeStable_Propagate() {
+static std::vector<LifeStable> partly_unknown_still_lifes() {
   std::vector<LifeStable> s;
   const LifeState block = LifeState::Parse("2o$2o!");
   for (int k = 0; k < 200; ++k) {
@@ -163,6 +163,11 @@ static void LifeStable_Propagate() {
     c.unknown = unk;
     s.push_back(c);
   }
+  return s;
+}
+
+static void LifeStable_Propagate() {
+  std::vector<LifeStable> s = partly_unknown_still_lifes();
   std::vector<LifeStable> cpu = s;
   std::vector<LifeStable::PropagateResult> want;
   for (auto &x : cpu) want.push_back(x.Propagate());
@@ -171,6 +176,26 @@ static void LifeStable_Propagate() {
     EXPECT_TRUE(got[i].consistent == want[i].consistent && got[i].changed == want[i].changed);
     EXPECT_TRUE(s[i] == cpu[i]);  // every plane (LifeStable::operator==, LifeStable.hpp:55)
   }
+}
+
+// LifeStable::StabiliseOptions() (LifeStable.hpp:677-693) through the
+// host-pointer form (lifeapi_stable_pass_batch, pass 5), after one
+// SynchroniseStateKnown so the counts are in sync as the reference assumes
+// (LifeStable.hpp:133-134): every plane and the PropagateResult
+static void LifeStable_StabiliseOptions() {
+  std::vector<LifeStable> s = partly_unknown_still_lifes();
+  for (auto &x : s) x.SynchroniseStateKnown();
+  std::vector<LifeStable> cpu = s;
+  std::vector<LifeStable::PropagateResult> want;
+  for (auto &x : cpu) want.push_back(x.StabiliseOptions());
+  const std::vector<lifeapi::PropagateResult> got = lifeapi::StabiliseOptionsBatch(std::span(s));
+  int changed = 0;
+  for (size_t i = 0; i < s.size(); ++i) {
+    EXPECT_TRUE(got[i].consistent == want[i].consistent && got[i].changed == want[i].changed);
+    EXPECT_TRUE(s[i] == cpu[i]);
+    changed += want[i].changed;
+  }
+  EXPECT_TRUE(changed > 0);  // the case exercises the pass, not just a no-op
 }
 
 // LifeState::Parse / RLE() (Parsing.hpp:143-204), batched
@@ -194,6 +219,7 @@ int main() {
   NeighbourCount_Planes();
   LifeWeld_Step();
   LifeStable_Propagate();
+  LifeStable_StabiliseOptions();
   Rle_RoundTrip();
   std::printf("%d checks, %d failures\n", g_checks, g_failures);
   return g_failures == 0 ? 0 : 1;

@@ -167,6 +167,58 @@ def edge_cases():
     return names, np.stack(out)
 
 
+def batch_digests() -> dict:
+    """6. batch digests (checksum of checksums over reference outputs) for
+    the bench workloads and the shard layouts bench.py checks per rank."""
+    dig = {}
+    for name, n, seed, g in (("config2", 1 << 20, 2, 1), ("config3", 1 << 16, 3, 1024)):
+        xin = P.fill(n, seed=seed)
+        out = R.step_batch(xin, g, nthreads=8)
+        dig[name] = {"universes": n, "seed": seed, "generations": g,
+                     "input_digest": f"{P.digest(P.hashes(xin)):016x}",
+                     "output_digest": f"{P.digest(P.hashes(out)):016x}",
+                     "output_pop_total": int(P.pop(out).astype(np.uint64).sum())}
+    # config 4: 16M universes, 8 shards of 2M; additive digests per shard
+    shard, total, totin = [], 0, 0
+    for k in range(8):
+        xin = P.fill(1 << 21, seed=4, first_universe=k << 21)
+        out = R.step_batch(xin, 1, nthreads=8)
+        di = P.digest(P.hashes(xin), k << 21)
+        do = P.digest(P.hashes(out), k << 21)
+        shard.append(f"{do:016x}")
+        total = (total + do) % 2**64
+        totin = (totin + di) % 2**64
+    dig["config4"] = {"universes": 1 << 24, "seed": 4, "generations": 1, "shards": 8,
+                      "input_digest": f"{totin:016x}", "output_digest": f"{total:016x}",
+                      "shard_output_digests": shard}
+    # bench.py weak scaling: rank r owns [r*2^20, (r+1)*2^20) of the seed-2 array;
+    # Step^1 output digest of each rank's shard (rank 0 == config 2)
+    weak = []
+    for k in range(8):
+        xin = P.fill(1 << 20, seed=2, first_universe=k << 20)
+        weak.append(f"{P.digest(P.hashes(R.step_batch(xin, 1, nthreads=8)), k << 20):016x}")
+    dig["weak_shards_seed2"] = {"universes_per_rank": 1 << 20, "seed": 2, "generations": 1,
+                                "shard_output_digests": weak}
+    # the same shard layouts at test sizes (tests/test_bench_ranks.py runs
+    # bench.py's rank path on them): config 4 as 16K universes in 8 chunks of
+    # 2K, config 2's weak shards as 2K universes per rank
+    shard, total = [], 0
+    for k in range(8):
+        xin = P.fill(1 << 11, seed=4, first_universe=k << 11)
+        do = P.digest(P.hashes(R.step_batch(xin, 1)), k << 11)
+        shard.append(f"{do:016x}")
+        total = (total + do) % 2**64
+    dig["config4_small"] = {"universes": 1 << 14, "seed": 4, "generations": 1, "shards": 8,
+                            "output_digest": f"{total:016x}", "shard_output_digests": shard}
+    weak = []
+    for k in range(8):
+        xin = P.fill(1 << 11, seed=2, first_universe=k << 11)
+        weak.append(f"{P.digest(P.hashes(R.step_batch(xin, 1)), k << 11):016x}")
+    dig["weak_shards_seed2_small"] = {"universes_per_rank": 1 << 11, "seed": 2, "generations": 1,
+                                      "shard_output_digests": weak}
+    return dig
+
+
 def main():
     meta = {"generator": "tests/golden/make_golden.py", "reference_lib": os.path.basename(R.path),
             "reference": "scorbiclife/LifeAPI snapshot 2025-02-22 (/root/reference)"}
@@ -279,37 +331,7 @@ def main():
                                                   "live2", "live3", "dead0", "dead1", "dead2",
                                                   "dead4", "dead5", "dead6"]}
 
-    # 6. full-size batch digests (checksum of checksums over reference outputs)
-    dig = {}
-    for name, n, seed, g in (("config2", 1 << 20, 2, 1), ("config3", 1 << 16, 3, 1024)):
-        xin = P.fill(n, seed=seed)
-        out = R.step_batch(xin, g, nthreads=8)
-        dig[name] = {"universes": n, "seed": seed, "generations": g,
-                     "input_digest": f"{P.digest(P.hashes(xin)):016x}",
-                     "output_digest": f"{P.digest(P.hashes(out)):016x}",
-                     "output_pop_total": int(P.pop(out).astype(np.uint64).sum())}
-    # config 4: 16M universes, 8 shards of 2M; additive digests per shard
-    shard, total, totin = [], 0, 0
-    for k in range(8):
-        xin = P.fill(1 << 21, seed=4, first_universe=k << 21)
-        out = R.step_batch(xin, 1, nthreads=8)
-        di = P.digest(P.hashes(xin), k << 21)
-        do = P.digest(P.hashes(out), k << 21)
-        shard.append(f"{do:016x}")
-        total = (total + do) % 2**64
-        totin = (totin + di) % 2**64
-    dig["config4"] = {"universes": 1 << 24, "seed": 4, "generations": 1, "shards": 8,
-                      "input_digest": f"{totin:016x}", "output_digest": f"{total:016x}",
-                      "shard_output_digests": shard}
-    # bench.py weak scaling: rank r owns [r*2^20, (r+1)*2^20) of the seed-2 array;
-    # Step^1 output digest of each rank's shard (rank 0 == config 2)
-    weak = []
-    for k in range(8):
-        xin = P.fill(1 << 20, seed=2, first_universe=k << 20)
-        weak.append(f"{P.digest(P.hashes(R.step_batch(xin, 1, nthreads=8)), k << 20):016x}")
-    dig["weak_shards_seed2"] = {"universes_per_rank": 1 << 20, "seed": 2, "generations": 1,
-                                "shard_output_digests": weak}
-    meta["digests"] = dig
+    meta["digests"] = batch_digests()
     with open(os.path.join(HERE, "golden.json"), "w") as f:
         json.dump(meta, f, indent=1)
     print(json.dumps(meta["digests"], indent=1))
@@ -406,6 +428,13 @@ def rle_fixture():
 if __name__ == "__main__":
     if "--only-rle" in sys.argv:
         rle_fixture()
+    elif "--only-digests" in sys.argv:  # refresh golden.json["digests"] only
+        gj = os.path.join(HERE, "golden.json")
+        with open(gj) as f:
+            m = json.load(f)
+        m["digests"] = batch_digests()
+        with open(gj, "w") as f:
+            json.dump(m, f, indent=1)
     elif "--only-stable" in sys.argv:  # refresh stable*.npz and golden.json["stable"]
         gj = os.path.join(HERE, "golden.json")
         with open(gj) as f:

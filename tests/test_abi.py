@@ -54,12 +54,21 @@ def test_gfx950_code_object_present():
     assert targets == {b"gfx950"}, targets
 
 
-def test_abi_version_and_defaults():
+def test_abi_version_and_shipped_kernels():
     import lifeapi_amd.hip as hip
-    assert hip.abi_version() == 1
-    c1, c3 = hip.default_cfg(1), hip.default_cfg(1024)
-    assert c1.xchg == 0 and c1.universes_per_wave in (1, 2, 4, 8)
-    assert c3.universes_per_wave in (1, 2, 4, 8)
+    assert hip.abi_version() == 2
+    assert hip.step_kernel_name(1).startswith("k_step<dpp")
+    assert hip.step_kernel_name(3).startswith("k_step_split<8-way")
+    assert "nt" in hip.step_kernel_name(31) and "nt" not in hip.step_kernel_name(32).split(",")[2]
+
+
+def test_no_tuning_knobs_in_product_library():
+    """The product exports only the drop-in entry points: the measured
+    alternatives live in the tuning build (tools/tune/liblifeapi_tune.so)."""
+    import lifeapi_amd.hip as hip
+    for name in ("lifeapi_step_batch_dev_cfg", "lifeapi_default_cfg", "lifeapi_refined_step_batch_dev_cfg",
+                 "lifeapi_tune_step_batch_dev_cfg"):
+        assert not hasattr(hip.lib, name), name
 
 
 def test_argument_validation_without_device():
@@ -75,11 +84,6 @@ def test_argument_validation_without_device():
     assert b"overlap" in L.lifeapi_last_error()
     # n == 0 is a no-op success even with null pointers
     assert L.lifeapi_step_batch_dev(None, None, 0, 1, None) == 0
-    # bad launch cfg
-    for bad in [(9, 4, 8, 0, 0), (0, 3, 8, 0, 0), (0, 1, 8, 0, 5),
-                (hip.XCHG_ASM, 1, 8, 0, 2)]:     # the hand-allocated loops are rules 4 and 8 only
-        cfg = hip.LaunchCfg(*bad)
-        assert L.lifeapi_step_batch_dev_cfg(4096, 8192 * 4, 1, 1, None, ctypes.byref(cfg)) == -1, bad
     assert L.lifeapi_fill_random_dev(4096, 1, 0, 0, 5, None) == -1
 
 

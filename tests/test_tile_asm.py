@@ -1,4 +1,4 @@
-"""The generated tile-layout generation loop (lifeapi_amd/csrc/tile_asm.inc,
+"""The generated tile-layout generation loop (tools/tune/tile_asm.inc,
 tools/gen_tile_asm.py) on CPU: the committed file is what the generator
 emits, no VALU reads two sources from one VGPR bank, and executing the
 assembly text on 64 simulated lanes steps 16 universes exactly as the oracle

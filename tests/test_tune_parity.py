@@ -1,0 +1,73 @@
+"""GPU parity of the TUNING build (tools/tune/liblifeapi_tune.so): every
+measured alternative to the shipped step kernels -- other networks, exchanges,
+layouts, tiles and assembly-loop schedules -- against the oracle, bit-exact.
+These configurations are not in the product library; the shipped ones are
+covered by tests/test_gpu_parity.py and tests/test_ref_gpu.py."""
+import itertools
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from test_gpu_parity import seam_cases, to_dev, to_host
+
+pytestmark = pytest.mark.gpu
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "tune"))
+
+ALL_CFGS = list(itertools.product(range(8), (1, 2, 4, 8), (0, 1), (0, 1, 2, 3, 4)))
+# the hand-allocated loop exists for rule 4 only
+ALL_CFGS += list(itertools.product((8,), (1, 2, 4, 8), (0, 1), (4,)))
+# the row-split layouts: LDS exchange, 1 or 2 groups of 2 / 4 universes
+ALL_CFGS += list(itertools.product((1,), (1, 2), (0, 1), (5, 6, 7)))
+# the tile layouts (4 / 2 columns per lane): one tile per wave
+ALL_CFGS += [(x, 1, nt, r) for r, xs in ((8, (0, 1, 8)), (9, (1,))) for x in xs for nt in (0, 1)]
+# the 6-LUT tail: split layouts (rules 10-12) and the 4-column tile (rule 13)
+ALL_CFGS += list(itertools.product((1,), (1, 2), (0, 1), (10, 11, 12)))
+ALL_CFGS += [(x, 1, nt, 13) for x in (0, 1) for nt in (0, 1)]
+# split layouts with part of the exchange by DPP (LIFEAPI_XCHG_LDS_DPP(d) = 16 + d)
+ALL_CFGS += [(16 + d, u, nt, 11) for d in (1, 2, 3, 4) for u in (1, 2) for nt in (0, 1)]
+ALL_CFGS += [(16 + d, 1, nt, 12) for d in (2, 4) for nt in (0, 1)]
+# the hand-allocated rule-11 loop (LIFEAPI_XCHG_ASM = 8)
+ALL_CFGS += [(8, u, nt, 11) for u in (1, 2) for nt in (0, 1)]
+ALL_CFGS += [(24 + k, 1, nt, 11) for k in (1, 2, 3) for nt in (0, 1)]  # its other schedules
+# the software-pipelined LDS loop (LIFEAPI_XCHG_LDS_PIPE = 9)
+ALL_CFGS += [(9, u, nt, r) for r in (6, 11, 12) for u in (1, 2) for nt in (0, 1)]
+
+
+
+
+@pytest.fixture(scope="module")
+def tune(hip):
+    import tune_hip
+    return tune_hip
+
+
+def test_tune_default_is_shipped(tune):
+    for g in (1, 2, 3, 31, 32, 1024):
+        c = tune.default_cfg(g)
+        assert (c.xchg, c.rule) == ((0, 3) if g <= 2 else (8, 11))
+
+
+@pytest.mark.parametrize("xchg,upw,nt,rule", ALL_CFGS)
+def test_step_all_cfgs(tune, port, xchg, upw, nt, rule):
+    n = 2048 + 3                               # ragged vs every U
+    x = port.fill(n, seed=1000 + xchg * 100 + upw * 10 + nt * 2 + rule)
+    x = np.concatenate([seam_cases(port), x])
+    cfg = tune.LaunchCfg(xchg, upw, 1, nt, rule)  # 1 block/CU: forces grid-striding
+    d = to_dev(x)
+    for gens in (1, 5):
+        got = to_host(tune.step(d, generations=gens, cfg=cfg))
+        want = port.step_batch(x, gens)
+        bad = np.nonzero((got != want).any(axis=1))[0]
+        assert bad.size == 0, f"gens={gens}: {bad.size} universes differ, first {bad[:8]}"
+
+
+
+
+def test_bad_cfgs_rejected(tune, hip):
+    import torch
+    d = torch.zeros((4, 64), dtype=torch.int64, device="cuda")
+    for bad in [(10, 4, 8, 0, 0), (0, 3, 8, 0, 0), (0, 1, 8, 0, 5), (8, 1, 8, 0, 2)]:
+        with pytest.raises(hip.LifeApiError):
+            tune.step(d, generations=1, cfg=tune.LaunchCfg(*bad))

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Generate the hand-allocated generation loop of the tile layout (RULE 8 with
 LIFEAPI_XCHG_ASM: 8-way row split, 4 columns per lane, LDS edge exchange) as
-inline gfx950 assembly: lifeapi_amd/csrc/tile_asm.inc.
+inline gfx950 assembly: tools/tune/tile_asm.inc (tuning build only).
 
 Why: a v_bitop3_b32 whose sources sit in two or three VGPRs of one bank (bank =
 vN mod 4) issues at about half rate on gfx950 (tools/bank_probe.hip:
@@ -29,7 +29,7 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-OUT = os.path.join(ROOT, "lifeapi_amd", "csrc", "tile_asm.inc")
+OUT = os.path.join(ROOT, "tools", "tune", "tile_asm.inc")
 
 S, C, P = 8, 4, 4            # row split, columns per lane, universes per group
 XOR3, MAJ, LE1, NAE, EVEN = 0x96, 0xE8, 0x17, 0x7E, 0x69

@@ -12,13 +12,15 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import lifeapi_amd.hip as hip  # noqa: E402
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tune"))
+import tune_hip  # noqa: E402  (tools/tune/liblifeapi_tune.so: explicit launch configurations)
 
 
 def main():
     n = 1 << 20
     a = hip.fill_random(n, seed=2)
     b = torch.empty_like(a)
-    cfgs = [None] + [hip.LaunchCfg(0, u, 0, nt, 3) for u, nt in itertools.product((2, 4, 8), (0, 1))]
+    cfgs = [None] + [tune_hip.LaunchCfg(0, u, 0, nt, 3) for u, nt in itertools.product((2, 4, 8), (0, 1))]
     res = {}
     for rnd in range(5):
         for ci, cfg in enumerate(cfgs):
@@ -27,10 +29,10 @@ def main():
                 e0.record()
                 for k in range(20):
                     if mode == "inplace":
-                        hip.step(a, out=a, generations=1, cfg=cfg)
+                        tune_hip.step(a, out=a, generations=1, cfg=cfg)
                     else:
                         src, dst = (a, b) if k % 2 == 0 else (b, a)
-                        hip.step(src, out=dst, generations=1, cfg=cfg)
+                        tune_hip.step(src, out=dst, generations=1, cfg=cfg)
                 e1.record()
                 e1.synchronize()
                 res.setdefault((ci, mode), []).append(e0.elapsed_time(e1) / 20)

@@ -19,6 +19,8 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import lifeapi_amd.hip as hip  # noqa: E402
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tune"))
+import tune_hip  # noqa: E402  (tools/tune/liblifeapi_tune.so: explicit launch configurations)
 
 
 def timeit(fn, reps):
@@ -35,6 +37,8 @@ def timeit(fn, reps):
 
 def tune_c5(args):
     """Config 5 (refined ternary step): prefetch x grid cap x occupancy bound."""
+    raise SystemExit("the config-5 launch variants were measured in round 1 (profiles/r01/tune_c5.jsonl); "
+                     "their tuning form is no longer built -- the shipped k_refined<1, 0> is fixed")
     import ctypes
     n = 1 << 18
     planes = hip.fill_random(n * 11, seed=6).reshape(n, 11 * 64)
@@ -46,7 +50,7 @@ def tune_c5(args):
     ok = {}
     for r in range(args.rounds):
         for c in cfgs:
-            cfg = hip.LaunchCfg(0, c[0], c[1], 1, c[2])
+            cfg = tune_hip.LaunchCfg(0, c[0], c[1], 1, c[2])
             run = lambda: hip._check(hip.lib.lifeapi_refined_step_batch_dev_cfg(  # noqa: E731
                 planes.data_ptr(), out.data_ptr(), n, s, ctypes.byref(cfg)))
             ms[c] += timeit(run, args.reps)
@@ -126,8 +130,8 @@ def main():
             copy_ms = []
         for r in range(args.rounds):
             for c in cfgs:
-                cfg = hip.LaunchCfg(*c)
-                ms[c] += timeit(lambda: hip.step(a, out=b, generations=g, cfg=cfg), args.reps)
+                cfg = tune_hip.LaunchCfg(*c)
+                ms[c] += timeit(lambda: tune_hip.step(a, out=b, generations=g, cfg=cfg), args.reps)
                 if r == 0:
                     torch.cuda.synchronize()
                     ok[c] = bool(torch.equal(b, ref))

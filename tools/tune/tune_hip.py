@@ -1,0 +1,65 @@
+"""ctypes binding of the TUNING build (tools/tune/liblifeapi_tune.so,
+lifeapi_tune.h): batched Step() with an explicit launch configuration.
+Loads the product binding (lifeapi_amd.hip) first, so both libraries share
+torch's HIP runtime and the product's error state."""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+import lifeapi_amd.hip as hip
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "liblifeapi_tune.so")
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"{LIB_PATH} is missing: build it with __graft_entry__.build()")
+lib = ctypes.CDLL(LIB_PATH)
+
+XCHG_DPP, XCHG_LDS, XCHG_BPERM, XCHG_MIX, XCHG_MIX1, XCHG_MIX3, XCHG_LDSR, XCHG_LDSR3, XCHG_ASM = range(9)
+XCHG_LDS_PIPE = 9
+
+
+def XCHG_ASM_V(k: int) -> int:
+    return 24 + k
+
+
+def XCHG_LDS_DPP(d: int) -> int:
+    return 16 + d
+
+
+class LaunchCfg(ctypes.Structure):
+    """lifeapi_launch_cfg (tools/tune/lifeapi_tune.h)."""
+
+    _fields_ = [("xchg", ctypes.c_int), ("universes_per_wave", ctypes.c_int),
+                ("blocks_per_cu", ctypes.c_int), ("nontemporal", ctypes.c_int),
+                ("rule", ctypes.c_int)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_vp, _sz, _u32, _int = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_int
+lib.lifeapi_tune_default_cfg.argtypes = [ctypes.POINTER(LaunchCfg), _u32]
+lib.lifeapi_tune_default_cfg.restype = None
+lib.lifeapi_tune_step_batch_dev_cfg.argtypes = [_vp, _vp, _sz, _u32, _vp, ctypes.POINTER(LaunchCfg)]
+lib.lifeapi_tune_step_batch_dev_cfg.restype = _int
+
+
+def default_cfg(generations: int = 1) -> LaunchCfg:
+    c = LaunchCfg()
+    lib.lifeapi_tune_default_cfg(ctypes.byref(c), generations)
+    return c
+
+
+def step(states: torch.Tensor, out: torch.Tensor | None = None, generations: int = 1,
+         cfg: LaunchCfg | None = None, stream=None) -> torch.Tensor:
+    n = hip._universes(states)
+    if out is None:
+        out = torch.empty_like(states)
+    if hip._universes(out, "out") != n:
+        raise ValueError("out has a different number of universes")
+    hip._check(lib.lifeapi_tune_step_batch_dev_cfg(states.data_ptr(), out.data_ptr(), n, generations,
+                                                   hip._stream(stream),
+                                                   ctypes.byref(cfg) if cfg is not None else None))
+    return out

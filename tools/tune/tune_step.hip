@@ -1,0 +1,400 @@
+// tune_step.hip -- the TUNING build of batched Step(): every measured
+// alternative to the shipped kernels (other rule networks, exchanges,
+// layouts, tiles and assembly-loop schedules), selectable per launch by
+// lifeapi_launch_cfg (lifeapi_tune.h).  Built into tools/tune/
+// liblifeapi_tune.so by __graft_entry__.build_tools(); used by
+// tools/tune.py and the ablation parity tests (tests/test_tune_parity.py).
+// Not part of the product library or its header: the shipped
+// configurations are fixed in lifeapi_amd/csrc/step.hip.
+#include <algorithm>
+
+#include "lifeapi_tune.h"
+#include "step_kernels.hpp"
+#include "tile_asm.inc"
+
+using namespace lifeapi_impl;
+
+static_assert(XDPP == LIFEAPI_XCHG_DPP && XLDS == LIFEAPI_XCHG_LDS && XBPERM == LIFEAPI_XCHG_BPERM &&
+                  XMIX == LIFEAPI_XCHG_MIX && XMIX1 == LIFEAPI_XCHG_MIX1 && XMIX3 == LIFEAPI_XCHG_MIX3 &&
+                  XLDSR == LIFEAPI_XCHG_LDSR && XLDSR3 == LIFEAPI_XCHG_LDSR3 && XASM == LIFEAPI_XCHG_ASM,
+              "device.hpp's exchange numbering");
+
+namespace {
+
+// `gens` generations of one universe in the (E, O) layout (RULE 4), as one
+// hand-allocated loop.  The compiler's allocation puts two or three sources
+// of about half of the v_bitop3 in one VGPR bank (tools/vbank.py), and such an
+// instruction issues at half rate (tools/bank_probe.hip).  Here every VALU
+// instruction reads its sources from distinct banks (bank = vN mod 4):
+//   A = (E, O) v0:v1 (banks 0,1)   R = right column v2:v3 (2,3)
+//   L = left column v5 (E, bank 1), v4 (O, bank 0)
+// The exchange goes through this wave's 512-B LDS slot (ds_write_b64 of A,
+// ds_read_b64 of the right neighbour's word, two ds_read_b32 of the left
+// one); a wave's LDS operations complete in order and each generation waits
+// for its reads before the next write.  Network: life_gen<_, 4>.
+__device__ __forceinline__ void gens_asm(W &a, uint32_t gens, uint32_t lds_self, uint32_t lds_prev,
+                                         uint32_t lds_next) {
+  asm volatile(
+      "v_mov_b32 v0, %[e]\n"
+      "v_mov_b32 v1, %[o]\n"
+      "s_cmp_eq_u32 %[g], 0\n"
+      "s_cbranch_scc1 2f\n"
+      "1:\n"
+      "ds_write_b64 %[as], v[0:1]\n"
+      "ds_read_b64 v[2:3], %[an]\n"
+      "ds_read_b32 v5, %[ap]\n"
+      "ds_read_b32 v4, %[ap] offset:4\n"
+      "s_sub_u32 %[g], %[g], 1\n"
+      "s_waitcnt lgkmcnt(0)\n"
+      "v_bitop3_b32 v8, v5, v0, v2 bitop3:0x96\n"      // h0 E = xor3(L, A, R)
+      "v_bitop3_b32 v9, v4, v1, v3 bitop3:0x96\n"      // h0 O
+      "v_bitop3_b32 v10, v5, v0, v2 bitop3:0xe8\n"     // h1 E = maj(L, A, R)
+      "v_bitop3_b32 v11, v4, v1, v3 bitop3:0xe8\n"     // h1 O
+      "v_alignbit_b32 v6, v9, v9, 31\n"                // u0 = rotl1(h0 O): row 2k-1
+      "v_alignbit_b32 v14, v8, v8, 1\n"                // d0 = rotr1(h0 E): row 2k+2
+      "v_alignbit_b32 v12, v11, v11, 31\n"             // u1
+      "v_alignbit_b32 v16, v10, v10, 1\n"              // d1
+      "v_bitop3_b32 v13, v6, v8, v9 bitop3:0x17\n"     // s0 E = SA <= 1
+      "v_bitop3_b32 v18, v6, v8, v9 bitop3:0x7e\n"     // s1 E = SA in {1,2}
+      "v_bitop3_b32 v20, v8, v9, v14 bitop3:0x17\n"    // s0 O
+      "v_bitop3_b32 v22, v8, v9, v14 bitop3:0x7e\n"    // s1 O
+      "v_bitop3_b32 v17, v12, v10, v11 bitop3:0x17\n"  // s2 E = SB <= 1
+      "v_bitop3_b32 v24, v12, v10, v11 bitop3:0x69\n"  // s3 E = SB in {0,2}
+      "v_bitop3_b32 v28, v10, v11, v16 bitop3:0x17\n"  // s2 O
+      "v_bitop3_b32 v21, v10, v11, v16 bitop3:0x69\n"  // s3 O
+      "v_bitop3_b32 v15, v13, v18, v0 bitop3:0x34\n"   // t1 E = T1(s0, s1, a)
+      "v_bitop3_b32 v19, v20, v22, v1 bitop3:0x34\n"   // t1 O
+      "v_bitop3_b32 v25, v17, v0, v15 bitop3:0x58\n"   // t2 E = T2(s2, a, t1)
+      "v_bitop3_b32 v23, v28, v1, v19 bitop3:0x58\n"   // t2 O
+      "v_bitop3_b32 v0, v18, v24, v25 bitop3:0x28\n"   // a E = T3(s1, s3, t2)
+      "v_bitop3_b32 v1, v22, v21, v23 bitop3:0x28\n"   // a O
+      "s_cmp_lg_u32 %[g], 0\n"
+      "s_cbranch_scc1 1b\n"
+      "2:\n"
+      "v_mov_b32 %[e], v0\n"
+      "v_mov_b32 %[o], v1\n"
+      : [e] "+v"(a.lo), [o] "+v"(a.hi), [g] "+s"(gens)
+      : [as] "v"(lds_self), [ap] "v"(lds_prev), [an] "v"(lds_next)
+      : "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v8", "v9", "v10", "v11", "v12", "v13", "v14",
+        "v15", "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v28", "scc",
+        "memory");
+  static_assert(kT1 == 0x34 && kT2 == 0x58 && kT3 == 0x28 && kLe1 == 0x17 && kNae == 0x7E &&
+                    kEven == 0x69 && kXor3 == 0x96 && kMaj == 0xE8,
+                "gens_asm spells out the RULE 4 tables");
+}
+
+// k_step with the hand-allocated RULE 4 loop (X == XASM)
+template <int X, int U, bool NT, int RULE>
+__global__ __launch_bounds__(kBlock) void k_step_asm4(const uint64_t *__restrict__ in,
+                                                 uint64_t *__restrict__ out, uint64_t n,
+                                                 uint32_t gens) {
+  __shared__ uint64_t lds[uses_lds(X) ? kWavesPerBlock * U * 2 * kWave : 1];
+  const int lane = threadIdx.x & (kWave - 1);
+  // wave index in the block, made provably wave-uniform so that the tail
+  // tests below are scalar branches
+  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock * U;
+  for (uint64_t u0 = ((uint64_t)blockIdx.x * kWavesPerBlock + wib) * U; u0 < n; u0 += stride) {
+    W a[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k)
+      a[k] = (u0 + k < n) ? ld<NT>(in + (u0 + k) * kWave + lane) : W{0u, 0u};
+    if constexpr (RULE == 4) {
+#pragma unroll
+      for (int k = 0; k < U; ++k) a[k] = to_eo(a[k]);
+    }
+    if constexpr (X == XASM) {
+      static_assert(RULE == 4, "the hand-allocated loop is the RULE 4 network");
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        // LDS byte addresses of this wave's slot: own word, left and right neighbours
+        const uint32_t base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)(
+            lds + (wib * U + k) * 2 * kWave);
+        gens_asm(a[k], gens, base + lane * 8u, base + ((lane + kWave - 1) & (kWave - 1)) * 8u,
+                 base + ((lane + 1) & (kWave - 1)) * 8u);
+      }
+    } else {
+      for (uint32_t g = 0; g < gens; ++g) {
+#pragma unroll
+        for (int k = 0; k < U; ++k)
+          a[k] = life_gen<X, RULE>(a[k], lds + (wib * U + k) * 2 * kWave, lane);
+      }
+    }
+    if constexpr (RULE == 4) {
+#pragma unroll
+      for (int k = 0; k < U; ++k) a[k] = from_eo(a[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k)
+      if (u0 + k < n) st<NT>(out + (u0 + k) * kWave + lane, a[k]);
+  }
+}
+
+// k_step for the tile layouts (gen_tile): a wave holds C groups of P = S/2
+// universes, lane i of group g columns C*i .. C*i+C-1 of each (C*8
+// contiguous bytes per universe: two dwordx4 loads for C = 4).
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+template <bool NT>
+__device__ __forceinline__ u64x2 ld2(const uint64_t *p) {
+  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(p));
+  else return *reinterpret_cast<const u64x2 *>(p);
+}
+template <bool NT>
+__device__ __forceinline__ void st2(uint64_t *p, u64x2 v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<u64x2 *>(p));
+  else *reinterpret_cast<u64x2 *>(p) = v;
+}
+
+template <int S, int C, int X, bool NT, int NET>
+__global__ __launch_bounds__(kBlock) void k_step_tile(const uint64_t *__restrict__ in,
+                                                      uint64_t *__restrict__ out, uint64_t n,
+                                                      uint32_t gens) {
+  constexpr int P = S / 2, LPG = kWave / C;
+  static_assert(C % 2 == 0, "columns are moved in pairs");
+  __shared__ uint32_t lds[X == XDPP ? 1 : kWavesPerBlock * 2 * S * kWave];  // 4 planes of 1 KiB per wave (S = 8)
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int grp = lane / LPG, col0 = (lane & (LPG - 1)) * C;
+  const uint64_t per_wave = (uint64_t)C * P;
+  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock * per_wave;
+  uint32_t *slot = lds + (X == XDPP ? 0 : wib * 2 * S * kWave);
+  // per-lane offsets stay 32-bit and the tile's base pointer wave-uniform, so
+  // little beyond the state is live across the generation loop
+  const uint32_t lane_off = (uint32_t)(grp * P * kWave + col0);
+  for (uint64_t u0 = ((uint64_t)blockIdx.x * kWavesPerBlock + wib) * per_wave; u0 < n; u0 += stride) {
+    const uint64_t left = n - u0;  // universes from u0 on (wave-uniform)
+    const uint64_t *src = in + u0 * kWave;
+    uint32_t off = lane_off, first = (uint32_t)(grp * P);
+    // opaque to the optimiser: keeps it from hoisting 64-bit copies of the
+    // lane offsets out of the loop (they would stay live across the generations)
+    asm volatile("" : "+v"(off), "+v"(first));
+    const uint32_t room = left < per_wave ? (uint32_t)left : (uint32_t)per_wave;
+    uint32_t r[C][S];
+    {
+      uint64_t w[P][C];
+#pragma unroll
+      for (int u = 0; u < P; ++u) {
+        const bool ok = first + u < room;
+#pragma unroll
+        for (int c = 0; c < C; c += 2) {
+          const u64x2 v = ok ? ld2<NT>(src + off + u * kWave + c) : u64x2{0, 0};
+          w[u][c] = v[0], w[u][c + 1] = v[1];
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        W cc[P];
+#pragma unroll
+        for (int u = 0; u < P; ++u) cc[u] = split(w[u][c]);
+        Split<S>::load(cc, r[c]);
+      }
+    }
+    if constexpr (X == XASM) {
+      static_assert(S == 8 && C == 4, "tile_asm.inc is the 8-way split, 4 columns per lane");
+      const uint32_t base =
+          (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)slot;
+      const int g0 = lane & ~(LPG - 1);
+      tile_gens_asm(r, gens, base + lane * 16u, base + (g0 | ((lane + LPG - 1) & (LPG - 1))) * 16u,
+                    base + (g0 | ((lane + 1) & (LPG - 1))) * 16u);
+    } else {
+      for (uint32_t it = 0; it < gens; ++it) gen_tile<S, C, X, NET>(r, slot, lane);
+    }
+    asm volatile("" : "+v"(off), "+v"(first));  // (store addresses: recomputed here)
+    uint64_t w[P][C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      W cc[P];
+      Split<S>::store(r[c], cc);
+#pragma unroll
+      for (int u = 0; u < P; ++u) w[u][c] = join(cc[u]);
+    }
+    uint64_t *dst = out + u0 * kWave;
+#pragma unroll
+    for (int u = 0; u < P; ++u) {
+      if (first + u < room) {
+#pragma unroll
+        for (int c = 0; c < C; c += 2) st2<NT>(dst + off + u * kWave + c, u64x2{w[u][c], w[u][c + 1]});
+      }
+    }
+  }
+}
+
+using StepFn = void (*)(const uint64_t *, uint64_t *, uint64_t, uint32_t);
+
+template <int X, int U, bool NT, int RULE>
+constexpr StepFn step_ptr() {
+  if constexpr (X == XASM) return k_step_asm4<X, U, NT, RULE>;
+  else return k_step<X, U, NT, RULE>;
+}
+
+template <int X, bool NT, int RULE>
+StepFn pick_u(int u) {
+  switch (u) {
+    case 1: return step_ptr<X, 1, NT, RULE>();
+    case 2: return step_ptr<X, 2, NT, RULE>();
+    case 4: return step_ptr<X, 4, NT, RULE>();
+    case 8: return step_ptr<X, 8, NT, RULE>();
+    default: return nullptr;
+  }
+}
+template <int X, int RULE>
+StepFn pick_nt(int u, bool nt) { return nt ? pick_u<X, true, RULE>(u) : pick_u<X, false, RULE>(u); }
+template <int X>
+StepFn pick_rule(int u, bool nt, int rule) {
+  if constexpr (X == XASM) {
+    return rule == 4 ? pick_nt<X, 4>(u, nt) : nullptr;
+  } else {
+    switch (rule) {
+      case 0: return pick_nt<X, 0>(u, nt);
+      case 1: return pick_nt<X, 1>(u, nt);
+      case 2: return pick_nt<X, 2>(u, nt);
+      case 3: return pick_nt<X, 3>(u, nt);
+      case 4: return pick_nt<X, 4>(u, nt);
+      default: return nullptr;
+    }
+  }
+}
+template <int S, int NET, int D = 0, int V = 0>
+StepFn pick_split(int groups, bool nt) {
+  switch (groups) {
+    case 1: return nt ? k_step_split<S, 1, true, NET, D, V> : k_step_split<S, 1, false, NET, D, V>;
+    case 2: return nt ? k_step_split<S, 2, true, NET, D, V> : k_step_split<S, 2, false, NET, D, V>;
+    default: return nullptr;
+  }
+}
+// universes one wave holds per universes_per_wave unit (rules 5-7, 10-12:
+// groups; rules 8, 9, 13: one tile of C groups)
+int group_size(int rule) {
+  switch (rule) {
+    case 5: case 10: return 2;
+    case 6: case 11: return 4;
+    case 7: case 12: return 8;
+    case 8: case 13: return 16;
+    case 9: return 8;
+    default: return 1;
+  }
+}
+
+template <int NET>
+StepFn pick_tile4(int xchg, bool nt) {
+  if (xchg == LIFEAPI_XCHG_LDS) return nt ? k_step_tile<8, 4, XLDS, true, NET> : k_step_tile<8, 4, XLDS, false, NET>;
+  if (xchg == LIFEAPI_XCHG_DPP) return nt ? k_step_tile<8, 4, XDPP, true, NET> : k_step_tile<8, 4, XDPP, false, NET>;
+  return nullptr;
+}
+
+StepFn pick_step(const lifeapi_launch_cfg &c) {
+  if (c.rule == 8 || c.rule == 9 || c.rule == 13) {  // tile layouts: one tile per wave
+    if (c.universes_per_wave != 1) return nullptr;
+    const bool nt = c.nontemporal != 0;
+    if (c.rule == 9)
+      return c.xchg == LIFEAPI_XCHG_LDS ? (nt ? k_step_tile<8, 2, XLDS, true, 7> : k_step_tile<8, 2, XLDS, false, 7>)
+                                        : nullptr;
+    if (c.rule == 13) return pick_tile4<6>(c.xchg, nt);
+    if (c.xchg == LIFEAPI_XCHG_ASM) return nt ? k_step_tile<8, 4, XASM, true, 7> : k_step_tile<8, 4, XASM, false, 7>;
+    return pick_tile4<7>(c.xchg, nt);
+  }
+  if ((c.rule >= 5 && c.rule <= 7) || (c.rule >= 10 && c.rule <= 12)) {  // split layouts
+    const bool nt = c.nontemporal != 0;
+    if (c.xchg == LIFEAPI_XCHG_ASM) {
+      return c.rule == 11 ? pick_split<8, 6, kAsmLoop>(c.universes_per_wave, nt) : nullptr;
+    }
+    if (c.xchg > LIFEAPI_XCHG_ASM_V(0) && c.xchg <= LIFEAPI_XCHG_ASM_V(3) && c.rule == 11 &&
+        c.universes_per_wave == 1) {  // the other schedules of the assembly loop
+      switch (c.xchg - LIFEAPI_XCHG_ASM_V(0)) {
+        case 1: return pick_split<8, 6, kAsmLoop, 1>(1, nt);
+        case 2: return pick_split<8, 6, kAsmLoop, 2>(1, nt);
+        default: return pick_split<8, 6, kAsmLoop, 3>(1, nt);
+      }
+    }
+    if (c.xchg == LIFEAPI_XCHG_LDS_PIPE) {
+      switch (c.rule) {
+        case 6: return pick_split<8, 7, kPipe>(c.universes_per_wave, nt);
+        case 11: return pick_split<8, 6, kPipe>(c.universes_per_wave, nt);
+        case 12: return pick_split<16, 6, kPipe>(c.universes_per_wave, nt);
+        default: return nullptr;
+      }
+    }
+    if (c.xchg > LIFEAPI_XCHG_LDS_DPP(0) && (c.rule == 11 || c.rule == 12)) {
+      // LDS for most registers, DPP for D of them
+      const int d = c.xchg - LIFEAPI_XCHG_LDS_DPP(0);
+      if (c.rule == 11) {
+        switch (d) {
+          case 1: return pick_split<8, 6, 1>(c.universes_per_wave, nt);
+          case 2: return pick_split<8, 6, 2>(c.universes_per_wave, nt);
+          case 3: return pick_split<8, 6, 3>(c.universes_per_wave, nt);
+          case 4: return pick_split<8, 6, 4>(c.universes_per_wave, nt);
+          default: return nullptr;
+        }
+      }
+      switch (d) {
+        case 2: return pick_split<16, 6, 2>(c.universes_per_wave, nt);
+        case 4: return pick_split<16, 6, 4>(c.universes_per_wave, nt);
+        default: return nullptr;
+      }
+    }
+    if (c.xchg != LIFEAPI_XCHG_LDS) return nullptr;
+    switch (c.rule) {
+      case 5: return pick_split<4, 7>(c.universes_per_wave, nt);
+      case 6: return pick_split<8, 7>(c.universes_per_wave, nt);
+      case 7: return pick_split<16, 7>(c.universes_per_wave, nt);
+      case 10: return pick_split<4, 6>(c.universes_per_wave, nt);
+      case 11: return pick_split<8, 6>(c.universes_per_wave, nt);
+      default: return pick_split<16, 6>(c.universes_per_wave, nt);
+    }
+  }
+  switch (c.xchg) {
+    case LIFEAPI_XCHG_DPP: return pick_rule<XDPP>(c.universes_per_wave, c.nontemporal != 0, c.rule);
+    case LIFEAPI_XCHG_LDS: return pick_rule<XLDS>(c.universes_per_wave, c.nontemporal != 0, c.rule);
+    case LIFEAPI_XCHG_BPERM: return pick_rule<XBPERM>(c.universes_per_wave, c.nontemporal != 0, c.rule);
+    case LIFEAPI_XCHG_MIX: return pick_rule<XMIX>(c.universes_per_wave, c.nontemporal != 0, c.rule);
+    case LIFEAPI_XCHG_MIX1: return pick_rule<XMIX1>(c.universes_per_wave, c.nontemporal != 0, c.rule);
+    case LIFEAPI_XCHG_MIX3: return pick_rule<XMIX3>(c.universes_per_wave, c.nontemporal != 0, c.rule);
+    case LIFEAPI_XCHG_LDSR: return pick_rule<XLDSR>(c.universes_per_wave, c.nontemporal != 0, c.rule);
+    case LIFEAPI_XCHG_LDSR3: return pick_rule<XLDSR3>(c.universes_per_wave, c.nontemporal != 0, c.rule);
+    case LIFEAPI_XCHG_ASM: return pick_rule<XASM>(c.universes_per_wave, c.nontemporal != 0, c.rule);
+    default: return nullptr;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+void lifeapi_tune_default_cfg(lifeapi_launch_cfg *cfg, uint32_t generations) {
+  if (!cfg) return;
+  cfg->blocks_per_cu = 0;
+  if (generations <= 2) {
+    cfg->xchg = LIFEAPI_XCHG_DPP;
+    cfg->rule = 3;
+    cfg->universes_per_wave = 4;
+    cfg->nontemporal = 1;
+  } else {
+    cfg->xchg = LIFEAPI_XCHG_ASM;
+    cfg->rule = 11;
+    cfg->universes_per_wave = 1;
+    cfg->nontemporal = generations < 32 ? 1 : 0;
+  }
+}
+
+int lifeapi_tune_step_batch_dev_cfg(const uint64_t *d_in, uint64_t *d_out, size_t n,
+                                    uint32_t generations, void *stream,
+                                    const lifeapi_launch_cfg *cfg) {
+  int rc = check_batch(d_in, d_out, n);
+  if (rc != LIFEAPI_OK || n == 0) return rc;
+  lifeapi_launch_cfg c;
+  if (cfg) c = *cfg;
+  else lifeapi_tune_default_cfg(&c, generations);
+  StepFn fn = pick_step(c);
+  if (!fn) return fail(LIFEAPI_E_INVALID, "unsupported launch cfg%s");
+  int cus = 0;
+  rc = device_cus(cus);
+  if (rc != LIFEAPI_OK) return rc;
+  const uint64_t per_wave = (uint64_t)c.universes_per_wave * group_size(c.rule);
+  const uint64_t waves = (n + per_wave - 1) / per_wave;
+  const unsigned grid = grid_for(waves, cus, c.blocks_per_cu);
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, d_in, d_out,
+                     (uint64_t)n, generations);
+  return launched("k_step (tuning) launch");
+}
+
+}  // extern "C"
