@@ -1,0 +1,91 @@
+"""GPU parity pinned DIRECTLY to the reference: the shipped HIP kernels
+against the reference's own code, compiled from /root/reference into
+oracle/_ref/libref_v{3,4}.so (oracle/Makefile, target ref; the .so travels to
+the GPU box prebuilt).  No restatement in between:
+
+* Step() / Step(n) (LifeAPI.hpp:1196-1216, 877-886) for the shipped
+  configurations -- gens 1 and 2 (k_step, natural layout), 3, 31 and 1024
+  (k_step_split, the assembly loop; nontemporal below 32) -- on a prefix of
+  the config-2 input generated on the device, plus seam cases, the
+  reference-shaped RandomState() draws and ragged batch sizes;
+* the full config-2 batch (1M universes x 1 gen) word for word;
+* LifeWeld::Step (LifeWeld.hpp:169-186) and the config-5 harness around the
+  reference's own unknown_step_refined fragment.
+
+Bit-exact on every word (integer work, no tolerance).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from test_gpu_parity import seam_cases, to_dev, to_host
+
+pytestmark = pytest.mark.gpu
+
+THREADS = max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+@pytest.fixture(scope="module")
+def R(hip):
+    from oracle.oracle import Ref
+    assert Ref.available(), "oracle/_ref was not built: run __graft_entry__.build() where /root/reference exists"
+    return Ref()
+
+
+def _check(got, want, what):
+    bad = np.nonzero((got != want).any(axis=1))[0]
+    assert bad.size == 0, f"{what}: {bad.size} universes differ from the reference, first {bad[:8]}"
+
+
+@pytest.mark.parametrize("gens", [1, 2, 3, 31, 1024])
+def test_shipped_step_vs_reference(hip, R, port, gens):
+    n = 1 << 14 if gens < 1024 else 1 << 12
+    d = hip.fill_random(n, seed=2)                      # config-2 prefix, generated on the device
+    x = np.concatenate([seam_cases(port), to_host(d),
+                        np.load(os.path.join(os.path.dirname(__file__), "golden", "randomstate_kat.npz"))["input"]])
+    got = to_host(hip.step(to_dev(x), generations=gens))
+    _check(got, R.step_batch(x, gens, nthreads=THREADS), f"Step^{gens} ({hip.step_kernel_name(gens)})")
+
+
+@pytest.mark.parametrize("n", [1, 3, 5, 63, 65, 4099])
+@pytest.mark.parametrize("gens", [1, 7])
+def test_ragged_vs_reference(hip, R, port, n, gens):
+    x = port.fill(n, seed=100 + n)
+    _check(to_host(hip.step(to_dev(x), generations=gens)), R.step_batch(x, gens, nthreads=THREADS),
+           f"n={n} gens={gens}")
+
+
+def test_inplace_vs_reference(hip, R, port):
+    x = port.fill(5003, seed=5)
+    d = to_dev(x)
+    hip.step(d, out=d, generations=1)
+    hip.step(d, out=d, generations=40)
+    _check(to_host(d), R.step_batch(x, 41, nthreads=THREADS), "in-place Step^1 then Step^40")
+
+
+def test_full_config2_vs_reference(hip, R):
+    n = 1 << 20
+    d = hip.fill_random(n, seed=2)
+    x = to_host(d)
+    _check(to_host(hip.step(d, generations=1)), R.step_batch(x, 1, nthreads=THREADS), "config 2, 1M x 1")
+
+
+def test_weld_vs_reference(hip, R, port):
+    rw = port.fill(300 * 4, seed=606).reshape(300, 256)
+    rw[:, 64:] &= port.fill(300 * 3, seed=607).reshape(300, 192) & port.fill(300 * 3, seed=608).reshape(300, 192)
+    for gens in (1, 5, 12, 40):
+        d = torch.from_numpy(rw.view(np.int64).copy()).cuda()
+        hip.weld_step(d, generations=gens)
+        got = d.cpu().numpy().view(np.uint64).reshape(-1, 256)
+        _check(got, R.weld_step(rw, gens), f"LifeWeld::Step^{gens}")
+
+
+def test_refined_vs_reference(hip, R):
+    n = 4096
+    d = hip.fill_random(n * 11, seed=66).reshape(n, 11 * 64)
+    got = hip.refined_step(d)
+    torch.cuda.synchronize()
+    x = d.cpu().numpy().view(np.uint64)
+    _check(got.cpu().numpy().view(np.uint64), R.refined_step(x), "unknown_step_refined harness")
