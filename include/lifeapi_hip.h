@@ -141,7 +141,10 @@ int lifeapi_parse_rle_batch_dev(const char *d_text, const uint64_t *d_offsets, s
 /* ---- host pointers, synchronous ----------------------------------------- */
 
 /* Stages through device memory of `device` (or of every visible device,
- * contiguous shards, when device == -1).                                  */
+ * contiguous shards, one host thread each, when device == -1; the
+ * environment variable LIFEAPI_HOST_SHARDS=k overrides that shard count,
+ * shard s running on device s mod count -- a rehearsal knob for machines
+ * with fewer GPUs).                                                        */
 int lifeapi_step_batch(const uint64_t *in, uint64_t *out, size_t n, uint32_t generations,
                        int device);
 int lifeapi_pop_batch(const uint64_t *states, uint32_t *pop, size_t n, int device);

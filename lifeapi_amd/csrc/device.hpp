@@ -232,6 +232,10 @@ template <int CTRL>
 __device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
 }
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp_mov64(uint64_t v) {
+  return (uint64_t)dpp_mov<CTRL>((uint32_t)v) | ((uint64_t)dpp_mov<CTRL>((uint32_t)(v >> 32)) << 32);
+}
 __device__ __forceinline__ uint32_t wave_sum_u32_dpp(uint32_t v) {
   v += dpp_mov<0xB1>(v);
   v += dpp_mov<0x4E>(v);

@@ -3,6 +3,7 @@
 // entry points that only stage data around a *_dev call.
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -309,28 +310,38 @@ int lifeapi_step_batch(const uint64_t *in, uint64_t *out, size_t n, uint32_t gen
   const int ndev = lifeapi_device_count();
   if (ndev <= 0) return fail(LIFEAPI_E_NODEVICE, "no HIP device visible%s");
   if (device >= ndev || device < -1) return fail(LIFEAPI_E_NODEVICE, "bad device index%s");
-  if (device >= 0 || ndev == 1)
+  // device -1: one contiguous shard per visible device, one host thread
+  // each.  LIFEAPI_HOST_SHARDS=k (k >= 1) overrides the shard count, shard s
+  // running on device s mod ndev: a rehearsal knob that runs this threaded
+  // path on a machine with fewer GPUs (tests/test_host_multidev.py).
+  int shards = ndev;
+  if (device < 0) {
+    if (const char *e = std::getenv("LIFEAPI_HOST_SHARDS")) {
+      const int k = std::atoi(e);
+      if (k >= 1) shards = k;
+    }
+  }
+  if (device >= 0 || shards == 1)
     return host_step_one_device(in, out, n, generations, device < 0 ? 0 : device);
-  // every visible device, contiguous shards, one host thread each; the whole
-  // arrays are pinned once here (shard boundaries share pages)
+  // the whole arrays are pinned once here (shard boundaries share pages)
   CallPins pins;
   pins.add(in, n * 512);
   if (out != in) pins.add(out, n * 512);
-  std::vector<int> rcs(ndev, LIFEAPI_OK);
-  std::vector<std::string> errs(ndev);
+  std::vector<int> rcs(shards, LIFEAPI_OK);
+  std::vector<std::string> errs(shards);
   std::vector<std::thread> pool;
-  for (int d = 0; d < ndev; ++d) {
-    const size_t lo = n * d / ndev, hi = n * (d + 1) / ndev;
-    pool.emplace_back([&, d, lo, hi] {
-      if (hi > lo) rcs[d] = host_step_one_device(in + lo * 64, out + lo * 64, hi - lo, generations, d);
-      errs[d] = g_err;
+  for (int k = 0; k < shards; ++k) {
+    const size_t lo = n * k / shards, hi = n * (k + 1) / shards;
+    pool.emplace_back([&, k, lo, hi] {
+      if (hi > lo) rcs[k] = host_step_one_device(in + lo * 64, out + lo * 64, hi - lo, generations, k % ndev);
+      errs[k] = g_err;
     });
   }
   for (auto &t : pool) t.join();
-  for (int d = 0; d < ndev; ++d)
-    if (rcs[d] != LIFEAPI_OK) {
-      g_err = errs[d];
-      return rcs[d];
+  for (int k = 0; k < shards; ++k)
+    if (rcs[k] != LIFEAPI_OK) {
+      g_err = errs[k];
+      return rcs[k];
     }
   return LIFEAPI_OK;
 }

@@ -42,21 +42,41 @@ __global__ __launch_bounds__(kBlock) void k_pop(const uint64_t *__restrict__ s,
   }
 }
 
-// build-defined universe hash: mix(sum_x mix(s[x] + (x+1)*G))
-__global__ __launch_bounds__(kBlock) void k_hash(const uint64_t *__restrict__ s,
-                                                 uint64_t *__restrict__ h, uint64_t n) {
+// build-defined universe hash: mix(sum_x mix(s[x] + (x+1)*G)).  The
+// per-word mix is heavy (four 64-bit multiplies), so the cross-lane sum must
+// be cheap: kHashU = 8 universes per wave, loaded lane = column (coalesced),
+// mixed, then transposed through LDS so that each 8-lane DPP group sums one
+// universe (8 values per lane, then 3 butterfly levels) -- one tree for all 8
+// universes instead of one per universe, and no v_readlane.  1M universes:
+// 0.122 -> 0.082 ms (4.5 -> 6.6 TB/s); 16M: 1.85 -> 1.38 ms (4.7 -> 6.3 TB/s)
+// against the per-universe DPP tree (profiles/r02/hash_ab.jsonl; one-shot
+// grid, every capped grid measured slower).
+constexpr int kHashU = 8;
+__global__ __launch_bounds__(kBlock) void k_hash(const uint64_t *__restrict__ s, uint64_t *__restrict__ h,
+                                                 uint64_t n) {
+  constexpr int LPU = kWave / kHashU;  // lanes per universe in the sum
+  __shared__ uint64_t buf[kWavesPerBlock][kHashU * kWave];
   const int lane = threadIdx.x & (kWave - 1);
-  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock * kRedU;
-  for (uint64_t u0 = ((uint64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave) * kRedU; u0 < n;
-       u0 += stride) {
-    uint64_t m[kRedU];
+  const int wib = threadIdx.x / kWave;
+  uint64_t *b = buf[wib];
+  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock * kHashU;
+  const uint64_t g = (uint64_t)(lane + 1) * kGolden;
+  for (uint64_t u0 = ((uint64_t)blockIdx.x * kWavesPerBlock + wib) * kHashU; u0 < n; u0 += stride) {
+    uint64_t m[kHashU];
 #pragma unroll
-    for (int k = 0; k < kRedU; ++k) m[k] = u0 + k < n ? ld_state(s + (u0 + k) * kWave + lane) : 0ull;
+    for (int k = 0; k < kHashU; ++k) m[k] = u0 + k < n ? ld_state(s + (u0 + k) * kWave + lane) : 0ull;
 #pragma unroll
-    for (int k = 0; k < kRedU; ++k) {
-      const uint64_t t = wave_sum_u64_dpp(mix64(m[k] + (uint64_t)(lane + 1) * kGolden));
-      if (lane == 0 && u0 + k < n) h[u0 + k] = mix64(t);
-    }
+    for (int k = 0; k < kHashU; ++k) b[k * kWave + lane] = mix64(m[k] + g);
+    __builtin_amdgcn_wave_barrier();
+    const int u = lane / LPU, j = (lane % LPU) * kHashU;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < kHashU; ++k) acc += b[u * kWave + j + k];
+    __builtin_amdgcn_wave_barrier();  // (the next iteration's writes come after these reads)
+    acc += dpp_mov64<0xB1>(acc);   // quad_perm [1,0,3,2]
+    acc += dpp_mov64<0x4E>(acc);   // quad_perm [2,3,0,1]
+    acc += dpp_mov64<0x141>(acc);  // row_half_mirror: the 8-lane sum in every lane
+    if (lane % LPU == 0 && u0 + u < n) h[u0 + u] = mix64(acc);
   }
 }
 
@@ -111,7 +131,7 @@ int lifeapi_hash_batch_dev(const uint64_t *d_states, uint64_t *d_hash, size_t n,
     return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_hash_batch_dev%s");
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
-  hipLaunchKernelGGL(k_hash, dim3(grid_for((n + kRedU - 1) / kRedU, cus, kRedBlocksPerCU)), dim3(kBlock), 0,
+  hipLaunchKernelGGL(k_hash, dim3(grid_for((n + kHashU - 1) / kHashU, cus, 0)), dim3(kBlock), 0,
                      (hipStream_t)stream, d_states, d_hash, (uint64_t)n);
   return launched("k_hash launch");
 }

@@ -1,0 +1,54 @@
+"""GPU: the multi-device branch of the host-pointer lifeapi_step_batch
+(device = -1: contiguous shards, one host thread each, the arrays pinned once
+for all shards; host.hip).  A 1-GPU box has one device, so the shard count is
+forced with LIFEAPI_HOST_SHARDS (shard s on device s mod ndev): the threads,
+the shard arithmetic and the shared pins all run as they would over 8 GPUs.  Checked against the reference's own Step() (oracle/_ref)
+where built, else the C port."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def shards(monkeypatch):
+    def set_(k):
+        monkeypatch.setenv("LIFEAPI_HOST_SHARDS", str(k))
+    return set_
+
+
+@pytest.fixture(scope="module")
+def stepper():
+    from oracle.oracle import Port, Ref
+    return Ref() if Ref.available() else Port()
+
+
+@pytest.mark.parametrize("k", [2, 3, 8])
+@pytest.mark.parametrize("n,gens", [(1, 1), (7, 3), (4099, 1), (20001, 5), (70000, 1)])
+def test_sharded_host_step(hip, stepper, shards, k, n, gens):
+    shards(k)
+    from oracle.oracle import Port
+    x = Port().fill(n, seed=900 + n + k)
+    got = hip.step_host(x, gens, device=-1)
+    assert (got == stepper.step_batch(x, gens)).all()
+
+
+def test_sharded_in_place_large(hip, stepper, shards):
+    # > kPinMinBytes, so the call pins the arrays once for all 4 shard threads
+    shards(4)
+    from oracle.oracle import Port
+    x = Port().fill(40000, seed=4242)
+    want = stepper.step_batch(x, 2)
+    hip.step_host(x, 2, device=-1, out=x)
+    assert (x == want).all()
+
+
+def test_bad_device_index(hip):
+    x = np.zeros((2, 64), np.uint64)
+    with pytest.raises(hip.LifeApiError) as e:
+        hip.step_host(x, 1, device=hip.device_count())
+    assert e.value.code == -2
+    with pytest.raises(hip.LifeApiError):
+        hip.step_host(x, 1, device=-2)

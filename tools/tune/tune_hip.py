@@ -63,3 +63,30 @@ def step(states: torch.Tensor, out: torch.Tensor | None = None, generations: int
                                                    hip._stream(stream),
                                                    ctypes.byref(cfg) if cfg is not None else None))
     return out
+
+
+lib.lifeapi_tune_step_clock.argtypes = [_vp, _vp, _sz, _u32, _vp, _vp]
+lib.lifeapi_tune_step_clock.restype = _int
+
+
+def step_clock(states: torch.Tensor, out: torch.Tensor, generations: int, stream=None):
+    """The shipped gens > 2 kernel with clock stamps; returns (out, stamps
+    int64 (waves, 4): t0, q0, t1, q1)."""
+    n = hip._universes(states)
+    stamps = torch.zeros(((n + 3) // 4, 4), dtype=torch.int64, device=states.device)
+    hip._check(lib.lifeapi_tune_step_clock(states.data_ptr(), out.data_ptr(), n, generations,
+                                           hip._stream(stream), stamps.data_ptr()))
+    return out, stamps
+
+
+lib.lifeapi_tune_hash.argtypes = [_vp, _vp, _sz, _int, _int, _vp]
+lib.lifeapi_tune_hash.restype = _int
+
+
+def hash_variant(states: torch.Tensor, variant: int, blocks_per_cu: int = 0, out=None, stream=None):
+    n = hip._universes(states)
+    if out is None:
+        out = torch.empty(n, dtype=torch.int64, device=states.device)
+    hip._check(lib.lifeapi_tune_hash(states.data_ptr(), out.data_ptr(), n, variant, blocks_per_cu,
+                                     hip._stream(stream)))
+    return out

@@ -356,9 +356,63 @@ StepFn pick_step(const lifeapi_launch_cfg &c) {
   }
 }
 
+// Diagnostic build of the shipped gens > 2 kernel (k_step_split<8, 1, NT,
+// 6, kAsmLoop>): the same load / layout change / assembly loop / store, with
+// the shader clock (s_memtime) and the 100 MHz real-time counter
+// (s_memrealtime) stamped around the generation loop of every wave, lane 0
+// writing {t0, q0, t1, q1} to a stamp buffer nothing else reads
+// (MI355X_MICROARCH.md, DVFS item 6).  The held clock is
+// (t1 - t0) / (q1 - q0) x 100 MHz.
+template <bool NT>
+__global__ __launch_bounds__(kBlock) void k_step_split_clock(const uint64_t *in, uint64_t *out, uint64_t n,
+                                                             uint32_t gens, uint64_t *stamps) {
+  constexpr int S = 8, P = 4;
+  __shared__ uint32_t lds[kWavesPerBlock * S * kWave];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerBlock + wib;
+  const uint64_t u0 = wave * P;
+  if (u0 >= n) return;
+  uint32_t r[S];
+  W c[P];
+#pragma unroll
+  for (int u = 0; u < P; ++u) c[u] = u0 + u < n ? ld<NT>(in + (u0 + u) * kWave + lane) : W{0u, 0u};
+  Split<S>::load(c, r);
+  const uint32_t base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)(lds + wib * S * kWave);
+  const uint32_t self = base + lane * 16u, prev = base + ((lane + kWave - 1) & (kWave - 1)) * 16u,
+                 next = base + ((lane + 1) & (kWave - 1)) * 16u;
+  const uint64_t t0 = __builtin_amdgcn_s_memtime(), q0 = __builtin_amdgcn_s_memrealtime();
+  split_gens_asm_v0(r, gens, self, prev, next);
+  const uint64_t t1 = __builtin_amdgcn_s_memtime(), q1 = __builtin_amdgcn_s_memrealtime();
+  Split<S>::store(r, c);
+#pragma unroll
+  for (int u = 0; u < P; ++u)
+    if (u0 + u < n) st<NT>(out + (u0 + u) * kWave + lane, c[u]);
+  if (lane == 0) {
+    stamps[wave * 4 + 0] = t0;
+    stamps[wave * 4 + 1] = q0;
+    stamps[wave * 4 + 2] = t1;
+    stamps[wave * 4 + 3] = q1;
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+/* the shipped gens > 2 kernel with clock stamps (see k_step_split_clock);
+ * d_stamps: 4 words per wave, one wave per 4 universes, one-shot grid      */
+int lifeapi_tune_step_clock(const uint64_t *d_in, uint64_t *d_out, size_t n, uint32_t generations,
+                            void *stream, uint64_t *d_stamps) {
+  int rc = check_batch(d_in, d_out, n);
+  if (rc != LIFEAPI_OK || n == 0) return rc;
+  if (!d_stamps) return fail(LIFEAPI_E_INVALID, "null stamp buffer%s");
+  const uint64_t waves = (n + 3) / 4;
+  hipLaunchKernelGGL(generations < 32 ? k_step_split_clock<true> : k_step_split_clock<false>,
+                     dim3((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock)), dim3(kBlock), 0,
+                     (hipStream_t)stream, d_in, d_out, (uint64_t)n, generations, d_stamps);
+  return launched("k_step_split_clock launch");
+}
 
 void lifeapi_tune_default_cfg(lifeapi_launch_cfg *cfg, uint32_t generations) {
   if (!cfg) return;
