@@ -5,6 +5,7 @@
 #include "device.hpp"
 #include "host.hpp"
 #include "split_layout.hpp"
+#include "stable_kernels.hpp"
 
 using namespace lifeapi_impl;
 
@@ -190,211 +191,6 @@ __global__ __launch_bounds__(kBlock) void k_weld_split(uint64_t *__restrict__ we
   }
 }
 
-// ---- LifeStable passes --------------------------------
-// One wave per LifeStable: lane x holds column x of its 10 planes {state,
-// unknown, live2, live3, dead0, dead1, dead2, dead4, dead5, dead6}
-// (LifeStable.hpp:41-53; options "1 = ruled out").  The espresso fragments
-// the passes #include (bitslicing/stable_count.hpp, stable_signal.hpp) are
-// v_bitop3 networks generated by tools/synth_sop.py from their complete
-// truth tables.  Whole-universe tests (abort, changed) are wave ballots.
-
-__device__ __forceinline__ W operator&(W a, W b) { return W{a.lo & b.lo, a.hi & b.hi}; }
-__device__ __forceinline__ W operator|(W a, W b) { return W{a.lo | b.lo, a.hi | b.hi}; }
-__device__ __forceinline__ W operator~(W a) { return W{~a.lo, ~a.hi}; }
-__device__ __forceinline__ bool wave_any(W a) { return __ballot((a.lo | a.hi) != 0u) != 0ull; }
-
-// all four bits of the inclusive 3x3 count (NeighbourCount.hpp:40-70)
-__device__ __forceinline__ void ncount4(W a, W &b3, W &b2, W &b1, W &b0) {
-  W L, R;
-  neighbour_cols<XDPP>(a, L, R, nullptr, 0);
-  const W h0 = lut3<kXor3>(L, a, R), h1 = lut3<kMaj>(L, a, R);
-  const W h0u = rot_up(h0), h0d = rot_dn(h0), h1u = rot_up(h1), h1d = rot_dn(h1);
-  const W fs = lut3<kXor3>(h0u, h0, h0d), fc = lut3<kMaj>(h0u, h0, h0d);
-  const W cs = lut3<kXor3>(h1u, h1, h1d), cc = lut3<kMaj>(h1u, h1, h1d);
-  constexpr uint32_t kAnd3 = (TA & TB & TC) & 0xFF;
-  b0 = fs;
-  b1 = W{fc.lo ^ cs.lo, fc.hi ^ cs.hi};
-  b2 = lut3<kCarry2>(cc, fc, cs);
-  b3 = lut3<kAnd3>(cc, fc, cs);
-}
-
-// LifeState::ZOIHollow (LifeAPI.hpp:541-562): the 8 neighbours' OR
-__device__ __forceinline__ W zoi_hollow(W s) {
-  const W m = rot_up(s) | rot_dn(s);
-  const W t = s | m;
-  W L, R;
-  neighbour_cols<XDPP>(t, L, R, nullptr, 0);
-  return L | m | R;
-}
-
-template <class T>
-__device__ __forceinline__ void stable_count_circuit(const T (&x)[9], T &l2, T &l3, T &d0, T &d1,
-                                                     T &d2, T &d4, T &d5, T &d6, T &abort) {
-#include "stable_count_circuit.inc"
-}
-template <class T>
-__device__ __forceinline__ void stable_signal_circuit(const T (&x)[17], T &signaloff, T &signalon,
-                                                      T &centeroff, T &centeron) {
-#include "stable_signal_circuit.inc"
-}
-
-// stable_vulnerable.hpp (LifeStable.hpp:400), 15 in / 4 out, same pipeline
-template <class T>
-__device__ __forceinline__ void stable_vulnerable_circuit(const T (&x)[15], T &vulnerable_on,
-                                                          T &vulnerable_off, T &vulnerable_center_on,
-                                                          T &vulnerable_center_off) {
-#include "stable_vulnerable_circuit.inc"
-}
-
-enum { PST, PUN, PL2, PL3, PD0, PD1, PD2, PD4, PD5, PD6 };
-
-// SynchroniseStateKnown, LifeStable.hpp:526-556
-__device__ __forceinline__ int stable_sync(W (&p)[10]) {
-  const W known_on = ~p[PUN] & p[PST];
-  const W maybe_dead = ~(p[PD0] & p[PD1] & p[PD2] & p[PD4] & p[PD5] & p[PD6]);
-  W changes = maybe_dead & known_on;
-#pragma unroll
-  for (int k = PD0; k <= PD6; ++k) p[k] = p[k] | known_on;
-  const W known_off = ~p[PUN] & ~p[PST];
-  const W maybe_live = ~(p[PL2] & p[PL3]);
-  changes = changes | (maybe_live & known_off);
-  p[PL2] = p[PL2] | known_off;
-  p[PL3] = p[PL3] | known_off;
-  if (wave_any(~maybe_live & ~maybe_dead)) return 0;
-  changes = changes | (~p[PST] & (maybe_live & ~maybe_dead));
-  p[PST] = p[PST] | (maybe_live & ~maybe_dead);
-  changes = changes | (~p[PUN] & (maybe_live & maybe_dead));
-  p[PUN] = p[PUN] & (maybe_live & maybe_dead);
-  return 1 | (wave_any(changes) ? 2 : 0);
-}
-
-// UpdateOptions, LifeStable.hpp:558-615 (stable_count.hpp at :591)
-__device__ __forceinline__ int stable_options(W (&p)[10]) {
-  const W off = ~p[PUN] & ~p[PST];
-  W s3, s2, s1, s0, o3, o2, o1, o0;
-  ncount4(p[PST], s3, s2, s1, s0);
-  ncount4(off, o3, o2, o1, o0);
-  const W x[9] = {s2, s1, s0, o3, o2, o1, o0, p[PST], off};
-  W r[8], ab;
-  stable_count_circuit(x, r[0], r[1], r[2], r[3], r[4], r[5], r[6], r[7], ab);
-  W changes = W{0u, 0u};
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    changes = changes | (r[k] & ~p[PL2 + k]);
-    p[PL2 + k] = p[PL2 + k] | r[k];
-  }
-  return (wave_any(ab) ? 0 : 1) | (wave_any(changes) ? 2 : 0);
-}
-
-// SignalNeighbours, LifeStable.hpp:617-675 (stable_signal.hpp at :654),
-// then SetOff / SetOn (:320-335)
-__device__ __forceinline__ int stable_signal(W (&p)[10]) {
-  W s3, s2, s1, s0, m3, m2, m1, m0;
-  ncount4(p[PST], s3, s2, s1, s0);
-  ncount4(p[PST] | p[PUN], m3, m2, m1, m0);
-  const W x[17] = {p[PL2], p[PL3], p[PD0], p[PD1], p[PD2], p[PD4], p[PD5], p[PD6], s2, s1, s0,
-                   m3, m2, m1, m0, p[PST], p[PUN]};
-  W soff, son, coff, con;
-  stable_signal_circuit(x, soff, son, coff, con);
-  const W off_zoi = zoi_hollow(soff) | coff, on_zoi = zoi_hollow(son) | con;
-  if (wave_any(off_zoi & on_zoi & p[PUN])) return 0;
-  const W changes = (off_zoi & p[PUN]) | (on_zoi & p[PUN]);
-  const W w_off = off_zoi & p[PUN];
-  p[PST] = p[PST] & ~w_off;
-  p[PUN] = p[PUN] & ~w_off;
-  p[PL2] = p[PL2] | w_off;
-  p[PL3] = p[PL3] | w_off;
-  const W w_on = on_zoi & p[PUN];
-  p[PST] = p[PST] | w_on;
-  p[PUN] = p[PUN] & ~w_on;
-#pragma unroll
-  for (int k = PD0; k <= PD6; ++k) p[k] = p[k] | w_on;
-  return 1 | (wave_any(changes) ? 2 : 0);
-}
-
-// PropagateStep, LifeStable.hpp:695-716
-__device__ __forceinline__ int stable_step(W (&p)[10]) {
-  const int k = stable_sync(p);
-  if (!(k & 1)) return 0;
-  const int o = stable_options(p);
-  if (!(o & 1)) return 0;
-  const int s = stable_signal(p);
-  if (!(s & 1)) return 0;
-  return 1 | ((k | o | s) & 2);
-}
-
-// PASS 0..3: one pass; 4: Propagate (LifeStable.hpp:718-729), at most
-// max_iters PropagateSteps (flag bit 2 set if that bound stopped it).
-template <int PASS>
-__global__ __launch_bounds__(kBlock) void k_stable(uint64_t *__restrict__ planes,
-                                                   uint8_t *__restrict__ flags, uint64_t n,
-                                                   uint32_t max_iters) {
-  const int lane = threadIdx.x & (kWave - 1);
-  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock;
-  for (uint64_t u = (uint64_t)blockIdx.x * kWavesPerBlock + wib; u < n; u += stride) {
-    uint64_t *q = planes + u * 10 * kWave + lane;
-    W p[10];
-#pragma unroll
-    for (int k = 0; k < 10; ++k) p[k] = ld<true>(q + k * kWave);
-    int r;
-    if constexpr (PASS == 0) r = stable_sync(p);
-    else if constexpr (PASS == 1) r = stable_options(p);
-    else if constexpr (PASS == 2) r = stable_signal(p);
-    else if constexpr (PASS == 3) r = stable_step(p);
-    else if constexpr (PASS == 5) {  // StabiliseOptions (LifeStable.hpp:677-693)
-      int ever = 0;
-      r = -1;
-      for (uint32_t it = 0; it < max_iters; ++it) {
-        const int k = stable_sync(p);
-        if (!(k & 1)) { r = 0; break; }
-        const int o = stable_options(p);
-        if (!(o & 1)) { r = 0; break; }
-        if (!((k | o) & 2)) { r = 1 | ever; break; }
-        ever = 2;
-      }
-      if (r < 0) r = 1 | ever | 4;
-    } else {
-      int ever = 0;
-      r = -1;
-      for (uint32_t it = 0; it < max_iters; ++it) {
-        const int s = stable_step(p);
-        if (!(s & 1)) { r = 0; break; }
-        if (!(s & 2)) { r = 1 | ever; break; }
-        ever = 2;
-      }
-      if (r < 0) r = 1 | ever | 4;
-    }
-#pragma unroll
-    for (int k = 0; k < 10; ++k) st<true>(q + k * kWave, p[k]);
-    if (lane == 0) flags[u] = (uint8_t)r;
-  }
-}
-
-// LifeStable::Vulnerable() (LifeStable.hpp:366-412), one wave per
-// LifeStable: the cells whose neighbourhood admits both an ON and an OFF
-// stable completion.  Reads the 10 planes, writes one LifeState.
-__global__ __launch_bounds__(kBlock) void k_stable_vulnerable(const uint64_t *__restrict__ planes,
-                                                              uint64_t *__restrict__ out, uint64_t n) {
-  const int lane = threadIdx.x & (kWave - 1);
-  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock;
-  for (uint64_t u = (uint64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave; u < n; u += stride) {
-    const uint64_t *q = planes + u * 10 * kWave + lane;
-    W p[10];
-#pragma unroll
-    for (int k = 0; k < 10; ++k) p[k] = ld<true>(q + k * kWave);
-    W s3, s2, s1, s0, u3, u2, u1, u0;
-    ncount4(p[PST], s3, s2, s1, s0);
-    ncount4(p[PUN], u3, u2, u1, u0);
-    const W x[15] = {p[PL2], p[PL3], p[PD0], p[PD1], p[PD2], p[PD4], p[PD5], p[PD6],
-                     s2,     s1,     s0,     u3,     u2,     u1,     u0};
-    W von, voff, vcon, vcoff;
-    stable_vulnerable_circuit(x, von, voff, vcon, vcoff);
-    const W on = zoi_hollow(von) | vcon, off = zoi_hollow(voff) | vcoff;
-    st<true>(out + u * kWave + lane, on & off);
-  }
-}
-
 // ---- config 5: the unknown_step_refined ternary step --------------------
 
 // bitslicing/unknown_step_refined.hpp:1-85 as a v_bitop3 network.  The
@@ -482,6 +278,8 @@ __global__ __launch_bounds__(kBlock, OCC > 0 ? OCC : 1) void k_refined(
 
 extern "C" {
 
+constexpr int kStableBlocksPerCU = 32;  // LifeStable kernels' grid cap (see below)
+
 static int counts_launch(const uint64_t *d_in, uint64_t *d_out, size_t n, int mode, void *stream) {
   if (n == 0) return LIFEAPI_OK;
   if (!d_in || !d_out || !aligned8(d_in) || !aligned8(d_out))
@@ -510,10 +308,13 @@ int lifeapi_stable_pass_batch_dev(uint64_t *d_planes, uint8_t *d_flags, size_t n
   if (rc != LIFEAPI_OK) return rc;
   using Fn = void (*)(uint64_t *, uint8_t *, uint64_t, uint32_t);
   const Fn fns[6] = {k_stable<0>, k_stable<1>, k_stable<2>, k_stable<3>, k_stable<4>, k_stable<5>};
-  // Single passes run best on a 32-blocks-per-CU grid that loops over the
-  // batch (+3..7 %, measured); Propagate's data-dependent iteration counts
-  // want one wave per universe instead.
-  hipLaunchKernelGGL(fns[pass], dim3(grid_for(n, cus, pass == 4 ? 0 : 32)), dim3(kBlock), 0, (hipStream_t)stream,
+  // Every pass, the looping ones (Propagate, StabiliseOptions) included,
+  // runs on a 32-blocks-per-CU grid that loops over the batch: on still
+  // lifes and soups around an unknown window with fresh options (the state a
+  // search propagates from) and on random planes, 64K LifeStables each, it
+  // is as fast as or up to 4 % faster than one wave per LifeStable, and
+  // 16 blocks per CU is slower (profiles/r02/stable_grid_ab.jsonl).
+  hipLaunchKernelGGL(fns[pass], dim3(grid_for(n, cus, kStableBlocksPerCU)), dim3(kBlock), 0, (hipStream_t)stream,
                      d_planes, d_flags, (uint64_t)n, max_iters ? max_iters : 1u << 20);
   return launched("k_stable launch");
 }
@@ -526,7 +327,9 @@ int lifeapi_stable_vulnerable_batch_dev(const uint64_t *d_planes, uint64_t *d_ou
   if (b < a + n * 10 * 512 && a < b + n * 512) return fail(LIFEAPI_E_INVALID, "out overlaps planes%s");
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
-  hipLaunchKernelGGL(k_stable_vulnerable, dim3(grid_for(n, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream,
+  // the same grid as the passes (2-5 % faster than one wave per LifeStable,
+  // profiles/r02/stable_grid_ab.jsonl)
+  hipLaunchKernelGGL(k_stable_vulnerable, dim3(grid_for(n, cus, kStableBlocksPerCU)), dim3(kBlock), 0, (hipStream_t)stream,
                      d_planes, d_out, (uint64_t)n);
   return launched("k_stable_vulnerable launch");
 }

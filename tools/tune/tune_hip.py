@@ -90,3 +90,26 @@ def hash_variant(states: torch.Tensor, variant: int, blocks_per_cu: int = 0, out
     hip._check(lib.lifeapi_tune_hash(states.data_ptr(), out.data_ptr(), n, variant, blocks_per_cu,
                                      hip._stream(stream)))
     return out
+
+
+lib.lifeapi_tune_stable_pass.argtypes = [_vp, _vp, _sz, _int, _u32, _int, _vp]
+lib.lifeapi_tune_stable_pass.restype = _int
+lib.lifeapi_tune_stable_vulnerable.argtypes = [_vp, _vp, _sz, _int, _vp]
+lib.lifeapi_tune_stable_vulnerable.restype = _int
+
+
+def stable_pass(planes: torch.Tensor, which: int, blocks_per_cu: int, max_iters: int = 0, stream=None):
+    n = planes.numel() // (10 * 64)
+    flags = torch.empty(n, dtype=torch.uint8, device=planes.device)
+    hip._check(lib.lifeapi_tune_stable_pass(planes.data_ptr(), flags.data_ptr(), n, which, max_iters,
+                                            blocks_per_cu, hip._stream(stream)))
+    return flags
+
+
+def stable_vulnerable(planes: torch.Tensor, blocks_per_cu: int, out=None, stream=None):
+    n = planes.numel() // (10 * 64)
+    if out is None:
+        out = torch.empty((n, 64), dtype=torch.int64, device=planes.device)
+    hip._check(lib.lifeapi_tune_stable_vulnerable(planes.data_ptr(), out.data_ptr(), n, blocks_per_cu,
+                                                  hip._stream(stream)))
+    return out

@@ -1,0 +1,38 @@
+// tune_stencils.hip -- TUNING build: the LifeStable kernels of the product
+// (stable_kernels.hpp) launched on an explicit grid, for the grid-cap A/Bs
+// behind stencils.hip's launch choices (tools/stable_grid_ab.py).
+#include "lifeapi_tune.h"
+#include "host.hpp"
+#include "stable_kernels.hpp"
+
+using namespace lifeapi_impl;
+
+extern "C" {
+
+int lifeapi_tune_stable_pass(uint64_t *d_planes, uint8_t *d_flags, size_t n, int pass, uint32_t max_iters,
+                             int blocks_per_cu, void *stream) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!d_planes || !d_flags || !aligned8(d_planes) || pass < 0 || pass > 5)
+    return fail(LIFEAPI_E_INVALID, "bad argument to lifeapi_tune_stable_pass%s");
+  int cus = 0, rc = device_cus(cus);
+  if (rc != LIFEAPI_OK) return rc;
+  using Fn = void (*)(uint64_t *, uint8_t *, uint64_t, uint32_t);
+  const Fn fns[6] = {k_stable<0>, k_stable<1>, k_stable<2>, k_stable<3>, k_stable<4>, k_stable<5>};
+  hipLaunchKernelGGL(fns[pass], dim3(grid_for(n, cus, blocks_per_cu)), dim3(kBlock), 0, (hipStream_t)stream,
+                     d_planes, d_flags, (uint64_t)n, max_iters ? max_iters : 1u << 20);
+  return launched("k_stable (tuning) launch");
+}
+
+int lifeapi_tune_stable_vulnerable(const uint64_t *d_planes, uint64_t *d_out, size_t n, int blocks_per_cu,
+                                   void *stream) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!d_planes || !d_out || !aligned8(d_planes) || !aligned8(d_out))
+    return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_tune_stable_vulnerable%s");
+  int cus = 0, rc = device_cus(cus);
+  if (rc != LIFEAPI_OK) return rc;
+  hipLaunchKernelGGL(k_stable_vulnerable, dim3(grid_for(n, cus, blocks_per_cu)), dim3(kBlock), 0,
+                     (hipStream_t)stream, d_planes, d_out, (uint64_t)n);
+  return launched("k_stable_vulnerable (tuning) launch");
+}
+
+}  // extern "C"
