@@ -113,3 +113,14 @@ def stable_vulnerable(planes: torch.Tensor, blocks_per_cu: int, out=None, stream
     hip._check(lib.lifeapi_tune_stable_vulnerable(planes.data_ptr(), out.data_ptr(), n, blocks_per_cu,
                                                   hip._stream(stream)))
     return out
+
+
+lib.lifeapi_tune_step_pair.argtypes = [_vp, _vp, _sz, _u32, _int, _vp]
+lib.lifeapi_tune_step_pair.restype = _int
+
+
+def step_pair(states: torch.Tensor, out: torch.Tensor, generations: int, variant: int = 0, stream=None):
+    n = hip._universes(states)
+    hip._check(lib.lifeapi_tune_step_pair(states.data_ptr(), out.data_ptr(), n, generations, variant,
+                                          hip._stream(stream)))
+    return out

@@ -11,6 +11,7 @@
 #include "lifeapi_tune.h"
 #include "step_kernels.hpp"
 #include "tile_asm.inc"
+#include "pair_asm.inc"
 
 using namespace lifeapi_impl;
 
@@ -396,9 +397,84 @@ __global__ __launch_bounds__(kBlock) void k_step_split_clock(const uint64_t *in,
   }
 }
 
+// The pair layout (tools/gen_pair_asm.py): two adjacent columns per lane, 32
+// lanes and 4 interleaved universes per group, 2 groups (8 universes) per
+// wave; the exchange moves only the outer columns.  V = schedule.  The
+// assembly loop pins v0..v63, so nothing lane-varying may stay live across
+// it: the lane index is re-derived afterwards (v_mbcnt, opaque to CSE) and
+// every address is rebuilt from it and wave-uniform scalars.
+__device__ __forceinline__ uint32_t lane_id_fresh() {
+  uint32_t l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n v_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+template <bool NT, int V>
+__global__ __launch_bounds__(kBlock) void k_step_pair(const uint64_t *in, uint64_t *out, uint64_t n, uint32_t gens) {
+  constexpr int S = 8, P = 4;
+  __shared__ uint32_t lds[kWavesPerBlock * 1024];  // 4 KiB per wave
+  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock * 2 * P;
+  for (uint64_t u0 = ((uint64_t)blockIdx.x * kWavesPerBlock + wib) * 2 * P; u0 < n; u0 += stride) {
+    const uint32_t room = n - u0 < 2 * P ? (uint32_t)(n - u0) : 2 * P;  // wave-uniform
+    uint32_t a[S], b[S];
+    {
+      const uint32_t lane = lane_id_fresh(), grp = lane >> 5, i = lane & 31;
+      const uint64_t *src = in + u0 * kWave;
+      W c0[P], c1[P];
+#pragma unroll
+      for (int u = 0; u < P; ++u) {
+        u64x2 v = {0, 0};
+        if (grp * P + u < room) v = ld2<NT>(src + ((grp * P + u) * kWave + 2 * i));
+        c0[u] = split(v[0]);
+        c1[u] = split(v[1]);
+      }
+      Split<S>::load(c0, a);
+      Split<S>::load(c1, b);
+    }
+    {
+      const uint32_t lane = lane_id_fresh();
+      const uint32_t base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)(lds + wib * 1024);
+      const uint32_t self = base + lane * 16u, prev = base + ((lane & 32) | ((lane + 31) & 31)) * 16u,
+                     next = base + ((lane & 32) | ((lane + 1) & 31)) * 16u;
+      if constexpr (V == 0) pair_gens_asm_v0(a, b, gens, self, prev, next);
+      else if constexpr (V == 1) pair_gens_asm_v1(a, b, gens, self, prev, next);
+      else if constexpr (V == 2) pair_gens_asm_v2(a, b, gens, self, prev, next);
+      else pair_gens_asm_v3(a, b, gens, self, prev, next);
+    }
+    {
+      const uint32_t lane = lane_id_fresh(), grp = lane >> 5, i = lane & 31;
+      uint64_t *dst = out + u0 * kWave;
+      W c0[P], c1[P];
+      Split<S>::store(a, c0);
+      Split<S>::store(b, c1);
+#pragma unroll
+      for (int u = 0; u < P; ++u)
+        if (grp * P + u < room) st2<NT>(dst + ((grp * P + u) * kWave + 2 * i), u64x2{join(c0[u]), join(c1[u])});
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+/* the pair layout (k_step_pair), schedule `variant` 0..3 */
+int lifeapi_tune_step_pair(const uint64_t *d_in, uint64_t *d_out, size_t n, uint32_t generations, int variant,
+                           void *stream) {
+  int rc = check_batch(d_in, d_out, n);
+  if (rc != LIFEAPI_OK || n == 0) return rc;
+  int cus = 0;
+  rc = device_cus(cus);
+  if (rc != LIFEAPI_OK) return rc;
+  const bool nt = generations < 32;
+  using Fn = void (*)(const uint64_t *, uint64_t *, uint64_t, uint32_t);
+  const Fn fns[2][4] = {{k_step_pair<false, 0>, k_step_pair<false, 1>, k_step_pair<false, 2>, k_step_pair<false, 3>},
+                        {k_step_pair<true, 0>, k_step_pair<true, 1>, k_step_pair<true, 2>, k_step_pair<true, 3>}};
+  if (variant < 0 || variant > 3) return fail(LIFEAPI_E_INVALID, "unknown pair schedule%s");
+  hipLaunchKernelGGL(fns[nt][variant], dim3(grid_for((n + 7) / 8, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream,
+                     d_in, d_out, (uint64_t)n, generations);
+  return launched("k_step_pair launch");
+}
 
 /* the shipped gens > 2 kernel with clock stamps (see k_step_split_clock);
  * d_stamps: 4 words per wave, one wave per 4 universes, one-shot grid      */
