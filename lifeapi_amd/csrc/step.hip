@@ -35,91 +35,6 @@ __global__ __launch_bounds__(kBlock) void k_step_contains(const uint64_t *in, ui
   }
 }
 
-// The same on the 8-way split layout (k_step_split): 4 universes per wave.
-// The target is put into the same register layout once, replicated for the
-// 4 universes; after every generation (r ^ w) & (w | u) is OR-ed over the
-// registers and one ballot per universe (its bits are every P-th) tests it,
-// with no branch per universe.  The check costs about 5 VALU per
-// universe-generation on top of the 18 of the step (+20-25 % measured,
-// profiles/r01/contains_bench.jsonl); branching around the bookkeeping
-// when no universe is clean measured slower still.
-// Without d_final, a wave stops once all its universes have hit.
-constexpr uint32_t kDiff = ((TA ^ TB) & (TB | TC)) & 0xFF;  // (s ^ wanted) & (wanted | unwanted)
-constexpr int kContainsNet = 6;  // tail network of the fused kernel (as k_step's default, rule 11)
-// the fused kernel runs the assembly loop of split_asm.inc (split_contains_asm)
-// for gens > 2; the compiled loop above stays for comparison
-constexpr bool kContainsAsm = true;
-template <int S, int NET, bool ASM = false>
-__global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *in, uint64_t *fin,
-                                                                const uint64_t *__restrict__ wanted,
-                                                                const uint64_t *__restrict__ unwanted,
-                                                                uint32_t *__restrict__ first, uint64_t n,
-                                                                uint32_t gens) {
-  constexpr int P = S / 2;
-  constexpr uint32_t every = P == 1 ? ~0u : P == 2 ? 0x55555555u : P == 4 ? 0x11111111u : 0x01010101u;
-  __shared__ uint32_t lds[kWavesPerBlock * S * kWave];
-  const int lane = threadIdx.x & (kWave - 1);
-  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  uint32_t tw[S], tu[S];
-  {
-    W c[P];
-#pragma unroll
-    for (int u = 0; u < P; ++u) c[u] = split(wanted[lane]);
-    Split<S>::load(c, tw);
-#pragma unroll
-    for (int u = 0; u < P; ++u) c[u] = split(unwanted[lane]);
-    Split<S>::load(c, tu);
-  }
-  uint32_t tm[S];  // wanted | unwanted (the assembly loop's second target plane)
-#pragma unroll
-  for (int j = 0; j < S; ++j) tm[j] = tw[j] | tu[j];
-
-  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock * P;
-  for (uint64_t u0 = ((uint64_t)blockIdx.x * kWavesPerBlock + wib) * P; u0 < n; u0 += stride) {
-    uint32_t r[S];
-    W c[P];
-#pragma unroll
-    for (int u = 0; u < P; ++u) c[u] = u0 + u < n ? split(in[(u0 + u) * kWave + lane]) : W{0u, 0u};
-    Split<S>::load(c, r);
-    uint32_t hit[P];
-#pragma unroll
-    for (int u = 0; u < P; ++u) hit[u] = 0;
-    uint32_t found = 0;
-    if constexpr (ASM) {  // split_asm.inc: the default generation loop with the test fused in
-      static_assert(S == 8 && NET == 6, "split_contains_asm is rule 11");
-      const uint32_t base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)(
-          lds + wib * S * kWave);
-      split_contains_asm(r, tw, tm, gens, base + lane * 16u, base + ((lane + kWave - 1) & (kWave - 1)) * 16u,
-                         base + ((lane + 1) & (kWave - 1)) * 16u, hit);
-    } else for (uint32_t g = 1; g <= gens; ++g) {
-      gen_split<S, NET>(r, lds + wib * S * kWave, lane);
-      uint32_t d = 0;
-#pragma unroll
-      for (int j = 0; j < S; ++j) d |= lut3<kDiff>(r[j], tw[j], tu[j]);
-      // straight-line: a ballot per universe, the bookkeeping in scalar registers
-      uint32_t clean = 0;
-#pragma unroll
-      for (int u = 0; u < P; ++u) clean |= (__ballot((d & (every << u)) != 0) == 0 ? 1u : 0u) << u;
-      const uint32_t fresh = clean & ~found;
-#pragma unroll
-      for (int u = 0; u < P; ++u) hit[u] = (fresh >> u) & 1 ? g : hit[u];
-      found |= fresh;
-      if (!fin && found == (1u << P) - 1) break;
-    }
-    if (fin) {
-      Split<S>::store(r, c);
-#pragma unroll
-      for (int u = 0; u < P; ++u)
-        if (u0 + u < n) fin[(u0 + u) * kWave + lane] = join(c[u]);
-    }
-    if (lane == 0) {
-#pragma unroll
-      for (int u = 0; u < P; ++u)
-        if (u0 + u < n) first[u0 + u] = hit[u];
-    }
-  }
-}
-
 using StepFn = void (*)(const uint64_t *, uint64_t *, uint64_t, uint32_t);
 
 // The shipped configurations (profiles/r01/tune_*.jsonl):

@@ -6,6 +6,7 @@ import os
 import sys
 
 import numpy as np
+import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
@@ -54,9 +55,11 @@ def test_simulated_two_group_loop_is_step(port):
         assert (gb == _to_split(port.step_batch(y, gens))).all(), gens
 
 
-def test_simulated_contains_loop(port):
-    """split_contains_asm: the same generations plus, after each, the first
-    generation at which each universe contains the target (LifeTarget.hpp:44-51)."""
+@pytest.mark.parametrize("lean", [False, True])
+def test_simulated_contains_loop(port, lean):
+    """split_contains_asm[_lean]: the same generations plus, after each, the
+    first generation at which each universe contains the target
+    (LifeTarget.hpp:44-51)."""
     x = port.fill(4, seed=80) & port.fill(4, seed=81)
     blk = np.zeros(64, np.uint64)
     blk[20] = blk[21] = np.uint64(0b11 << 30)
@@ -69,8 +72,8 @@ def test_simulated_contains_loop(port):
     x[2][20] = np.uint64(0b111 << 30)                 # no block
     w = _to_split(np.stack([blk] * 4))
     m = _to_split(np.stack([blk | ring] * 4))
-    for gens in (1, 4):
-        got, hits = g.simulate_contains(_to_split(x), w, m, gens)
+    for gens in (1, 4, 9):
+        got, hits = g.simulate_contains(_to_split(x), w, m, gens, lean)
         s, exp = x.copy(), [0] * 4
         for k in range(1, gens + 1):
             s = port.step_batch(s, 1)

@@ -71,3 +71,36 @@ def test_bad_cfgs_rejected(tune, hip):
     for bad in [(10, 4, 8, 0, 0), (0, 3, 8, 0, 0), (0, 1, 8, 0, 5), (8, 1, 8, 0, 2)]:
         with pytest.raises(hip.LifeApiError):
             tune.step(d, generations=1, cfg=tune.LaunchCfg(*bad))
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("gens", [3, 6, 37])
+@pytest.mark.parametrize("with_final", [False, True])
+def test_step_contains_variants(tune, port, variant, gens, with_final):
+    """The fused Step + Contains kernels of the tuning build (0 compiled loop,
+    1 assembly loop, 2 lean bookkeeping = shipped) against the oracle's
+    step-then-Contains loop (LifeTarget.hpp:44-51), ragged n, planted hits."""
+    import torch
+    n = 1003
+    x = port.fill(n, seed=223) & port.fill(n, seed=224) & port.fill(n, seed=225)
+    blk = np.zeros(64, np.uint64)
+    blk[10] = blk[11] = np.uint64(0b11 << 40)
+    ring = np.zeros(64, np.uint64)
+    for c in (9, 10, 11, 12):
+        ring[c] = np.uint64(0b1111 << 39)
+    ring &= ~blk
+    x[::5] &= ~ring & ~blk
+    x[::10] |= blk
+    fin = torch.empty((n, 64), dtype=torch.int64, device="cuda") if with_final else None
+    got = tune.step_contains(to_dev(x), to_dev(blk[None]), to_dev(ring[None]), gens, variant, final=fin)
+    got = got.cpu().numpy()
+    exp = np.zeros(n, np.int64)
+    s = x.copy()
+    for g in range(1, gens + 1):
+        s = port.step_batch(s, 1)
+        hit = (((s ^ blk) & (blk | ring)) == 0).all(axis=1)
+        exp[(exp == 0) & hit] = g
+    assert (got == exp).all(), np.nonzero(got != exp)[0][:10]
+    assert (exp > 0).any()
+    if with_final:
+        assert (to_host(fin) == port.step_batch(x, gens)).all()

@@ -1,49 +1,57 @@
 #!/usr/bin/env python3
-"""Fused Step + Contains on the config-3 shape: this build's library against a
-previous build's (build/ab/liblifeapi_hip_prev.so), same inputs and process,
-HIP-event timing; checks both give the same first generations and states."""
-import ctypes
+"""Fused Step + Contains A/B on the config-3 shape (64K universes x 1024
+gens; and 4K x 4096 with hits): the plain shipped step, the shipped fused
+kernel, and the tuning build's variants (0 compiled loop, 1 assembly loop,
+2 assembly loop with lean SALU bookkeeping), launches interleaved after a
+2 s warm-up.  Results must equal the shipped fused kernel's."""
 import json
 import os
+import statistics
 import sys
+import time
 
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools", "tune"))
 import lifeapi_amd.hip as hip  # noqa: E402
+import tune_hip  # noqa: E402
 
-
-def main():
-    libs = {"current": hip.lib, "previous": ctypes.CDLL(os.path.join(ROOT, "build", "ab", "liblifeapi_hip_prev.so"))}
-    vp = ctypes.c_void_p
-    for L in libs.values():
-        L.lifeapi_step_contains_batch_dev.argtypes = [vp, vp, vp, vp, vp, ctypes.c_size_t, ctypes.c_uint32, vp]
-    n, g = 1 << 16, 1024
-    x = hip.fill_random(n, seed=3)
-    w = x[0:1].clone()  # a target that occurs: universe 0's own start state
-    u = torch.zeros_like(w)
-    stream = torch.cuda.current_stream().cuda_stream
-    res = {}
-    for rnd in range(3):
-        for name, L in libs.items():
-            first = torch.empty(n, dtype=torch.int32, device="cuda")
-            fin = torch.empty_like(x)
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record()
-            assert L.lifeapi_step_contains_batch_dev(x.data_ptr(), fin.data_ptr(), w.data_ptr(), u.data_ptr(),
-                                                     first.data_ptr(), n, g, stream) == 0
-            b.record()
-            b.synchronize()
-            res.setdefault(name, []).append(a.elapsed_time(b))
-            res[name + "_out"] = (first, fin)
-    assert torch.equal(res["current_out"][0], res["previous_out"][0])
-    assert torch.equal(res["current_out"][1], res["previous_out"][1])
-    for name in libs:
-        ms = sorted(res[name])[1]
-        print(json.dumps({"lib": name, "universes": n, "gens": g, "ms_median": ms,
-                          "universe_gen_per_s": n * g / ms * 1e3}), flush=True)
-
-
-if __name__ == "__main__":
-    main()
+n, g = 1 << 16, 1024
+x = hip.fill_random(n, seed=3)
+w = torch.zeros((1, 64), dtype=torch.int64, device="cuda")
+w[0, 10] = w[0, 11] = 3 << 40                       # a block ...
+u = torch.zeros((1, 64), dtype=torch.int64, device="cuda")
+for c in (9, 10, 11, 12):
+    u[0, c] = 15 << 39
+u &= ~w                                              # ... and its empty ring
+outs = {k: torch.empty_like(x) for k in ("step", "ship", "v0", "v1", "v2")}
+firsts = {}
+kern = {
+    "step": lambda: hip.step(x, out=outs["step"], generations=g),
+    "ship": lambda: firsts.__setitem__("ship", hip.step_contains(x, w, u, g, final=outs["ship"])[0]),
+}
+for v in range(3):
+    kern[f"v{v}"] = (lambda vv: lambda: firsts.__setitem__(
+        f"v{vv}", tune_hip.step_contains(x, w, u, g, vv, final=outs[f"v{vv}"])))(v)
+t0 = time.time()
+while time.time() - t0 < 2.0:
+    for f in kern.values():
+        f()
+    torch.cuda.synchronize()
+ms = {k: [] for k in kern}
+for _ in range(10):
+    for k, f in kern.items():
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        f()
+        e1.record()
+        e1.synchronize()
+        ms[k].append(e0.elapsed_time(e1))
+hits = int((firsts["ship"] > 0).sum().item())
+for k in kern:
+    same = None if k == "step" else bool(torch.equal(firsts[k], firsts["ship"]) and torch.equal(outs[k], outs["ship"]))
+    print(json.dumps({"kernel": k, "ms_median": statistics.median(ms[k]), "ms_min": min(ms[k]),
+                      "over_step": statistics.median(ms[k]) / statistics.median(ms["step"]),
+                      "equal_to_shipped": same, "universes_with_hit": hits}), flush=True)

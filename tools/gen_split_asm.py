@@ -282,7 +282,11 @@ OR3 = 0xFE         # a | b | c
 ORAND = 0xA8       # (a | b) & c
 
 
-def contains_check():
+def contains_check(lean=False):
+    """lean: the per-universe bookkeeping on the fast path is 2 SALU per
+    universe (s_cmp_eq_u64 + s_addc_u32 building the clean mask, universe 0
+    in bit 3) and one s_andn2 + branch; a hit (rare) branches to a slow path
+    that records it.  Otherwise 8 SALU per universe per generation."""
     al = Alloc()
     d = []
     for j in range(S):
@@ -294,6 +298,19 @@ def contains_check():
     lines += [op(x, d[0], d[1], d[2], OR3), op(y, d[3], d[4], d[5], OR3), op(z, d[6], d[7], x, OR3)]
     t = al.get(0)
     lines.append("s_add_u32 %[gc], %[gc], 1")
+    if lean:
+        ts = [t, al.get(1), al.get(2), al.get(3)]
+        for u in range(P):
+            lines += [f"v_bitop3_b32 v{ts[u]}, v{y}, v{z}, %[m{u}] bitop3:0x{ORAND:02x}",
+                      f"v_cmp_ne_u32_e64 %[cmp{u}], 0, v{ts[u]}"]
+        lines.append("s_mov_b32 %[c], 0")
+        for u in range(P):
+            lines += [f"s_cmp_eq_u64 %[cmp{u}], 0",       # SCC = universe u clean
+                      "s_addc_u32 %[c], %[c], %[c]"]      # c = 2c + SCC
+        lines += ["s_andn2_b32 %[c], %[c], %[found]",     # fresh hits; SCC = any
+                  "s_cbranch_scc1 3f",
+                  "4:"]
+        return lines
     for u in range(P):
         lines += [f"v_bitop3_b32 v{t}, v{y}, v{z}, %[m{u}] bitop3:0x{ORAND:02x}",
                   f"v_cmp_ne_u32_e64 %[cmp], 0, v{t}",
@@ -306,17 +323,34 @@ def contains_check():
     return lines
 
 
-def contains_body():
+def contains_slowpath():
+    """the lean check's hit handler, placed after the loop: record gc for
+    every fresh universe (bit 3 - u of c) and jump back"""
+    lines = ["3:", "s_or_b32 %[found], %[found], %[c]"]
+    for u in range(P):
+        lines += [f"s_bitcmp1_b32 %[c], {P - 1 - u}",
+                  f"s_cselect_b32 %[h{u}], %[gc], %[h{u}]"]
+    return lines + ["s_branch 4b"]
+
+
+def contains_body(lean=False):
     """the default schedule's body with the check after rows 6..7 (all eight
     rows final), before the plane-1 exchange"""
     b = body(DEFAULT)
     k = b.index(exchange(1)[0])
-    return b[:k] + contains_check() + b[k:]
+    return b[:k] + contains_check(lean) + b[k:]
 
 
-def emit_contains():
-    lines = ["s_cmp_eq_u32 %[g], 0", "s_cbranch_scc1 2f"] + prologue(DEFAULT) + ["1:"] + contains_body() + \
-        ["s_cmp_lg_u32 %[g], 0", "s_cbranch_scc1 1b", "s_waitcnt lgkmcnt(0)", "2:"]
+def contains_text(lean=False):
+    lines = ["s_cmp_eq_u32 %[g], 0", "s_cbranch_scc1 2f"] + prologue(DEFAULT) + ["1:"] + contains_body(lean) + \
+        ["s_cmp_lg_u32 %[g], 0", "s_cbranch_scc1 1b", "s_waitcnt lgkmcnt(0)"]
+    if lean:
+        lines += ["s_branch 2f"] + contains_slowpath()
+    return lines + ["2:"]
+
+
+def emit_contains(lean=False):
+    lines = contains_text(lean)
     asm = "\n".join(f'      "{l}\\n"' for l in lines)
     outs = ",\n".join([f'        "+{{v{R[j]}}}"(r[{j}])' for j in range(S)] +
                       [f'        [h{u}] "+s"(hit[{u}])' for u in range(P)])
@@ -325,20 +359,30 @@ def emit_contains():
                     [f'[m{u}] "s"(0x11111111u << {u})' for u in range(P)])
     pinned = sorted({x for x in L + RR + H1 + H0 + [H0U, H0D, H1U, H1D] + TEMPS})
     clob = ", ".join(f'"v{x}"' for x in pinned)
+    if lean:
+        name, cmps = "split_contains_asm_lean", "uint64_t cmp0, cmp1, cmp2, cmp3;"
+        cmp_outs = "[cmp0] \"=&s\"(cmp0), [cmp1] \"=&s\"(cmp1), [cmp2] \"=&s\"(cmp2), [cmp3] \"=&s\"(cmp3)"
+        doc = ("// The same with the per-universe bookkeeping cut to two SALU per universe on\n"
+               "// the fast path (the clean mask built by s_cmp + s_addc; hits branch to a\n"
+               "// slow path after the loop).")
+    else:
+        name, cmps = "split_contains_asm", "uint64_t cmp;"
+        cmp_outs = "[cmp] \"=&s\"(cmp)"
+        doc = ("// Fused Step + Contains on the default schedule: after every generation the\n"
+               "// containment test of all four universes (hit[u] = first generation whose\n"
+               "// state contains the target, 0 = none yet).  w / m: the target's wanted and\n"
+               f"// wanted | unwanted planes in the same register layout.  {N_VGPR_C} VGPRs pinned.")
     return f"""
-// Fused Step + Contains on the default schedule: after every generation the
-// containment test of all four universes (hit[u] = first generation whose
-// state contains the target, 0 = none yet).  w / m: the target's wanted and
-// wanted | unwanted planes in the same register layout.  {N_VGPR_C} VGPRs pinned.
-__device__ __forceinline__ void split_contains_asm(uint32_t (&r)[8], const uint32_t (&w)[8],
-                                                   const uint32_t (&m)[8], uint32_t gens, uint32_t a_self,
-                                                   uint32_t a_prev, uint32_t a_next, uint32_t (&hit)[4]) {{
+{doc}
+__device__ __forceinline__ void {name}(uint32_t (&r)[8], const uint32_t (&w)[8],
+                                   const uint32_t (&m)[8], uint32_t gens, uint32_t a_self,
+                                   uint32_t a_prev, uint32_t a_next, uint32_t (&hit)[4]) {{
   uint32_t gc = 0, found = 0, c;
-  uint64_t cmp;
+  {cmps}
   asm volatile(
 {asm}
       : {outs.strip()},
-        [g] "+s"(gens), [gc] "+s"(gc), [found] "+s"(found), [c] "=&s"(c), [cmp] "=&s"(cmp)
+        [g] "+s"(gens), [gc] "+s"(gc), [found] "+s"(found), [c] "=&s"(c), {cmp_outs}
       : "{{v{A_SELF}}}"(a_self), "{{v{A_PREV}}}"(a_prev), "{{v{A_NEXT}}}"(a_next),
         {ins}
       : {clob}, "scc", "memory");
@@ -346,17 +390,17 @@ __device__ __forceinline__ void split_contains_asm(uint32_t (&r)[8], const uint3
 """
 
 
-def simulate_contains(r, w, m, gens):
-    """numpy run of split_contains_asm: returns (r, hits[4])"""
+def simulate_contains(r, w, m, gens, lean=False):
+    """numpy run of split_contains_asm[_lean]: returns (r, hits[4])"""
     v = np.zeros((N_VGPR_C, 64), np.uint32)
     v[:8] = r
     v[W_REGS] = w
     v[M_REGS] = m
     hits, found = [0] * P, 0
     lds_plane = {}
-    seq = prologue(DEFAULT) + (contains_body() * gens if gens else [])
-    gc = 0
-    cmp = 0
+    seq = prologue(DEFAULT) + (contains_body(lean) * gens if gens else [])
+    gc, c, scc = 0, 0, 0
+    cmp = {}
     for l in seq:
         if l.startswith("s_add_u32 %[gc]"):
             gc += 1
@@ -366,18 +410,36 @@ def simulate_contains(r, w, m, gens):
             v[d] = (v[a] | v[b]) & np.uint32(0x11111111 << u)
         elif l.startswith("v_cmp_ne_u32_e64"):
             t = int(re.findall(r"v(\d+)", l)[-1])
-            cmp = int((v[t] != 0).any())
+            key = re.search(r"%\[(cmp\d?)\]", l)[1]
+            cmp[key] = int((v[t] != 0).any())
+        elif l.startswith("s_cmp_eq_u64"):
+            scc = int(cmp[re.search(r"%\[(cmp\d?)\]", l)[1]] == 0)
+        elif l.startswith("s_mov_b32 %[c], 0"):
+            c = 0
+        elif l.startswith("s_addc_u32 %[c]"):
+            c = 2 * c + scc
         elif l.startswith("s_cselect_b32 %[c]"):
             bit = int(l.split(",")[1])
-            c = bit if cmp == 0 else 0
+            c = bit if scc else 0
         elif l.startswith("s_andn2_b32 %[c]"):
             c &= ~found
+            scc = int(c != 0)
+        elif l.startswith("s_cbranch_scc1 3f"):
+            if scc:                       # the slow path (contains_slowpath)
+                found |= c
+                for u in range(P):
+                    if c >> (P - 1 - u) & 1:
+                        hits[u] = gc
+        elif l.startswith("s_cmp_lg_u32 %[c]"):
+            scc = int(c != 0)
         elif l.startswith("s_cselect_b32 %[h"):
             u = int(re.search(r"%\[h(\d)\]", l)[1])
-            if c:
+            if scc:
                 hits[u] = gc
         elif l.startswith("s_or_b32 %[found]"):
             found |= c
+        elif l == "4:":
+            pass
         else:
             _exec(v, l, lds_plane)
     return v[:8].copy(), hits
@@ -504,7 +566,7 @@ def emit():
 #pragma once
 
 namespace lifeapi_impl {{
-{fns}{emit2()}{emit_contains()}
+{fns}{emit2()}{emit_contains()}{emit_contains(lean=True)}
 }}  // namespace lifeapi_impl
 """
 

@@ -124,3 +124,16 @@ def step_pair(states: torch.Tensor, out: torch.Tensor, generations: int, variant
     hip._check(lib.lifeapi_tune_step_pair(states.data_ptr(), out.data_ptr(), n, generations, variant,
                                           hip._stream(stream)))
     return out
+
+
+lib.lifeapi_tune_step_contains.argtypes = [_vp, _vp, _vp, _vp, _vp, _sz, _u32, _int, _vp]
+lib.lifeapi_tune_step_contains.restype = _int
+
+
+def step_contains(states, wanted, unwanted, generations, variant, final=None, stream=None):
+    n = hip._universes(states)
+    first = torch.empty(n, dtype=torch.int32, device=states.device)
+    hip._check(lib.lifeapi_tune_step_contains(states.data_ptr(), None if final is None else final.data_ptr(),
+                                              wanted.data_ptr(), unwanted.data_ptr(), first.data_ptr(), n,
+                                              generations, variant, hip._stream(stream)))
+    return first
