@@ -28,7 +28,8 @@ def test_inc_is_generated():
 
 def test_register_budget_and_banks():
     for v in g.VARIANTS:
-        n, bad = g.check_banks(g.body(v))
+        body = g.alt_gen(2, False) if v.startswith("alt") else g.body(v)
+        n, bad = g.check_banks(body)
         assert n == 136 and len(bad) == 32, v      # 128 bitop3 + 8 alignbit; the h-layer only
         assert all(ln.split()[-1] in ("bitop3:0x96", "bitop3:0xe8") for ln in bad)
     text = open(g.OUT).read()
@@ -40,7 +41,7 @@ def test_simulated_loop_is_step(port, variant):
     x = port.fill(8, seed=91)
     x[3] = port.parse("bo$2bo$3o!")          # a glider crossing the seams
     x[6] = np.roll(port.parse("2o$2o!"), 63)
-    for gens in (1, 2, 7):
+    for gens in (1, 2, 3, 7, 8):
         got = g.simulate(*_pack(x), gens, variant)
         want = _pack(port.step_batch(x, gens))
         assert (got[0] == want[0]).all() and (got[1] == want[1]).all(), (variant, gens)

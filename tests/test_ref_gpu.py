@@ -89,3 +89,23 @@ def test_refined_vs_reference(hip, R):
     torch.cuda.synchronize()
     x = d.cpu().numpy().view(np.uint64)
     _check(got.cpu().numpy().view(np.uint64), R.refined_step(x), "unknown_step_refined harness")
+
+
+@pytest.mark.parametrize("gens", [1, 3])
+def test_batch_beyond_2_32_words(hip, R, port, gens):
+    """A batch of 2^26 + 5 universes (2^32 + 320 words, 32 GiB per buffer):
+    every index in the fill, the step kernels and their grid arithmetic must be
+    64-bit.  Universes on both sides of the 2^32-word boundary and the ragged
+    tail are checked against the reference (the fill is indexable, so the
+    oracle regenerates exactly those universes)."""
+    n = (1 << 26) + 5
+    d = hip.fill_random(n, seed=77)
+    out = hip.step(d, generations=gens)
+    torch.cuda.synchronize()
+    for first in (0, (1 << 26) - 3, n - 40):
+        k = min(40, n - first)
+        x = port.fill(k, seed=77, first_universe=first)
+        assert (to_host(d[first:first + k]) == x).all(), f"fill differs at universe {first}"
+        _check(to_host(out[first:first + k]), R.step_batch(x, gens), f"Step^{gens} at universe {first}")
+    del d, out
+    torch.cuda.empty_cache()

@@ -23,7 +23,7 @@ a = hip.fill_random(n, seed=3)
 ref = hip.step(a, generations=gens)
 outs = {}
 kern = {"shipped": lambda o: hip.step(a, out=o, generations=gens)}
-for v in range(4):
+for v in range(6):
     kern[f"pair_v{v}"] = (lambda vv: (lambda o: tune_hip.step_pair(a, o, gens, vv)))(v)
 for k in kern:
     outs[k] = torch.empty_like(a)

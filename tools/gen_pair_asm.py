@@ -117,8 +117,10 @@ def tail_ops(j, r, h0, h1, rot, al):
             op(r[j], g1, g5, r[j], N6)], (g1, g2, g3, g5)   # next = g4 & (g5 | a)
 
 
-def tails(col):
+def tails(col, h1set=None):
     r, h0, h1 = (A, H0A, H1A) if col == 0 else (B, H0B, H1B)
+    if h1set is not None:
+        h1 = h1set
     al = Pool(TEMPS)
     out = []
     for j in range(0, S, 2):
@@ -154,8 +156,75 @@ def reads(col):
 # schedules: "plain" -- the whole exchange at the top of each generation;
 # "pipeA" -- A is published right after its tails (B's tails overlap it);
 # "*_prio" -- s_setprio 2 from the arrival of the exchange until A is
-# published (as rule 11's default).
-VARIANTS = ("plain", "pipeA", "pipeA_prio", "plain_prio")
+# published (as rule 11's default);
+# "alt" -- the read buffers X (v18..25) and Y (v26..33) swap roles every
+# generation (loop unrolled by two): the column whose tails finish first is
+# published at once and the next generation's read of it goes into the
+# buffer its h1 just vacated, so each generation's first exchange is in
+# flight behind the other column's tails; "alt_prio" adds s_setprio 2 from
+# the arrival of the exchange until the next reads are issued.
+VARIANTS = ("plain", "pipeA", "pipeA_prio", "plain_prio", "alt", "alt_prio")
+X, Y = L, R
+
+
+def hl(col, lin, js):
+    """h-layer of column col with the neighbour column in lin; h1 overwrites lin"""
+    out = []
+    for j in js:
+        if col == 0:
+            out += [op(H0A[j], lin[j], A[j], B[j], XOR3), op(lin[j], lin[j], A[j], B[j], MAJ)]
+        else:
+            out += [op(H0B[j], A[j], B[j], lin[j], XOR3), op(lin[j], A[j], B[j], lin[j], MAJ)]
+    return out
+
+
+def rd(kind, regs):
+    """kind "L": B of lane i-1; "R": A of lane i+1"""
+    offs, addr = (OFF_B, A_PREV) if kind == "L" else (OFF_A, A_NEXT)
+    return [f"ds_read_b128 v[{regs[4 * k]}:{regs[4 * k] + 3}], v{addr}" + (f" offset:{offs[k]}" if offs[k] else "")
+            for k in range(2)]
+
+
+def alt_gen(kind, prio):
+    """one generation of the alternating schedule.  kind 2: L data pending in
+    X (issued first), R data in Y; kind 1: R data in X first, L data in Y.
+    Outstanding at entry, in order: a write pair, the first read pair, a
+    write pair, the second read pair."""
+    first_col = 0 if kind == 2 else 1          # the column whose neighbour data arrives first
+    other = 1 - first_col
+    lines = ["s_waitcnt lgkmcnt(5)"]
+    if prio:
+        lines.append("s_setprio 2")
+    lines += hl(first_col, X, range(4)) + ["s_waitcnt lgkmcnt(4)"] + hl(first_col, X, range(4, 8))
+    lines += ["s_waitcnt lgkmcnt(1)"] + hl(other, Y, range(4)) + ["s_waitcnt lgkmcnt(0)"] + hl(other, Y, range(4, 8))
+    # the first column's tails (h1 in X), publish it, read its next-gen
+    # neighbour copy into X; then the other column (h1 in Y) and Y
+    lines += tails(first_col, X) + writes(first_col) + rd("R" if first_col == 0 else "L", X)
+    if prio:
+        lines.append("s_setprio 0")
+    lines += tails(other, Y) + writes(other) + rd("L" if first_col == 0 else "R", Y)
+    return lines
+
+
+def alt_prologue():
+    # entering kind 2: W_B, L -> X, W_A, R -> Y
+    return writes(1) + rd("L", X) + writes(0) + rd("R", Y)
+
+
+def alt_text(prio):
+    return (["s_cmp_eq_u32 %[g], 0", "s_cbranch_scc1 2f"] + alt_prologue() +
+            ["s_lshr_b32 %[p], %[g], 1", "s_cmp_eq_u32 %[p], 0", "s_cbranch_scc1 3f", "1:",
+             "s_sub_u32 %[p], %[p], 1"] + alt_gen(2, prio) + alt_gen(1, prio) +
+            ["s_cmp_lg_u32 %[p], 0", "s_cbranch_scc1 1b", "3:", "s_bitcmp1_b32 %[g], 0", "s_cbranch_scc0 4f"] +
+            alt_gen(2, prio) + ["4:", "s_waitcnt lgkmcnt(0)", "2:"])
+
+
+def alt_seq(gens, prio):
+    """the straight-line instruction sequence alt_text executes for `gens`"""
+    if gens == 0:
+        return []
+    return alt_prologue() + (alt_gen(2, prio) + alt_gen(1, prio)) * (gens // 2) + \
+        (alt_gen(2, prio) if gens % 2 else [])
 
 
 def prologue(variant):
@@ -180,6 +249,8 @@ def body(variant):
 
 
 def asm_text(variant):
+    if variant.startswith("alt"):
+        return alt_text(variant.endswith("prio"))
     return ["s_cmp_eq_u32 %[g], 0", "s_cbranch_scc1 2f"] + prologue(variant) + ["1:"] + body(variant) + \
         ["s_cmp_lg_u32 %[g], 0", "s_cbranch_scc1 1b", "s_waitcnt lgkmcnt(0)", "2:"]
 
@@ -206,7 +277,10 @@ def simulate(a, b, gens, variant=VARIANTS[0]):
     lane = np.arange(64)
     prev = (lane & 32) | ((lane + 31) & 31)
     nxt = (lane & 32) | ((lane + 1) & 31)
-    seq = prologue(variant) + body(variant) * gens if gens else []
+    if variant.startswith("alt"):
+        seq = alt_seq(gens, variant.endswith("prio"))
+    else:
+        seq = prologue(variant) + body(variant) * gens if gens else []
     for ln in seq:
         if ln.startswith("ds_write_b128"):
             off = int(re.search(r"offset:(\d+)", ln)[1]) if "offset" in ln else 0
@@ -243,10 +317,11 @@ def fn_text(name, variant):
 // schedule "{variant}" (see tools/gen_pair_asm.py)
 __device__ __forceinline__ void {name}(uint32_t (&a)[8], uint32_t (&b)[8], uint32_t gens, uint32_t a_self,
                                        uint32_t a_prev, uint32_t a_next) {{
+  uint32_t p;
   asm volatile(
 {asm}
       : {outs.strip()},
-        [g] "+s"(gens)
+        [g] "+s"(gens), [p] "=&s"(p)
       : "{{v{A_SELF}}}"(a_self), "{{v{A_PREV}}}"(a_prev), "{{v{A_NEXT}}}"(a_next)
       : {clob}, "scc", "memory");
 }}

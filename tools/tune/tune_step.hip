@@ -439,7 +439,9 @@ __global__ __launch_bounds__(kBlock) void k_step_pair(const uint64_t *in, uint64
       if constexpr (V == 0) pair_gens_asm_v0(a, b, gens, self, prev, next);
       else if constexpr (V == 1) pair_gens_asm_v1(a, b, gens, self, prev, next);
       else if constexpr (V == 2) pair_gens_asm_v2(a, b, gens, self, prev, next);
-      else pair_gens_asm_v3(a, b, gens, self, prev, next);
+      else if constexpr (V == 3) pair_gens_asm_v3(a, b, gens, self, prev, next);
+      else if constexpr (V == 4) pair_gens_asm_v4(a, b, gens, self, prev, next);
+      else pair_gens_asm_v5(a, b, gens, self, prev, next);
     }
     {
       const uint32_t lane = lane_id_fresh(), grp = lane >> 5, i = lane & 31;
@@ -480,7 +482,7 @@ int lifeapi_tune_step_contains(const uint64_t *d_in, uint64_t *d_final, const ui
   return launched("k_step_contains_split (tuning) launch");
 }
 
-/* the pair layout (k_step_pair), schedule `variant` 0..3 */
+/* the pair layout (k_step_pair), schedule `variant` 0..5 */
 int lifeapi_tune_step_pair(const uint64_t *d_in, uint64_t *d_out, size_t n, uint32_t generations, int variant,
                            void *stream) {
   int rc = check_batch(d_in, d_out, n);
@@ -490,9 +492,11 @@ int lifeapi_tune_step_pair(const uint64_t *d_in, uint64_t *d_out, size_t n, uint
   if (rc != LIFEAPI_OK) return rc;
   const bool nt = generations < 32;
   using Fn = void (*)(const uint64_t *, uint64_t *, uint64_t, uint32_t);
-  const Fn fns[2][4] = {{k_step_pair<false, 0>, k_step_pair<false, 1>, k_step_pair<false, 2>, k_step_pair<false, 3>},
-                        {k_step_pair<true, 0>, k_step_pair<true, 1>, k_step_pair<true, 2>, k_step_pair<true, 3>}};
-  if (variant < 0 || variant > 3) return fail(LIFEAPI_E_INVALID, "unknown pair schedule%s");
+  const Fn fns[2][6] = {{k_step_pair<false, 0>, k_step_pair<false, 1>, k_step_pair<false, 2>, k_step_pair<false, 3>,
+                         k_step_pair<false, 4>, k_step_pair<false, 5>},
+                        {k_step_pair<true, 0>, k_step_pair<true, 1>, k_step_pair<true, 2>, k_step_pair<true, 3>,
+                         k_step_pair<true, 4>, k_step_pair<true, 5>}};
+  if (variant < 0 || variant > 5) return fail(LIFEAPI_E_INVALID, "unknown pair schedule%s");
   hipLaunchKernelGGL(fns[nt][variant], dim3(grid_for((n + 7) / 8, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream,
                      d_in, d_out, (uint64_t)n, generations);
   return launched("k_step_pair launch");
