@@ -234,6 +234,55 @@ def test_host_api_concurrent_shared_input(hip, port):
     assert hip.lib.lifeapi_host_unregister(x.ctypes.data) != 0
 
 
+def test_host_api_small_and_partial_overlaps_of_a_pinned_range(hip, port):
+    """While large calls pin a shared array per call, other threads make small
+    calls (< 8 MiB, never pinned by themselves) inside it and large calls on
+    ranges that only partly overlap it: every call takes a reference on each
+    pin it touches (host.hip pin_acquire), so no copy of theirs can run from
+    memory another call unpins.  All results must match the oracle, and the
+    array ends unregistered."""
+    import threading
+    n = 48_000                                   # 24 MiB
+    x = port.fill(n, seed=31)
+    want = port.step_batch(x, 2)
+    errs = []
+
+    def big():
+        o = np.zeros_like(x)
+        for _ in range(3):
+            hip.step_host(x, 2, out=o)
+            if not (o == want).all():
+                errs.append("big mismatch")
+
+    def small(lo):
+        for _ in range(6):
+            got = hip.step_host(x[lo:lo + 1000], 2)        # 500 KiB inside the pinned range
+            if not (got == want[lo:lo + 1000]).all():
+                errs.append(f"small mismatch at {lo}")
+
+    def partial(lo):
+        for _ in range(3):
+            got = hip.step_host(x[lo:lo + 30_000], 2)      # 15 MiB straddling other calls' ranges
+            if not (got == want[lo:lo + 30_000]).all():
+                errs.append(f"partial mismatch at {lo}")
+
+    def guard(fn, *a):
+        try:
+            fn(*a)
+        except Exception as e:  # noqa: BLE001 - reported below
+            errs.append(repr(e))
+
+    ts = [threading.Thread(target=guard, args=(big,)), threading.Thread(target=guard, args=(big,)),
+          threading.Thread(target=guard, args=(small, 100)), threading.Thread(target=guard, args=(small, 40_000)),
+          threading.Thread(target=guard, args=(partial, 0)), threading.Thread(target=guard, args=(partial, 18_000))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs, errs
+    assert hip.lib.lifeapi_host_unregister(x.ctypes.data) != 0
+
+
 @pytest.mark.parametrize("gens", [2, 40])
 def test_host_step_contains(hip, port, gens):
     """lifeapi_step_contains_batch on host arrays (natural layout for gens <= 2,
