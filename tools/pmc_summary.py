@@ -38,9 +38,9 @@ def main(prof_dir: str, out_json: str, universes: int = 1 << 20):
     cw, ncw = mean_counter(p("calib_WRITE_SIZE", "calib_counter_collection.csv"), "k_copy", "WRITE_SIZE")
     ff, wf = known / (cf * 1024), known / (cw * 1024)
 
-    def entry(name_sub, label, algo):
-        sf, nsf = mean_counter(p("pmc_FETCH_SIZE", "bench_counter_collection.csv"), name_sub, "FETCH_SIZE")
-        sw, nsw = mean_counter(p("pmc_WRITE_SIZE", "bench_counter_collection.csv"), name_sub, "WRITE_SIZE")
+    def entry(name_sub, label, algo, run="pmc", out="bench"):
+        sf, nsf = mean_counter(p(f"{run}_FETCH_SIZE", f"{out}_counter_collection.csv"), name_sub, "FETCH_SIZE")
+        sw, nsw = mean_counter(p(f"{run}_WRITE_SIZE", f"{out}_counter_collection.csv"), name_sub, "WRITE_SIZE")
         fetch_b, write_b = sf * 1024 * ff, sw * 1024 * wf
         return {"kernel": label, "kernel_name_match": name_sub,
                 "raw": {"FETCH_SIZE_KiB_mean": sf, "WRITE_SIZE_KiB_mean": sw, "dispatches": [nsf, nsw]},
@@ -56,14 +56,17 @@ def main(prof_dir: str, out_json: str, universes: int = 1 << 20):
                         "FETCH_SIZE_KiB_mean": cf, "WRITE_SIZE_KiB_mean": cw,
                         "fetch_factor": ff, "write_factor": wf, "dispatches": [ncf, ncw]}
     try:  # config 3: 1024 generations in VGPRs, HBM touched once per universe
+        # (its own passes over tools/c3_once.py when present, else the bench's)
+        run, out = ("c3", "c3") if os.path.isdir(p("c3_FETCH_SIZE")) else ("pmc", "bench")
         d["config3"] = entry("k_step_split<8, 1, false, 6, -3,",
-                             "k_step_split<S=8, G=1, NET 6, asm loop> (rule 11; config 3: 64K universes x 1024 gens)", (1 << 16) * 1024)
-    except SystemExit:
+                             "k_step_split<S=8, G=1, NET 6, asm loop> (rule 11; config 3: 64K universes x 1024 gens)",
+                             (1 << 16) * 1024, run, out)
+    except (SystemExit, OSError):
         pass
     try:  # config 5 (present when the bench ran its secondaries under the PMC passes)
         d["config5"] = entry("k_refined<1, 0>", "k_refined (config 5: 256K universes, 11 planes in, 3 out)",
                              (1 << 18) * 7168)
-    except SystemExit:
+    except (SystemExit, OSError):
         pass
     with open(out_json, "w") as f:
         json.dump(d, f, indent=1)
