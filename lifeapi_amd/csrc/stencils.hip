@@ -278,7 +278,7 @@ __global__ __launch_bounds__(kBlock, OCC > 0 ? OCC : 1) void k_refined(
 
 extern "C" {
 
-constexpr int kStableBlocksPerCU = 32;  // LifeStable kernels' grid cap (see below)
+constexpr int kStableBlocksPerCU = 32;  // grid cap of the single LifeStable passes (see below)
 
 static int counts_launch(const uint64_t *d_in, uint64_t *d_out, size_t n, int mode, void *stream) {
   if (n == 0) return LIFEAPI_OK;
@@ -308,13 +308,16 @@ int lifeapi_stable_pass_batch_dev(uint64_t *d_planes, uint8_t *d_flags, size_t n
   if (rc != LIFEAPI_OK) return rc;
   using Fn = void (*)(uint64_t *, uint8_t *, uint64_t, uint32_t);
   const Fn fns[6] = {k_stable<0>, k_stable<1>, k_stable<2>, k_stable<3>, k_stable<4>, k_stable<5>};
-  // Every pass, the looping ones (Propagate, StabiliseOptions) included,
-  // runs on a 32-blocks-per-CU grid that loops over the batch: on still
-  // lifes and soups around an unknown window with fresh options (the state a
-  // search propagates from) and on random planes, 64K LifeStables each, it
-  // is as fast as or up to 4 % faster than one wave per LifeStable, and
-  // 16 blocks per CU is slower (profiles/r02/stable_grid_ab.jsonl).
-  hipLaunchKernelGGL(fns[pass], dim3(grid_for(n, cus, kStableBlocksPerCU)), dim3(kBlock), 0, (hipStream_t)stream,
+  // Grid (same-process A/Bs on realistic partially-unknown LifeStables --
+  // still lifes around an unknown window with fresh options, the state a
+  // search propagates from -- and on soups and random planes;
+  // profiles/r02/stable_grid_ab.jsonl at 64K, stable_grid_ab_1m.jsonl at 1M):
+  // the single passes and StabiliseOptions run on a 32-blocks-per-CU grid
+  // that loops over the batch (4-7 % faster on the still-life inputs at 1M,
+  // even at 64K); Propagate, whose iteration count varies per LifeStable,
+  // keeps one wave per LifeStable (4 % slower capped at 1M).
+  hipLaunchKernelGGL(fns[pass], dim3(grid_for(n, cus, pass == 4 ? 0 : kStableBlocksPerCU)), dim3(kBlock), 0,
+                     (hipStream_t)stream,
                      d_planes, d_flags, (uint64_t)n, max_iters ? max_iters : 1u << 20);
   return launched("k_stable launch");
 }
@@ -327,9 +330,9 @@ int lifeapi_stable_vulnerable_batch_dev(const uint64_t *d_planes, uint64_t *d_ou
   if (b < a + n * 10 * 512 && a < b + n * 512) return fail(LIFEAPI_E_INVALID, "out overlaps planes%s");
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
-  // the same grid as the passes (2-5 % faster than one wave per LifeStable,
-  // profiles/r02/stable_grid_ab.jsonl)
-  hipLaunchKernelGGL(k_stable_vulnerable, dim3(grid_for(n, cus, kStableBlocksPerCU)), dim3(kBlock), 0, (hipStream_t)stream,
+  // one wave per LifeStable: capped at 32 blocks per CU it was 12 % slower
+  // on the still-life inputs at 1M (equal at 64K; profiles/r02/stable_grid_ab*.jsonl)
+  hipLaunchKernelGGL(k_stable_vulnerable, dim3(grid_for(n, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream,
                      d_planes, d_out, (uint64_t)n);
   return launched("k_stable_vulnerable launch");
 }

@@ -26,7 +26,8 @@ import tune_hip  # noqa: E402
 from oracle.oracle import Port  # noqa: E402  (pattern parsing and seeded fills for the inputs only)
 
 P = Port()
-N, DISTINCT = 1 << 16, 2048
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 16
+DISTINCT = 2048
 
 
 def rect(x0, y0, w, h):
