@@ -207,16 +207,43 @@ __global__ __launch_bounds__(kBlock) void k_step_split(const uint64_t *in, uint6
 // with no branch per universe.  The check costs 19 VALU per wave-generation
 // on top of the step's 68 (8 differences, 3 OR3, and per universe a masked
 // OR + compare: +28 % VALU, and +28 % time with the lean bookkeeping,
-// profiles/r02/contains_ab.jsonl).
+// profiles/r02/contains_ab.jsonl); on a target spanning h <= 8 rows, h
+// differences and fewer ORs (13 VALU for h = 4: +26 % time).
 // Without d_final, a wave stops once all its universes have hit.
 constexpr uint32_t kDiff = ((TA ^ TB) & (TB | TC)) & 0xFF;  // (s ^ wanted) & (wanted | unwanted)
 constexpr int kContainsNet = 6;  // tail network of the fused kernel (as k_step's default, rule 11)
 // ASM: 0 = the compiled loop below, 1 = the assembly loop of split_asm.inc
 // (split_contains_asm), 2 = its lean-bookkeeping variant
 // (split_contains_asm_lean: two SALU per universe and generation instead of
-// eight; 1.668 against 1.760 ms on config 3, profiles/r02/contains_ab.jsonl);
+// eight; 1.668 against 1.760 ms on config 3, profiles/r02/contains_ab.jsonl),
+// 3 = the lean loop on the target's row window: every wave finds the
+// smallest cyclic window [y0, y0 + h) of rows that holds all of the target's
+// care cells (wanted | unwanted) and, when h <= 8, rotates the universes and
+// the target up by y0 rows (Life on the torus commutes with translation, and
+// so does Contains), so that the care rows are the split layout's residues
+// 0..h-1 and the test differences only h of the 8 registers
+// (split_contains_asm_lean_h<h>); d_final is rotated back.  On config 3
+// with a block + ring target (h = 4): 1.621 ms against 1.670 for 2 and 1.291
+// for the plain step (profiles/r02/contains_ab_window.jsonl).
 // step.hip ships kContainsAsm
-constexpr int kContainsAsm = 2;
+constexpr int kContainsAsm = 3;
+
+__device__ __forceinline__ uint64_t rotr64(uint64_t v, uint32_t k) {
+  return (v >> k) | (v << ((64 - k) & 63));
+}
+// the smallest cyclic window [y0, y0 + h) of rows holding every set bit of
+// rm (wave-uniform); h = 1 for an empty mask
+__device__ __forceinline__ void care_window(uint64_t rm, uint32_t &y0, uint32_t &h) {
+  y0 = 0;
+  h = 1;
+  if (rm == 0) return;
+  h = 65;
+  for (uint32_t y = 0; y < 64; ++y) {
+    if (!((rm >> y) & 1)) continue;
+    const uint32_t hh = 64 - __builtin_clzll(rotr64(rm, y));
+    if (hh < h) h = hh, y0 = y;
+  }
+}
 template <int S, int NET, int ASM = 0>
 __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *in, uint64_t *fin,
                                                                 const uint64_t *__restrict__ wanted,
@@ -228,14 +255,23 @@ __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *
   __shared__ uint32_t lds[kWavesPerBlock * S * kWave];
   const int lane = threadIdx.x & (kWave - 1);
   const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  uint32_t y0 = 0, h = S;  // the row window of ASM 3 (else: no rotation, all registers)
+  if constexpr (ASM == 3) {
+    uint64_t rm = 0;
+    for (int x = 0; x < kWave; ++x) rm |= wanted[x] | unwanted[x];  // uniform: scalar loads
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)rm);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(rm >> 32));
+    care_window((uint64_t)lo | (uint64_t)hi << 32, y0, h);
+    if (h > S) y0 = 0, h = S;
+  }
   uint32_t tw[S], tu[S];
   {
     W c[P];
 #pragma unroll
-    for (int u = 0; u < P; ++u) c[u] = split(wanted[lane]);
+    for (int u = 0; u < P; ++u) c[u] = split(rotr64(wanted[lane], y0));
     Split<S>::load(c, tw);
 #pragma unroll
-    for (int u = 0; u < P; ++u) c[u] = split(unwanted[lane]);
+    for (int u = 0; u < P; ++u) c[u] = split(rotr64(unwanted[lane], y0));
     Split<S>::load(c, tu);
   }
   uint32_t tm[S];  // wanted | unwanted (the assembly loop's second target plane)
@@ -247,7 +283,7 @@ __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *
     uint32_t r[S];
     W c[P];
 #pragma unroll
-    for (int u = 0; u < P; ++u) c[u] = u0 + u < n ? split(in[(u0 + u) * kWave + lane]) : W{0u, 0u};
+    for (int u = 0; u < P; ++u) c[u] = u0 + u < n ? split(rotr64(in[(u0 + u) * kWave + lane], y0)) : W{0u, 0u};
     Split<S>::load(c, r);
     uint32_t hit[P];
 #pragma unroll
@@ -257,9 +293,21 @@ __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *
       static_assert(S == 8 && NET == 6, "split_contains_asm is rule 11");
       const uint32_t base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)(
           lds + wib * S * kWave);
-      if constexpr (ASM == 2)
-        split_contains_asm_lean(r, tw, tm, gens, base + lane * 16u, base + ((lane + kWave - 1) & (kWave - 1)) * 16u,
-                                base + ((lane + 1) & (kWave - 1)) * 16u, hit);
+      const uint32_t self = base + lane * 16u, prev = base + ((lane + kWave - 1) & (kWave - 1)) * 16u,
+                     next = base + ((lane + 1) & (kWave - 1)) * 16u;
+      if constexpr (ASM == 3) {
+        switch (h) {  // wave-uniform
+          case 1: split_contains_asm_lean_h1(r, tw, tm, gens, self, prev, next, hit); break;
+          case 2: split_contains_asm_lean_h2(r, tw, tm, gens, self, prev, next, hit); break;
+          case 3: split_contains_asm_lean_h3(r, tw, tm, gens, self, prev, next, hit); break;
+          case 4: split_contains_asm_lean_h4(r, tw, tm, gens, self, prev, next, hit); break;
+          case 5: split_contains_asm_lean_h5(r, tw, tm, gens, self, prev, next, hit); break;
+          case 6: split_contains_asm_lean_h6(r, tw, tm, gens, self, prev, next, hit); break;
+          case 7: split_contains_asm_lean_h7(r, tw, tm, gens, self, prev, next, hit); break;
+          default: split_contains_asm_lean(r, tw, tm, gens, self, prev, next, hit); break;
+        }
+      } else if constexpr (ASM == 2)
+        split_contains_asm_lean(r, tw, tm, gens, self, prev, next, hit);
       else
         split_contains_asm(r, tw, tm, gens, base + lane * 16u, base + ((lane + kWave - 1) & (kWave - 1)) * 16u,
                            base + ((lane + 1) & (kWave - 1)) * 16u, hit);
@@ -282,7 +330,7 @@ __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *
       Split<S>::store(r, c);
 #pragma unroll
       for (int u = 0; u < P; ++u)
-        if (u0 + u < n) fin[(u0 + u) * kWave + lane] = join(c[u]);
+        if (u0 + u < n) fin[(u0 + u) * kWave + lane] = rotr64(join(c[u]), (64 - y0) & 63);
     }
     if (lane == 0) {
 #pragma unroll

@@ -81,3 +81,45 @@ def test_simulated_contains_loop(port, lean):
                 if not exp[u] and (((s[u] ^ blk) & (blk | ring)) == 0).all():
                     exp[u] = k
         assert (got == _to_split(s)).all() and hits == exp, (gens, hits, exp)
+
+
+def _rot_rows(states, k):
+    """rotate every column word down by k rows (row k becomes row 0)"""
+    k %= 64
+    s = np.asarray(states, dtype=np.uint64)
+    if k == 0:
+        return s.copy()
+    return (s >> np.uint64(k)) | (s << np.uint64(64 - k))
+
+
+@pytest.mark.parametrize("h", range(1, 9))
+def test_simulated_windowed_contains(port, h):
+    """split_contains_asm_lean_h<h>: with the universes and the target rotated
+    so that the target's care rows lie in rows 0..h-1 (residues 0..h-1 of the
+    8-way split), differencing only registers 0..h-1 gives the same first-hit
+    generations as the full test on the unrotated states."""
+    rng = np.random.default_rng(100 + h)
+    y0 = int(rng.integers(64))
+    rows = np.uint64(((((1 << h) - 1) << y0) | (((1 << h) - 1) >> (64 - y0))) & ((1 << 64) - 1))  # rows y0.. (mod 64)
+    wanted = np.zeros(64, np.uint64)
+    care = np.zeros(64, np.uint64)
+    for c in range(20, 26):
+        care[c] = rows
+        wanted[c] = rows & np.uint64(int(rng.integers(1 << 62)))
+    unwanted = care & ~wanted
+    x = port.fill(4, seed=300 + h) & port.fill(4, seed=400 + h)
+    x[1] = (x[1] & ~care) | wanted                      # contained at generation 0 ...
+    x[3] = wanted.copy()                                # ... and a bare copy of the wanted cells
+    gens = 6
+    exp, s = [0] * 4, x.copy()
+    for k in range(1, gens + 1):
+        s = port.step_batch(s, 1)
+        for u in range(4):
+            if not exp[u] and (((s[u] ^ wanted) & (wanted | unwanted)) == 0).all():
+                exp[u] = k
+    xr, wr, mr = _rot_rows(x, y0), _rot_rows(wanted, y0), _rot_rows(wanted | unwanted, y0)
+    assert (_rot_rows(care, y0) >> np.uint64(h) == 0).all()   # care rows now in 0..h-1
+    got, hits = g.simulate_contains(_to_split(xr), _to_split(np.stack([wr] * 4)),
+                                    _to_split(np.stack([mr] * 4)), gens, lean=True, h=h)
+    assert hits == exp, (h, y0, hits, exp)
+    assert (got == _to_split(_rot_rows(s, y0))).all()

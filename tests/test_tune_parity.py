@@ -73,7 +73,7 @@ def test_bad_cfgs_rejected(tune, hip):
             tune.step(d, generations=1, cfg=tune.LaunchCfg(*bad))
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 @pytest.mark.parametrize("gens", [3, 6, 37])
 @pytest.mark.parametrize("with_final", [False, True])
 def test_step_contains_variants(tune, port, variant, gens, with_final):
@@ -104,3 +104,55 @@ def test_step_contains_variants(tune, port, variant, gens, with_final):
     assert (exp > 0).any()
     if with_final:
         assert (to_host(fin) == port.step_batch(x, gens)).all()
+
+
+
+def _target(kind):
+    """(wanted, unwanted) with care rows: a block + ring straddling the row
+    seam (rows 62..1: window 4 across 63 -> 0), a tall one (12 rows: no
+    window <= 8), a one-row target, and an empty target (always contained)"""
+    w, u = np.zeros(64, np.uint64), np.zeros(64, np.uint64)
+    if kind == "seam":
+        for c in (30, 31):
+            w[c] = np.uint64((1 << 63) | 1)
+        for c in (29, 30, 31, 32):
+            u[c] = np.uint64((3 << 62) | 3)
+        u &= ~w
+    elif kind == "tall":
+        w[5] = np.uint64(0b111 << 20)
+        for c in (4, 5, 6):
+            u[c] = np.uint64(0xFFF << 16)
+        u &= ~w
+    elif kind == "row":
+        for c in range(10, 20):
+            u[c] = np.uint64(1 << 7)
+    return w, u
+
+
+@pytest.mark.parametrize("kind", ["seam", "tall", "row", "empty"])
+@pytest.mark.parametrize("with_final", [False, True])
+def test_step_contains_row_window(tune, hip, port, kind, with_final):
+    """variant 3 (the target's row window, universes rotated into it and
+    back) against the oracle and against the shipped kernel, for targets
+    whose window wraps the row seam, exceeds 8 rows, is one row, or is empty."""
+    import torch
+    n, gens = 2001, 9
+    w, u = _target(kind)
+    x = port.fill(n, seed=501) & port.fill(n, seed=502)
+    x[::3] &= ~(w | u)
+    x[::6] |= w
+    fin = torch.empty((n, 64), dtype=torch.int64, device="cuda") if with_final else None
+    got = tune.step_contains(to_dev(x), to_dev(w[None]), to_dev(u[None]), gens, 3, final=fin).cpu().numpy()
+    exp = np.zeros(n, np.int64)
+    s = x.copy()
+    for g in range(1, gens + 1):
+        s = port.step_batch(s, 1)
+        hit = (((s ^ w) & (w | u)) == 0).all(axis=1)
+        exp[(exp == 0) & hit] = g
+    assert (got == exp).all(), np.nonzero(got != exp)[0][:10]
+    if kind == "empty":
+        assert (exp == 1).all()
+    if with_final:
+        assert (to_host(fin) == port.step_batch(x, gens)).all()
+    ship, _ = hip.step_contains(to_dev(x), to_dev(w[None]), to_dev(u[None]), gens)
+    assert (ship.cpu().numpy() == exp).all()

@@ -282,24 +282,51 @@ OR3 = 0xFE         # a | b | c
 ORAND = 0xA8       # (a | b) & c
 
 
-def contains_check(lean=False):
+def _or_to_two(d, al):
+    """OR-reduce the difference registers d to two values (y, z) with
+    y | z = OR(d), in as few OR3 as possible; (lines, y, z)"""
+    h = len(d)
+    if h == 1:
+        return [], d[0], d[0]
+    if h == 2:
+        return [], d[0], d[1]
+    x = al.get(1)
+    lines = [op(x, d[0], d[1], d[2], OR3)]
+    if h == 3:
+        return lines, x, x
+    if h == 4:
+        return lines, x, d[3]
+    y = al.get(2)
+    if h == 5:
+        return lines + [op(y, d[3], d[4], d[4], OR3)], x, y
+    lines.append(op(y, d[3], d[4], d[5], OR3))
+    if h == 6:
+        return lines, x, y
+    z = al.get(3)
+    if h == 7:
+        return lines + [op(z, d[6], x, x, OR3)], y, z
+    return lines + [op(z, d[6], d[7], x, OR3)], y, z
+
+
+def contains_check(lean=False, h=S):
     """lean: the per-universe bookkeeping on the fast path is 2 SALU per
     universe (s_cmp_eq_u64 + s_addc_u32 building the clean mask, universe 0
     in bit 3) and one s_andn2 + branch; a hit (rare) branches to a slow path
-    that records it.  Otherwise 8 SALU per universe per generation."""
+    that records it.  Otherwise 8 SALU per universe per generation.
+    h < 8 (lean only): the target's care rows all lie in residues 0..h-1 of
+    the 8-way split (the kernel rotates universes and target so), so only
+    registers 0..h-1 are differenced."""
     al = Alloc()
     d = []
-    for j in range(S):
+    for j in range(h):
         t = al.get(j)
         d.append(t)
-    lines = [op(d[j], R[j], W_REGS[j], M_REGS[j], DIFF) for j in range(S)]
-    x, y = al.get(1), al.get(2)
-    z = al.get(3)
-    lines += [op(x, d[0], d[1], d[2], OR3), op(y, d[3], d[4], d[5], OR3), op(z, d[6], d[7], x, OR3)]
-    t = al.get(0)
-    lines.append("s_add_u32 %[gc], %[gc], 1")
+    lines = [op(d[j], R[j], W_REGS[j], M_REGS[j], DIFF) for j in range(h)]
     if lean:
-        ts = [t, al.get(1), al.get(2), al.get(3)]
+        red, y, z = _or_to_two(d, al)
+        lines += red
+        lines.append("s_add_u32 %[gc], %[gc], 1")
+        ts = [al.get(b) for b in range(P)]
         for u in range(P):
             lines += [f"v_bitop3_b32 v{ts[u]}, v{y}, v{z}, %[m{u}] bitop3:0x{ORAND:02x}",
                       f"v_cmp_ne_u32_e64 %[cmp{u}], 0, v{ts[u]}"]
@@ -311,6 +338,12 @@ def contains_check(lean=False):
                   "s_cbranch_scc1 3f",
                   "4:"]
         return lines
+    assert h == S
+    x, y = al.get(1), al.get(2)
+    z = al.get(3)
+    lines += [op(x, d[0], d[1], d[2], OR3), op(y, d[3], d[4], d[5], OR3), op(z, d[6], d[7], x, OR3)]
+    t = al.get(0)
+    lines.append("s_add_u32 %[gc], %[gc], 1")
     for u in range(P):
         lines += [f"v_bitop3_b32 v{t}, v{y}, v{z}, %[m{u}] bitop3:0x{ORAND:02x}",
                   f"v_cmp_ne_u32_e64 %[cmp], 0, v{t}",
@@ -333,24 +366,24 @@ def contains_slowpath():
     return lines + ["s_branch 4b"]
 
 
-def contains_body(lean=False):
+def contains_body(lean=False, h=S):
     """the default schedule's body with the check after rows 6..7 (all eight
     rows final), before the plane-1 exchange"""
     b = body(DEFAULT)
     k = b.index(exchange(1)[0])
-    return b[:k] + contains_check(lean) + b[k:]
+    return b[:k] + contains_check(lean, h) + b[k:]
 
 
-def contains_text(lean=False):
-    lines = ["s_cmp_eq_u32 %[g], 0", "s_cbranch_scc1 2f"] + prologue(DEFAULT) + ["1:"] + contains_body(lean) + \
+def contains_text(lean=False, h=S):
+    lines = ["s_cmp_eq_u32 %[g], 0", "s_cbranch_scc1 2f"] + prologue(DEFAULT) + ["1:"] + contains_body(lean, h) + \
         ["s_cmp_lg_u32 %[g], 0", "s_cbranch_scc1 1b", "s_waitcnt lgkmcnt(0)"]
     if lean:
         lines += ["s_branch 2f"] + contains_slowpath()
     return lines + ["2:"]
 
 
-def emit_contains(lean=False):
-    lines = contains_text(lean)
+def emit_contains(lean=False, h=S):
+    lines = contains_text(lean, h)
     asm = "\n".join(f'      "{l}\\n"' for l in lines)
     outs = ",\n".join([f'        "+{{v{R[j]}}}"(r[{j}])' for j in range(S)] +
                       [f'        [h{u}] "+s"(hit[{u}])' for u in range(P)])
@@ -360,11 +393,14 @@ def emit_contains(lean=False):
     pinned = sorted({x for x in L + RR + H1 + H0 + [H0U, H0D, H1U, H1D] + TEMPS})
     clob = ", ".join(f'"v{x}"' for x in pinned)
     if lean:
-        name, cmps = "split_contains_asm_lean", "uint64_t cmp0, cmp1, cmp2, cmp3;"
+        name = "split_contains_asm_lean" + ("" if h == S else f"_h{h}")
+        cmps = "uint64_t cmp0, cmp1, cmp2, cmp3;"
         cmp_outs = "[cmp0] \"=&s\"(cmp0), [cmp1] \"=&s\"(cmp1), [cmp2] \"=&s\"(cmp2), [cmp3] \"=&s\"(cmp3)"
         doc = ("// The same with the per-universe bookkeeping cut to two SALU per universe on\n"
                "// the fast path (the clean mask built by s_cmp + s_addc; hits branch to a\n"
-               "// slow path after the loop).")
+               "// slow path after the loop)" +
+               ("." if h == S else f", differencing only registers 0..{h - 1} (a target whose\n"
+                f"// care rows the kernel has rotated into residues 0..{h - 1})."))
     else:
         name, cmps = "split_contains_asm", "uint64_t cmp;"
         cmp_outs = "[cmp] \"=&s\"(cmp)"
@@ -390,15 +426,15 @@ __device__ __forceinline__ void {name}(uint32_t (&r)[8], const uint32_t (&w)[8],
 """
 
 
-def simulate_contains(r, w, m, gens, lean=False):
-    """numpy run of split_contains_asm[_lean]: returns (r, hits[4])"""
+def simulate_contains(r, w, m, gens, lean=False, h=S):
+    """numpy run of split_contains_asm[_lean[_h<h>]]: returns (r, hits[4])"""
     v = np.zeros((N_VGPR_C, 64), np.uint32)
     v[:8] = r
     v[W_REGS] = w
     v[M_REGS] = m
     hits, found = [0] * P, 0
     lds_plane = {}
-    seq = prologue(DEFAULT) + (contains_body(lean) * gens if gens else [])
+    seq = prologue(DEFAULT) + (contains_body(lean, h) * gens if gens else [])
     gc, c, scc = 0, 0, 0
     cmp = {}
     for l in seq:
@@ -566,7 +602,7 @@ def emit():
 #pragma once
 
 namespace lifeapi_impl {{
-{fns}{emit2()}{emit_contains()}{emit_contains(lean=True)}
+{fns}{emit2()}{emit_contains()}{emit_contains(lean=True)}{"".join(emit_contains(True, h) for h in range(1, S))}
 }}  // namespace lifeapi_impl
 """
 

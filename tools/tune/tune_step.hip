@@ -461,7 +461,8 @@ __global__ __launch_bounds__(kBlock) void k_step_pair(const uint64_t *in, uint64
 extern "C" {
 
 /* fused Step + Contains on the split layout: variant 0 = compiled loop,
- * 1 = assembly loop (shipped), 2 = assembly loop with lean bookkeeping */
+ * 1 = assembly loop, 2 = with lean bookkeeping, 3 = lean on the target's
+ * row window */
 int lifeapi_tune_step_contains(const uint64_t *d_in, uint64_t *d_final, const uint64_t *d_wanted,
                                const uint64_t *d_unwanted, uint32_t *d_first_gen, size_t n, uint32_t generations,
                                int variant, void *stream) {
@@ -474,9 +475,9 @@ int lifeapi_tune_step_contains(const uint64_t *d_in, uint64_t *d_final, const ui
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
   using Fn = void (*)(const uint64_t *, uint64_t *, const uint64_t *, const uint64_t *, uint32_t *, uint64_t, uint32_t);
-  const Fn fns[3] = {k_step_contains_split<8, kContainsNet, 0>, k_step_contains_split<8, kContainsNet, 1>,
-                     k_step_contains_split<8, kContainsNet, 2>};
-  if (variant < 0 || variant > 2) return fail(LIFEAPI_E_INVALID, "unknown contains variant%s");
+  const Fn fns[4] = {k_step_contains_split<8, kContainsNet, 0>, k_step_contains_split<8, kContainsNet, 1>,
+                     k_step_contains_split<8, kContainsNet, 2>, k_step_contains_split<8, kContainsNet, 3>};
+  if (variant < 0 || variant > 3) return fail(LIFEAPI_E_INVALID, "unknown contains variant%s");
   hipLaunchKernelGGL(fns[variant], dim3(grid_for((n + 3) / 4, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream, d_in,
                      d_final, d_wanted, d_unwanted, d_first_gen, (uint64_t)n, generations);
   return launched("k_step_contains_split (tuning) launch");
