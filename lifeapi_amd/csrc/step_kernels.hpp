@@ -222,7 +222,8 @@ constexpr int kContainsNet = 6;  // tail network of the fused kernel (as k_step'
 // the target up by y0 rows (Life on the torus commutes with translation, and
 // so does Contains), so that the care rows are the split layout's residues
 // 0..h-1 and the test differences only h of the 8 registers
-// (split_contains_asm_lean_h<h>); d_final is rotated back.  On config 3
+// (split_contains_asm_lean_h<h>); d_final is rotated back.  4 = 3 with the
+// test's scalar part after the plane-1 exchange (split_contains_asm_lean_late*).  On config 3
 // with a block + ring target (h = 4): 1.621 ms against 1.670 for 2 and 1.291
 // for the plain step (profiles/r02/contains_ab_window.jsonl).
 // step.hip ships kContainsAsm
@@ -256,7 +257,7 @@ __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *
   const int lane = threadIdx.x & (kWave - 1);
   const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   uint32_t y0 = 0, h = S;  // the row window of ASM 3 (else: no rotation, all registers)
-  if constexpr (ASM == 3) {
+  if constexpr (ASM >= 3) {
     uint64_t rm = 0;
     for (int x = 0; x < kWave; ++x) rm |= wanted[x] | unwanted[x];  // uniform: scalar loads
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)rm);
@@ -295,7 +296,18 @@ __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *
           lds + wib * S * kWave);
       const uint32_t self = base + lane * 16u, prev = base + ((lane + kWave - 1) & (kWave - 1)) * 16u,
                      next = base + ((lane + 1) & (kWave - 1)) * 16u;
-      if constexpr (ASM == 3) {
+      if constexpr (ASM == 4) {
+        switch (h) {  // wave-uniform
+          case 1: split_contains_asm_lean_late_h1(r, tw, tm, gens, self, prev, next, hit); break;
+          case 2: split_contains_asm_lean_late_h2(r, tw, tm, gens, self, prev, next, hit); break;
+          case 3: split_contains_asm_lean_late_h3(r, tw, tm, gens, self, prev, next, hit); break;
+          case 4: split_contains_asm_lean_late_h4(r, tw, tm, gens, self, prev, next, hit); break;
+          case 5: split_contains_asm_lean_late_h5(r, tw, tm, gens, self, prev, next, hit); break;
+          case 6: split_contains_asm_lean_late_h6(r, tw, tm, gens, self, prev, next, hit); break;
+          case 7: split_contains_asm_lean_late_h7(r, tw, tm, gens, self, prev, next, hit); break;
+          default: split_contains_asm_lean_late(r, tw, tm, gens, self, prev, next, hit); break;
+        }
+      } else if constexpr (ASM == 3) {
         switch (h) {  // wave-uniform
           case 1: split_contains_asm_lean_h1(r, tw, tm, gens, self, prev, next, hit); break;
           case 2: split_contains_asm_lean_h2(r, tw, tm, gens, self, prev, next, hit); break;

@@ -15,6 +15,7 @@ import gen_split_asm as g  # noqa: E402
 
 def test_inc_is_generated():
     assert open(g.OUT).read() == g.emit()
+    assert open(g.OUT_TUNE).read() == g.emit_tune()
 
 
 def test_bank_rules():
@@ -92,8 +93,9 @@ def _rot_rows(states, k):
     return (s >> np.uint64(k)) | (s << np.uint64(64 - k))
 
 
+@pytest.mark.parametrize("late", [False, True])
 @pytest.mark.parametrize("h", range(1, 9))
-def test_simulated_windowed_contains(port, h):
+def test_simulated_windowed_contains(port, h, late):
     """split_contains_asm_lean_h<h>: with the universes and the target rotated
     so that the target's care rows lie in rows 0..h-1 (residues 0..h-1 of the
     8-way split), differencing only registers 0..h-1 gives the same first-hit
@@ -120,6 +122,6 @@ def test_simulated_windowed_contains(port, h):
     xr, wr, mr = _rot_rows(x, y0), _rot_rows(wanted, y0), _rot_rows(wanted | unwanted, y0)
     assert (_rot_rows(care, y0) >> np.uint64(h) == 0).all()   # care rows now in 0..h-1
     got, hits = g.simulate_contains(_to_split(xr), _to_split(np.stack([wr] * 4)),
-                                    _to_split(np.stack([mr] * 4)), gens, lean=True, h=h)
+                                    _to_split(np.stack([mr] * 4)), gens, lean=True, h=h, late=late)
     assert hits == exp, (h, y0, hits, exp)
     assert (got == _to_split(_rot_rows(s, y0))).all()

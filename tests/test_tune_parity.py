@@ -73,7 +73,7 @@ def test_bad_cfgs_rejected(tune, hip):
             tune.step(d, generations=1, cfg=tune.LaunchCfg(*bad))
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("gens", [3, 6, 37])
 @pytest.mark.parametrize("with_final", [False, True])
 def test_step_contains_variants(tune, port, variant, gens, with_final):
@@ -131,7 +131,8 @@ def _target(kind):
 
 @pytest.mark.parametrize("kind", ["seam", "tall", "row", "empty"])
 @pytest.mark.parametrize("with_final", [False, True])
-def test_step_contains_row_window(tune, hip, port, kind, with_final):
+@pytest.mark.parametrize("variant", [3, 4])
+def test_step_contains_row_window(tune, hip, port, kind, with_final, variant):
     """variant 3 (the target's row window, universes rotated into it and
     back) against the oracle and against the shipped kernel, for targets
     whose window wraps the row seam, exceeds 8 rows, is one row, or is empty."""
@@ -142,7 +143,7 @@ def test_step_contains_row_window(tune, hip, port, kind, with_final):
     x[::3] &= ~(w | u)
     x[::6] |= w
     fin = torch.empty((n, 64), dtype=torch.int64, device="cuda") if with_final else None
-    got = tune.step_contains(to_dev(x), to_dev(w[None]), to_dev(u[None]), gens, 3, final=fin).cpu().numpy()
+    got = tune.step_contains(to_dev(x), to_dev(w[None]), to_dev(u[None]), gens, variant, final=fin).cpu().numpy()
     exp = np.zeros(n, np.int64)
     s = x.copy()
     for g in range(1, gens + 1):

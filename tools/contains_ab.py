@@ -26,13 +26,13 @@ u = torch.zeros((1, 64), dtype=torch.int64, device="cuda")
 for c in (9, 10, 11, 12):
     u[0, c] = 15 << 39
 u &= ~w                                              # ... and its empty ring
-outs = {k: torch.empty_like(x) for k in ("step", "ship", "v0", "v1", "v2", "v3")}
+outs = {k: torch.empty_like(x) for k in ("step", "ship", "v0", "v1", "v2", "v3", "v4")}
 firsts = {}
 kern = {
     "step": lambda: hip.step(x, out=outs["step"], generations=g),
     "ship": lambda: firsts.__setitem__("ship", hip.step_contains(x, w, u, g, final=outs["ship"])[0]),
 }
-for v in range(4):
+for v in range(5):
     kern[f"v{v}"] = (lambda vv: lambda: firsts.__setitem__(
         f"v{vv}", tune_hip.step_contains(x, w, u, g, vv, final=outs[f"v{vv}"])))(v)
 t0 = time.time()

@@ -330,14 +330,7 @@ def contains_check(lean=False, h=S):
         for u in range(P):
             lines += [f"v_bitop3_b32 v{ts[u]}, v{y}, v{z}, %[m{u}] bitop3:0x{ORAND:02x}",
                       f"v_cmp_ne_u32_e64 %[cmp{u}], 0, v{ts[u]}"]
-        lines.append("s_mov_b32 %[c], 0")
-        for u in range(P):
-            lines += [f"s_cmp_eq_u64 %[cmp{u}], 0",       # SCC = universe u clean
-                      "s_addc_u32 %[c], %[c], %[c]"]      # c = 2c + SCC
-        lines += ["s_andn2_b32 %[c], %[c], %[found]",     # fresh hits; SCC = any
-                  "s_cbranch_scc1 3f",
-                  "4:"]
-        return lines
+        return lines + contains_salu()
     assert h == S
     x, y = al.get(1), al.get(2)
     z = al.get(3)
@@ -356,6 +349,18 @@ def contains_check(lean=False, h=S):
     return lines
 
 
+def contains_salu():
+    """the lean check's scalar part: the clean mask from the four compares
+    (universe 0 in bit 3), fresh hits, and the branch to the slow path"""
+    lines = ["s_mov_b32 %[c], 0"]
+    for u in range(P):
+        lines += [f"s_cmp_eq_u64 %[cmp{u}], 0",       # SCC = universe u clean
+                  "s_addc_u32 %[c], %[c], %[c]"]      # c = 2c + SCC
+    return lines + ["s_andn2_b32 %[c], %[c], %[found]",     # fresh hits; SCC = any
+                    "s_cbranch_scc1 3f",
+                    "4:"]
+
+
 def contains_slowpath():
     """the lean check's hit handler, placed after the loop: record gc for
     every fresh universe (bit 3 - u of c) and jump back"""
@@ -366,24 +371,32 @@ def contains_slowpath():
     return lines + ["s_branch 4b"]
 
 
-def contains_body(lean=False, h=S):
+def contains_body(lean=False, h=S, late=False):
     """the default schedule's body with the check after rows 6..7 (all eight
-    rows final), before the plane-1 exchange"""
+    rows final), before the plane-1 exchange; late (lean only): the check's
+    scalar part after that exchange, so the compares' results have landed
+    in their SGPRs when the SALU reads them"""
     b = body(DEFAULT)
     k = b.index(exchange(1)[0])
-    return b[:k] + contains_check(lean, h) + b[k:]
+    chk = contains_check(lean, h)
+    if not late:
+        return b[:k] + chk + b[k:]
+    sal = contains_salu()
+    assert chk[-len(sal):] == sal
+    return b[:k] + chk[:-len(sal)] + b[k:] + sal
 
 
-def contains_text(lean=False, h=S):
-    lines = ["s_cmp_eq_u32 %[g], 0", "s_cbranch_scc1 2f"] + prologue(DEFAULT) + ["1:"] + contains_body(lean, h) + \
+def contains_text(lean=False, h=S, late=False):
+    lines = ["s_cmp_eq_u32 %[g], 0", "s_cbranch_scc1 2f"] + prologue(DEFAULT) + ["1:"] + \
+        contains_body(lean, h, late) + \
         ["s_cmp_lg_u32 %[g], 0", "s_cbranch_scc1 1b", "s_waitcnt lgkmcnt(0)"]
     if lean:
         lines += ["s_branch 2f"] + contains_slowpath()
     return lines + ["2:"]
 
 
-def emit_contains(lean=False, h=S):
-    lines = contains_text(lean, h)
+def emit_contains(lean=False, h=S, late=False):
+    lines = contains_text(lean, h, late)
     asm = "\n".join(f'      "{l}\\n"' for l in lines)
     outs = ",\n".join([f'        "+{{v{R[j]}}}"(r[{j}])' for j in range(S)] +
                       [f'        [h{u}] "+s"(hit[{u}])' for u in range(P)])
@@ -393,7 +406,7 @@ def emit_contains(lean=False, h=S):
     pinned = sorted({x for x in L + RR + H1 + H0 + [H0U, H0D, H1U, H1D] + TEMPS})
     clob = ", ".join(f'"v{x}"' for x in pinned)
     if lean:
-        name = "split_contains_asm_lean" + ("" if h == S else f"_h{h}")
+        name = "split_contains_asm_lean" + ("_late" if late else "") + ("" if h == S else f"_h{h}")
         cmps = "uint64_t cmp0, cmp1, cmp2, cmp3;"
         cmp_outs = "[cmp0] \"=&s\"(cmp0), [cmp1] \"=&s\"(cmp1), [cmp2] \"=&s\"(cmp2), [cmp3] \"=&s\"(cmp3)"
         doc = ("// The same with the per-universe bookkeeping cut to two SALU per universe on\n"
@@ -426,7 +439,7 @@ __device__ __forceinline__ void {name}(uint32_t (&r)[8], const uint32_t (&w)[8],
 """
 
 
-def simulate_contains(r, w, m, gens, lean=False, h=S):
+def simulate_contains(r, w, m, gens, lean=False, h=S, late=False):
     """numpy run of split_contains_asm[_lean[_h<h>]]: returns (r, hits[4])"""
     v = np.zeros((N_VGPR_C, 64), np.uint32)
     v[:8] = r
@@ -434,7 +447,7 @@ def simulate_contains(r, w, m, gens, lean=False, h=S):
     v[M_REGS] = m
     hits, found = [0] * P, 0
     lds_plane = {}
-    seq = prologue(DEFAULT) + (contains_body(lean, h) * gens if gens else [])
+    seq = prologue(DEFAULT) + (contains_body(lean, h, late) * gens if gens else [])
     gc, c, scc = 0, 0, 0
     cmp = {}
     for l in seq:
@@ -586,32 +599,72 @@ __device__ __forceinline__ void {name}(uint32_t (&r)[8], uint32_t gens, uint32_t
 """
 
 
+OUT_TUNE = os.path.join(ROOT, "tools", "tune", "split_asm_tune.inc")
+
+_SIG_LOOP = "(uint32_t (&r)[8], uint32_t gens, uint32_t a_self, uint32_t a_prev, uint32_t a_next)"
+_SIG_CONT = ("(uint32_t (&r)[8], const uint32_t (&w)[8], const uint32_t (&m)[8], uint32_t gens, "
+             "uint32_t a_self, uint32_t a_prev, uint32_t a_next, uint32_t (&hit)[4])")
+_SIG_TWO = "(uint32_t (&a)[8], uint32_t (&b)[8], uint32_t gens, uint32_t a_self, uint32_t a_prev, uint32_t a_next)"
+
+
+def _ablation_decls():
+    """forward declarations of the tuning build's loops: step_kernels.hpp
+    names them in template branches the product never instantiates"""
+    names = [(f"split_gens_asm_v{k}", _SIG_LOOP) for k in range(1, len(VARIANTS))]
+    names += [("split_gens_asm2", _SIG_TWO), ("split_contains_asm", _SIG_CONT)]
+    names += [("split_contains_asm_lean_late" + ("" if h == S else f"_h{h}"), _SIG_CONT) for h in range(1, S + 1)]
+    return "".join(f"__device__ __forceinline__ void {n}{sig};\n" for n, sig in names)
+
+
 def emit():
     n, bad = check_banks(body())
-    fns = "".join(fn_text(f"split_gens_asm_v{k}", v) for k, v in enumerate(VARIANTS))
     return f"""// split_asm.inc -- GENERATED by tools/gen_split_asm.py; do not edit.
 // The generation loop of rule 11 (8-way row split, 4 universes per wave,
 // LDS exchange, the 6-LUT tail) with hand-allocated VGPRs: of its {n} VALU
 // per generation only the {len(bad)} h-layer ones read two sources from one
 // bank (see the generator).  {N_VGPR} VGPRs pinned.
 //
-// split_gens_asm_v<k>(r, gens, a_self, a_prev, a_next): r is gen_split's r[j]
+// split_gens_asm_v0(r, gens, a_self, a_prev, a_next): r is gen_split's r[j]
 // for S = 8; a_self / a_prev / a_next are the LDS byte addresses of this
-// lane's / lane i-1's / lane i+1's 16-B slot in the wave's two 1-KiB planes.
-// The variants differ only in schedule: {", ".join(f"v{k} = {v}" for k, v in enumerate(VARIANTS))}.
+// lane's / lane i-1's / lane i+1's 16-B slot in the wave's two 1-KiB planes
+// (schedule "{VARIANTS[0]}").  split_contains_asm_lean[_h<h>]: the same loop
+// with the fused Contains test (k_step_contains_split).  The measured
+// alternatives (other schedules, two groups per wave, the round-1 contains
+// bookkeeping, a late scalar test) are generated into
+// tools/tune/split_asm_tune.inc for the tuning build; they are only declared
+// here.
 #pragma once
 
 namespace lifeapi_impl {{
-{fns}{emit2()}{emit_contains()}{emit_contains(lean=True)}{"".join(emit_contains(True, h) for h in range(1, S))}
+{fn_text("split_gens_asm_v0", VARIANTS[0])}{emit_contains(lean=True)}{"".join(emit_contains(True, h) for h in range(1, S))}
+{_ablation_decls()}
+}}  // namespace lifeapi_impl
+"""
+
+
+def emit_tune():
+    fns = "".join(fn_text(f"split_gens_asm_v{k}", v) for k, v in enumerate(VARIANTS) if k)
+    return f"""// split_asm_tune.inc -- GENERATED by tools/gen_split_asm.py; do not edit.
+// The tuning build's variants of the rule-11 assembly loop (see
+// lifeapi_amd/csrc/split_asm.inc and the generator): schedules
+// {", ".join(f"v{k} = {v}" for k, v in enumerate(VARIANTS) if k)}; two groups per wave
+// (split_gens_asm2); the round-1 fused-Contains bookkeeping
+// (split_contains_asm); the lean test with its scalar part late
+// (split_contains_asm_lean_late[_h<h>]).
+#pragma once
+
+namespace lifeapi_impl {{
+{fns}{emit2()}{emit_contains()}{"".join(emit_contains(True, h, True) for h in range(1, S + 1))}
 }}  // namespace lifeapi_impl
 """
 
 
 if __name__ == "__main__":
-    text = emit()
+    texts = {OUT: emit(), OUT_TUNE: emit_tune()}
     if "--check" in sys.argv:
-        sys.exit(0 if open(OUT).read() == text else 1)
-    with open(OUT, "w") as f:
-        f.write(text)
+        sys.exit(0 if all(open(p).read() == t for p, t in texts.items()) else 1)
+    for p, t in texts.items():
+        with open(p, "w") as f:
+            f.write(t)
     n, bad = check_banks(body())
-    print(f"{OUT}: {n} VALU, {len(bad)} with a bank conflict")
+    print(f"{OUT} (+ {OUT_TUNE}): {n} VALU, {len(bad)} with a bank conflict")

@@ -10,6 +10,7 @@
 
 #include "lifeapi_tune.h"
 #include "step_kernels.hpp"
+#include "split_asm_tune.inc"
 #include "tile_asm.inc"
 #include "pair_asm.inc"
 
@@ -475,9 +476,10 @@ int lifeapi_tune_step_contains(const uint64_t *d_in, uint64_t *d_final, const ui
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
   using Fn = void (*)(const uint64_t *, uint64_t *, const uint64_t *, const uint64_t *, uint32_t *, uint64_t, uint32_t);
-  const Fn fns[4] = {k_step_contains_split<8, kContainsNet, 0>, k_step_contains_split<8, kContainsNet, 1>,
-                     k_step_contains_split<8, kContainsNet, 2>, k_step_contains_split<8, kContainsNet, 3>};
-  if (variant < 0 || variant > 3) return fail(LIFEAPI_E_INVALID, "unknown contains variant%s");
+  const Fn fns[5] = {k_step_contains_split<8, kContainsNet, 0>, k_step_contains_split<8, kContainsNet, 1>,
+                     k_step_contains_split<8, kContainsNet, 2>, k_step_contains_split<8, kContainsNet, 3>,
+                     k_step_contains_split<8, kContainsNet, 4>};
+  if (variant < 0 || variant > 4) return fail(LIFEAPI_E_INVALID, "unknown contains variant%s");
   hipLaunchKernelGGL(fns[variant], dim3(grid_for((n + 3) / 4, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream, d_in,
                      d_final, d_wanted, d_unwanted, d_first_gen, (uint64_t)n, generations);
   return launched("k_step_contains_split (tuning) launch");
