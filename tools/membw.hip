@@ -7,6 +7,11 @@
 //   membw         the full sweep
 //   membw calib   only the step kernel's shape (dwordx2, U=4, nt, one-shot
 //                 grid): the byte-counter calibration run for rocprofv3
+//   membw pingpong <universes>
+//                 the step kernel's shape as the bench runs it: ping-pong
+//                 between two buffers of <universes> x 512 B (1M: 1 GiB
+//                 footprint, partly served from the 256 MB Infinity Cache;
+//                 16M: 16 GiB, not)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -96,7 +101,41 @@ int run(const char *name, void *a, void *b, size_t bytes, int cus) {
   return 0;
 }
 
+int pingpong(u64 universes) {
+  const size_t bytes = universes * 512;
+  void *a, *b;
+  CHECK(hipMalloc(&a, bytes));
+  CHECK(hipMalloc(&b, bytes));
+  CHECK(hipMemset(a, 0x5a, bytes));
+  CHECK(hipMemset(b, 0x3c, bytes));
+  const u64 nvec = bytes / sizeof(u32x2), rows = nvec / 64;
+  const u64 blocks = (rows / 4 + 3) / 4;
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  std::vector<float> ms;
+  for (int rep = 0; rep < 30; ++rep) {
+    void *src = rep & 1 ? b : a, *dst = rep & 1 ? a : b;
+    CHECK(hipEventRecord(e0, 0));
+    hipLaunchKernelGGL((k_copy<u32x2, 4, 3>), dim3(blocks), dim3(256), 0, 0, (const u32x2 *)src, (u32x2 *)dst, nvec);
+    CHECK(hipEventRecord(e1, 0));
+    CHECK(hipEventSynchronize(e1));
+    float t;
+    CHECK(hipEventElapsedTime(&t, e0, e1));
+    if (rep >= 6) ms.push_back(t);
+  }
+  std::sort(ms.begin(), ms.end());
+  std::printf("{\"variant\": \"dwordx2 pingpong\", \"U\": 4, \"mode\": 3, \"universes\": %llu, \"ms_best\": %.4f, "
+              "\"ms_median\": %.4f, \"GBps_best\": %.1f, \"GBps_median\": %.1f}\n",
+              universes, ms.front(), ms[ms.size() / 2], 2.0 * bytes / (ms.front() * 1e-3) / 1e9,
+              2.0 * bytes / (ms[ms.size() / 2] * 1e-3) / 1e9);
+  CHECK(hipFree(a));
+  CHECK(hipFree(b));
+  return 0;
+}
+
 int main(int argc, char **argv) {
+  if (argc > 2 && std::string(argv[1]) == "pingpong") return pingpong(std::stoull(argv[2]));
   g_calib = argc > 1 && std::string(argv[1]) == "calib";
   const size_t bytes = size_t(1) << 29;  // 2^20 universes x 512 B
   void *a, *b;
