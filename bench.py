@@ -177,11 +177,14 @@ def median_launch_ms(hip, rt, a, b, gens, reps=10):
     return sorted(ms)[len(ms) // 2], ms
 
 
-def copy_ceiling():
-    """Best median GB/s of the same-shape HBM copy kernel (tools/membw.hip)
-    measured on MI355X and committed under profiles/; context for the roofline."""
-    path = os.path.join(ROOT, "profiles", "r01", "membw.jsonl")
-    best = None
+def copy_ceiling(n: int):
+    """Median GB/s of a plain copy with the step kernel's access shape,
+    ping-ponged between two buffers of n universes as this bench does
+    (tools/membw.hip `pingpong`, measured on MI355X and committed under
+    profiles/): the streaming ceiling for this footprint, context for the
+    roofline.  The nearest measured footprint is used."""
+    path = os.path.join(ROOT, "profiles", "r02", "membw_pingpong.jsonl")
+    rows = []
     try:
         with open(path) as f:
             for line in f:
@@ -189,11 +192,14 @@ def copy_ceiling():
                     d = json.loads(line)
                 except ValueError:
                     continue
-                if d.get("mode") in (0, 1, 2, 3) and "GBps_median" in d:
-                    best = max(best or 0.0, d["GBps_median"])
+                if "universes" in d and "GBps_median" in d:
+                    rows.append(d)
     except OSError:
         return None, None
-    return best, os.path.relpath(path, ROOT)
+    if not rows:
+        return None, None
+    best = min(rows, key=lambda d: abs(np.log2(d["universes"]) - np.log2(max(n, 1))))
+    return best["GBps_median"], f"{os.path.relpath(path, ROOT)} ({best['universes']} universes)"
 
 
 def load_pmc_traffic(n: int):
@@ -559,7 +565,7 @@ def main(argv=None):
             torch.cuda.empty_cache()
             secondary["config4"] = secondary_config4_1gpu(hip, rt)
 
-    ceiling, ceiling_src = copy_ceiling()
+    ceiling, ceiling_src = copy_ceiling(n)
     cpu = None
     if want_cpu:
         cpu = cpu_baseline(x_cpu, args.cpu_seconds)
