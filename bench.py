@@ -28,7 +28,6 @@ Prints ONE JSON line on rank 0 (contract: task brief).
 from __future__ import annotations
 
 import argparse
-import importlib
 import json
 import os
 import socket
@@ -101,11 +100,11 @@ def _free_port() -> int:
 
 
 def spawn_ranks(n: int, argv: list[str]) -> int:
-    """Start `n` ranks of this script under torch.distributed.run as a CHILD
-    process (this process has not touched the GPU and never execs) and
-    return its exit status."""
+    """Start `n` ranks of the launching script (normally this one) under
+    torch.distributed.run as a CHILD process (this process has not touched
+    the GPU and never execs) and return its exit status."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(sys.argv[0]), *argv]
     log("+ " + " ".join(cmd))
     return subprocess.call(cmd)
 
@@ -134,16 +133,8 @@ class HipRuntime:
 
 
 def load_kernels(backend: str, local_rank: int, world: int):
-    """The HIP library (lifeapi_amd.hip) and its runtime.  LIFEAPI_BENCH_STUB
-    names a CPU stand-in module used ONLY by tests/test_bench_ranks.py to
-    rehearse this rank logic without a GPU; it is refused when a GPU is
-    visible, and the line it prints says so."""
-    stub = os.environ.get("LIFEAPI_BENCH_STUB")
-    if stub:
-        if torch.cuda.is_available():
-            raise RuntimeError("LIFEAPI_BENCH_STUB is for GPU-less rank rehearsals only")
-        mod = importlib.import_module(stub)
-        return mod, mod.Runtime(local_rank)
+    """The HIP library (lifeapi_amd.hip) and this rank's runtime.  There is
+    no fallback: without a GPU or the built library this raises."""
     import lifeapi_amd.hip as hip
     return hip, HipRuntime(local_rank, world, backend)
 
@@ -615,7 +606,7 @@ def main(argv=None):
             "secondary": secondary,
         }
         if rt.kind != "hip":
-            line["kernel_backend"] = f"STUB {os.environ.get('LIFEAPI_BENCH_STUB')} (CPU rank rehearsal, not a measurement)"
+            line["kernel_backend"] = f"STUB {rt.kind} (CPU rank rehearsal, not a measurement)"
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

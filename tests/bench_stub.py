@@ -1,8 +1,8 @@
 """TEST INFRASTRUCTURE ONLY: a CPU stand-in for ``lifeapi_amd.hip`` with which
 tests/test_bench_ranks.py rehearses bench.py's rank logic (rank spawning,
 barrier + MAX timing, per-shard first-launch verification, hash all-gather)
-on a machine without a GPU.  bench.py loads it only when LIFEAPI_BENCH_STUB
-names it, refuses it when a GPU is visible, and marks its line as a stub.
+on a machine without a GPU, through tests/bench_rank_runner.py (which swaps
+it in for bench.py's kernel loader; bench.py never loads it).
 The compute is the oracle's C port (oracle/lifeapi_oracle.c), so the digests
 it produces are checked against the reference-generated golden digests,
 exactly as the GPU ranks' are.  Never a measurement.
@@ -31,7 +31,7 @@ class _Event:
 
 
 class Runtime:
-    kind = "stub"
+    kind = "oracle-port stub"
 
     def __init__(self, local_rank: int):
         self.device = torch.device("cpu")

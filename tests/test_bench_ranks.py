@@ -4,9 +4,10 @@
 ranks itself, shard the problem, run the timed region with its barrier and
 MAX over ranks, verify every rank's shard of the first launch against the
 reference-generated digests (tests/golden/golden.json, *_small entries) and
-all-gather the per-universe hashes.  The HIP kernels are replaced by the
-oracle-backed CPU stand-in tests/bench_stub.py (bench.py refuses it when a
-GPU is visible); everything else is the code the GPU ranks run.
+all-gather the per-universe hashes.  tests/bench_rank_runner.py runs
+bench.py's main() with the HIP kernels replaced by the oracle-backed CPU
+stand-in tests/bench_stub.py (bench.py itself has no such path); everything
+else is the code the GPU ranks run.
 """
 import json
 import os
@@ -20,12 +21,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _bench(*args, timeout=240):
-    env = dict(os.environ, LIFEAPI_BENCH_BACKEND="gloo", LIFEAPI_BENCH_STUB="tests.bench_stub",
-               HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="", MASTER_ADDR="127.0.0.1",
-               OMP_NUM_THREADS="1")
+    env = dict(os.environ, LIFEAPI_BENCH_BACKEND="gloo", HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="",
+               MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
         env.pop(k, None)
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], cwd=ROOT, env=env,
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "bench_rank_runner.py"), *args], cwd=ROOT, env=env,
                        capture_output=True, text=True, timeout=timeout)
     assert r.returncode == 0, r.stderr[-4000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -44,7 +44,7 @@ def _expected_collect(total, seed, gens_done):
 def test_bench_gpus2_strong_config4_spawns_two_ranks():
     line, err = _bench("--gpus", "2", "--config", "4", "--universes", str(1 << 14),
                        "--steps", "3", "--warmup", "2", "--no-cpu-baseline")
-    assert "torch.distributed.run" in err          # bench.py started the ranks itself
+    assert "torch.distributed.run" in err and "bench_rank_runner.py" in err  # bench.py's spawner started the ranks
     assert line["n_gpus"] == 2 and line["collective_world_size"] == 2
     assert line["scaling"] == "strong"
     assert line["config"]["global_universes"] == 1 << 14
