@@ -95,7 +95,16 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
   if (generations > 2) {  // the layout of the shipped step for gens > 2
-    hipLaunchKernelGGL((k_step_contains_split<8, kContainsNet, kContainsAsm>), dim3(grid_for((n + 3) / 4, cus, 0)), dim3(kBlock), 0,
+    // two kernels, one per register layout (a target window of <= 4 rows in
+    // 64 VGPRs, 8 waves per SIMD; wider ones): each wave finds the window and
+    // only the matching kernel works (step_kernels.hpp kContainsLo/Hi)
+    const dim3 grid(grid_for((n + 3) / 4, cus, 0));
+    hipLaunchKernelGGL((k_step_contains_split<8, kContainsNet, kContainsLo>), grid, dim3(kBlock), 0,
+                       (hipStream_t)stream, d_in, d_final, d_wanted, d_unwanted, d_first_gen,
+                       (uint64_t)n, generations);
+    rc = launched("k_step_contains_split launch");
+    if (rc != LIFEAPI_OK) return rc;
+    hipLaunchKernelGGL((k_step_contains_split<8, kContainsNet, kContainsHi>), grid, dim3(kBlock), 0,
                        (hipStream_t)stream, d_in, d_final, d_wanted, d_unwanted, d_first_gen,
                        (uint64_t)n, generations);
   } else {

@@ -203,31 +203,43 @@ __global__ __launch_bounds__(kBlock) void k_step_split(const uint64_t *in, uint6
 // The same on the 8-way split layout (k_step_split): 4 universes per wave.
 // The target is put into the same register layout once, replicated for the
 // 4 universes; after every generation (r ^ w) & (w | u) is OR-ed over the
-// registers and one ballot per universe (its bits are every P-th) tests it,
-// with no branch per universe.  The check costs 19 VALU per wave-generation
-// on top of the step's 68 (8 differences, 3 OR3, and per universe a masked
-// OR + compare: +28 % VALU, and +28 % time with the lean bookkeeping,
-// profiles/r02/contains_ab.jsonl); on a target spanning h <= 8 rows, h
-// differences and fewer ORs (13 VALU for h = 4: +26 % time).
-// Without d_final, a wave stops once all its universes have hit.
+// registers and tested per universe (its bits are every P-th).
+// Without d_final, a wave of the compiled loop stops once all its universes
+// have hit.
 constexpr uint32_t kDiff = ((TA ^ TB) & (TB | TC)) & 0xFF;  // (s ^ wanted) & (wanted | unwanted)
 constexpr int kContainsNet = 6;  // tail network of the fused kernel (as k_step's default, rule 11)
-// ASM: 0 = the compiled loop below, 1 = the assembly loop of split_asm.inc
-// (split_contains_asm), 2 = its lean-bookkeeping variant
-// (split_contains_asm_lean: two SALU per universe and generation instead of
-// eight; 1.668 against 1.760 ms on config 3, profiles/r02/contains_ab.jsonl),
-// 3 = the lean loop on the target's row window: every wave finds the
-// smallest cyclic window [y0, y0 + h) of rows that holds all of the target's
-// care cells (wanted | unwanted) and, when h <= 8, rotates the universes and
-// the target up by y0 rows (Life on the torus commutes with translation, and
-// so does Contains), so that the care rows are the split layout's residues
-// 0..h-1 and the test differences only h of the 8 registers
-// (split_contains_asm_lean_h<h>); d_final is rotated back.  4 = 3 with the
-// test's scalar part after the plane-1 exchange (split_contains_asm_lean_late*).  On config 3
-// with a block + ring target (h = 4): 1.621 ms against 1.670 for 2 and 1.291
-// for the plain step (profiles/r02/contains_ab_window.jsonl).
-// step.hip ships kContainsAsm
-constexpr int kContainsAsm = 3;
+// ASM selects the loop (times: config 3, 64K universes x 1024 generations,
+// a block + ring target, against the plain step's 1.27-1.30 ms;
+// profiles/r02/contains_ab*.jsonl):
+//   0  the compiled loop below (a ballot per universe and generation)
+//   1  the assembly loop of split_asm.inc with the test after every
+//      generation: 8 differences, 3 OR3, per universe a masked OR + compare
+//      and 8 SALU (1.760 ms)
+//   2  1 with lean bookkeeping: two SALU per universe and generation, hits
+//      on a slow path (1.668)
+//   3  2 on the target's row window: every wave finds the smallest cyclic
+//      window [y0, y0 + h) of rows that holds all of the target's care cells
+//      (wanted | unwanted) and, when h <= 8, rotates the universes and the
+//      target up by y0 rows (Life on the torus commutes with translation,
+//      and so does Contains), so that the care rows are the split layout's
+//      residues 0..h-1 and the test differences only h of the 8 registers;
+//      d_final is rotated back (1.558-1.621; 78-87 VGPRs, 5-6 waves/SIMD)
+//   4  3 with the scalar part after the plane-1 exchange (no gain)
+//   5  3 with the test batched over eight generations for h <= 7: each
+//      generation's OR of differences occupies bits 0..3 only, so it packs
+//      into a nibble of one word, whose lane OR (DPP) and scalar test run
+//      once per block (1.456; 92 VGPRs, 4 waves)
+//   6  3 in the low register layout: a window of at most 4 rows, the target
+//      in v52..v59 (1.563: the occupancy alone gains nothing)
+//   7  5 in the low layout (1.397, +9.8 %: 64 VGPRs, 8 waves)
+//   8  the rest of 5: windows of more than 4 rows (batched up to 7, the
+//      per-generation test on 8 and on targets with no window)
+// 6 and 7 do nothing for a window wider than 4 rows, 8 nothing for the
+// others.  step.hip ships the pair kContainsLo + kContainsHi, launched one
+// after the other: every wave of both finds the same window, so exactly one
+// of them works and the other's waves return at once.
+constexpr int kContainsLo = 7, kContainsHi = 8;
+constexpr uint32_t kLowRows = 4;  // tools/gen_split_asm.py LOW_H
 
 __device__ __forceinline__ uint64_t rotr64(uint64_t v, uint32_t k) {
   return (v >> k) | (v << ((64 - k) & 63));
@@ -264,6 +276,8 @@ __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *
     const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(rm >> 32));
     care_window((uint64_t)lo | (uint64_t)hi << 32, y0, h);
     if (h > S) y0 = 0, h = S;
+    if ((ASM == 6 || ASM == 7) && h > kLowRows) return;  // the low layout: windows of <= 4 rows only
+    if (ASM == 8 && h <= kLowRows) return;                // ... and 8 the rest
   }
   uint32_t tw[S], tu[S];
   {
@@ -281,22 +295,50 @@ __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *
 
   const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock * P;
   for (uint64_t u0 = ((uint64_t)blockIdx.x * kWavesPerBlock + wib) * P; u0 < n; u0 += stride) {
+    // the wave's universes u0 .. u0 + avail - 1 from scalar bases: a 64-bit
+    // lane address or a vector copy of n kept across the loop would cost
+    // VGPRs, and the low layout's occupancy hangs on the last four
+    const uint64_t left = n - u0;
+    const uint32_t avail = (left >> 2) ? (uint32_t)P : (uint32_t)left;
+    const uint64_t *src = in + u0 * kWave;
     uint32_t r[S];
     W c[P];
 #pragma unroll
-    for (int u = 0; u < P; ++u) c[u] = u0 + u < n ? split(rotr64(in[(u0 + u) * kWave + lane], y0)) : W{0u, 0u};
+    for (int u = 0; u < P; ++u) c[u] = (uint32_t)u < avail ? split(rotr64(src[u * kWave + lane], y0)) : W{0u, 0u};
     Split<S>::load(c, r);
     uint32_t hit[P];
 #pragma unroll
     for (int u = 0; u < P; ++u) hit[u] = 0;
     uint32_t found = 0;
     if constexpr (ASM) {  // split_asm.inc: the default generation loop with the test fused in
-      static_assert(S == 8 && NET == 6, "split_contains_asm is rule 11");
+      static_assert(S == 8 && NET == 6 && P == 4, "split_contains_asm is rule 11");
       const uint32_t base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)(
           lds + wib * S * kWave);
       const uint32_t self = base + lane * 16u, prev = base + ((lane + kWave - 1) & (kWave - 1)) * 16u,
                      next = base + ((lane + 1) & (kWave - 1)) * 16u;
-      if constexpr (ASM == 4) {
+      if constexpr (ASM == 8) {
+        switch (h) {  // wave-uniform, > kLowRows
+          case 5: split_contains_asm_batch_h5(r, tw, tm, gens, self, prev, next, hit); break;
+          case 6: split_contains_asm_batch_h6(r, tw, tm, gens, self, prev, next, hit); break;
+          case 7: split_contains_asm_batch_h7(r, tw, tm, gens, self, prev, next, hit); break;
+          default: split_contains_asm_lean(r, tw, tm, gens, self, prev, next, hit); break;
+        }
+      } else if constexpr (ASM == 6) {
+        split_contains_asm_lean_lo(r, tw, tm, gens, self, prev, next, hit);
+      } else if constexpr (ASM == 7) {
+        split_contains_asm_batch_lo(r, tw, tm, gens, self, prev, next, hit);
+      } else if constexpr (ASM == 5) {
+        switch (h) {  // wave-uniform
+          case 1: split_contains_asm_batch_h1(r, tw, tm, gens, self, prev, next, hit); break;
+          case 2: split_contains_asm_batch_h2(r, tw, tm, gens, self, prev, next, hit); break;
+          case 3: split_contains_asm_batch_h3(r, tw, tm, gens, self, prev, next, hit); break;
+          case 4: split_contains_asm_batch_h4(r, tw, tm, gens, self, prev, next, hit); break;
+          case 5: split_contains_asm_batch_h5(r, tw, tm, gens, self, prev, next, hit); break;
+          case 6: split_contains_asm_batch_h6(r, tw, tm, gens, self, prev, next, hit); break;
+          case 7: split_contains_asm_batch_h7(r, tw, tm, gens, self, prev, next, hit); break;
+          default: split_contains_asm_lean(r, tw, tm, gens, self, prev, next, hit); break;
+        }
+      } else if constexpr (ASM == 4) {
         switch (h) {  // wave-uniform
           case 1: split_contains_asm_lean_late_h1(r, tw, tm, gens, self, prev, next, hit); break;
           case 2: split_contains_asm_lean_late_h2(r, tw, tm, gens, self, prev, next, hit); break;
@@ -340,14 +382,15 @@ __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *
     }
     if (fin) {
       Split<S>::store(r, c);
+      uint64_t *dst = fin + u0 * kWave;
 #pragma unroll
       for (int u = 0; u < P; ++u)
-        if (u0 + u < n) fin[(u0 + u) * kWave + lane] = rotr64(join(c[u]), (64 - y0) & 63);
+        if ((uint32_t)u < avail) dst[u * kWave + lane] = rotr64(join(c[u]), (64 - y0) & 63);
     }
     if (lane == 0) {
 #pragma unroll
       for (int u = 0; u < P; ++u)
-        if (u0 + u < n) first[u0 + u] = hit[u];
+        if ((uint32_t)u < avail) first[u0 + u] = hit[u];
     }
   }
 }

@@ -125,3 +125,59 @@ def test_simulated_windowed_contains(port, h, late):
                                     _to_split(np.stack([mr] * 4)), gens, lean=True, h=h, late=late)
     assert hits == exp, (h, y0, hits, exp)
     assert (got == _to_split(_rot_rows(s, y0))).all()
+
+
+@pytest.mark.parametrize("low", [False, True])
+@pytest.mark.parametrize("h", range(1, 8))
+def test_simulated_batched_contains(port, h, low):
+    """split_contains_asm_batch_h<h> / _batch_lo (the test batched over eight
+    generations: a nibble per generation, one DPP lane OR and one scalar
+    test per block, gens % 8 leading single generations)
+    against the oracle's step-then-Contains loop, for generation counts with
+    every remainder and hits at every position of a block."""
+    if low and h > g.LOW_H:
+        pytest.skip("the low layout takes targets of at most 4 rows")
+    rng = np.random.default_rng(700 + h)
+    y0 = int(rng.integers(64))
+    rows = np.uint64(((((1 << h) - 1) << y0) | (((1 << h) - 1) >> (64 - y0))) & ((1 << 64) - 1))
+    care = np.zeros(64, np.uint64)
+    for c in range(30, 33):
+        care[c] = rows
+    # the target is universe 0's window at generation 13; universes 1 and 2
+    # start 5 and 9 generations ahead, so the hits land at different places
+    # in a block (and earlier, if the window matches by chance)
+    for seed in range(800 + 16 * h, 816 + 16 * h):  # a soup whose window at generation 13 is busy
+        base = port.fill(1, seed=seed)[0]
+        wanted = port.step_batch(base[None], 13)[0] & care
+        if sum(bin(int(v)).count("1") for v in wanted) >= max(2, h):
+            break
+    unwanted = care & ~wanted
+    x = np.stack([base, port.step_batch(base[None], 5)[0], port.step_batch(base[None], 9)[0],
+                  port.fill(1, seed=950 + h)[0]])
+    xr, wr, mr = _rot_rows(x, y0), _rot_rows(wanted, y0), _rot_rows(wanted | unwanted, y0)
+    W, M = _to_split(np.stack([wr] * 4)), _to_split(np.stack([mr] * 4))
+    with g.layout(low):
+        for gens in (0, 1, 2, 3, 7, 8, 9, 15, 16, 21):
+            exp, s = [0] * 4, x.copy()
+            for k in range(1, gens + 1):
+                s = port.step_batch(s, 1)
+                for u in range(4):
+                    if not exp[u] and (((s[u] ^ wanted) & (wanted | unwanted)) == 0).all():
+                        exp[u] = k
+            got, hits = g.simulate_batch(_to_split(xr), W, M, gens, h if not low else g.LOW_H)
+            assert hits == exp, (h, gens, hits, exp)
+            assert (got == _to_split(_rot_rows(s, y0))).all()
+        assert len({e for e in exp[:3] if e}) >= 2, exp  # hits at two or more distinct generations
+
+
+def test_batched_dpp_chain_reaches_lane_63():
+    """the six in-place DPP ORs leave the OR of all 64 lanes in lane 63, for
+    single-lane words at every lane (the simulator's DPP model: row_shr
+    within rows of 16 lanes, row_bcast 15 / 31 into the masked rows)"""
+    a = g.ACC_HI
+    for lane in range(64):
+        v = np.zeros((g.N_VGPR_C, 64), np.uint32)
+        v[a, lane] = 1 << (lane % 32)
+        for line in g.batch_chain():
+            g._dpp(v, line)
+        assert v[a, 63] == 1 << (lane % 32), lane

@@ -73,13 +73,17 @@ def test_bad_cfgs_rejected(tune, hip):
             tune.step(d, generations=1, cfg=tune.LaunchCfg(*bad))
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
-@pytest.mark.parametrize("gens", [3, 6, 37])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("gens", [3, 6, 8, 9, 37])
 @pytest.mark.parametrize("with_final", [False, True])
 def test_step_contains_variants(tune, port, variant, gens, with_final):
-    """The fused Step + Contains kernels of the tuning build (0 compiled loop,
-    1 assembly loop, 2 lean bookkeeping = shipped) against the oracle's
-    step-then-Contains loop (LifeTarget.hpp:44-51), ragged n, planted hits."""
+    """The fused Step + Contains kernels of the tuning build (step_kernels.hpp
+    kContainsAsm: 0 compiled loop ... 7 batched, low layout) against the
+    oracle's step-then-Contains loop (LifeTarget.hpp:44-51), ragged n,
+    planted hits; gens 3 / 6 / 8 / 9 / 37 = 0 / 0 / 1 / 1 / 4 blocks of
+    eight after 3 / 6 / 0 / 1 / 5 single generations for the batched test.
+    (Variant 8 takes only windows wider than this 4-row target: see
+    test_step_contains_row_window.)"""
     import torch
     n = 1003
     x = port.fill(n, seed=223) & port.fill(n, seed=224) & port.fill(n, seed=225)
@@ -126,17 +130,28 @@ def _target(kind):
     elif kind == "row":
         for c in range(10, 20):
             u[c] = np.uint64(1 << 7)
+    elif kind == "six":
+        for c in range(21, 25):
+            w[c] = np.uint64(0xF << 31)
+        for c in range(20, 26):
+            u[c] = np.uint64(0x3F << 30)
+        u &= ~w
     return w, u
 
 
-@pytest.mark.parametrize("kind", ["seam", "tall", "row", "empty"])
+@pytest.mark.parametrize("kind", ["seam", "tall", "row", "empty", "six"])
 @pytest.mark.parametrize("with_final", [False, True])
-@pytest.mark.parametrize("variant", [3, 4])
+@pytest.mark.parametrize("variant", [3, 4, 5, 6, 7, 8])
 def test_step_contains_row_window(tune, hip, port, kind, with_final, variant):
-    """variant 3 (the target's row window, universes rotated into it and
-    back) against the oracle and against the shipped kernel, for targets
-    whose window wraps the row seam, exceeds 8 rows, is one row, or is empty."""
+    """variants 3..8 (the target's row window, universes rotated into it and
+    back) against the oracle and against the shipped kernel pair, for
+    targets whose window wraps the row seam, exceeds 8 rows, is one row, is
+    empty, or is six rows (batched in the high layout)."""
     import torch
+    if variant in (6, 7) and kind in ("tall", "six"):
+        pytest.skip("the low-layout variants take windows of at most 4 rows")
+    if variant == 8 and kind not in ("tall", "six"):
+        pytest.skip("variant 8 takes windows of more than 4 rows")
     n, gens = 2001, 9
     w, u = _target(kind)
     x = port.fill(n, seed=501) & port.fill(n, seed=502)
@@ -157,3 +172,21 @@ def test_step_contains_row_window(tune, hip, port, kind, with_final, variant):
         assert (to_host(fin) == port.step_batch(x, gens)).all()
     ship, _ = hip.step_contains(to_dev(x), to_dev(w[None]), to_dev(u[None]), gens)
     assert (ship.cpu().numpy() == exp).all()
+
+
+@pytest.mark.parametrize("caps", [(1, 1), (8, 5), (0, 0)])
+@pytest.mark.parametrize("kind", ["seam", "six", "tall"])
+def test_step_contains_pair_capped_grid(tune, hip, port, caps, kind):
+    """the shipped pair (7 then 8) with capped grids: every wave strides over
+    several groups of universes, and the kernel with nothing to do returns"""
+    import torch
+    n, gens = 3001, 11
+    w, u = _target(kind)
+    x = port.fill(n, seed=601) & port.fill(n, seed=602)
+    x[::4] &= ~(w | u)
+    x[::8] |= w
+    fin = torch.empty((n, 64), dtype=torch.int64, device="cuda")
+    got = tune.step_contains_pair(to_dev(x), to_dev(w[None]), to_dev(u[None]), gens, *caps, final=fin)
+    ship, shipfin = hip.step_contains(to_dev(x), to_dev(w[None]), to_dev(u[None]), gens, final=torch.empty_like(fin))
+    assert torch.equal(got, ship) and torch.equal(fin, shipfin)
+    assert (to_host(fin) == port.step_batch(x, gens)).all()

@@ -15,7 +15,7 @@ The other 52 (the tails and the ring rotates) are conflict-free here:
   r[j]  bank j        (v0..v7, the ds_write_b128 tuples)
   L[j]  bank j + 2    (ds_read_b128 at v[10:13], v[14:17])
   R[j]  bank j        (ds_read_b128 at v[20:23], v[24:27]); h1[j] overwrites R[j]
-                      (h1[3] in v55: see H1)
+                      (h1[3] in v51: see H1)
   h0[j] bank j + 1,  h1[j] bank j  (vertical triples j-1, j, j+1 span 3 banks;
         maj(h1[j+1], h1[j-1], h0[j+1]) needs h0's offset odd against h1's)
   tail temps by bank: g1/g4 j+1, g2 j+2, g3 j+3, g5 j+2 (g4, g5 and r[j]
@@ -46,12 +46,13 @@ L = [10 + j for j in range(4)] + [14 + j - 4 for j in range(4, 8)]
 RR = [20 + j for j in range(4)] + [24 + j - 4 for j in range(4, 8)]
 # h1[j] overwrites R[j], except h1[3]: rows 4..7's tails still read it after
 # the next generation's plane-0 reads have refilled v[20:23] (PIPE)
-H1 = RR[:3] + [55] + RR[4:]
+H1 = RR[:3] + [51] + RR[4:]
 H0 = [29 + j for j in range(8)]                 # bank j + 1
 H0U, H0D, H1U, H1D = 40, 41, 39, 44              # banks 0, 1, 3, 0 (as h0[-1], h0[8], h1[-1], h1[8])
-TEMPS = [8, 9, 18, 19, 28, 37, 38, 42, 43, 45, 46, 47, 48, 49, 50, 51]
-A_SELF, A_PREV, A_NEXT = 52, 53, 54
-N_VGPR = 56
+# three per bank: a pair of interleaved tails needs at most three of one bank
+TEMPS = [8, 9, 18, 19, 28, 37, 38, 42, 43, 45, 47, 48]
+A_SELF, A_PREV, A_NEXT = 46, 49, 50
+N_VGPR = 52
 
 
 class Alloc:
@@ -274,9 +275,16 @@ __device__ __forceinline__ void split_gens_asm2(uint32_t (&a)[8], uint32_t (&b)[
 # after each generation, d = OR_j (r_j ^ w_j) & m_j (m = wanted | unwanted,
 # LifeTarget.hpp:44-51), one ballot per universe (its bits are every 4th),
 # and the first generation with an empty ballot is kept per universe in SGPRs.
-W_REGS = [57, 58, 59, 60, 61, 62, 63, 64]        # w_j: bank j + 1
-M_REGS = [66, 67, 56, 65, 70, 71, 68, 69]        # m_j: bank j + 2
-N_VGPR_C = 72
+W_REGS = [53, 54, 55, 56, 57, 58, 59, 60]        # w_j: bank j + 1
+M_REGS = [62, 63, 52, 61, 66, 67, 64, 65]        # m_j: bank j + 2
+N_VGPR_C = 68
+# the "low" layout for targets of at most 4 rows: w_0..3 / m_0..3 in v52..v59
+# (same banks) and the batched test's block word in v60, so that the
+# kernel's VGPR count, and with it the waves per SIMD, stays at the plain
+# step's 8 (at most 64 VGPRs) instead of 5 (87 VGPRs with all eight rows)
+W_LO = [53, 54, 55, 56]
+M_LO = [58, 59, 52, 57]
+LOW_H = 4
 DIFF = 0x28        # (r ^ w) & m
 OR3 = 0xFE         # a | b | c
 ORAND = 0xA8       # (a | b) & c
@@ -308,6 +316,25 @@ def _or_to_two(d, al):
     return lines + [op(z, d[6], d[7], x, OR3)], y, z
 
 
+_LAYOUT = {"low": False}
+
+
+def _wm():
+    return (W_LO, M_LO) if _LAYOUT["low"] else (W_REGS, M_REGS)
+
+
+class layout:
+    """with layout(low): the generators use the low register layout"""
+    def __init__(self, low):
+        self.low = low
+
+    def __enter__(self):
+        self.prev, _LAYOUT["low"] = _LAYOUT["low"], self.low
+
+    def __exit__(self, *a):
+        _LAYOUT["low"] = self.prev
+
+
 def contains_check(lean=False, h=S):
     """lean: the per-universe bookkeeping on the fast path is 2 SALU per
     universe (s_cmp_eq_u64 + s_addc_u32 building the clean mask, universe 0
@@ -321,10 +348,13 @@ def contains_check(lean=False, h=S):
     for j in range(h):
         t = al.get(j)
         d.append(t)
-    lines = [op(d[j], R[j], W_REGS[j], M_REGS[j], DIFF) for j in range(h)]
+    wr, mr = _wm()
+    lines = [op(d[j], R[j], wr[j], mr[j], DIFF) for j in range(h)]
     if lean:
         red, y, z = _or_to_two(d, al)
         lines += red
+        for t in set(d) - {y, z}:  # consumed: the masked ORs may reuse them
+            al.put(t)
         lines.append("s_add_u32 %[gc], %[gc], 1")
         ts = [al.get(b) for b in range(P)]
         for u in range(P):
@@ -396,17 +426,20 @@ def contains_text(lean=False, h=S, late=False):
 
 
 def emit_contains(lean=False, h=S, late=False):
+    low = _LAYOUT["low"]
+    wr, mr = _wm()
     lines = contains_text(lean, h, late)
     asm = "\n".join(f'      "{l}\\n"' for l in lines)
     outs = ",\n".join([f'        "+{{v{R[j]}}}"(r[{j}])' for j in range(S)] +
                       [f'        [h{u}] "+s"(hit[{u}])' for u in range(P)])
-    ins = ", ".join([f'"{{v{W_REGS[j]}}}"(w[{j}])' for j in range(S)] +
-                    [f'"{{v{M_REGS[j]}}}"(m[{j}])' for j in range(S)] +
+    nt = h if low else S
+    ins = ", ".join([f'"{{v{wr[j]}}}"(w[{j}])' for j in range(nt)] +
+                    [f'"{{v{mr[j]}}}"(m[{j}])' for j in range(nt)] +
                     [f'[m{u}] "s"(0x11111111u << {u})' for u in range(P)])
     pinned = sorted({x for x in L + RR + H1 + H0 + [H0U, H0D, H1U, H1D] + TEMPS})
     clob = ", ".join(f'"v{x}"' for x in pinned)
     if lean:
-        name = "split_contains_asm_lean" + ("_late" if late else "") + ("" if h == S else f"_h{h}")
+        name = "split_contains_asm_lean" + ("_late" if late else "") + ("_lo" if low else "" if h == S else f"_h{h}")
         cmps = "uint64_t cmp0, cmp1, cmp2, cmp3;"
         cmp_outs = "[cmp0] \"=&s\"(cmp0), [cmp1] \"=&s\"(cmp1), [cmp2] \"=&s\"(cmp2), [cmp3] \"=&s\"(cmp3)"
         doc = ("// The same with the per-universe bookkeeping cut to two SALU per universe on\n"
@@ -443,8 +476,9 @@ def simulate_contains(r, w, m, gens, lean=False, h=S, late=False):
     """numpy run of split_contains_asm[_lean[_h<h>]]: returns (r, hits[4])"""
     v = np.zeros((N_VGPR_C, 64), np.uint32)
     v[:8] = r
-    v[W_REGS] = w
-    v[M_REGS] = m
+    wr, mr = _wm()
+    v[wr] = w[:len(wr)]
+    v[mr] = m[:len(mr)]
     hits, found = [0] * P, 0
     lds_plane = {}
     seq = prologue(DEFAULT) + (contains_body(lean, h, late) * gens if gens else [])
@@ -492,6 +526,308 @@ def simulate_contains(r, w, m, gens, lean=False, h=S, late=False):
         else:
             _exec(v, l, lds_plane)
     return v[:8].copy(), hits
+
+
+# ---- the batched test (split_contains_asm_batch_h<h>, h <= 7): the same
+# differences, but the cross-lane part runs once per EIGHT generations.  With
+# the target's care rows rotated into rows 0..h-1, every difference register
+# is zero outside its bits 0..3 (row j of the four universes), and so is
+# their OR x_k; generation k of a block therefore packs into bits 4k..4k+3 of
+# one word with a single v_lshl_or_b32 (x_0 is written as is).  The OR of that
+# word over the 64 lanes is a DPP chain (row_shr 1/2/4/8, row_bcast 15/31)
+# issued inside the next block's first h-layer, so that its two-wait-state
+# hazards are filled by independent work, then one v_readlane and one s_nor:
+# universe u is clean at generation k iff bit 4k + u is clear in every lane.
+# Per wave-generation (h = 4): 4 differences, 2 ORs, 1 shift-OR and 7 / 8
+# for the chain = 7.9 VALU against 13, and 3 SALU per block instead of 12 per
+# generation.  gens % 8 leading generations run the lean per-generation loop.
+# The block word needs one register, free in both layouts: w[7] (h <= 7) or
+# v60 (low).
+ACC_HI, ACC_LO = 60, 60
+KB = 8             # generations per block
+BATCH_MAX_H = 7
+OR2 = 0xFC         # a | b
+
+
+def _acc():
+    return ACC_LO if _LAYOUT["low"] else ACC_HI
+
+
+def _or_into(d, dst, al):
+    """dst = OR of registers d (OR3 tree, the last OR writing dst)"""
+    lines, d = [], list(d)
+    while len(d) > 3:
+        t = al.get(len(lines) + 1)
+        lines.append(op(t, d[0], d[1], d[2], OR3))
+        d = d[3:] + [t]
+    a, b, c = (d + d[-1:] * 2)[:3]
+    return lines + [op(dst, a, b, c, OR3)]
+
+
+def batch_x(h, k, al):
+    """generation k of the block: ACC = x_k (k = 0) or ACC |= x_k << 4k,
+    x_k = OR_j (r_j ^ w_j) & m_j over the h care registers"""
+    acc = _acc()
+    wr, mr = _wm()
+    if h == 1 and k == 0:
+        return [op(acc, R[0], wr[0], mr[0], DIFF)]
+    d = [al.get(j) for j in range(h)]
+    lines = [op(d[j], R[j], wr[j], mr[j], DIFF) for j in range(h)]
+    if k == 0:
+        return lines + _or_into(d, acc, al)
+    if h == 1:
+        return lines + [f"v_lshl_or_b32 v{acc}, v{d[0]}, {4 * k}, v{acc}"]
+    x = al.get(3)
+    return lines + _or_into(d, x, al) + [f"v_lshl_or_b32 v{acc}, v{x}, {4 * k}, v{acc}"]
+
+
+def batch_chain():
+    """the lane OR of the block word into lane 63 (six in-place DPP ORs)"""
+    a = _acc()
+    return [f"v_or_b32_dpp v{a}, v{a}, v{a} row_shr:{n} row_mask:0xf bank_mask:0xf" for n in (1, 2, 4, 8)] + \
+           [f"v_or_b32_dpp v{a}, v{a}, v{a} row_bcast:15 row_mask:0xa bank_mask:0xf",
+            f"v_or_b32_dpp v{a}, v{a}, v{a} row_bcast:31 row_mask:0xc bank_mask:0xf"]
+
+
+def batch_check(slow, back):
+    """the pending block's scalar test: c = generations x universes clean and
+    not yet found (nibble k, bit u); any -> the slow path"""
+    return ["s_nor_b32 %[c], %[rl], %[fm]",            # SCC = c != 0
+            f"s_cbranch_scc1 {slow}f",
+            f"{back}:"]
+
+
+def batch_slowpath(lbl, back):
+    """record the first clean generation of every fresh universe: nibble k of
+    c is generation gc - 7 + k (gc already counts the pending block)"""
+    lines = [f"{lbl}:", f"s_sub_u32 %[gk], %[gc], {KB - 1}"]
+    for k in range(KB):
+        lines += [f"s_bfe_u32 %[t], %[c], 0x{(4 << 16) | (4 * k):x}",
+                  "s_andn2_b32 %[t], %[t], %[fu]",
+                  "s_or_b32 %[fu], %[fu], %[t]"]
+        for u in range(P):
+            lines += [f"s_bitcmp1_b32 %[t], {u}",
+                      f"s_cselect_b32 %[h{u}], %[gk], %[h{u}]"]
+        lines.append("s_add_u32 %[gk], %[gk], 1")
+    return lines + ["s_mul_i32 %[fm], %[fu], 0x11111111", f"s_branch {back}b"]
+
+
+def batch_block(h):
+    """eight generations; the first carries the previous block's lane OR and
+    scalar test between its h-layer's VALU"""
+    acc = _acc()
+    out = []
+    for k in range(KB):
+        b = body(DEFAULT)
+        if k:
+            b.remove("s_sub_u32 %[g], %[g], 1")
+        else:   # the pending chain, two VALU apart (DPP reads a fresh VGPR after 2 wait states)
+            chain = batch_chain() + [f"v_readlane_b32 %[rl], v{acc}, 63"]
+            valu = [i for i, l in enumerate(b) if l.startswith("v_")]
+            pos = {valu[2 * i]: c for i, c in enumerate(chain[:6])}
+            pos[valu[13]] = chain[6]
+            nb = []
+            for i, l in enumerate(b):
+                if i in pos:
+                    nb.append(pos[i])
+                nb.append(l)
+                if i == valu[15]:
+                    nb += batch_check(8, 9)
+            b = nb
+        ex = b.index(exchange(1)[0])
+        chk = batch_x(h, k, Alloc())
+        if k == KB - 1:
+            chk.append(f"s_add_u32 %[gc], %[gc], {KB}")
+        out += b[:ex] + chk + b[ex:]
+    return out
+
+
+def batch_text(h):
+    acc = _acc()
+    assert 1 <= h <= (LOW_H if _LAYOUT["low"] else BATCH_MAX_H)
+    lean = [l.replace("%[g]", "%[rem]") for l in contains_body(True, h)]
+    flush = []
+    for c in batch_chain():
+        flush += [c, "s_nop 1"]
+    flush += [f"v_readlane_b32 %[rl], v{acc}, 63"] + batch_check(10, 11)
+    return (["s_cmp_eq_u32 %[g], 0", "s_cbranch_scc1 2f"] + prologue(DEFAULT) +
+            [f"s_and_b32 %[rem], %[g], {KB - 1}", "s_lshr_b32 %[g], %[g], 3",
+             "s_cmp_eq_u32 %[rem], 0", "s_cbranch_scc1 5f", "1:"] + lean +
+            ["s_cmp_lg_u32 %[rem], 0", "s_cbranch_scc1 1b",
+             "5:", "s_cmp_eq_u32 %[g], 0", "s_cbranch_scc1 7f",
+             f"v_mov_b32 v{acc}, -1",                   # no pending block
+             "s_brev_b32 %[fu], %[found]", "s_lshr_b32 %[fu], %[fu], 28",  # bit 3 - u -> bit u
+             "s_mul_i32 %[fm], %[fu], 0x11111111", "6:"] + batch_block(h) +
+            ["s_cmp_lg_u32 %[g], 0", "s_cbranch_scc1 6b"] + flush +
+            ["7:", "s_waitcnt lgkmcnt(0)", "s_branch 2f"] + contains_slowpath() +
+            batch_slowpath(8, 9) + batch_slowpath(10, 11) + ["2:"])
+
+
+def emit_batch(h):
+    low = _LAYOUT["low"]
+    wr, mr = _wm()
+    asm = "\n".join(f'      "{l}\\n"' for l in batch_text(h))
+    outs = ",\n".join([f'        "+{{v{R[j]}}}"(r[{j}])' for j in range(S)] +
+                      [f'        [h{u}] "+s"(hit[{u}])' for u in range(P)])
+    ins = ", ".join([f'"{{v{wr[j]}}}"(w[{j}])' for j in range(h)] +
+                    [f'"{{v{mr[j]}}}"(m[{j}])' for j in range(h)] +
+                    [f'[m{u}] "s"(0x11111111u << {u})' for u in range(P)])
+    used = set(wr[:h] + mr[:h])
+    extra = [ACC_LO] if low else W_REGS + M_REGS
+    pinned = sorted({x for x in L + RR + H1 + H0 + [H0U, H0D, H1U, H1D] + TEMPS + extra} - used)
+    clob = ", ".join(f'"v{x}"' for x in pinned)
+    name = "split_contains_asm_batch_lo" if low else f"split_contains_asm_batch_h{h}"
+    return f"""
+// The lean test batched over eight generations (rows 0..{h - 1}): per block one
+// lane OR (DPP) and one scalar test of a word holding a nibble per generation{
+    ""  if not low else ";" + chr(10) + "// the low register layout (any target of at most 4 rows)"}.
+__device__ __forceinline__ void {name}(uint32_t (&r)[8], const uint32_t (&w)[8],
+                                   const uint32_t (&m)[8], uint32_t gens, uint32_t a_self,
+                                   uint32_t a_prev, uint32_t a_next, uint32_t (&hit)[4]) {{
+  uint32_t gc = 0, found = 0, c, rem, fu, fm, rl, t, gk;
+  uint64_t cmp0, cmp1, cmp2, cmp3;
+  asm volatile(
+{asm}
+      : {outs.strip()},
+        [g] "+s"(gens), [gc] "+s"(gc), [found] "+s"(found), [c] "=&s"(c), [rem] "=&s"(rem),
+        [fu] "=&s"(fu), [fm] "=&s"(fm), [rl] "=&s"(rl), [t] "=&s"(t), [gk] "=&s"(gk),
+        [cmp0] "=&s"(cmp0), [cmp1] "=&s"(cmp1), [cmp2] "=&s"(cmp2), [cmp3] "=&s"(cmp3)
+      : "{{v{A_SELF}}}"(a_self), "{{v{A_PREV}}}"(a_prev), "{{v{A_NEXT}}}"(a_next),
+        {ins}
+      : {clob}, "scc", "memory");
+}}
+"""
+
+
+def _dpp(v, l):
+    d = int(re.search(r"v_or_b32_dpp v(\d+)", l)[1])
+    a, b = (int(x) for x in re.findall(r"v(\d+)", l)[1:3])
+    rm = int(re.search(r"row_mask:0x([0-9a-f]+)", l)[1], 16)
+    src, ok = np.zeros(64, np.uint32), np.zeros(64, bool)
+    lane = np.arange(64)
+    if "row_shr" in l:
+        n = int(re.search(r"row_shr:(\d+)", l)[1])
+        ok = lane % 16 >= n
+        src[ok] = v[a][lane[ok] - n]
+    else:
+        n = int(re.search(r"row_bcast:(\d+)", l)[1])
+        ok = lane >= 16 if n == 15 else lane >= 32
+        src[ok] = v[a][(lane[ok] // 16) * 16 - 1] if n == 15 else v[a][31]
+    ok &= (rm >> (lane // 16)) & 1 == 1
+    out = v[d].copy()
+    out[ok] = src[ok] | v[b][ok]
+    v[d] = out
+
+
+def simulate_batch(r, w, m, gens, h):
+    """numpy run of split_contains_asm_batch_h<h>: returns (r, hits[4])"""
+    v = np.zeros((N_VGPR_C, 64), np.uint32)
+    v[:8] = r
+    wr, mr = _wm()
+    v[wr[:h]] = w[:h]
+    v[mr[:h]] = m[:h]
+    text = batch_text(h)
+    lbl = {l[:-1]: i for i, l in enumerate(text) if re.fullmatch(r"\d+:", l)}
+    sg = {"g": gens, "gc": 0, "found": 0, "hits": [0] * P}
+    sgk = {f"m{u}": 0x11111111 << u for u in range(P)}
+    scc, lds_plane, pc, steps = 0, {}, 0, 0
+
+    def val(x):
+        x = x.strip()
+        if x.startswith("%[h"):
+            return sg["hits"][int(x[3])]
+        if x.startswith("%["):
+            k = x[2:-1]
+            return sgk[k] if k in sgk else sg[k]
+        return int(x, 0) & 0xFFFFFFFF
+
+    def setv(x, y):
+        x = x.strip()
+        if x.startswith("%[h"):
+            sg["hits"][int(x[3])] = y & 0xFFFFFFFF
+        else:
+            sg[x[2:-1]] = y & 0xFFFFFFFF
+
+    def jump(t):
+        n, d = t[:-1], t[-1]
+        cands = [i for i, l in enumerate(text) if l == n + ":"]
+        return min(i for i in cands if i > pc) if d == "f" else max(i for i in cands if i < pc)
+
+    while pc < len(text):
+        l = text[pc]
+        steps += 1
+        assert steps < 10 ** 7
+        npc = pc + 1
+        ops = l.split(None, 1)
+        mn, args = ops[0], (ops[1].split(",") if len(ops) > 1 else [])
+        if re.fullmatch(r"\d+:", l) or mn in ("s_waitcnt", "s_setprio", "s_nop"):
+            pass
+        elif mn == "s_cbranch_scc1":
+            if scc:
+                npc = jump(args[0].strip())
+        elif mn == "s_branch":
+            npc = jump(args[0].strip())
+        elif mn == "s_cmp_eq_u32":
+            scc = int(val(args[0]) == val(args[1]))
+        elif mn == "s_cmp_lg_u32":
+            scc = int(val(args[0]) != val(args[1]))
+        elif mn == "s_cmp_eq_u64":
+            scc = int(sg[args[0].strip()[2:-1]] == 0)
+        elif mn in ("s_add_u32", "s_sub_u32", "s_and_b32", "s_lshr_b32", "s_or_b32", "s_andn2_b32", "s_mul_i32",
+                    "s_addc_u32", "s_nor_b32"):
+            a, b = val(args[1]), val(args[2])
+            y = {"s_add_u32": a + b, "s_sub_u32": a - b, "s_and_b32": a & b, "s_lshr_b32": a >> b,
+                 "s_or_b32": a | b, "s_andn2_b32": a & ~b, "s_mul_i32": a * b, "s_addc_u32": a + b + scc,
+                 "s_nor_b32": ~(a | b)}[mn]
+            if mn in ("s_and_b32", "s_lshr_b32", "s_or_b32", "s_andn2_b32", "s_nor_b32"):
+                scc = int(y & 0xFFFFFFFF != 0)
+            setv(args[0], y)
+        elif mn == "s_mov_b32":
+            setv(args[0], val(args[1]))
+        elif mn == "s_brev_b32":
+            setv(args[0], int(f"{val(args[1]):032b}"[::-1], 2))
+        elif mn == "s_bfe_u32":
+            a, sel = val(args[1]), val(args[2])
+            setv(args[0], (a >> (sel & 31)) & ((1 << (sel >> 16)) - 1))
+        elif mn == "s_bitcmp1_b32":
+            scc = val(args[0]) >> val(args[1]) & 1
+        elif mn == "s_cselect_b32":
+            setv(args[0], val(args[1]) if scc else val(args[2]))
+        elif mn == "v_cmp_ne_u32_e64":
+            sg[args[0].strip()[2:-1]] = int((v[int(args[2].strip()[1:])] != 0).any())
+        elif mn == "v_bitop3_b32" and "%[" in l:
+            d, a, b = (int(x) for x in re.findall(r"v(\d+)", l)[:3])
+            c = np.uint32(val(re.search(r"(%\[\w+\])", l)[1]))
+            tt = int(l.rsplit(":", 1)[1], 16)
+            out = np.zeros(64, np.uint32)
+            for k in range(8):
+                if tt >> k & 1:
+                    out |= (v[a] if k & 4 else ~v[a]) & (v[b] if k & 2 else ~v[b]) & (c if k & 1 else ~c)
+            v[d] = out
+        elif mn == "v_perm_b32":
+            d, s0, s1 = (int(x) for x in re.findall(r"v(\d+)", l)[:3])
+            sel = val(args[3])
+            src = (v[s0].astype(np.uint64) << np.uint64(32)) | v[s1].astype(np.uint64)
+            out = np.zeros(64, np.uint64)
+            for i in range(4):
+                bsel = sel >> (8 * i) & 0xFF
+                assert bsel < 8
+                out |= ((src >> np.uint64(8 * bsel)) & np.uint64(0xFF)) << np.uint64(8 * i)
+            v[d] = out.astype(np.uint32)
+        elif mn == "v_lshl_or_b32":
+            d, a = (int(x) for x in re.findall(r"v(\d+)", l)[:2])
+            c = int(re.findall(r"v(\d+)", l)[2])
+            v[d] = (v[a] << np.uint32(int(args[2]))) | v[c]
+        elif mn == "v_or_b32_dpp":
+            _dpp(v, l)
+        elif mn == "v_readlane_b32":
+            setv(args[0], int(v[int(args[1].strip()[1:])][int(args[2])]))
+        elif mn == "v_mov_b32":
+            v[int(args[0].strip()[1:])] = np.uint32(val(args[1]))
+        else:
+            _exec(v, l, lds_plane)
+        pc = npc
+    return v[:8].copy(), sg["hits"]
 
 
 def _exec(v, l, lds_plane):
@@ -607,13 +943,27 @@ _SIG_CONT = ("(uint32_t (&r)[8], const uint32_t (&w)[8], const uint32_t (&m)[8],
 _SIG_TWO = "(uint32_t (&a)[8], uint32_t (&b)[8], uint32_t gens, uint32_t a_self, uint32_t a_prev, uint32_t a_next)"
 
 
+# what the product include defines: the step loop, the full lean test (any
+# target), the batched test for windows of 5..7 rows and, in the low layout,
+# for windows of at most 4 rows; everything else is the tuning build's
+PRODUCT_BATCH_H = range(LOW_H + 1, BATCH_MAX_H + 1)
+
+
 def _ablation_decls():
     """forward declarations of the tuning build's loops: step_kernels.hpp
     names them in template branches the product never instantiates"""
     names = [(f"split_gens_asm_v{k}", _SIG_LOOP) for k in range(1, len(VARIANTS))]
     names += [("split_gens_asm2", _SIG_TWO), ("split_contains_asm", _SIG_CONT)]
+    names += [(f"split_contains_asm_lean_h{h}", _SIG_CONT) for h in range(1, S)]
     names += [("split_contains_asm_lean_late" + ("" if h == S else f"_h{h}"), _SIG_CONT) for h in range(1, S + 1)]
+    names += [(f"split_contains_asm_batch_h{h}", _SIG_CONT) for h in range(1, LOW_H + 1)]
+    names += [("split_contains_asm_lean_lo", _SIG_CONT)]
     return "".join(f"__device__ __forceinline__ void {n}{sig};\n" for n, sig in names)
+
+
+def _low_batch():
+    with layout(True):
+        return emit_batch(LOW_H)
 
 
 def emit():
@@ -627,19 +977,27 @@ def emit():
 // split_gens_asm_v0(r, gens, a_self, a_prev, a_next): r is gen_split's r[j]
 // for S = 8; a_self / a_prev / a_next are the LDS byte addresses of this
 // lane's / lane i-1's / lane i+1's 16-B slot in the wave's two 1-KiB planes
-// (schedule "{VARIANTS[0]}").  split_contains_asm_lean[_h<h>]: the same loop
-// with the fused Contains test (k_step_contains_split).  The measured
+// (schedule "{VARIANTS[0]}").  The same loop with the fused Contains test
+// (k_step_contains_split): split_contains_asm_batch_lo (a target window of at
+// most 4 rows, the test batched over eight generations, 61 VGPRs pinned),
+// split_contains_asm_batch_h<5..7> (windows of 5..7 rows) and
+// split_contains_asm_lean (any target, per generation).  The measured
 // alternatives (other schedules, two groups per wave, the round-1 contains
-// bookkeeping, a late scalar test) are generated into
-// tools/tune/split_asm_tune.inc for the tuning build; they are only declared
-// here.
+// bookkeeping, the per-generation test on narrower windows, a late scalar
+// test) are generated into tools/tune/split_asm_tune.inc for the tuning
+// build; they are only declared here.
 #pragma once
 
 namespace lifeapi_impl {{
-{fn_text("split_gens_asm_v0", VARIANTS[0])}{emit_contains(lean=True)}{"".join(emit_contains(True, h) for h in range(1, S))}
+{fn_text("split_gens_asm_v0", VARIANTS[0])}{emit_contains(lean=True)}{"".join(emit_batch(h) for h in PRODUCT_BATCH_H)}{_low_batch()}
 {_ablation_decls()}
 }}  // namespace lifeapi_impl
 """
+
+
+def _low_lean():
+    with layout(True):
+        return emit_contains(True, LOW_H)
 
 
 def emit_tune():
@@ -649,12 +1007,14 @@ def emit_tune():
 // lifeapi_amd/csrc/split_asm.inc and the generator): schedules
 // {", ".join(f"v{k} = {v}" for k, v in enumerate(VARIANTS) if k)}; two groups per wave
 // (split_gens_asm2); the round-1 fused-Contains bookkeeping
-// (split_contains_asm); the lean test with its scalar part late
-// (split_contains_asm_lean_late[_h<h>]).
+// (split_contains_asm); the per-generation lean test on windows of 1..7 rows
+// (split_contains_asm_lean_h<h>, and _lo in the low layout), with its scalar
+// part late (split_contains_asm_lean_late[_h<h>]); the batched test on
+// windows of 1..4 rows in the high layout (split_contains_asm_batch_h<h>).
 #pragma once
 
 namespace lifeapi_impl {{
-{fns}{emit2()}{emit_contains()}{"".join(emit_contains(True, h, True) for h in range(1, S + 1))}
+{fns}{emit2()}{emit_contains()}{"".join(emit_contains(True, h) for h in range(1, S))}{"".join(emit_contains(True, h, True) for h in range(1, S + 1))}{"".join(emit_batch(h) for h in range(1, LOW_H + 1))}{_low_lean()}
 }}  // namespace lifeapi_impl
 """
 

@@ -137,3 +137,17 @@ def step_contains(states, wanted, unwanted, generations, variant, final=None, st
                                               wanted.data_ptr(), unwanted.data_ptr(), first.data_ptr(), n,
                                               generations, variant, hip._stream(stream)))
     return first
+
+
+lib.lifeapi_tune_step_contains_pair.argtypes = [_vp, _vp, _vp, _vp, _vp, _sz, _u32, _int, _int, _vp]
+lib.lifeapi_tune_step_contains_pair.restype = _int
+
+
+def step_contains_pair(states, wanted, unwanted, generations, cap_lo, cap_hi, final=None, stream=None):
+    """the shipped fused pair with each grid capped (blocks per CU, 0 = none)"""
+    n = hip._universes(states)
+    first = torch.empty(n, dtype=torch.int32, device=states.device)
+    hip._check(lib.lifeapi_tune_step_contains_pair(
+        states.data_ptr(), None if final is None else final.data_ptr(), wanted.data_ptr(), unwanted.data_ptr(),
+        first.data_ptr(), n, generations, cap_lo, cap_hi, hip._stream(stream)))
+    return first

@@ -461,9 +461,8 @@ __global__ __launch_bounds__(kBlock) void k_step_pair(const uint64_t *in, uint64
 
 extern "C" {
 
-/* fused Step + Contains on the split layout: variant 0 = compiled loop,
- * 1 = assembly loop, 2 = with lean bookkeeping, 3 = lean on the target's
- * row window */
+/* fused Step + Contains on the split layout: variant = step_kernels.hpp's
+ * ASM (0 compiled loop ... 7 / 8 the shipped pair's halves) */
 int lifeapi_tune_step_contains(const uint64_t *d_in, uint64_t *d_final, const uint64_t *d_wanted,
                                const uint64_t *d_unwanted, uint32_t *d_first_gen, size_t n, uint32_t generations,
                                int variant, void *stream) {
@@ -476,12 +475,39 @@ int lifeapi_tune_step_contains(const uint64_t *d_in, uint64_t *d_final, const ui
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
   using Fn = void (*)(const uint64_t *, uint64_t *, const uint64_t *, const uint64_t *, uint32_t *, uint64_t, uint32_t);
-  const Fn fns[5] = {k_step_contains_split<8, kContainsNet, 0>, k_step_contains_split<8, kContainsNet, 1>,
+  const Fn fns[9] = {k_step_contains_split<8, kContainsNet, 0>, k_step_contains_split<8, kContainsNet, 1>,
                      k_step_contains_split<8, kContainsNet, 2>, k_step_contains_split<8, kContainsNet, 3>,
-                     k_step_contains_split<8, kContainsNet, 4>};
-  if (variant < 0 || variant > 4) return fail(LIFEAPI_E_INVALID, "unknown contains variant%s");
+                     k_step_contains_split<8, kContainsNet, 4>, k_step_contains_split<8, kContainsNet, 5>,
+                     k_step_contains_split<8, kContainsNet, 6>, k_step_contains_split<8, kContainsNet, 7>,
+                     k_step_contains_split<8, kContainsNet, 8>};
+  if (variant < 0 || variant > 8) return fail(LIFEAPI_E_INVALID, "unknown contains variant%s");
   hipLaunchKernelGGL(fns[variant], dim3(grid_for((n + 3) / 4, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream, d_in,
                      d_final, d_wanted, d_unwanted, d_first_gen, (uint64_t)n, generations);
+  return launched("k_step_contains_split (tuning) launch");
+}
+
+/* the shipped pair (variants 7 then 8) with each kernel's grid capped at
+ * cap_lo / cap_hi blocks per CU (0 = one block per 4 waves of work)      */
+int lifeapi_tune_step_contains_pair(const uint64_t *d_in, uint64_t *d_final, const uint64_t *d_wanted,
+                                    const uint64_t *d_unwanted, uint32_t *d_first_gen, size_t n,
+                                    uint32_t generations, int cap_lo, int cap_hi, void *stream) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!d_in || !d_wanted || !d_unwanted || !d_first_gen || generations <= 2 || cap_lo < 0 || cap_hi < 0)
+    return fail(LIFEAPI_E_INVALID, "bad argument%s");
+  if (d_final) {
+    int rc = check_batch(d_in, d_final, n);
+    if (rc != LIFEAPI_OK) return rc;
+  }
+  int cus = 0, rc = device_cus(cus);
+  if (rc != LIFEAPI_OK) return rc;
+  hipLaunchKernelGGL((k_step_contains_split<8, kContainsNet, kContainsLo>), dim3(grid_for((n + 3) / 4, cus, cap_lo)),
+                     dim3(kBlock), 0, (hipStream_t)stream, d_in, d_final, d_wanted, d_unwanted, d_first_gen,
+                     (uint64_t)n, generations);
+  rc = launched("k_step_contains_split (tuning) launch");
+  if (rc != LIFEAPI_OK) return rc;
+  hipLaunchKernelGGL((k_step_contains_split<8, kContainsNet, kContainsHi>), dim3(grid_for((n + 3) / 4, cus, cap_hi)),
+                     dim3(kBlock), 0, (hipStream_t)stream, d_in, d_final, d_wanted, d_unwanted, d_first_gen,
+                     (uint64_t)n, generations);
   return launched("k_step_contains_split (tuning) launch");
 }
 
