@@ -405,7 +405,46 @@ def secondary_config3(hip, rt, cpu_seconds=0.0):
                                        "VALU slots per universe-gen; peak 1024 SIMDs x 1 op / 2 clk x 2.4 GHz "
                                        "(DESIGN.md 5.2)"},
             "reference_op_equivalent_Tops": OPS_PER_UNIVERSE_GEN * gps / 1e12,
+            "search_loop": config3_search_loop(hip, rt, a, med),
             "cpu_baseline": cpu}
+
+
+def config3_search_loop(hip, rt, a, step_ms):
+    """Config 3 as callers consume Step (LifeTarget.hpp:44-51): the fused
+    Step + Contains kernel pair on the same input, a 2 x 2 block with its
+    empty ring as the target, final states written; first-hit generations and
+    final states checked against the reference's own Step() + Contains() loop
+    (tests/golden/golden.json digests.config3_contains, ref_shim.cpp)."""
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "golden.json")) as f:
+            gold = json.load(f)["digests"]["config3_contains"]
+    except (OSError, ValueError, KeyError):
+        return None
+    n, gens = a.shape[0], gold["generations"]
+    tw, tu = (torch.from_numpy(np.array([[int(v, 16) for v in gold[k]]], dtype=np.uint64).view(np.int64))
+              .to(a.device) for k in ("wanted", "unwanted"))
+    fin = torch.empty_like(a)
+    first, _ = hip.step_contains(a, tw, tu, gens, final=fin, stream=rt.stream)
+    rt.sync()
+    fd = f"{batch_digest(first.cpu().numpy().astype(np.uint64)):016x}"
+    od = f"{batch_digest(hip.hashes(fin, stream=rt.stream).cpu().numpy()):016x}"
+    hits = int((first > 0).sum().item())
+    for _ in range(20):  # warm, as the plain step before it
+        hip.step_contains(a, tw, tu, gens, final=fin, stream=rt.stream)
+    ms = []
+    for _ in range(20):
+        e0, e1 = rt.event(), rt.event()
+        e0.record(rt.stream)
+        hip.step_contains(a, tw, tu, gens, final=fin, stream=rt.stream)
+        e1.record(rt.stream)
+        e1.synchronize()
+        ms.append(e0.elapsed_time(e1))
+    med = float(np.median(ms))
+    return {"workload": f"config3 search loop: {n} universes x {gens} generations, Step + Contains(LifeTarget) "
+                        "after every generation (one fused launch pair)",
+            "kernel_ms": med, "kernel_ms_all": ms, "over_plain_step": med / step_ms,
+            "hits": hits, "first_digest": fd, "output_digest": od,
+            "verified": fd == gold["first_digest"] and hits == gold["hits"] and od == gold["output_digest"]}
 
 
 def secondary_config4_1gpu(hip, rt, steps=10):

@@ -244,6 +244,15 @@ __device__ __forceinline__ uint32_t wave_sum_u32_dpp(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_readlane(v, 0) + (uint32_t)__builtin_amdgcn_readlane(v, 16) +
          (uint32_t)__builtin_amdgcn_readlane(v, 32) + (uint32_t)__builtin_amdgcn_readlane(v, 48);
 }
+// the OR of v over the wave, the same way (wave-uniform)
+__device__ __forceinline__ uint32_t wave_or_u32_dpp(uint32_t v) {
+  v |= dpp_mov<0xB1>(v);
+  v |= dpp_mov<0x4E>(v);
+  v |= dpp_mov<0x141>(v);
+  v |= dpp_mov<0x140>(v);
+  return (uint32_t)__builtin_amdgcn_readlane(v, 0) | (uint32_t)__builtin_amdgcn_readlane(v, 16) |
+         (uint32_t)__builtin_amdgcn_readlane(v, 32) | (uint32_t)__builtin_amdgcn_readlane(v, 48);
+}
 __device__ __forceinline__ uint64_t wave_sum_u64_dpp(uint64_t v) {
   auto step = [&](auto mov) __attribute__((always_inline)) {
     v += (uint64_t)mov((uint32_t)v) | ((uint64_t)mov((uint32_t)(v >> 32)) << 32);

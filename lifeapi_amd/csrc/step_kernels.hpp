@@ -245,17 +245,26 @@ __device__ __forceinline__ uint64_t rotr64(uint64_t v, uint32_t k) {
   return (v >> k) | (v << ((64 - k) & 63));
 }
 // the smallest cyclic window [y0, y0 + h) of rows holding every set bit of
-// rm (wave-uniform); h = 1 for an empty mask
+// rm (wave-uniform; h = 1 for an empty mask): the complement of the longest
+// cyclic run of empty rows, found by binary lifting (run_k bit p = rows
+// p .. p + k - 1 all empty) in a few dozen scalar instructions
 __device__ __forceinline__ void care_window(uint64_t rm, uint32_t &y0, uint32_t &h) {
   y0 = 0;
   h = 1;
   if (rm == 0) return;
-  h = 65;
-  for (uint32_t y = 0; y < 64; ++y) {
-    if (!((rm >> y) & 1)) continue;
-    const uint32_t hh = 64 - __builtin_clzll(rotr64(rm, y));
-    if (hh < h) h = hh, y0 = y;
+  uint64_t run[6];
+  run[0] = ~rm;  // runs of 1
+#pragma unroll
+  for (int k = 1; k < 6; ++k) run[k] = run[k - 1] & rotr64(run[k - 1], 1u << (k - 1));  // runs of 2^k
+  uint64_t cur = ~0ull;  // starts of runs of length len
+  uint32_t len = 0;
+#pragma unroll
+  for (int k = 5; k >= 0; --k) {
+    const uint64_t t = cur & rotr64(run[k], len);
+    if (t) cur = t, len += 1u << k;
   }
+  h = 64 - len;
+  y0 = len ? ((uint32_t)__builtin_ctzll(cur) + len) & 63 : 0;
 }
 template <int S, int NET, int ASM = 0>
 __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *in, uint64_t *fin,
@@ -270,10 +279,8 @@ __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *
   const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   uint32_t y0 = 0, h = S;  // the row window of ASM 3 (else: no rotation, all registers)
   if constexpr (ASM >= 3) {
-    uint64_t rm = 0;
-    for (int x = 0; x < kWave; ++x) rm |= wanted[x] | unwanted[x];  // uniform: scalar loads
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)rm);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(rm >> 32));
+    const uint64_t col = wanted[lane] | unwanted[lane];  // this lane's column of care cells
+    const uint32_t lo = wave_or_u32_dpp((uint32_t)col), hi = wave_or_u32_dpp((uint32_t)(col >> 32));
     care_window((uint64_t)lo | (uint64_t)hi << 32, y0, h);
     if (h > S) y0 = 0, h = S;
     if ((ASM == 6 || ASM == 7) && h > kLowRows) return;  // the low layout: windows of <= 4 rows only

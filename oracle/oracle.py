@@ -222,6 +222,8 @@ class Ref:
         L.ref_weld_step.argtypes = [_u64p, ctypes.c_uint]
         L.ref_unknown_step_refined.argtypes = [_u64p, _u64p]
         L.ref_refined_step_batch.argtypes = [_u64p, _u64p, ctypes.c_size_t]
+        L.ref_step_contains_batch.argtypes = [_u64p, _u64p, ctypes.c_size_t, ctypes.c_uint, _u64p, _u64p,
+                                              ctypes.POINTER(ctypes.c_uint32), ctypes.c_int]
 
     @staticmethod
     def available() -> bool:
@@ -233,6 +235,17 @@ class Ref:
         out = universes(src.shape[0])
         self.lib.ref_step_batch(_p64(src), _p64(out), src.shape[0], gens, nthreads)
         return out
+
+    def step_contains_batch(self, states, wanted, unwanted, gens: int, nthreads: int = 1):
+        """(first, final): the reference's Step() then Contains(LifeTarget)
+        after every generation (ref_shim.cpp ref_step_contains_batch)"""
+        src = np.ascontiguousarray(states, dtype=np.uint64).reshape(-1, 64)
+        w, u = (np.ascontiguousarray(x, dtype=np.uint64).reshape(64) for x in (wanted, unwanted))
+        out = universes(src.shape[0])
+        first = np.zeros(src.shape[0], dtype=np.uint32)
+        self.lib.ref_step_contains_batch(_p64(src), _p64(out), src.shape[0], gens, _p64(w), _p64(u),
+                                         first.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), nthreads)
+        return first, out
 
     def _each(self, fn, states):
         out = universes(np.asarray(states).reshape(-1, 64).shape[0])

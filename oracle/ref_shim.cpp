@@ -242,4 +242,31 @@ void ref_step_batch(const uint64_t *in, uint64_t *out, size_t n, unsigned gens, 
   for (auto &th : pool) th.join();
 }
 
+// The search-loop idiom on the reference's own types: Step() then
+// Contains(LifeTarget) after every generation (LifeAPI.hpp:1196-1216,
+// LifeTarget.hpp:44-51); first[u] = the first generation (1..gens) whose
+// state contains the target, 0 = none; out (may be NULL) = Stepped(gens).
+void ref_step_contains_batch(const uint64_t *in, uint64_t *out, size_t n, unsigned gens, const uint64_t *wanted,
+                             const uint64_t *unwanted, uint32_t *first, int nthreads) {
+  if (nthreads < 1) nthreads = 1;
+  const LifeTarget target(load(wanted), load(unwanted));
+  auto work = [=, &target](size_t lo, size_t hi) {
+    for (size_t u = lo; u < hi; ++u) {
+      LifeState t = load(in + u * 64);
+      uint32_t f = 0;
+      for (unsigned g = 1; g <= gens; ++g) {
+        t.Step();
+        if (!f && t.Contains(target)) f = g;
+      }
+      first[u] = f;
+      if (out) store(t, out + u * 64);
+    }
+  };
+  if (nthreads == 1) { work(0, n); return; }
+  std::vector<std::thread> pool;
+  for (int k = 0; k < nthreads; ++k)
+    pool.emplace_back(work, n * k / nthreads, n * (k + 1) / nthreads);
+  for (auto &th : pool) th.join();
+}
+
 }  // extern "C"

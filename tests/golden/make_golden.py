@@ -178,6 +178,21 @@ def batch_digests() -> dict:
                      "input_digest": f"{P.digest(P.hashes(xin)):016x}",
                      "output_digest": f"{P.digest(P.hashes(out)):016x}",
                      "output_pop_total": int(P.pop(out).astype(np.uint64).sum())}
+    # config 3 as the search loop (LifeTarget.hpp:44-51): Step() then
+    # Contains() after every generation, a 2 x 2 block with its empty ring
+    # as the target; batch_digest over the first-hit generations
+    xin = P.fill(1 << 16, seed=3)
+    wanted, unwanted = np.zeros(64, np.uint64), np.zeros(64, np.uint64)
+    wanted[10] = wanted[11] = np.uint64(3 << 40)
+    for c in (9, 10, 11, 12):
+        unwanted[c] = np.uint64(15 << 39)
+    unwanted &= ~wanted
+    first, out = R.step_contains_batch(xin, wanted, unwanted, 1024, nthreads=8)
+    dig["config3_contains"] = {
+        "universes": 1 << 16, "seed": 3, "generations": 1024,
+        "wanted": [f"{int(v):016x}" for v in wanted], "unwanted": [f"{int(v):016x}" for v in unwanted],
+        "first_digest": f"{P.digest(first.astype(np.uint64)):016x}", "hits": int((first > 0).sum()),
+        "output_digest": f"{P.digest(P.hashes(out)):016x}"}
     # config 4: 16M universes, 8 shards of 2M; additive digests per shard
     shard, total, totin = [], 0, 0
     for k in range(8):

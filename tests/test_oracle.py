@@ -316,6 +316,30 @@ def test_port_equals_reference_live(port, ref):
         assert (ref.neighbour_count(x[u]) == port.neighbour_count(x[u])).all()
 
 
+def test_reference_search_loop_equals_port(port, ref):
+    """ref_shim.cpp's ref_step_contains_batch (the reference's Step() then
+    Contains(LifeTarget) per generation) against the port's per-generation
+    loop, with planted still-life hits; it is what the config-3 search-loop
+    golden digests come from"""
+    w, u = np.zeros(64, np.uint64), np.zeros(64, np.uint64)
+    w[10] = w[11] = np.uint64(3 << 40)
+    for c in (9, 10, 11, 12):
+        u[c] = np.uint64(15 << 39)
+    u &= ~w
+    x = port.fill(300, seed=707) & port.fill(300, seed=708) & port.fill(300, seed=709)
+    clear = np.zeros(64, np.uint64)
+    clear[2:20] = np.uint64(0x3FFFF << 32)             # an empty 18 x 18 region around the target
+    x[::5] = (x[::5] & ~clear) | w
+    first, fin = ref.step_contains_batch(x, w, u, 13, nthreads=2)
+    exp, s = np.zeros(300, np.uint32), x.copy()
+    for g in range(1, 14):
+        s = port.step_batch(s, 1)
+        hit = np.array([port.contains(s[k], w, u) for k in range(300)])
+        exp[(exp == 0) & hit] = g
+    assert (first == exp).all() and (fin == s).all()
+    assert (exp > 0).sum() >= 60
+
+
 def test_reference_random_state_shape(ref, port):
     rs = np.stack([ref.random_state() for _ in range(64)])
     assert ((rs >> np.uint64(61)) == 1).all()

@@ -109,3 +109,79 @@ def test_batch_beyond_2_32_words(hip, R, port, gens):
         _check(to_host(out[first:first + k]), R.step_batch(x, gens), f"Step^{gens} at universe {first}")
     del d, out
     torch.cuda.empty_cache()
+
+
+def _targets():
+    """a 2 x 2 block + empty ring (4-row window: the low-layout kernel) and a
+    loaf + its 6 x 6 box (6 rows: the other kernel of the shipped pair);
+    both still lifes"""
+    blk_w, blk_u = np.zeros(64, np.uint64), np.zeros(64, np.uint64)
+    blk_w[10] = blk_w[11] = np.uint64(3 << 40)
+    for c in (9, 10, 11, 12):
+        blk_u[c] = np.uint64(15 << 39)
+    loaf_w, loaf_u = np.zeros(64, np.uint64), np.zeros(64, np.uint64)
+    for c, rows in zip(range(21, 25), ((1,), (0, 2), (0, 3), (1, 2))):  # .oo. / o..o / .o.o / ..o.
+        loaf_w[c] = np.uint64(sum(1 << (31 + r) for r in rows))
+    for c in range(20, 26):
+        loaf_u[c] = np.uint64(0x3F << 30)
+    return [(blk_w, blk_u & ~blk_w), (loaf_w, loaf_u & ~loaf_w)]
+
+
+@pytest.mark.parametrize("which", [0, 1])
+@pytest.mark.parametrize("gens", [2, 9, 64])
+def test_step_contains_vs_reference(hip, R, port, which, gens):
+    """the shipped fused Step + Contains pair against the reference's own
+    Step() + Contains(LifeTarget) loop (ref_shim.cpp, LifeTarget.hpp:44-51):
+    first-hit generations and final states, with planted targets"""
+    w, u = _targets()[which]
+    n = 4099
+    x = port.fill(n, seed=31 + which) & port.fill(n, seed=41 + which) & port.fill(n, seed=51 + which)
+    clear = np.zeros(64, np.uint64)
+    clear[2:30] = np.uint64(((1 << 28) - 1) << 22)   # an empty region around both targets
+    x[::7] = (x[::7] & ~clear) | w                   # contained from generation 1 (still lifes)
+    fin = torch.empty((n, 64), dtype=torch.int64, device="cuda")
+    first, _ = hip.step_contains(to_dev(x), to_dev(w[None]), to_dev(u[None]), gens, final=fin)
+    exp_first, exp_fin = R.step_contains_batch(x, w, u, gens, nthreads=THREADS)
+    assert (first.cpu().numpy().astype(np.uint32) == exp_first).all()
+    assert (exp_first > 0).sum() >= n // 14
+    _check(to_host(fin), exp_fin, f"final states after the fused kernel, gens={gens}")
+
+
+def test_config3_search_loop_vs_reference_digest(hip):
+    """config 3 as the search loop, full size (64K x 1024): the digests the
+    reference's own loop produced (tests/golden/make_golden.py)"""
+    import json
+    from lifeapi_amd.digest import batch_digest
+    with open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")) as f:
+        gold = json.load(f)["digests"]["config3_contains"]
+    w, u = (np.array([int(v, 16) for v in gold[k]], dtype=np.uint64) for k in ("wanted", "unwanted"))
+    d = hip.fill_random(gold["universes"], seed=gold["seed"])
+    fin = torch.empty_like(d)
+    first, _ = hip.step_contains(d, to_dev(w[None]), to_dev(u[None]), gold["generations"], final=fin)
+    assert int((first > 0).sum().item()) == gold["hits"]
+    assert f"{batch_digest(first.cpu().numpy().astype(np.uint64)):016x}" == gold["first_digest"]
+    assert f"{batch_digest(hip.hashes(fin).cpu().numpy()):016x}" == gold["output_digest"]
+
+
+def test_step_contains_random_windows_vs_reference(hip, R, port):
+    """the shipped pair on 48 targets with random row windows (1..12 rows,
+    also 20 and 64, anywhere including across the row seam) and columns:
+    each target is universe 0's box after 3 generations, so universe 0 hits;
+    first-hit generations and final states against the reference's loop"""
+    rng = np.random.default_rng(4242)
+    n, gens = 257, 6
+    x = port.fill(n, seed=91) & port.fill(n, seed=92)
+    for t in range(48):
+        h = int(rng.choice([1, 2, 3, 4, 5, 6, 7, 8, 9, 12, 20, 64]))
+        y0 = int(rng.integers(64))
+        rows = np.uint64(sum(1 << ((y0 + i) % 64) for i in range(h)))
+        cols = sorted({int(c) for c in rng.integers(0, 64, size=int(rng.integers(1, 6)))})
+        box = np.zeros(64, np.uint64)
+        box[cols] = rows
+        ahead = port.step_batch(x[:1], 3)[0]
+        w, u = ahead & box, box & ~ahead
+        first, _ = hip.step_contains(to_dev(x), to_dev(w[None]), to_dev(u[None]), gens)
+        exp, _ = R.step_contains_batch(x, w, u, gens)
+        got = first.cpu().numpy().astype(np.uint32)
+        assert (got == exp).all(), (t, h, y0, cols, np.nonzero(got != exp)[0][:8])
+        assert 1 <= exp[0] <= 3

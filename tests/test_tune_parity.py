@@ -130,9 +130,9 @@ def _target(kind):
     elif kind == "row":
         for c in range(10, 20):
             u[c] = np.uint64(1 << 7)
-    elif kind == "six":
-        for c in range(21, 25):
-            w[c] = np.uint64(0xF << 31)
+    elif kind == "six":   # a loaf (still life) in its 6 x 6 box
+        for c, rows in zip(range(21, 25), ((1,), (0, 2), (0, 3), (1, 2))):
+            w[c] = np.uint64(sum(1 << (31 + r) for r in rows))
         for c in range(20, 26):
             u[c] = np.uint64(0x3F << 30)
         u &= ~w

@@ -5,7 +5,7 @@ kernel, and the tuning build's variants (step_kernels.hpp: 0 compiled loop,
 1 assembly loop, 2 lean SALU bookkeeping, 3 on the target's row window, 4 its
 scalar test late, 5 batched over four generations, 6 / 7 = 3 / 5 in the low
 register layout, 8 = the wider windows; argv: the variants to run, default
-0..7, and "six" for a 6-row target (4 x 4 block + ring) instead), launches
+0..7, and "six" for a 6-row target (a loaf in its 6 x 6 box) instead), launches
 interleaved after a 2 s warm-up.  Results must equal the shipped fused
 kernel's."""
 import json
@@ -27,9 +27,9 @@ x = hip.fill_random(n, seed=3)
 SIX = "six" in sys.argv[1:]
 w = torch.zeros((1, 64), dtype=torch.int64, device="cuda")
 u = torch.zeros((1, 64), dtype=torch.int64, device="cuda")
-if SIX:
-    for c in range(21, 25):
-        w[0, c] = 0xF << 31
+if SIX:                                              # a loaf in its 6 x 6 box
+    for c, rows in zip(range(21, 25), ((1,), (0, 2), (0, 3), (1, 2))):
+        w[0, c] = sum(1 << (31 + r) for r in rows)
     for c in range(20, 26):
         u[0, c] = 0x3F << 30
 else:
@@ -71,4 +71,4 @@ for k in kern:
     print(json.dumps({"kernel": k, "ms_median": statistics.median(ms[k]), "ms_min": min(ms[k]),
                       "over_step": statistics.median(ms[k]) / statistics.median(ms["step"]),
                       "equal_to_shipped": same, "universes_with_hit": hits,
-                      "target": "4x4 block + ring (6 rows)" if SIX else "2x2 block + ring (4 rows)"}), flush=True)
+                      "target": "loaf + 6x6 box (6 rows)" if SIX else "2x2 block + ring (4 rows)"}), flush=True)
