@@ -244,6 +244,16 @@ __device__ __forceinline__ uint32_t wave_sum_u32_dpp(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_readlane(v, 0) + (uint32_t)__builtin_amdgcn_readlane(v, 16) +
          (uint32_t)__builtin_amdgcn_readlane(v, 32) + (uint32_t)__builtin_amdgcn_readlane(v, 48);
 }
+// The lane index, re-derived (v_mbcnt in an opaque asm, so the compiler
+// cannot CSE it with an earlier copy): kernels whose hand-allocated loops
+// pin most of the VGPRs call it after the loop instead of keeping the lane
+// (and addresses built from it) live across it.
+__device__ __forceinline__ uint32_t lane_id_fresh() {
+  uint32_t l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n v_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+
 // the OR of v over the wave, the same way (wave-uniform)
 __device__ __forceinline__ uint32_t wave_or_u32_dpp(uint32_t v) {
   v |= dpp_mov<0xB1>(v);

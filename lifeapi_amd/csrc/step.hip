@@ -96,17 +96,21 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
   if (rc != LIFEAPI_OK) return rc;
   if (generations > 2) {  // the layout of the shipped step for gens > 2
     // two kernels, one per register layout (a target window of <= 4 rows in
-    // 64 VGPRs, 8 waves per SIMD; wider ones): each wave finds the window and
-    // only the matching kernel works (step_kernels.hpp kContainsLo/Hi)
+    // 62 VGPRs, 8 waves per SIMD; the rest in 70, 7 waves): each wave finds
+    // the window and only the matching kernel works (step_kernels.hpp
+    // kContainsLo / kContainsHi)
+    using Fn = void (*)(const uint64_t *, uint64_t *, const uint64_t *, const uint64_t *, uint32_t *, uint64_t,
+                        uint32_t);
+    const Fn fns[2] = {k_step_contains_split<8, kContainsNet, kContainsLo>,
+                       k_step_contains_split<8, kContainsNet, kContainsHi>};
     const dim3 grid(grid_for((n + 3) / 4, cus, 0));
-    hipLaunchKernelGGL((k_step_contains_split<8, kContainsNet, kContainsLo>), grid, dim3(kBlock), 0,
-                       (hipStream_t)stream, d_in, d_final, d_wanted, d_unwanted, d_first_gen,
-                       (uint64_t)n, generations);
-    rc = launched("k_step_contains_split launch");
-    if (rc != LIFEAPI_OK) return rc;
-    hipLaunchKernelGGL((k_step_contains_split<8, kContainsNet, kContainsHi>), grid, dim3(kBlock), 0,
-                       (hipStream_t)stream, d_in, d_final, d_wanted, d_unwanted, d_first_gen,
-                       (uint64_t)n, generations);
+    for (const Fn fn : fns) {
+      hipLaunchKernelGGL(fn, grid, dim3(kBlock), 0, (hipStream_t)stream, d_in, d_final, d_wanted, d_unwanted,
+                         d_first_gen, (uint64_t)n, generations);
+      rc = launched("k_step_contains_split launch");
+      if (rc != LIFEAPI_OK) return rc;
+    }
+    return LIFEAPI_OK;
   } else {
     hipLaunchKernelGGL(k_step_contains, dim3(grid_for(n, cus, 0)), dim3(kBlock), 0,
                        (hipStream_t)stream, d_in, d_final, d_wanted, d_unwanted, d_first_gen,

@@ -235,9 +235,12 @@ constexpr int kContainsNet = 6;  // tail network of the fused kernel (as k_step'
 //   8  the rest of 5: windows of more than 4 rows (batched up to 7, the
 //      per-generation test on 8 and on targets with no window)
 // 6 and 7 do nothing for a window wider than 4 rows, 8 nothing for the
-// others.  step.hip ships the pair kContainsLo + kContainsHi, launched one
-// after the other: every wave of both finds the same window, so exactly one
-// of them works and the other's waves return at once.
+// others.  step.hip ships kContainsLo then kContainsHi: every wave of both
+// finds the same window, so exactly one of them works and the other's waves
+// return at once.  Each wave-uniform choice of loop runs its own copy of the
+// pass over the universes (`universes` below), so the register allocator
+// sees one assembly loop's pins at a time: 8 takes 70 VGPRs (7 waves per
+// SIMD), where one shared pass took 84 (5), and 7 takes 62 (8 waves).
 constexpr int kContainsLo = 7, kContainsHi = 8;
 constexpr uint32_t kLowRows = 4;  // tools/gen_split_asm.py LOW_H
 
@@ -300,105 +303,107 @@ __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *
 #pragma unroll
   for (int j = 0; j < S; ++j) tm[j] = tw[j] | tu[j];
 
-  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock * P;
-  for (uint64_t u0 = ((uint64_t)blockIdx.x * kWavesPerBlock + wib) * P; u0 < n; u0 += stride) {
-    // the wave's universes u0 .. u0 + avail - 1 from scalar bases: a 64-bit
-    // lane address or a vector copy of n kept across the loop would cost
-    // VGPRs, and the low layout's occupancy hangs on the last four
-    const uint64_t left = n - u0;
-    const uint32_t avail = (left >> 2) ? (uint32_t)P : (uint32_t)left;
-    const uint64_t *src = in + u0 * kWave;
-    uint32_t r[S];
-    W c[P];
-#pragma unroll
-    for (int u = 0; u < P; ++u) c[u] = (uint32_t)u < avail ? split(rotr64(src[u * kWave + lane], y0)) : W{0u, 0u};
-    Split<S>::load(c, r);
-    uint32_t hit[P];
-#pragma unroll
-    for (int u = 0; u < P; ++u) hit[u] = 0;
-    uint32_t found = 0;
-    if constexpr (ASM) {  // split_asm.inc: the default generation loop with the test fused in
-      static_assert(S == 8 && NET == 6 && P == 4, "split_contains_asm is rule 11");
-      const uint32_t base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)(
-          lds + wib * S * kWave);
-      const uint32_t self = base + lane * 16u, prev = base + ((lane + kWave - 1) & (kWave - 1)) * 16u,
-                     next = base + ((lane + 1) & (kWave - 1)) * 16u;
-      if constexpr (ASM == 8) {
-        switch (h) {  // wave-uniform, > kLowRows
-          case 5: split_contains_asm_batch_h5(r, tw, tm, gens, self, prev, next, hit); break;
-          case 6: split_contains_asm_batch_h6(r, tw, tm, gens, self, prev, next, hit); break;
-          case 7: split_contains_asm_batch_h7(r, tw, tm, gens, self, prev, next, hit); break;
-          default: split_contains_asm_lean(r, tw, tm, gens, self, prev, next, hit); break;
-        }
-      } else if constexpr (ASM == 6) {
-        split_contains_asm_lean_lo(r, tw, tm, gens, self, prev, next, hit);
-      } else if constexpr (ASM == 7) {
-        split_contains_asm_batch_lo(r, tw, tm, gens, self, prev, next, hit);
-      } else if constexpr (ASM == 5) {
-        switch (h) {  // wave-uniform
-          case 1: split_contains_asm_batch_h1(r, tw, tm, gens, self, prev, next, hit); break;
-          case 2: split_contains_asm_batch_h2(r, tw, tm, gens, self, prev, next, hit); break;
-          case 3: split_contains_asm_batch_h3(r, tw, tm, gens, self, prev, next, hit); break;
-          case 4: split_contains_asm_batch_h4(r, tw, tm, gens, self, prev, next, hit); break;
-          case 5: split_contains_asm_batch_h5(r, tw, tm, gens, self, prev, next, hit); break;
-          case 6: split_contains_asm_batch_h6(r, tw, tm, gens, self, prev, next, hit); break;
-          case 7: split_contains_asm_batch_h7(r, tw, tm, gens, self, prev, next, hit); break;
-          default: split_contains_asm_lean(r, tw, tm, gens, self, prev, next, hit); break;
-        }
-      } else if constexpr (ASM == 4) {
-        switch (h) {  // wave-uniform
-          case 1: split_contains_asm_lean_late_h1(r, tw, tm, gens, self, prev, next, hit); break;
-          case 2: split_contains_asm_lean_late_h2(r, tw, tm, gens, self, prev, next, hit); break;
-          case 3: split_contains_asm_lean_late_h3(r, tw, tm, gens, self, prev, next, hit); break;
-          case 4: split_contains_asm_lean_late_h4(r, tw, tm, gens, self, prev, next, hit); break;
-          case 5: split_contains_asm_lean_late_h5(r, tw, tm, gens, self, prev, next, hit); break;
-          case 6: split_contains_asm_lean_late_h6(r, tw, tm, gens, self, prev, next, hit); break;
-          case 7: split_contains_asm_lean_late_h7(r, tw, tm, gens, self, prev, next, hit); break;
-          default: split_contains_asm_lean_late(r, tw, tm, gens, self, prev, next, hit); break;
-        }
-      } else if constexpr (ASM == 3) {
-        switch (h) {  // wave-uniform
-          case 1: split_contains_asm_lean_h1(r, tw, tm, gens, self, prev, next, hit); break;
-          case 2: split_contains_asm_lean_h2(r, tw, tm, gens, self, prev, next, hit); break;
-          case 3: split_contains_asm_lean_h3(r, tw, tm, gens, self, prev, next, hit); break;
-          case 4: split_contains_asm_lean_h4(r, tw, tm, gens, self, prev, next, hit); break;
-          case 5: split_contains_asm_lean_h5(r, tw, tm, gens, self, prev, next, hit); break;
-          case 6: split_contains_asm_lean_h6(r, tw, tm, gens, self, prev, next, hit); break;
-          case 7: split_contains_asm_lean_h7(r, tw, tm, gens, self, prev, next, hit); break;
-          default: split_contains_asm_lean(r, tw, tm, gens, self, prev, next, hit); break;
-        }
-      } else if constexpr (ASM == 2)
-        split_contains_asm_lean(r, tw, tm, gens, self, prev, next, hit);
-      else
-        split_contains_asm(r, tw, tm, gens, base + lane * 16u, base + ((lane + kWave - 1) & (kWave - 1)) * 16u,
-                           base + ((lane + 1) & (kWave - 1)) * 16u, hit);
-    } else for (uint32_t g = 1; g <= gens; ++g) {
-      gen_split<S, NET>(r, lds + wib * S * kWave, lane);
-      uint32_t d = 0;
-#pragma unroll
-      for (int j = 0; j < S; ++j) d |= lut3<kDiff>(r[j], tw[j], tu[j]);
-      // straight-line: a ballot per universe, the bookkeeping in scalar registers
-      uint32_t clean = 0;
-#pragma unroll
-      for (int u = 0; u < P; ++u) clean |= (__ballot((d & (every << u)) != 0) == 0 ? 1u : 0u) << u;
-      const uint32_t fresh = clean & ~found;
-#pragma unroll
-      for (int u = 0; u < P; ++u) hit[u] = (fresh >> u) & 1 ? g : hit[u];
-      found |= fresh;
-      if (!fin && found == (1u << P) - 1) break;
-    }
-    if (fin) {
-      Split<S>::store(r, c);
-      uint64_t *dst = fin + u0 * kWave;
+  // one pass over this wave's groups of P universes with `gens_loop(r, hit)`
+  // as the generation loop; every wave-uniform choice of loop (below) gets
+  // its own copy of this pass, so that each assembly loop's pinned registers
+  // are all the register allocator sees around it
+  auto universes = [&](auto &&gens_loop) __attribute__((always_inline)) {
+    const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock * P;
+    for (uint64_t u0 = ((uint64_t)blockIdx.x * kWavesPerBlock + wib) * P; u0 < n; u0 += stride) {
+      // the wave's universes u0 .. u0 + avail - 1 from scalar bases: a 64-bit
+      // lane address or a vector copy of n kept across the loop would cost
+      // VGPRs, and the low layout's occupancy hangs on the last four
+      const uint64_t left = n - u0;
+      const uint32_t avail = (left >> 2) ? (uint32_t)P : (uint32_t)left;
+      const uint64_t *src = in + u0 * kWave;
+      const uint32_t ln = lane_id_fresh();
+      uint32_t r[S];
+      W c[P];
 #pragma unroll
       for (int u = 0; u < P; ++u)
-        if ((uint32_t)u < avail) dst[u * kWave + lane] = rotr64(join(c[u]), (64 - y0) & 63);
-    }
-    if (lane == 0) {
+        c[u] = (uint32_t)u < avail ? split(rotr64(src[u * kWave + ln], y0)) : W{0u, 0u};
+      Split<S>::load(c, r);
+      uint32_t hit[P];
 #pragma unroll
-      for (int u = 0; u < P; ++u)
-        if ((uint32_t)u < avail) first[u0 + u] = hit[u];
+      for (int u = 0; u < P; ++u) hit[u] = 0;
+      gens_loop(r, hit);
+      const uint32_t ln2 = lane_id_fresh();  // not kept live across the loop
+      if (fin) {
+        Split<S>::store(r, c);
+        uint64_t *dst = fin + u0 * kWave;
+#pragma unroll
+        for (int u = 0; u < P; ++u)
+          if ((uint32_t)u < avail) dst[u * kWave + ln2] = rotr64(join(c[u]), (64 - y0) & 63);
+      }
+      if (ln2 == 0) {
+#pragma unroll
+        for (int u = 0; u < P; ++u)
+          if ((uint32_t)u < avail) first[u0 + u] = hit[u];
+      }
     }
+  };
+  if constexpr (ASM) {  // split_asm.inc: the default generation loop with the test fused in
+    static_assert(S == 8 && NET == 6 && P == 4, "split_contains_asm is rule 11");
+    const uint32_t base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)(
+        lds + wib * S * kWave);
+    const uint32_t self = base + lane * 16u, prev = base + ((lane + kWave - 1) & (kWave - 1)) * 16u,
+                   next = base + ((lane + 1) & (kWave - 1)) * 16u;
+#define LIFEAPI_RUN(fn)                                                                          \
+  universes([&](uint32_t(&r)[S], uint32_t(&hit)[P]) __attribute__((always_inline)) {            \
+    fn(r, tw, tm, gens, self, prev, next, hit);                                                  \
+  })
+#define LIFEAPI_BY_H(pre, wide)                                                                  \
+  switch (h) { /* wave-uniform */                                                                \
+    case 1: LIFEAPI_RUN(pre##1); break;                                                          \
+    case 2: LIFEAPI_RUN(pre##2); break;                                                          \
+    case 3: LIFEAPI_RUN(pre##3); break;                                                          \
+    case 4: LIFEAPI_RUN(pre##4); break;                                                          \
+    case 5: LIFEAPI_RUN(pre##5); break;                                                          \
+    case 6: LIFEAPI_RUN(pre##6); break;                                                          \
+    case 7: LIFEAPI_RUN(pre##7); break;                                                          \
+    default: LIFEAPI_RUN(wide); break;                                                           \
+  }
+    if constexpr (ASM == 2) {
+      LIFEAPI_RUN(split_contains_asm_lean);
+    } else if constexpr (ASM == 8) {
+      if (h == 5) LIFEAPI_RUN(split_contains_asm_batch_h5);
+      else if (h == 6) LIFEAPI_RUN(split_contains_asm_batch_h6);
+      else if (h == 7) LIFEAPI_RUN(split_contains_asm_batch_h7);
+      else LIFEAPI_RUN(split_contains_asm_lean);
+    } else if constexpr (ASM == 7) {
+      LIFEAPI_RUN(split_contains_asm_batch_lo);
+    } else if constexpr (ASM == 6) {
+      LIFEAPI_RUN(split_contains_asm_lean_lo);
+    } else if constexpr (ASM == 5) {
+      LIFEAPI_BY_H(split_contains_asm_batch_h, split_contains_asm_lean)
+    } else if constexpr (ASM == 4) {
+      LIFEAPI_BY_H(split_contains_asm_lean_late_h, split_contains_asm_lean_late)
+    } else if constexpr (ASM == 3) {
+      LIFEAPI_BY_H(split_contains_asm_lean_h, split_contains_asm_lean)
+    } else {
+      LIFEAPI_RUN(split_contains_asm);
+    }
+#undef LIFEAPI_BY_H
+#undef LIFEAPI_RUN
+  } else {
+    universes([&](uint32_t(&r)[S], uint32_t(&hit)[P]) __attribute__((always_inline)) {
+      uint32_t found = 0;
+      for (uint32_t g = 1; g <= gens; ++g) {
+        gen_split<S, NET>(r, lds + wib * S * kWave, lane);
+        uint32_t d = 0;
+#pragma unroll
+        for (int j = 0; j < S; ++j) d |= lut3<kDiff>(r[j], tw[j], tu[j]);
+        // straight-line: a ballot per universe, the bookkeeping in scalar registers
+        uint32_t clean = 0;
+#pragma unroll
+        for (int u = 0; u < P; ++u) clean |= (__ballot((d & (every << u)) != 0) == 0 ? 1u : 0u) << u;
+        const uint32_t fresh = clean & ~found;
+#pragma unroll
+        for (int u = 0; u < P; ++u) hit[u] = (fresh >> u) & 1 ? g : hit[u];
+        found |= fresh;
+        if (!fin && found == (1u << P) - 1) break;
+      }
+    });
   }
 }
 

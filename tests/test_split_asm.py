@@ -127,16 +127,17 @@ def test_simulated_windowed_contains(port, h, late):
     assert (got == _to_split(_rot_rows(s, y0))).all()
 
 
-@pytest.mark.parametrize("low", [False, True])
+@pytest.mark.parametrize("lay", ["high", "low"])
 @pytest.mark.parametrize("h", range(1, 8))
-def test_simulated_batched_contains(port, h, low):
+def test_simulated_batched_contains(port, h, lay):
     """split_contains_asm_batch_h<h> / _batch_lo (the test batched over eight
     generations: a nibble per generation, one DPP lane OR and one scalar
-    test per block, gens % 8 leading single generations)
+    test per block, gens % 8 leading single generations; the full and low
+    register layouts)
     against the oracle's step-then-Contains loop, for generation counts with
     every remainder and hits at every position of a block."""
-    if low and h > g.LOW_H:
-        pytest.skip("the low layout takes targets of at most 4 rows")
+    if lay == "low" and h > g.LOW_H:
+        pytest.skip(f"the {lay} layout does not take a {h}-row window")
     rng = np.random.default_rng(700 + h)
     y0 = int(rng.integers(64))
     rows = np.uint64(((((1 << h) - 1) << y0) | (((1 << h) - 1) >> (64 - y0))) & ((1 << 64) - 1))
@@ -156,7 +157,7 @@ def test_simulated_batched_contains(port, h, low):
                   port.fill(1, seed=950 + h)[0]])
     xr, wr, mr = _rot_rows(x, y0), _rot_rows(wanted, y0), _rot_rows(wanted | unwanted, y0)
     W, M = _to_split(np.stack([wr] * 4)), _to_split(np.stack([mr] * 4))
-    with g.layout(low):
+    with g.layout(lay):
         for gens in (0, 1, 2, 3, 7, 8, 9, 15, 16, 21):
             exp, s = [0] * 4, x.copy()
             for k in range(1, gens + 1):
@@ -164,7 +165,7 @@ def test_simulated_batched_contains(port, h, low):
                 for u in range(4):
                     if not exp[u] and (((s[u] ^ wanted) & (wanted | unwanted)) == 0).all():
                         exp[u] = k
-            got, hits = g.simulate_batch(_to_split(xr), W, M, gens, h if not low else g.LOW_H)
+            got, hits = g.simulate_batch(_to_split(xr), W, M, gens, g.LOW_H if lay == "low" else h)
             assert hits == exp, (h, gens, hits, exp)
             assert (got == _to_split(_rot_rows(s, y0))).all()
         assert len({e for e in exp[:3] if e}) >= 2, exp  # hits at two or more distinct generations

@@ -143,15 +143,14 @@ def _target(kind):
 @pytest.mark.parametrize("with_final", [False, True])
 @pytest.mark.parametrize("variant", [3, 4, 5, 6, 7, 8])
 def test_step_contains_row_window(tune, hip, port, kind, with_final, variant):
-    """variants 3..8 (the target's row window, universes rotated into it and
-    back) against the oracle and against the shipped kernel pair, for
+    """variants 3..8 (the target's row window, universes rotated into it
+    and back) against the oracle and against the shipped kernels, for
     targets whose window wraps the row seam, exceeds 8 rows, is one row, is
-    empty, or is six rows (batched in the high layout)."""
+    empty, or is six rows (batched in the full layout)."""
     import torch
-    if variant in (6, 7) and kind in ("tall", "six"):
-        pytest.skip("the low-layout variants take windows of at most 4 rows")
-    if variant == 8 and kind not in ("tall", "six"):
-        pytest.skip("variant 8 takes windows of more than 4 rows")
+    own = {6: ("seam", "row", "empty"), 7: ("seam", "row", "empty"), 8: ("tall", "six")}
+    if variant in own and kind not in own[variant]:
+        pytest.skip(f"variant {variant} does not take this window")
     n, gens = 2001, 9
     w, u = _target(kind)
     x = port.fill(n, seed=501) & port.fill(n, seed=502)
@@ -177,8 +176,9 @@ def test_step_contains_row_window(tune, hip, port, kind, with_final, variant):
 @pytest.mark.parametrize("caps", [(1, 1), (8, 5), (0, 0)])
 @pytest.mark.parametrize("kind", ["seam", "six", "tall"])
 def test_step_contains_pair_capped_grid(tune, hip, port, caps, kind):
-    """the shipped pair (7 then 8) with capped grids: every wave strides over
-    several groups of universes, and the kernel with nothing to do returns"""
+    """the two-kernel form (7 then 8) with capped grids: every wave strides
+    over several groups of universes, and the kernel with nothing to do
+    returns"""
     import torch
     n, gens = 3001, 11
     w, u = _target(kind)

@@ -4,7 +4,8 @@ gens; and 4K x 4096 with hits): the plain shipped step, the shipped fused
 kernel, and the tuning build's variants (step_kernels.hpp: 0 compiled loop,
 1 assembly loop, 2 lean SALU bookkeeping, 3 on the target's row window, 4 its
 scalar test late, 5 batched over four generations, 6 / 7 = 3 / 5 in the low
-register layout, 8 = the wider windows; argv: the variants to run, default
+register layout, 8 = the wider windows (shipped: 7 then 8); argv: the
+variants to run, default
 0..7, and "six" for a 6-row target (a loaf in its 6 x 6 box) instead), launches
 interleaved after a 2 s warm-up.  Results must equal the shipped fused
 kernel's."""
@@ -57,8 +58,10 @@ while time.time() - t0 < 2.0:
         f()
     torch.cuda.synchronize()
 ms = {k: [] for k in kern}
-for _ in range(10):
-    for k, f in kern.items():
+REPS = 30
+for rep in range(REPS):
+    order = list(kern.items())
+    for k, f in order[rep % len(order):] + order[:rep % len(order)]:  # rotate who runs first
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         f()

@@ -316,23 +316,24 @@ def _or_to_two(d, al):
     return lines + [op(z, d[6], d[7], x, OR3)], y, z
 
 
-_LAYOUT = {"low": False}
+_LAYOUT = {"name": "high"}
 
 
 def _wm():
-    return (W_LO, M_LO) if _LAYOUT["low"] else (W_REGS, M_REGS)
+    return {"low": (W_LO, M_LO), "high": (W_REGS, M_REGS)}[_LAYOUT["name"]]
 
 
 class layout:
-    """with layout(low): the generators use the low register layout"""
-    def __init__(self, low):
-        self.low = low
+    """with layout(name): the generators use register layout name ("high",
+    "low"; True / False = "low" / "high")"""
+    def __init__(self, name):
+        self.name = {True: "low", False: "high"}.get(name, name)
 
     def __enter__(self):
-        self.prev, _LAYOUT["low"] = _LAYOUT["low"], self.low
+        self.prev, _LAYOUT["name"] = _LAYOUT["name"], self.name
 
     def __exit__(self, *a):
-        _LAYOUT["low"] = self.prev
+        _LAYOUT["name"] = self.prev
 
 
 def contains_check(lean=False, h=S):
@@ -426,7 +427,7 @@ def contains_text(lean=False, h=S, late=False):
 
 
 def emit_contains(lean=False, h=S, late=False):
-    low = _LAYOUT["low"]
+    low = _LAYOUT["name"] == "low"
     wr, mr = _wm()
     lines = contains_text(lean, h, late)
     asm = "\n".join(f'      "{l}\\n"' for l in lines)
@@ -474,7 +475,7 @@ __device__ __forceinline__ void {name}(uint32_t (&r)[8], const uint32_t (&w)[8],
 
 def simulate_contains(r, w, m, gens, lean=False, h=S, late=False):
     """numpy run of split_contains_asm[_lean[_h<h>]]: returns (r, hits[4])"""
-    v = np.zeros((N_VGPR_C, 64), np.uint32)
+    v = np.zeros((72, 64), np.uint32)
     v[:8] = r
     wr, mr = _wm()
     v[wr] = w[:len(wr)]
@@ -550,7 +551,7 @@ OR2 = 0xFC         # a | b
 
 
 def _acc():
-    return ACC_LO if _LAYOUT["low"] else ACC_HI
+    return {"low": ACC_LO, "high": ACC_HI}[_LAYOUT["name"]]
 
 
 def _or_into(d, dst, al):
@@ -644,7 +645,7 @@ def batch_block(h):
 
 def batch_text(h):
     acc = _acc()
-    assert 1 <= h <= (LOW_H if _LAYOUT["low"] else BATCH_MAX_H)
+    assert 1 <= h <= {"low": LOW_H, "high": BATCH_MAX_H}[_LAYOUT["name"]]
     lean = [l.replace("%[g]", "%[rem]") for l in contains_body(True, h)]
     flush = []
     for c in batch_chain():
@@ -664,23 +665,24 @@ def batch_text(h):
 
 
 def emit_batch(h):
-    low = _LAYOUT["low"]
+    lay = _LAYOUT["name"]
     wr, mr = _wm()
     asm = "\n".join(f'      "{l}\\n"' for l in batch_text(h))
     outs = ",\n".join([f'        "+{{v{R[j]}}}"(r[{j}])' for j in range(S)] +
                       [f'        [h{u}] "+s"(hit[{u}])' for u in range(P)])
-    ins = ", ".join([f'"{{v{wr[j]}}}"(w[{j}])' for j in range(h)] +
-                    [f'"{{v{mr[j]}}}"(m[{j}])' for j in range(h)] +
+    nt = h
+    ins = ", ".join([f'"{{v{wr[j]}}}"(w[{j}])' for j in range(nt)] +
+                    [f'"{{v{mr[j]}}}"(m[{j}])' for j in range(nt)] +
                     [f'[m{u}] "s"(0x11111111u << {u})' for u in range(P)])
-    used = set(wr[:h] + mr[:h])
-    extra = [ACC_LO] if low else W_REGS + M_REGS
+    used = set(wr[:nt] + mr[:nt])
+    extra = {"low": [ACC_LO], "high": W_REGS + M_REGS}[lay]
     pinned = sorted({x for x in L + RR + H1 + H0 + [H0U, H0D, H1U, H1D] + TEMPS + extra} - used)
     clob = ", ".join(f'"v{x}"' for x in pinned)
-    name = "split_contains_asm_batch_lo" if low else f"split_contains_asm_batch_h{h}"
+    name = {"low": "split_contains_asm_batch_lo", "high": f"split_contains_asm_batch_h{h}"}[lay]
+    note = {"low": ";\n// the low register layout (any target of at most 4 rows)", "high": ""}[lay]
     return f"""
 // The lean test batched over eight generations (rows 0..{h - 1}): per block one
-// lane OR (DPP) and one scalar test of a word holding a nibble per generation{
-    ""  if not low else ";" + chr(10) + "// the low register layout (any target of at most 4 rows)"}.
+// lane OR (DPP) and one scalar test of a word holding a nibble per generation{note}.
 __device__ __forceinline__ void {name}(uint32_t (&r)[8], const uint32_t (&w)[8],
                                    const uint32_t (&m)[8], uint32_t gens, uint32_t a_self,
                                    uint32_t a_prev, uint32_t a_next, uint32_t (&hit)[4]) {{
@@ -721,7 +723,7 @@ def _dpp(v, l):
 
 def simulate_batch(r, w, m, gens, h):
     """numpy run of split_contains_asm_batch_h<h>: returns (r, hits[4])"""
-    v = np.zeros((N_VGPR_C, 64), np.uint32)
+    v = np.zeros((72, 64), np.uint32)
     v[:8] = r
     wr, mr = _wm()
     v[wr[:h]] = w[:h]
@@ -962,7 +964,7 @@ def _ablation_decls():
 
 
 def _low_batch():
-    with layout(True):
+    with layout("low"):
         return emit_batch(LOW_H)
 
 
@@ -980,8 +982,8 @@ def emit():
 // (schedule "{VARIANTS[0]}").  The same loop with the fused Contains test
 // (k_step_contains_split): split_contains_asm_batch_lo (a target window of at
 // most 4 rows, the test batched over eight generations, 61 VGPRs pinned),
-// split_contains_asm_batch_h<5..7> (windows of 5..7 rows) and
-// split_contains_asm_lean (any target, per generation).  The measured
+// split_contains_asm_batch_h<5..7> (windows of 5..7 rows, 68 pinned) and
+// split_contains_asm_lean (any target, per generation, 68 pinned).  The measured
 // alternatives (other schedules, two groups per wave, the round-1 contains
 // bookkeeping, the per-generation test on narrower windows, a late scalar
 // test) are generated into tools/tune/split_asm_tune.inc for the tuning
@@ -1009,8 +1011,8 @@ def emit_tune():
 // (split_gens_asm2); the round-1 fused-Contains bookkeeping
 // (split_contains_asm); the per-generation lean test on windows of 1..7 rows
 // (split_contains_asm_lean_h<h>, and _lo in the low layout), with its scalar
-// part late (split_contains_asm_lean_late[_h<h>]); the batched test on
-// windows of 1..4 rows in the high layout (split_contains_asm_batch_h<h>).
+// part late (split_contains_asm_lean_late[_h<h>]); the batched test in the
+// full layout on windows of 1..4 rows (split_contains_asm_batch_h<1..4>).
 #pragma once
 
 namespace lifeapi_impl {{

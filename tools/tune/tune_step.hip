@@ -404,11 +404,6 @@ __global__ __launch_bounds__(kBlock) void k_step_split_clock(const uint64_t *in,
 // assembly loop pins v0..v63, so nothing lane-varying may stay live across
 // it: the lane index is re-derived afterwards (v_mbcnt, opaque to CSE) and
 // every address is rebuilt from it and wave-uniform scalars.
-__device__ __forceinline__ uint32_t lane_id_fresh() {
-  uint32_t l;
-  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n v_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
-  return l;
-}
 template <bool NT, int V>
 __global__ __launch_bounds__(kBlock) void k_step_pair(const uint64_t *in, uint64_t *out, uint64_t n, uint32_t gens) {
   constexpr int S = 8, P = 4;
@@ -486,7 +481,7 @@ int lifeapi_tune_step_contains(const uint64_t *d_in, uint64_t *d_final, const ui
   return launched("k_step_contains_split (tuning) launch");
 }
 
-/* the shipped pair (variants 7 then 8) with each kernel's grid capped at
+/* the two-kernel form (variants 7 then 8) with each kernel's grid capped at
  * cap_lo / cap_hi blocks per CU (0 = one block per 4 waves of work)      */
 int lifeapi_tune_step_contains_pair(const uint64_t *d_in, uint64_t *d_final, const uint64_t *d_wanted,
                                     const uint64_t *d_unwanted, uint32_t *d_first_gen, size_t n,
@@ -500,12 +495,12 @@ int lifeapi_tune_step_contains_pair(const uint64_t *d_in, uint64_t *d_final, con
   }
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
-  hipLaunchKernelGGL((k_step_contains_split<8, kContainsNet, kContainsLo>), dim3(grid_for((n + 3) / 4, cus, cap_lo)),
+  hipLaunchKernelGGL((k_step_contains_split<8, kContainsNet, 7>), dim3(grid_for((n + 3) / 4, cus, cap_lo)),
                      dim3(kBlock), 0, (hipStream_t)stream, d_in, d_final, d_wanted, d_unwanted, d_first_gen,
                      (uint64_t)n, generations);
   rc = launched("k_step_contains_split (tuning) launch");
   if (rc != LIFEAPI_OK) return rc;
-  hipLaunchKernelGGL((k_step_contains_split<8, kContainsNet, kContainsHi>), dim3(grid_for((n + 3) / 4, cus, cap_hi)),
+  hipLaunchKernelGGL((k_step_contains_split<8, kContainsNet, 8>), dim3(grid_for((n + 3) / 4, cus, cap_hi)),
                      dim3(kBlock), 0, (hipStream_t)stream, d_in, d_final, d_wanted, d_unwanted, d_first_gen,
                      (uint64_t)n, generations);
   return launched("k_step_contains_split (tuning) launch");
