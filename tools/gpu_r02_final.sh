@@ -9,7 +9,7 @@
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R"
-O="$R/gpurun_out/r02f"
+O="$R/gpurun_out/${OUT_TAG:-r02final}"
 mkdir -p "$O"
 timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread --maxfail=20 \
   -p no:cacheprovider > "$O/pytest_gpu.log" 2>&1
