@@ -37,12 +37,13 @@ int fail_hip(hipError_t e, const char *what) {
 
 struct DevInfo {
   int cus = 0;
+  size_t lds_per_cu = 0;
   bool ok = false;
 };
 std::mutex g_info_mu;
 std::vector<DevInfo> g_info;
 
-int device_cus(int &cus) {
+static int device_info(DevInfo &out) {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return fail_hip(e, "hipGetDevice");
@@ -56,9 +57,25 @@ int device_cus(int &cus) {
       return fail(LIFEAPI_E_NODEVICE, "device is %s, this library is built for gfx950 only",
                   p.gcnArchName);
     g_info[dev].cus = p.multiProcessorCount;
+    g_info[dev].lds_per_cu = p.maxSharedMemoryPerMultiProcessor;
     g_info[dev].ok = true;
   }
-  cus = g_info[dev].cus;
+  out = g_info[dev];
+  return LIFEAPI_OK;
+}
+
+int device_cus(int &cus) {
+  DevInfo d;
+  const int rc = device_info(d);
+  cus = d.cus;
+  return rc;
+}
+
+int occupancy_lds(int blocks_per_cu, unsigned &bytes) {
+  DevInfo d;
+  const int rc = device_info(d);
+  if (rc != LIFEAPI_OK) return rc;
+  bytes = (unsigned)((d.lds_per_cu / (size_t)blocks_per_cu + 511) & ~(size_t)511);
   return LIFEAPI_OK;
 }
 

@@ -20,6 +20,9 @@ int fail(int code, const char *fmt, const char *arg = nullptr);
 int fail_hip(hipError_t e, const char *what);
 // CUs of the current device, which must be a gfx950
 int device_cus(int &cus);
+// unused dynamic LDS per block that leaves room for at most blocks_per_cu
+// resident blocks on a CU of the current device (an occupancy cap)
+int occupancy_lds(int blocks_per_cu, unsigned &bytes);
 bool aligned8(const void *p);
 // n universes in / out: non-null, 8-byte aligned, equal or disjoint
 int check_batch(const void *in, const void *out, size_t n);

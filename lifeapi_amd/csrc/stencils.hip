@@ -278,7 +278,9 @@ __global__ __launch_bounds__(kBlock, OCC > 0 ? OCC : 1) void k_refined(
 
 extern "C" {
 
-constexpr int kStableBlocksPerCU = 32;  // grid cap of the single LifeStable passes (see below)
+// LifeStable kernels: one wave per LifeStable, at most this many blocks (of
+// kWavesPerBlock waves) resident per CU (see lifeapi_stable_pass_batch_dev)
+constexpr int kStableResidentBlocks = 4;
 
 static int counts_launch(const uint64_t *d_in, uint64_t *d_out, size_t n, int mode, void *stream) {
   if (n == 0) return LIFEAPI_OK;
@@ -308,16 +310,28 @@ int lifeapi_stable_pass_batch_dev(uint64_t *d_planes, uint8_t *d_flags, size_t n
   if (rc != LIFEAPI_OK) return rc;
   using Fn = void (*)(uint64_t *, uint8_t *, uint64_t, uint32_t);
   const Fn fns[6] = {k_stable<0>, k_stable<1>, k_stable<2>, k_stable<3>, k_stable<4>, k_stable<5>};
-  // Grid (same-process A/Bs on realistic partially-unknown LifeStables --
-  // still lifes around an unknown window with fresh options, the state a
-  // search propagates from -- and on soups and random planes;
-  // profiles/r02/stable_grid_ab.jsonl at 64K, stable_grid_ab_1m.jsonl at 1M):
-  // the single passes and StabiliseOptions run on a 32-blocks-per-CU grid
-  // that loops over the batch (4-7 % faster on the still-life inputs at 1M,
-  // even at 64K); Propagate, whose iteration count varies per LifeStable,
-  // keeps one wave per LifeStable (4 % slower capped at 1M).
-  hipLaunchKernelGGL(fns[pass], dim3(grid_for(n, cus, pass == 4 ? 0 : kStableBlocksPerCU)), dim3(kBlock), 0,
-                     (hipStream_t)stream,
+  // Launch shape (same-process A/Bs, tools/stable_grid_ab.py, on still lifes
+  // around an unknown window with fresh options -- the state a search
+  // propagates from --, sparse soups and random planes, 64K and 1M
+  // LifeStables; profiles/r02/stable_occupancy_*.jsonl): one wave per
+  // LifeStable with at most 4 blocks resident per CU, set by unused dynamic
+  // LDS, for every pass but Propagate (below).  Every pass reads and writes its 5 KiB in place; fewer concurrent
+  // streams per CU serve that better (the in-place copy of the same shape,
+  // build/membw inplace: 5.73 TB/s uncapped, 5.87 at 2 blocks per CU).  At
+  // 1M: 5-10 % faster than one wave per LifeStable unlimited or a
+  // 32-blocks-per-CU grid that loops over the batch on soups and random
+  // planes, within 1-4 % of the looping grid on still lifes, where that one
+  // had been best; at 64K the best or within 2 % everywhere.
+  // Propagate (pass 4) loops PropagateStep to its fixpoint, a data-dependent
+  // amount of VALU work per LifeStable: it keeps every wave slot (4 blocks
+  // resident: +1.4 % on still lifes at 1M, and 8 % slower on tools/rows_bench.py's
+  // random planes, whose fixpoints take more steps).
+  unsigned lds = 0;
+  if (pass != 4) {
+    rc = occupancy_lds(kStableResidentBlocks, lds);
+    if (rc != LIFEAPI_OK) return rc;
+  }
+  hipLaunchKernelGGL(fns[pass], dim3(grid_for(n, cus, 0)), dim3(kBlock), lds, (hipStream_t)stream,
                      d_planes, d_flags, (uint64_t)n, max_iters ? max_iters : 1u << 20);
   return launched("k_stable launch");
 }
@@ -330,9 +344,13 @@ int lifeapi_stable_vulnerable_batch_dev(const uint64_t *d_planes, uint64_t *d_ou
   if (b < a + n * 10 * 512 && a < b + n * 512) return fail(LIFEAPI_E_INVALID, "out overlaps planes%s");
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
-  // one wave per LifeStable: capped at 32 blocks per CU it was 12 % slower
-  // on the still-life inputs at 1M (equal at 64K; profiles/r02/stable_grid_ab*.jsonl)
-  hipLaunchKernelGGL(k_stable_vulnerable, dim3(grid_for(n, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream,
+  // as the passes: one wave per LifeStable, at most 4 blocks resident per
+  // CU (0.96-0.97 ms at 1M against 0.97-1.00 unlimited and 1.02-1.04 on a
+  // looping grid; profiles/r02/stable_occupancy_*.jsonl)
+  unsigned lds = 0;
+  rc = occupancy_lds(kStableResidentBlocks, lds);
+  if (rc != LIFEAPI_OK) return rc;
+  hipLaunchKernelGGL(k_stable_vulnerable, dim3(grid_for(n, cus, 0)), dim3(kBlock), lds, (hipStream_t)stream,
                      d_planes, d_out, (uint64_t)n);
   return launched("k_stable_vulnerable launch");
 }

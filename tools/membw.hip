@@ -12,6 +12,12 @@
 //                 between two buffers of <universes> x 512 B (1M: 1 GiB
 //                 footprint, partly served from the 256 MB Infinity Cache;
 //                 16M: 16 GiB, not)
+//   membw inplace <objects> <planes>
+//                 the LifeStable kernels' shape: one wave per object reads
+//                 its <planes> x 512 B (contiguous) and writes them back in
+//                 place (nontemporal, as k_stable), at grid caps 0 (one wave
+//                 per object), 8 and 32 blocks per CU, and uncapped with the
+//                 blocks per CU limited by unused dynamic LDS
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -64,6 +70,61 @@ __global__ __launch_bounds__(256) void k_copy(const T *__restrict__ in, T *__res
     }
   }
   if constexpr ((MODE & 4) != 0) out[wave * 64 + lane] = acc;  // keep the loads live
+}
+
+// read-modify-write in place of P planes of 512 B per object, one wave per
+// object (grid-strided when the grid is capped)
+template <int P>
+__global__ __launch_bounds__(256) void k_inplace(u32x2 *buf, u64 n) {
+  const int lane = threadIdx.x & 63;
+  const u64 stride = (u64)gridDim.x * 4;
+  for (u64 u = (u64)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); u < n; u += stride) {
+    u32x2 *q = buf + u * P * 64 + lane;
+    u32x2 v[P];
+#pragma unroll
+    for (int k = 0; k < P; ++k) v[k] = __builtin_nontemporal_load(q + k * 64);
+#pragma unroll
+    for (int k = 0; k < P; ++k) __builtin_nontemporal_store(v[k] ^ u32x2{1u, 0u}, q + k * 64);
+  }
+}
+
+template <int P>
+int inplace(u64 objects, int cus) {
+  const size_t bytes = objects * P * 512;
+  void *a;
+  CHECK(hipMalloc(&a, bytes));
+  CHECK(hipMemset(a, 0x5a, bytes));
+  // grid caps (bpc), then occupancy caps through unused dynamic LDS: at
+  // most 160 KiB / lds blocks (of 4 waves) per CU
+  const int caps[][2] = {{0, 0}, {8, 0}, {32, 0}, {0, 0}, {0, 20 << 10}, {0, 27 << 10}, {0, 40 << 10},
+                         {0, 54 << 10}, {0, 80 << 10}};
+  for (const auto &cap : caps) {
+    const int bpc = cap[0], lds = cap[1];
+    u64 blocks = (objects + 3) / 4;
+    if (bpc) blocks = std::min<u64>(blocks, (u64)cus * bpc);
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    std::vector<float> ms;
+    for (int rep = 0; rep < 20; ++rep) {
+      CHECK(hipEventRecord(e0, 0));
+      hipLaunchKernelGGL((k_inplace<P>), dim3(blocks), dim3(256), lds, 0, (u32x2 *)a, objects);
+      CHECK(hipEventRecord(e1, 0));
+      CHECK(hipEventSynchronize(e1));
+      float t;
+      CHECK(hipEventElapsedTime(&t, e0, e1));
+      if (rep >= 5) ms.push_back(t);
+    }
+    std::sort(ms.begin(), ms.end());
+    std::printf("{\"variant\": \"inplace dwordx2 nt\", \"planes\": %d, \"objects\": %llu, \"blocks_per_cu\": %d, "
+                "\"dyn_lds\": %d, \"ms_best\": %.4f, \"ms_median\": %.4f, \"GBps_best\": %.1f, \"GBps_median\": %.1f}\n",
+                P, objects, bpc, lds, ms.front(), ms[ms.size() / 2], 2.0 * bytes / (ms.front() * 1e-3) / 1e9,
+                2.0 * bytes / (ms[ms.size() / 2] * 1e-3) / 1e9);
+    CHECK(hipEventDestroy(e0));
+    CHECK(hipEventDestroy(e1));
+  }
+  CHECK(hipFree(a));
+  return 0;
 }
 
 static bool g_calib = false;
@@ -136,6 +197,18 @@ int pingpong(u64 universes) {
 
 int main(int argc, char **argv) {
   if (argc > 2 && std::string(argv[1]) == "pingpong") return pingpong(std::stoull(argv[2]));
+  if (argc > 3 && std::string(argv[1]) == "inplace") {
+    hipDeviceProp_t p;
+    CHECK(hipGetDeviceProperties(&p, 0));
+    const u64 n = std::stoull(argv[2]);
+    switch (std::stoi(argv[3])) {
+      case 1: return inplace<1>(n, p.multiProcessorCount);
+      case 4: return inplace<4>(n, p.multiProcessorCount);
+      case 10: return inplace<10>(n, p.multiProcessorCount);
+      case 11: return inplace<11>(n, p.multiProcessorCount);
+      default: std::fprintf(stderr, "planes: 1, 4, 10 or 11\n"); return 2;
+    }
+  }
   g_calib = argc > 1 && std::string(argv[1]) == "calib";
   const size_t bytes = size_t(1) << 29;  // 2^20 universes x 512 B
   void *a, *b;

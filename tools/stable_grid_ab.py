@@ -6,7 +6,8 @@ families of 64K LifeStables each:
   soup  -- sparse random soups around an unknown window, fresh options,
   random -- random planes (the round-1 A/B's input).
 Every pass (0 sync .. 5 stabilise) and Vulnerable, at grid caps 0 (one wave
-per LifeStable), 16 and 32 blocks per CU, through the tuning build; each
+per LifeStable), 16 and 32 blocks per CU (or argv[2]; -k = one wave per
+LifeStable, at most k blocks resident per CU), through the tuning build; each
 timed launch starts from the same pristine planes.  One JSON line per
 (family, pass, cap): median ms over 7 launches, and whether the result
 equals the cap-0 result."""
@@ -23,10 +24,16 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools", "tune"))
 import lifeapi_amd.hip as hip  # noqa: E402
 import tune_hip  # noqa: E402
-from oracle.oracle import Port  # noqa: E402  (pattern parsing and seeded fills for the inputs only)
 
-P = Port()
+
+def fill(n, seed):
+    """n seeded universes from the product's own fill (lifeapi_fill_random_dev)"""
+    return hip.fill_random(n, seed=seed).cpu().numpy().view(np.uint64)
+
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 16
+# grid caps (blocks per CU; 0 = one wave per LifeStable; -k = that, with at
+# most k blocks resident per CU): argv[2], comma-separated
+CAPS = [int(c) for c in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0, 16, 32]
 DISTINCT = 2048
 
 
@@ -44,8 +51,8 @@ def moved(s, dx, dy):
 
 
 def family(kind, rng):
-    lifes = [P.parse(r) for r in ("2o$2o!", "b2o$o2bo$b2o!", "2o$obo$bo!", "2b2o$bobo$bo$2o!",
-                                   "b2o$o2bo$bobo$2bo!", "bo$obo$bo!")]
+    lifes = list(hip.parse_rle_host(["2o$2o!", "b2o$o2bo$b2o!", "2o$obo$bo!", "2b2o$bobo$bo$2o!",
+                                     "b2o$o2bo$bobo$2bo!", "bo$obo$bo!"])[0])
     out = np.zeros((DISTINCT, 10, 64), np.uint64)
     for u in range(DISTINCT):
         w, h = int(rng.integers(6, 24)), int(rng.integers(6, 24))
@@ -56,10 +63,10 @@ def family(kind, rng):
                 st |= moved(lifes[int(rng.integers(len(lifes)))], int(rng.integers(64)), int(rng.integers(64)))
             out[u, 0], out[u, 1] = st & ~unk, unk
         elif kind == "soup":
-            f = P.fill(2, seed=int(rng.integers(1 << 30)))
+            f = fill(2, seed=int(rng.integers(1 << 30)))
             out[u, 0], out[u, 1] = f[0] & f[1] & ~unk, unk
         else:
-            f, g, k = (P.fill(10, seed=int(rng.integers(1 << 30))) for _ in range(3))
+            f, g, k = (fill(10, seed=int(rng.integers(1 << 30))) for _ in range(3))
             out[u, 0], out[u, 1], out[u, 2:] = f[0], g[1] & unk, f[2:] & g[2:] & k[2:]
     return np.tile(out.reshape(DISTINCT, 640), (N // DISTINCT, 1))
 
@@ -83,7 +90,7 @@ for kind in ("still", "soup", "random"):
     work = torch.empty_like(pristine)
     for which in list(range(6)) + ["vulnerable"]:
         base = None
-        for cap in (0, 16, 32):
+        for cap in CAPS:
             def run(prep, which=which, cap=cap):
                 if prep:
                     work.copy_(pristine)

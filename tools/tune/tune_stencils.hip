@@ -18,8 +18,11 @@ int lifeapi_tune_stable_pass(uint64_t *d_planes, uint8_t *d_flags, size_t n, int
   if (rc != LIFEAPI_OK) return rc;
   using Fn = void (*)(uint64_t *, uint8_t *, uint64_t, uint32_t);
   const Fn fns[6] = {k_stable<0>, k_stable<1>, k_stable<2>, k_stable<3>, k_stable<4>, k_stable<5>};
-  hipLaunchKernelGGL(fns[pass], dim3(grid_for(n, cus, blocks_per_cu)), dim3(kBlock), 0, (hipStream_t)stream,
-                     d_planes, d_flags, (uint64_t)n, max_iters ? max_iters : 1u << 20);
+  // blocks_per_cu < 0: uncapped grid, at most -blocks_per_cu blocks resident
+  // per CU (unused dynamic LDS out of the CU's 160 KiB)
+  const unsigned lds = blocks_per_cu < 0 ? ((160u << 10) / (unsigned)-blocks_per_cu + 511u) & ~511u : 0u;
+  hipLaunchKernelGGL(fns[pass], dim3(grid_for(n, cus, blocks_per_cu > 0 ? blocks_per_cu : 0)), dim3(kBlock), lds,
+                     (hipStream_t)stream, d_planes, d_flags, (uint64_t)n, max_iters ? max_iters : 1u << 20);
   return launched("k_stable (tuning) launch");
 }
 
@@ -30,8 +33,9 @@ int lifeapi_tune_stable_vulnerable(const uint64_t *d_planes, uint64_t *d_out, si
     return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_tune_stable_vulnerable%s");
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
-  hipLaunchKernelGGL(k_stable_vulnerable, dim3(grid_for(n, cus, blocks_per_cu)), dim3(kBlock), 0,
-                     (hipStream_t)stream, d_planes, d_out, (uint64_t)n);
+  const unsigned lds = blocks_per_cu < 0 ? ((160u << 10) / (unsigned)-blocks_per_cu + 511u) & ~511u : 0u;
+  hipLaunchKernelGGL(k_stable_vulnerable, dim3(grid_for(n, cus, blocks_per_cu > 0 ? blocks_per_cu : 0)),
+                     dim3(kBlock), lds, (hipStream_t)stream, d_planes, d_out, (uint64_t)n);
   return launched("k_stable_vulnerable (tuning) launch");
 }
 
