@@ -173,7 +173,8 @@ def copy_ceiling(n: int):
     ping-ponged between two buffers of n universes as this bench does
     (tools/membw.hip `pingpong`, measured on MI355X and committed under
     profiles/): the streaming ceiling for this footprint, context for the
-    roofline.  The nearest measured footprint is used."""
+    roofline.  The nearest measured footprint is used, and the best of the
+    occupancy settings measured there."""
     path = os.path.join(ROOT, "profiles", "r02", "membw_pingpong.jsonl")
     rows = []
     try:
@@ -189,8 +190,10 @@ def copy_ceiling(n: int):
         return None, None
     if not rows:
         return None, None
-    best = min(rows, key=lambda d: abs(np.log2(d["universes"]) - np.log2(max(n, 1))))
-    return best["GBps_median"], f"{os.path.relpath(path, ROOT)} ({best['universes']} universes)"
+    near = min(rows, key=lambda d: abs(np.log2(d["universes"]) - np.log2(max(n, 1))))["universes"]
+    best = max((d for d in rows if d["universes"] == near), key=lambda d: d["GBps_median"])
+    return best["GBps_median"], (f"{os.path.relpath(path, ROOT)} ({near} universes, "
+                                 f"{best.get('resident_blocks', 0) or 'all'} blocks resident per CU)")
 
 
 def load_pmc_traffic(n: int):

@@ -46,17 +46,24 @@ using StepFn = void (*)(const uint64_t *, uint64_t *, uint64_t, uint32_t);
 //   generations, as the hand-allocated loop of split_asm.inc; nontemporal
 //   below 32 generations.  One-shot grids: every capped grid-stride grid
 //   measured slower.
+// The streaming kernel runs with at most 6 blocks (24 waves) resident per CU
+// instead of the 8 its registers allow, set by unused dynamic LDS: fewer
+// concurrent streams per CU, better served by HBM (tools/step_occupancy_ab.py,
+// profiles/r02/step_occupancy.jsonl, same process: +2 % at 1M universes,
+// +2.4 % at 2M, +4.7 % at 4M, +7 % at 16M; 4 and 5 resident blocks nearly
+// as good, 7 and 8 not, 2-3 far worse, and grid-stride caps 7-19 % slower).
 struct StepLaunch {
   StepFn fn;
   uint64_t universes_per_wave;
+  int resident_blocks;  // per CU, 0 = as many as fit
   const char *name;
 };
 StepLaunch shipped_step(uint32_t gens) {
-  if (gens <= 2) return {k_step<XDPP, 4, true, 3>, 4, "k_step<dpp, 4 universes/wave, nt, 7-LUT network>"};
+  if (gens <= 2) return {k_step<XDPP, 4, true, 3>, 4, 6, "k_step<dpp, 4 universes/wave, nt, 7-LUT network>"};
   if (gens < 32)
-    return {k_step_split<8, 1, true, 6, kAsmLoop>, 4,
+    return {k_step_split<8, 1, true, 6, kAsmLoop>, 4, 0,
             "k_step_split<8-way split, 4 universes/wave, nt, 6-LUT tail, assembly loop>"};
-  return {k_step_split<8, 1, false, 6, kAsmLoop>, 4,
+  return {k_step_split<8, 1, false, 6, kAsmLoop>, 4, 0,
           "k_step_split<8-way split, 4 universes/wave, 6-LUT tail, assembly loop>"};
 }
 
@@ -75,7 +82,12 @@ int lifeapi_step_batch_dev(const uint64_t *d_in, uint64_t *d_out, size_t n, uint
   if (rc != LIFEAPI_OK) return rc;
   const StepLaunch l = shipped_step(generations);
   const uint64_t waves = (n + l.universes_per_wave - 1) / l.universes_per_wave;
-  hipLaunchKernelGGL(l.fn, dim3(grid_for(waves, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream, d_in,
+  unsigned lds = 0;
+  if (l.resident_blocks) {
+    rc = occupancy_lds(l.resident_blocks, lds);
+    if (rc != LIFEAPI_OK) return rc;
+  }
+  hipLaunchKernelGGL(l.fn, dim3(grid_for(waves, cus, 0)), dim3(kBlock), lds, (hipStream_t)stream, d_in,
                      d_out, (uint64_t)n, generations);
   return launched("k_step launch");
 }

@@ -11,7 +11,8 @@
 //                 the step kernel's shape as the bench runs it: ping-pong
 //                 between two buffers of <universes> x 512 B (1M: 1 GiB
 //                 footprint, partly served from the 256 MB Infinity Cache;
-//                 16M: 16 GiB, not)
+//                 16M: 16 GiB, not); with as many blocks resident per CU
+//                 as fit and with at most 4, 5, 6 (unused dynamic LDS)
 //   membw inplace <objects> <planes>
 //                 the LifeStable kernels' shape: one wave per object reads
 //                 its <planes> x 512 B (contiguous) and writes them back in
@@ -169,27 +170,36 @@ int pingpong(u64 universes) {
   CHECK(hipMalloc(&b, bytes));
   CHECK(hipMemset(a, 0x5a, bytes));
   CHECK(hipMemset(b, 0x3c, bytes));
+  hipDeviceProp_t p;
+  CHECK(hipGetDeviceProperties(&p, 0));
   const u64 nvec = bytes / sizeof(u32x2), rows = nvec / 64;
   const u64 blocks = (rows / 4 + 3) / 4;
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
-  std::vector<float> ms;
-  for (int rep = 0; rep < 30; ++rep) {
-    void *src = rep & 1 ? b : a, *dst = rep & 1 ? a : b;
-    CHECK(hipEventRecord(e0, 0));
-    hipLaunchKernelGGL((k_copy<u32x2, 4, 3>), dim3(blocks), dim3(256), 0, 0, (const u32x2 *)src, (u32x2 *)dst, nvec);
-    CHECK(hipEventRecord(e1, 0));
-    CHECK(hipEventSynchronize(e1));
-    float t;
-    CHECK(hipEventElapsedTime(&t, e0, e1));
-    if (rep >= 6) ms.push_back(t);
+  // as many blocks resident per CU as fit, then at most 4 / 5 / 6 (unused
+  // dynamic LDS), as the step kernel can be launched
+  for (int resident : {0, 4, 5, 6}) {
+    const unsigned lds = resident ? (unsigned)((p.maxSharedMemoryPerMultiProcessor / resident + 511) & ~511ull) : 0u;
+    std::vector<float> ms;
+    for (int rep = 0; rep < 30; ++rep) {
+      void *src = rep & 1 ? b : a, *dst = rep & 1 ? a : b;
+      CHECK(hipEventRecord(e0, 0));
+      hipLaunchKernelGGL((k_copy<u32x2, 4, 3>), dim3(blocks), dim3(256), lds, 0, (const u32x2 *)src, (u32x2 *)dst,
+                         nvec);
+      CHECK(hipEventRecord(e1, 0));
+      CHECK(hipEventSynchronize(e1));
+      float t;
+      CHECK(hipEventElapsedTime(&t, e0, e1));
+      if (rep >= 6) ms.push_back(t);
+    }
+    std::sort(ms.begin(), ms.end());
+    std::printf("{\"variant\": \"dwordx2 pingpong\", \"U\": 4, \"mode\": 3, \"universes\": %llu, "
+                "\"resident_blocks\": %d, \"ms_best\": %.4f, \"ms_median\": %.4f, \"GBps_best\": %.1f, "
+                "\"GBps_median\": %.1f}\n",
+                universes, resident, ms.front(), ms[ms.size() / 2], 2.0 * bytes / (ms.front() * 1e-3) / 1e9,
+                2.0 * bytes / (ms[ms.size() / 2] * 1e-3) / 1e9);
   }
-  std::sort(ms.begin(), ms.end());
-  std::printf("{\"variant\": \"dwordx2 pingpong\", \"U\": 4, \"mode\": 3, \"universes\": %llu, \"ms_best\": %.4f, "
-              "\"ms_median\": %.4f, \"GBps_best\": %.1f, \"GBps_median\": %.1f}\n",
-              universes, ms.front(), ms[ms.size() / 2], 2.0 * bytes / (ms.front() * 1e-3) / 1e9,
-              2.0 * bytes / (ms[ms.size() / 2] * 1e-3) / 1e9);
   CHECK(hipFree(a));
   CHECK(hipFree(b));
   return 0;

@@ -572,7 +572,14 @@ int lifeapi_tune_step_batch_dev_cfg(const uint64_t *d_in, uint64_t *d_out, size_
   const uint64_t per_wave = (uint64_t)c.universes_per_wave * group_size(c.rule);
   const uint64_t waves = (n + per_wave - 1) / per_wave;
   const unsigned grid = grid_for(waves, cus, c.blocks_per_cu);
-  hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, d_in, d_out,
+  // blocks_per_cu < 0: no grid cap, at most -blocks_per_cu blocks resident
+  // per CU (unused dynamic LDS on top of the kernel's own)
+  unsigned lds = 0;
+  if (c.blocks_per_cu < 0) {
+    rc = occupancy_lds(-c.blocks_per_cu, lds);
+    if (rc != LIFEAPI_OK) return rc;
+  }
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), lds, (hipStream_t)stream, d_in, d_out,
                      (uint64_t)n, generations);
   return launched("k_step (tuning) launch");
 }
