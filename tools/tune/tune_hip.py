@@ -106,6 +106,16 @@ def stable_pass(planes: torch.Tensor, which: int, blocks_per_cu: int, max_iters:
     return flags
 
 
+lib.lifeapi_tune_stencil.argtypes = [_int, _vp, _vp, _sz, _int, _vp]
+lib.lifeapi_tune_stencil.restype = _int
+
+
+def stencil(kind: int, inp: torch.Tensor, out, n: int, resident: int, stream=None):
+    """kind 0..2 k_counts, 3 k_weld (1 gen, in place on inp), 4 k_refined"""
+    hip._check(lib.lifeapi_tune_stencil(kind, inp.data_ptr(), None if out is None else out.data_ptr(), n, resident,
+                                        hip._stream(stream)))
+
+
 def stable_vulnerable(planes: torch.Tensor, blocks_per_cu: int, out=None, stream=None):
     n = planes.numel() // (10 * 64)
     if out is None:

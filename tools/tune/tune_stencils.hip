@@ -1,9 +1,12 @@
 // tune_stencils.hip -- TUNING build: the LifeStable kernels of the product
 // (stable_kernels.hpp) launched on an explicit grid, for the grid-cap A/Bs
-// behind stencils.hip's launch choices (tools/stable_grid_ab.py).
+// behind stencils.hip's launch choices (tools/stable_grid_ab.py); and the
+// other streaming stencils (stencil_kernels.hpp) with an occupancy cap
+// (tools/stencil_occupancy_ab.py).
 #include "lifeapi_tune.h"
 #include "host.hpp"
 #include "stable_kernels.hpp"
+#include "stencil_kernels.hpp"
 
 using namespace lifeapi_impl;
 
@@ -37,6 +40,36 @@ int lifeapi_tune_stable_vulnerable(const uint64_t *d_planes, uint64_t *d_out, si
   hipLaunchKernelGGL(k_stable_vulnerable, dim3(grid_for(n, cus, blocks_per_cu > 0 ? blocks_per_cu : 0)),
                      dim3(kBlock), lds, (hipStream_t)stream, d_planes, d_out, (uint64_t)n);
   return launched("k_stable_vulnerable (tuning) launch");
+}
+
+/* the product's streaming stencils with at most `resident` blocks per CU
+ * (0 = as many as fit): kind 0..2 = k_counts<kind> (NeighbourCount,
+ * InteractionCounts, ...AndNext; in = n universes, out = their planes),
+ * 3 = k_weld one generation (in place on in = n LifeWelds), 4 = k_refined
+ * (in = n x 11 planes, out = n x 3 planes)                                */
+int lifeapi_tune_stencil(int kind, const uint64_t *d_in, uint64_t *d_out, size_t n, int resident, void *stream) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!d_in || kind < 0 || kind > 4 || resident < 0 || (kind != 3 && !d_out))
+    return fail(LIFEAPI_E_INVALID, "bad argument to lifeapi_tune_stencil%s");
+  int cus = 0, rc = device_cus(cus);
+  if (rc != LIFEAPI_OK) return rc;
+  unsigned lds = 0;
+  if (resident) {
+    rc = occupancy_lds(resident, lds);
+    if (rc != LIFEAPI_OK) return rc;
+  }
+  const dim3 grid(grid_for(n, cus, 0));
+  switch (kind) {
+    case 0: hipLaunchKernelGGL(k_counts<0>, grid, dim3(kBlock), lds, (hipStream_t)stream, d_in, d_out, (uint64_t)n); break;
+    case 1: hipLaunchKernelGGL(k_counts<1>, grid, dim3(kBlock), lds, (hipStream_t)stream, d_in, d_out, (uint64_t)n); break;
+    case 2: hipLaunchKernelGGL(k_counts<2>, grid, dim3(kBlock), lds, (hipStream_t)stream, d_in, d_out, (uint64_t)n); break;
+    case 3:
+      hipLaunchKernelGGL(k_weld, grid, dim3(kBlock), lds, (hipStream_t)stream, (uint64_t *)d_in, (uint64_t)n, 1u);
+      break;
+    default:
+      hipLaunchKernelGGL((k_refined<1, 0>), grid, dim3(kBlock), lds, (hipStream_t)stream, d_in, d_out, (uint64_t)n);
+  }
+  return launched("stencil (tuning) launch");
 }
 
 }  // extern "C"
