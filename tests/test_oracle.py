@@ -250,12 +250,12 @@ def test_net6_truth():
 
 
 def test_weld_tail_truth():
-    """The 10-gate LifeWeld tail of k_weld_split (weld_tail, stencils.hip:
+    """The 10-gate LifeWeld tail of k_weld_split (weld_tail, stencil_kernels.hpp:
     gates and tables parsed from the source) behind the h-layer, on all 512
     neighbourhoods x 8 frozen counts, against LifeWeld::Step's adder chain and
     rule (LifeWeld.hpp:169-186: count bits 2..0 + frozen, mod 8)."""
     import re
-    src = open(os.path.join(os.path.dirname(GOLD), "..", "lifeapi_amd", "csrc", "stencils.hip")).read()
+    src = open(os.path.join(os.path.dirname(GOLD), "..", "lifeapi_amd", "csrc", "stencil_kernels.hpp")).read()
     tabs = {"kMaj": 0xE8, "kXor3": 0x96}
     tabs.update({k: int(v, 16) for k, v in re.findall(r"\b(kW\d) = 0x([0-9A-Fa-f]+)", src)})
     body = src[src.index("uint32_t weld_tail("):]
