@@ -185,3 +185,17 @@ def test_step_contains_random_windows_vs_reference(hip, R, port):
         got = first.cpu().numpy().astype(np.uint32)
         assert (got == exp).all(), (t, h, y0, cols, np.nonzero(got != exp)[0][:8])
         assert 1 <= exp[0] <= 3
+
+
+@pytest.mark.parametrize("which", [0, 1])
+def test_step_contains_in_place_vs_reference(hip, R, port, which):
+    """d_final == d_in (the search loop stepping its own batch): each wave
+    reads its universes before it writes them, in both kernels of the pair"""
+    w, u = _targets()[which]
+    n, gens = 2053, 13
+    x = port.fill(n, seed=61 + which) & port.fill(n, seed=71 + which)
+    d = to_dev(x)
+    first, _ = hip.step_contains(d, to_dev(w[None]), to_dev(u[None]), gens, final=d)
+    exp_first, exp_fin = R.step_contains_batch(x, w, u, gens, nthreads=THREADS)
+    assert (first.cpu().numpy().astype(np.uint32) == exp_first).all()
+    _check(to_host(d), exp_fin, "in-place final states")
