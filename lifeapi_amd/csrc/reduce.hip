@@ -3,44 +3,11 @@
 // build-defined hash, and the seeded RandomState()-style fill.
 #include "device.hpp"
 #include "host.hpp"
+#include "reduce_kernels.hpp"
 
 using namespace lifeapi_impl;
 
 namespace {
-
-// The per-universe reductions below take kRedU universes per wave, all loads
-// issued before the first reduction (one wave per universe and a grid-stride
-// loop left them latency-bound at 36-60 % of HBM, tools/rows_bench.py), and
-// sum over the wave by DPP (wave_sum_*_dpp), not through ds_bpermute.
-constexpr int kRedU = 4;
-
-// The states are read once: nontemporal loads, and a grid of at most 32
-// blocks per CU looping over the batch (full grids and plain loads were 6-20 %
-// slower, profiles/r01/red_ab.jsonl).
-constexpr int kRedBlocksPerCU = 32;
-
-__device__ __forceinline__ uint64_t ld_state(const uint64_t *p) { return __builtin_nontemporal_load(p); }
-
-// GetPop (LifeAPI.hpp:290-298): two universes' popcounts per 32-bit reduction
-__global__ __launch_bounds__(kBlock) void k_pop(const uint64_t *__restrict__ s,
-                                                uint32_t *__restrict__ pop, uint64_t n) {
-  const int lane = threadIdx.x & (kWave - 1);
-  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock * kRedU;
-  for (uint64_t u0 = ((uint64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave) * kRedU; u0 < n;
-       u0 += stride) {
-    uint32_t c[kRedU];
-#pragma unroll
-    for (int k = 0; k < kRedU; ++k) c[k] = u0 + k < n ? (uint32_t)__popcll(ld_state(s + (u0 + k) * kWave + lane)) : 0u;
-#pragma unroll
-    for (int k = 0; k < kRedU; k += 2) {
-      const uint32_t t = wave_sum_u32_dpp(c[k] | c[k + 1] << 16);  // each sum <= 4096
-      if (lane == 0) {
-        if (u0 + k < n) pop[u0 + k] = t & 0xFFFF;
-        if (u0 + k + 1 < n) pop[u0 + k + 1] = t >> 16;
-      }
-    }
-  }
-}
 
 // build-defined universe hash: mix(sum_x mix(s[x] + (x+1)*G)).  The
 // per-word mix is heavy (four 64-bit multiplies), so the cross-lane sum must
@@ -80,26 +47,6 @@ __global__ __launch_bounds__(kBlock) void k_hash(const uint64_t *__restrict__ s,
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_contains(const uint64_t *__restrict__ s,
-                                                     const uint64_t *__restrict__ wanted,
-                                                     const uint64_t *__restrict__ unwanted,
-                                                     uint8_t *__restrict__ out, uint64_t n) {
-  const int lane = threadIdx.x & (kWave - 1);
-  const W w = split(wanted[lane]), uw = split(unwanted[lane]);
-  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock * kRedU;
-  for (uint64_t u0 = ((uint64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave) * kRedU; u0 < n;
-       u0 += stride) {
-    W a[kRedU];
-#pragma unroll
-    for (int k = 0; k < kRedU; ++k) a[k] = u0 + k < n ? split(ld_state(s + (u0 + k) * kWave + lane)) : W{0u, 0u};
-#pragma unroll
-    for (int k = 0; k < kRedU; ++k) {
-      const bool c = wave_contains(a[k], w, uw);
-      if (lane == 0 && u0 + k < n) out[u0 + k] = c ? 1 : 0;
-    }
-  }
-}
-
 __global__ __launch_bounds__(kBlock) void k_fill(uint64_t *__restrict__ out, uint64_t nwords,
                                                  uint64_t seed, uint64_t first_word, int mode) {
   const uint64_t stride = (uint64_t)gridDim.x * kBlock;
@@ -120,7 +67,7 @@ int lifeapi_pop_batch_dev(const uint64_t *d_states, uint32_t *d_pop, size_t n, v
     return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_pop_batch_dev%s");
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
-  hipLaunchKernelGGL(k_pop, dim3(grid_for((n + kRedU - 1) / kRedU, cus, kRedBlocksPerCU)), dim3(kBlock), 0,
+  hipLaunchKernelGGL(k_pop<kRedU>, dim3(grid_for((n + kRedU - 1) / kRedU, cus, kRedBlocksPerCU)), dim3(kBlock), 0,
                      (hipStream_t)stream, d_states, d_pop, (uint64_t)n);
   return launched("k_pop launch");
 }
@@ -145,7 +92,10 @@ int lifeapi_contains_batch_dev(const uint64_t *d_states, const uint64_t *d_wante
     return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_contains_batch_dev%s");
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
-  hipLaunchKernelGGL(k_contains, dim3(grid_for((n + kRedU - 1) / kRedU, cus, kRedBlocksPerCU)), dim3(kBlock), 0,
+  // 8 universes per wave, one-shot grid: 0.0867 ms on 1M against 0.0892 for
+  // 4 per wave on the capped grid (tools/reduce_ab.py, profiles/r02/reduce_ab.jsonl;
+  // GetPop keeps 4 on the capped grid, which measured best for it)
+  hipLaunchKernelGGL(k_contains<8>, dim3(grid_for((n + 7) / 8, cus, 0)), dim3(kBlock), 0,
                      (hipStream_t)stream, d_states, d_wanted, d_unwanted, d_out, (uint64_t)n);
   return launched("k_contains launch");
 }

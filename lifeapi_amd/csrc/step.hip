@@ -10,31 +10,6 @@ using namespace lifeapi_impl;
 
 namespace {
 
-// Step + Contains fused: first generation in 1..gens whose state contains the
-// target (0 = never); the state keeps stepping to `gens` for d_final.  `in`
-// and `fin` may be the same array (the host form stages through one buffer),
-// so neither is __restrict__: each wave loads its universes before it stores
-// them, and no wave touches another's universes.
-__global__ __launch_bounds__(kBlock) void k_step_contains(const uint64_t *in, uint64_t *fin,
-                                                          const uint64_t *__restrict__ wanted,
-                                                          const uint64_t *__restrict__ unwanted,
-                                                          uint32_t *__restrict__ first,
-                                                          uint64_t n, uint32_t gens) {
-  const int lane = threadIdx.x & (kWave - 1);
-  const W w = split(wanted[lane]), uw = split(unwanted[lane]);
-  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock;
-  for (uint64_t u = (uint64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave; u < n; u += stride) {
-    W a = split(in[u * kWave + lane]);
-    uint32_t hit = 0;
-    for (uint32_t g = 1; g <= gens; ++g) {
-      a = life_gen<XDPP, 3>(a, nullptr, lane);
-      if (hit == 0 && wave_contains(a, w, uw)) hit = g;
-    }
-    if (fin) fin[u * kWave + lane] = join(a);
-    if (lane == 0) first[u] = hit;
-  }
-}
-
 using StepFn = void (*)(const uint64_t *, uint64_t *, uint64_t, uint32_t);
 
 // The shipped configurations (profiles/r01/tune_*.jsonl):
@@ -124,7 +99,12 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
     }
     return LIFEAPI_OK;
   } else {
-    hipLaunchKernelGGL(k_step_contains, dim3(grid_for(n, cus, 0)), dim3(kBlock), 0,
+    // 8 universes per wave, every block slot (tools/filter_ab.py,
+    // profiles/r02/filter_ab.jsonl, 1M universes x 1 generation, same
+    // process): 0.087 ms = 6.25 TB/s on the 516 B per universe of the bare
+    // filter, 0.181 ms with final states (5.96 TB/s on 1028 B); 4 per wave
+    // 0.107 / 0.179, with fewer blocks resident slower; one per wave 0.229
+    hipLaunchKernelGGL(k_step_contains<8>, dim3(grid_for((n + 7) / 8, cus, 0)), dim3(kBlock), 0,
                        (hipStream_t)stream, d_in, d_final, d_wanted, d_unwanted, d_first_gen,
                        (uint64_t)n, generations);
   }

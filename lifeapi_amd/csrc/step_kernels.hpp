@@ -200,6 +200,51 @@ __global__ __launch_bounds__(kBlock) void k_step_split(const uint64_t *in, uint6
   }
 }
 
+// Step + Contains fused for gens <= 2 (k_step_contains_split takes more):
+// first generation in 1..gens whose state contains the target (0 = never);
+// the state keeps stepping to `gens` for d_final.  The streaming step's
+// shape -- U universes per wave, loads issued first, nontemporal -- so the
+// search filter of SURVEY 8(f) row 1 reads 512 B and writes 4 B per
+// universe.  `in` and `fin` may be the same array (the host form stages
+// through one buffer), so neither is __restrict__: each wave loads its
+// universes before it stores them, and no wave touches another's universes.
+template <int U>
+__global__ __launch_bounds__(kBlock) void k_step_contains(const uint64_t *in, uint64_t *fin,
+                                                          const uint64_t *__restrict__ wanted,
+                                                          const uint64_t *__restrict__ unwanted,
+                                                          uint32_t *__restrict__ first,
+                                                          uint64_t n, uint32_t gens) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const W w = split(wanted[lane]), uw = split(unwanted[lane]);
+  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock * U;
+  for (uint64_t u0 = ((uint64_t)blockIdx.x * kWavesPerBlock + wib) * U; u0 < n; u0 += stride) {
+    W a[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) a[k] = (u0 + k < n) ? ld<true>(in + (u0 + k) * kWave + lane) : W{0u, 0u};
+    uint32_t hit[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) hit[k] = 0;
+    for (uint32_t g = 1; g <= gens; ++g) {
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        a[k] = life_gen<XDPP, 3>(a[k], nullptr, lane);
+        if (hit[k] == 0 && wave_contains(a[k], w, uw)) hit[k] = g;
+      }
+    }
+    if (fin) {
+#pragma unroll
+      for (int k = 0; k < U; ++k)
+        if (u0 + k < n) st<true>(fin + (u0 + k) * kWave + lane, a[k]);
+    }
+    // lanes 0..U-1 write the U first-hit generations with one store
+    uint32_t h = hit[0];
+#pragma unroll
+    for (int k = 1; k < U; ++k) h = lane == k ? hit[k] : h;
+    if (lane < U && u0 + lane < n) first[u0 + lane] = h;
+  }
+}
+
 // The same on the 8-way split layout (k_step_split): 4 universes per wave.
 // The target is put into the same register layout once, replicated for the
 // 4 universes; after every generation (r ^ w) & (w | u) is OR-ed over the

@@ -66,6 +66,9 @@ def main():
     report("k_hash", n, 520, timed(lambda: hip.hashes(x)))
     w = x[:1].clone()
     report("k_contains", n, 513, timed(lambda: hip.contains(x, w, w)))
+    report("k_step_contains 1 gen (first hit only)", n, 516, timed(lambda: hip.step_contains(x, w, w, 1)))
+    report("k_step_contains 1 gen + final states", n, 1028,
+           timed(lambda: hip.step_contains(x, w, w, 1, final=y)))
     report("k_fill", n, 512, timed(lambda: hip.fill_random(n, seed=9)))
     report("k_counts NeighbourCount", n, 512 + 2048, timed(lambda: hip.neighbour_count(x)))
     report("k_counts InteractionCounts", n, 512 + 1536, timed(lambda: hip.interaction_counts(x)))

@@ -106,6 +106,19 @@ def stable_pass(planes: torch.Tensor, which: int, blocks_per_cu: int, max_iters:
     return flags
 
 
+lib.lifeapi_tune_reduce.argtypes = [_int, _vp, _vp, _vp, _vp, _sz, _int, _int, _vp]
+lib.lifeapi_tune_reduce.restype = _int
+
+
+def reduce(kind: int, states, out, upw: int, blocks_per_cu: int, wanted=None, unwanted=None, stream=None):
+    """kind 0 GetPop (out int32), 1 Contains (out uint8)"""
+    n = hip._universes(states)
+    hip._check(lib.lifeapi_tune_reduce(kind, states.data_ptr(), None if wanted is None else wanted.data_ptr(),
+                                       None if unwanted is None else unwanted.data_ptr(), out.data_ptr(), n, upw,
+                                       blocks_per_cu, hip._stream(stream)))
+    return out
+
+
 lib.lifeapi_tune_stencil.argtypes = [_int, _vp, _vp, _sz, _int, _vp]
 lib.lifeapi_tune_stencil.restype = _int
 
@@ -146,6 +159,20 @@ def step_contains(states, wanted, unwanted, generations, variant, final=None, st
     hip._check(lib.lifeapi_tune_step_contains(states.data_ptr(), None if final is None else final.data_ptr(),
                                               wanted.data_ptr(), unwanted.data_ptr(), first.data_ptr(), n,
                                               generations, variant, hip._stream(stream)))
+    return first
+
+
+lib.lifeapi_tune_step_contains_nat.argtypes = [_vp, _vp, _vp, _vp, _vp, _sz, _u32, _int, _int, _vp]
+lib.lifeapi_tune_step_contains_nat.restype = _int
+
+
+def step_contains_nat(states, wanted, unwanted, generations, upw, resident, final=None, stream=None):
+    """the natural-layout fused kernel (gens <= 2), upw universes per wave"""
+    n = hip._universes(states)
+    first = torch.empty(n, dtype=torch.int32, device=states.device)
+    hip._check(lib.lifeapi_tune_step_contains_nat(
+        states.data_ptr(), None if final is None else final.data_ptr(), wanted.data_ptr(), unwanted.data_ptr(),
+        first.data_ptr(), n, generations, upw, resident, hip._stream(stream)))
     return first
 
 

@@ -481,6 +481,29 @@ int lifeapi_tune_step_contains(const uint64_t *d_in, uint64_t *d_final, const ui
   return launched("k_step_contains_split (tuning) launch");
 }
 
+/* the natural-layout fused kernel (gens <= 2) with `upw` universes per wave
+ * and at most `resident` blocks per CU (0 = as many as fit)               */
+int lifeapi_tune_step_contains_nat(const uint64_t *d_in, uint64_t *d_final, const uint64_t *d_wanted,
+                                   const uint64_t *d_unwanted, uint32_t *d_first_gen, size_t n,
+                                   uint32_t generations, int upw, int resident, void *stream) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!d_in || !d_wanted || !d_unwanted || !d_first_gen || resident < 0) return fail(LIFEAPI_E_INVALID, "bad argument%s");
+  int cus = 0, rc = device_cus(cus);
+  if (rc != LIFEAPI_OK) return rc;
+  unsigned lds = 0;
+  if (resident) {
+    rc = occupancy_lds(resident, lds);
+    if (rc != LIFEAPI_OK) return rc;
+  }
+  using Fn = void (*)(const uint64_t *, uint64_t *, const uint64_t *, const uint64_t *, uint32_t *, uint64_t, uint32_t);
+  Fn fn = upw == 1 ? (Fn)k_step_contains<1> : upw == 2 ? (Fn)k_step_contains<2> : upw == 4 ? (Fn)k_step_contains<4>
+        : upw == 8 ? (Fn)k_step_contains<8> : nullptr;
+  if (!fn) return fail(LIFEAPI_E_INVALID, "universes per wave: 1, 2, 4 or 8%s");
+  hipLaunchKernelGGL(fn, dim3(grid_for((n + upw - 1) / upw, cus, 0)), dim3(kBlock), lds, (hipStream_t)stream, d_in,
+                     d_final, d_wanted, d_unwanted, d_first_gen, (uint64_t)n, generations);
+  return launched("k_step_contains (tuning) launch");
+}
+
 /* the two-kernel form (variants 7 then 8) with each kernel's grid capped at
  * cap_lo / cap_hi blocks per CU (0 = one block per 4 waves of work)      */
 int lifeapi_tune_step_contains_pair(const uint64_t *d_in, uint64_t *d_final, const uint64_t *d_wanted,
