@@ -128,7 +128,7 @@ def _targets():
 
 
 @pytest.mark.parametrize("which", [0, 1])
-@pytest.mark.parametrize("gens", [2, 9, 64])
+@pytest.mark.parametrize("gens", [1, 2, 9, 64])
 def test_step_contains_vs_reference(hip, R, port, which, gens):
     """the shipped fused Step + Contains pair against the reference's own
     Step() + Contains(LifeTarget) loop (ref_shim.cpp, LifeTarget.hpp:44-51):
@@ -187,12 +187,14 @@ def test_step_contains_random_windows_vs_reference(hip, R, port):
         assert 1 <= exp[0] <= 3
 
 
+@pytest.mark.parametrize("gens", [1, 2, 13])
 @pytest.mark.parametrize("which", [0, 1])
-def test_step_contains_in_place_vs_reference(hip, R, port, which):
+def test_step_contains_in_place_vs_reference(hip, R, port, which, gens):
     """d_final == d_in (the search loop stepping its own batch): each wave
-    reads its universes before it writes them, in both kernels of the pair"""
+    reads its universes before it writes them, in the one-generation filter
+    kernel (8 universes per wave) and in both kernels of the pair"""
     w, u = _targets()[which]
-    n, gens = 2053, 13
+    n = 2053
     x = port.fill(n, seed=61 + which) & port.fill(n, seed=71 + which)
     d = to_dev(x)
     first, _ = hip.step_contains(d, to_dev(w[None]), to_dev(u[None]), gens, final=d)
