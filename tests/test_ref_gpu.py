@@ -201,3 +201,24 @@ def test_step_contains_in_place_vs_reference(hip, R, port, which, gens):
     exp_first, exp_fin = R.step_contains_batch(x, w, u, gens, nthreads=THREADS)
     assert (first.cpu().numpy().astype(np.uint32) == exp_first).all()
     _check(to_host(d), exp_fin, "in-place final states")
+
+
+def test_eater_pairs_vs_reference(hip, R):
+    """tests/InteractionTest.cpp:7-27's workload: two eaters, the second at
+    every offset in [-10, 10)^2, stepped once -- 400 interacting
+    configurations on the GPU against the reference's own Step(); and
+    InteractionCountsAndNext's 'next' plane equal to that step
+    (LifeAPI.hpp:997-1040)."""
+    eater = R.parse("2b2o$bobo$bo$2o!")   # Parse, not ConstantParse (SURVEY.md 4)
+
+    def moved(s, dx, dy):
+        s = np.roll(s, dx)
+        dy %= 64
+        return (s << np.uint64(dy)) | (s >> np.uint64((64 - dy) % 64)) if dy else s.copy()
+
+    base = moved(eater, 20, 20)
+    x = np.stack([base | moved(base, dx, dy) for dx in range(-10, 10) for dy in range(-10, 10)])
+    want = R.step_batch(x, 1)
+    _check(to_host(hip.step(to_dev(x), generations=1)), want, "eater pairs, Step()")
+    nxt = hip.interaction_counts(to_dev(x), with_next=True)[:, 3].cpu().numpy().view(np.uint64)
+    _check(nxt, want, "eater pairs, InteractionCountsAndNext next")
