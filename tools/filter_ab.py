@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """The one-generation search filter (Step + Contains, natural layout,
 SURVEY 8(f) row 1) through the tuning build: universes per wave x resident
-blocks per CU, with and without final states; launches interleaved, 30 each
+blocks per CU (RES: > 0 resident blocks, < 0 a grid-stride grid of that
+many blocks per CU), with and without final states; launches interleaved, 30 each
 after warm-up; results equal to the shipped entry point's.
 usage: python tools/filter_ab.py [universes]"""
 import json
@@ -27,7 +28,9 @@ for c in (9, 10, 11, 12):
     u[0, c] = 15 << 39
 u &= ~w
 ref, _ = hip.step_contains(x, w, u, 1)
-KEYS = [(upw, res, wf) for upw in (1, 2, 4, 8) for res in (0, 4, 6) for wf in (False, True)]
+RES = [int(c) for c in os.environ.get("RES", "0,4,6").split(",")]  # > 0 resident blocks, < 0 grid-stride cap
+UPWS = [int(c) for c in os.environ.get("UPW", "1,2,4,8").split(",")]
+KEYS = [(upw, res, wf) for upw in UPWS for res in RES for wf in (False, True)]
 for k in KEYS:
     got = tune_hip.step_contains_nat(x, w, u, 1, k[0], k[1], final=fin if k[2] else None)
     assert torch.equal(got, ref), k

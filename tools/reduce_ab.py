@@ -21,7 +21,8 @@ x = hip.fill_random(n, seed=7)
 w = x[:1].clone()
 pop_ref, con_ref = hip.pop(x), hip.contains(x, w, w)
 outs = {0: torch.empty(n, dtype=torch.int32, device="cuda"), 1: torch.empty(n, dtype=torch.uint8, device="cuda")}
-KEYS = [(kind, upw, cap) for kind in (0, 1) for upw in (4, 8) for cap in (32, 0, -4, -6)]
+CAPS = [int(c) for c in os.environ.get("CAPS", "32,0,-4,-6").split(",")]
+KEYS = [(kind, upw, cap) for kind in (0, 1) for upw in (4, 8) for cap in CAPS]
 for k in KEYS:
     tune_hip.reduce(k[0], x, outs[k[0]], k[1], k[2], w, w)
     torch.cuda.synchronize()

@@ -487,11 +487,12 @@ int lifeapi_tune_step_contains_nat(const uint64_t *d_in, uint64_t *d_final, cons
                                    const uint64_t *d_unwanted, uint32_t *d_first_gen, size_t n,
                                    uint32_t generations, int upw, int resident, void *stream) {
   if (n == 0) return LIFEAPI_OK;
-  if (!d_in || !d_wanted || !d_unwanted || !d_first_gen || resident < 0) return fail(LIFEAPI_E_INVALID, "bad argument%s");
+  if (!d_in || !d_wanted || !d_unwanted || !d_first_gen) return fail(LIFEAPI_E_INVALID, "bad argument%s");
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
   unsigned lds = 0;
-  if (resident) {
+  const int cap = resident < 0 ? -resident : 0;  // resident < 0: a grid-stride grid of -resident blocks per CU
+  if (resident > 0) {
     rc = occupancy_lds(resident, lds);
     if (rc != LIFEAPI_OK) return rc;
   }
@@ -499,7 +500,7 @@ int lifeapi_tune_step_contains_nat(const uint64_t *d_in, uint64_t *d_final, cons
   Fn fn = upw == 1 ? (Fn)k_step_contains<1> : upw == 2 ? (Fn)k_step_contains<2> : upw == 4 ? (Fn)k_step_contains<4>
         : upw == 8 ? (Fn)k_step_contains<8> : nullptr;
   if (!fn) return fail(LIFEAPI_E_INVALID, "universes per wave: 1, 2, 4 or 8%s");
-  hipLaunchKernelGGL(fn, dim3(grid_for((n + upw - 1) / upw, cus, 0)), dim3(kBlock), lds, (hipStream_t)stream, d_in,
+  hipLaunchKernelGGL(fn, dim3(grid_for((n + upw - 1) / upw, cus, cap)), dim3(kBlock), lds, (hipStream_t)stream, d_in,
                      d_final, d_wanted, d_unwanted, d_first_gen, (uint64_t)n, generations);
   return launched("k_step_contains (tuning) launch");
 }
