@@ -164,7 +164,8 @@ int lifeapi_contains_batch(const uint64_t *states, const uint64_t *wanted, const
 /* host form of lifeapi_step_contains_batch_dev: the search-loop idiom
  * "for g in 1..gens: s.Step(); if (s.Contains(target)) ..." (LifeAPI.hpp:
  * 1196-1216, LifeTarget.hpp:44-51) over n host universes; final (may be NULL,
- * may equal in) receives Stepped(gens)                                     */
+ * may equal in) receives Stepped(gens); device -1 shards the batch over all
+ * visible GPUs as lifeapi_step_batch does                                  */
 int lifeapi_step_contains_batch(const uint64_t *in, uint64_t *final_states, const uint64_t *wanted,
                                 const uint64_t *unwanted, uint32_t *first_gen, size_t n,
                                 uint32_t generations, int device);

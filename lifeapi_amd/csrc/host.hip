@@ -294,6 +294,48 @@ int host_device(int device) {
   return device;
 }
 
+// device >= 0: fn(0, n, device) on that device.  device -1: one contiguous
+// shard per visible device, fn(lo, hi, dev) on one host thread each, with the
+// given host ranges page-locked once for all shards (shard boundaries share
+// pages).  LIFEAPI_HOST_SHARDS=k (k >= 1) overrides the shard count, shard s
+// running on device s mod ndev: a rehearsal knob that runs the threaded path
+// on a machine with fewer GPUs (tests/test_host_multidev.py).  The first
+// failing shard's code and message are returned.
+template <class F>
+int over_devices(size_t n, int device, const std::pair<const void *, size_t> *ranges, int nranges, F &&fn) {
+  const int ndev = lifeapi_device_count();
+  if (ndev <= 0) return fail(LIFEAPI_E_NODEVICE, "no HIP device visible%s");
+  if (device >= ndev || device < -1) return fail(LIFEAPI_E_NODEVICE, "bad device index%s");
+  int shards = ndev;
+  if (device < 0) {
+    if (const char *e = std::getenv("LIFEAPI_HOST_SHARDS")) {
+      const int k = std::atoi(e);
+      if (k >= 1) shards = k;
+    }
+  }
+  if (device >= 0 || shards == 1) return fn(0, n, device < 0 ? 0 : device);
+  CallPins pins;
+  for (int r = 0; r < nranges; ++r)
+    if (ranges[r].first) pins.add(ranges[r].first, ranges[r].second);
+  std::vector<int> rcs(shards, LIFEAPI_OK);
+  std::vector<std::string> errs(shards);
+  std::vector<std::thread> pool;
+  for (int k = 0; k < shards; ++k) {
+    const size_t lo = n * k / shards, hi = n * (k + 1) / shards;
+    pool.emplace_back([&, k, lo, hi] {
+      if (hi > lo) rcs[k] = fn(lo, hi, k % ndev);
+      errs[k] = g_err;
+    });
+  }
+  for (auto &t : pool) t.join();
+  for (int k = 0; k < shards; ++k)
+    if (rcs[k] != LIFEAPI_OK) {
+      g_err = errs[k];
+      return rcs[k];
+    }
+  return LIFEAPI_OK;
+}
+
 int host_step_one_device(const uint64_t *in, uint64_t *out, size_t n, uint32_t gens, int dev) {
   const HostIO io[1] = {{in, out, 512}};
   return host_chunked(dev, n, io, 1,
@@ -324,43 +366,10 @@ int lifeapi_step_batch(const uint64_t *in, uint64_t *out, size_t n, uint32_t gen
                        int device) {
   int rc = check_batch(in, out, n);
   if (rc != LIFEAPI_OK || n == 0) return rc;
-  const int ndev = lifeapi_device_count();
-  if (ndev <= 0) return fail(LIFEAPI_E_NODEVICE, "no HIP device visible%s");
-  if (device >= ndev || device < -1) return fail(LIFEAPI_E_NODEVICE, "bad device index%s");
-  // device -1: one contiguous shard per visible device, one host thread
-  // each.  LIFEAPI_HOST_SHARDS=k (k >= 1) overrides the shard count, shard s
-  // running on device s mod ndev: a rehearsal knob that runs this threaded
-  // path on a machine with fewer GPUs (tests/test_host_multidev.py).
-  int shards = ndev;
-  if (device < 0) {
-    if (const char *e = std::getenv("LIFEAPI_HOST_SHARDS")) {
-      const int k = std::atoi(e);
-      if (k >= 1) shards = k;
-    }
-  }
-  if (device >= 0 || shards == 1)
-    return host_step_one_device(in, out, n, generations, device < 0 ? 0 : device);
-  // the whole arrays are pinned once here (shard boundaries share pages)
-  CallPins pins;
-  pins.add(in, n * 512);
-  if (out != in) pins.add(out, n * 512);
-  std::vector<int> rcs(shards, LIFEAPI_OK);
-  std::vector<std::string> errs(shards);
-  std::vector<std::thread> pool;
-  for (int k = 0; k < shards; ++k) {
-    const size_t lo = n * k / shards, hi = n * (k + 1) / shards;
-    pool.emplace_back([&, k, lo, hi] {
-      if (hi > lo) rcs[k] = host_step_one_device(in + lo * 64, out + lo * 64, hi - lo, generations, k % ndev);
-      errs[k] = g_err;
-    });
-  }
-  for (auto &t : pool) t.join();
-  for (int k = 0; k < shards; ++k)
-    if (rcs[k] != LIFEAPI_OK) {
-      g_err = errs[k];
-      return rcs[k];
-    }
-  return LIFEAPI_OK;
+  const std::pair<const void *, size_t> ranges[2] = {{in, n * 512}, {out != in ? out : nullptr, n * 512}};
+  return over_devices(n, device, ranges, 2, [&](size_t lo, size_t hi, int dev) {
+    return host_step_one_device(in + lo * 64, out + lo * 64, hi - lo, generations, dev);
+  });
 }
 
 int lifeapi_host_register(void *p, size_t bytes) {
@@ -511,18 +520,9 @@ int lifeapi_contains_batch(const uint64_t *states, const uint64_t *wanted, const
   return rc;
 }
 
-int lifeapi_step_contains_batch(const uint64_t *in, uint64_t *final_states, const uint64_t *wanted,
-                                const uint64_t *unwanted, uint32_t *first_gen, size_t n,
-                                uint32_t generations, int device) {
-  if (n == 0) return LIFEAPI_OK;
-  if (!in || !wanted || !unwanted || !first_gen || !aligned8(in))
-    return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_step_contains_batch%s");
-  if (final_states) {
-    const int rc = check_batch(in, final_states, n);
-    if (rc != LIFEAPI_OK) return rc;
-  }
-  const int dev = host_device(device);
-  if (dev < 0) return dev;
+static int host_step_contains_one_device(const uint64_t *in, uint64_t *final_states, const uint64_t *wanted,
+                                         const uint64_t *unwanted, uint32_t *first_gen, size_t n,
+                                         uint32_t generations, int dev) {
   DeviceGuard guard;
   hipError_t e = hipSetDevice(dev);
   if (e != hipSuccess) return fail_hip(e, "hipSetDevice");
@@ -552,6 +552,24 @@ int lifeapi_step_contains_batch(const uint64_t *in, uint64_t *final_states, cons
   }
   (void)hipFree(dt);
   return rc;
+}
+
+int lifeapi_step_contains_batch(const uint64_t *in, uint64_t *final_states, const uint64_t *wanted,
+                                const uint64_t *unwanted, uint32_t *first_gen, size_t n,
+                                uint32_t generations, int device) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!in || !wanted || !unwanted || !first_gen || !aligned8(in))
+    return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_step_contains_batch%s");
+  if (final_states) {
+    const int rc = check_batch(in, final_states, n);
+    if (rc != LIFEAPI_OK) return rc;
+  }
+  const std::pair<const void *, size_t> ranges[3] = {
+      {in, n * 512}, {final_states != in ? final_states : nullptr, n * 512}, {first_gen, n * 4}};
+  return over_devices(n, device, ranges, 3, [&](size_t lo, size_t hi, int dev) {
+    return host_step_contains_one_device(in + lo * 64, final_states ? final_states + lo * 64 : nullptr, wanted,
+                                         unwanted, first_gen + lo, hi - lo, generations, dev);
+  });
 }
 
 }  // extern "C"

@@ -1,6 +1,6 @@
-"""GPU: the multi-device branch of the host-pointer lifeapi_step_batch
-(device = -1: contiguous shards, one host thread each, the arrays pinned once
-for all shards; host.hip).  A 1-GPU box has one device, so the shard count is
+"""GPU: the multi-device branch of the host-pointer lifeapi_step_batch and
+lifeapi_step_contains_batch (device = -1: contiguous shards, one host thread
+each, the arrays pinned once for all shards; host.hip over_devices).  A 1-GPU box has one device, so the shard count is
 forced with LIFEAPI_HOST_SHARDS (shard s on device s mod ndev): the threads,
 the shard arithmetic and the shared pins all run as they would over 8 GPUs.  Checked against the reference's own Step() (oracle/_ref)
 where built, else the C port."""
@@ -43,6 +43,41 @@ def test_sharded_in_place_large(hip, stepper, shards):
     want = stepper.step_batch(x, 2)
     hip.step_host(x, 2, device=-1, out=x)
     assert (x == want).all()
+
+
+@pytest.mark.parametrize("k", [2, 3])
+@pytest.mark.parametrize("n,gens,keep", [(5, 1, True), (4099, 2, False), (20001, 13, True)])
+def test_sharded_host_search_loop(hip, shards, k, n, gens, keep):
+    """the search loop (Step + Contains every generation) sharded the same
+    way: first-hit generations and final states against the reference's own
+    loop (oracle/_ref ref_step_contains_batch) where built, else the port"""
+    shards(k)
+    from oracle.oracle import Port, Ref
+    P = Port()
+    w, u = np.zeros(64, np.uint64), np.zeros(64, np.uint64)
+    w[10] = w[11] = np.uint64(3 << 40)
+    for c in (9, 10, 11, 12):
+        u[c] = np.uint64(15 << 39)
+    u &= ~w
+    x = P.fill(n, seed=300 + n) & P.fill(n, seed=301 + n) & P.fill(n, seed=302 + n)
+    clear = np.zeros(64, np.uint64)
+    clear[2:20] = np.uint64(0x3FFFF << 32)
+    x[::5] = (x[::5] & ~clear) | w
+    fin = np.empty_like(x) if keep else None
+    first = hip.step_contains_host(x, w, u, gens, final=fin, device=-1)
+    if Ref.available():
+        want_first, want_fin = Ref().step_contains_batch(x, w, u, gens, nthreads=4)
+    else:
+        want_first, s = np.zeros(n, np.uint32), x.copy()
+        for g in range(1, gens + 1):
+            s = P.step_batch(s, 1)
+            hit = np.array([P.contains(s[i], w, u) for i in range(n)])
+            want_first[(want_first == 0) & hit] = g
+        want_fin = s
+    assert (first == want_first).all()
+    assert (want_first > 0).any()
+    if keep:
+        assert (fin == want_fin).all()
 
 
 def test_bad_device_index(hip):
