@@ -149,8 +149,9 @@ int lifeapi_step_batch(const uint64_t *in, uint64_t *out, size_t n, uint32_t gen
                        int device);
 int lifeapi_pop_batch(const uint64_t *states, uint32_t *pop, size_t n, int device);
 /* host-pointer forms of the *_dev entry points above (same layouts); each
- * stages through `device` (-1 = device 0) in chunks of <= 64 MiB per
- * array, two chunks in flight (one per direction of the link)            */
+ * stages through `device` in chunks of <= 64 MiB per array, two chunks in
+ * flight (one per direction of the link); device -1 shards over every
+ * visible device as above                                                 */
 int lifeapi_weld_step_batch(uint64_t *welds, size_t n, uint32_t generations, int device);
 int lifeapi_stable_pass_batch(uint64_t *planes, uint8_t *flags, size_t n, int pass,
                               uint32_t max_iters, int device);

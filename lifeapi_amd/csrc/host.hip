@@ -336,6 +336,24 @@ int over_devices(size_t n, int device, const std::pair<const void *, size_t> *ra
   return LIFEAPI_OK;
 }
 
+// host_chunked over device(s): device >= 0 one device, -1 every visible one
+// (over_devices), each shard's arrays offset by its first universe
+int host_batch(size_t n, int device, const HostIO *io, int nio, ChunkFn fn, const void *arg) {
+  std::pair<const void *, size_t> ranges[8];
+  int nr = 0;
+  for (int i = 0; i < nio && nr < 7; ++i) {
+    if (io[i].src) ranges[nr++] = {io[i].src, n * io[i].bytes};
+    if (io[i].dst && io[i].dst != io[i].src) ranges[nr++] = {io[i].dst, n * io[i].bytes};
+  }
+  return over_devices(n, device, ranges, nr, [&](size_t lo, size_t hi, int dev) {
+    HostIO sh[4];
+    for (int i = 0; i < nio; ++i)
+      sh[i] = {io[i].src ? (const char *)io[i].src + lo * io[i].bytes : nullptr,
+               io[i].dst ? (char *)io[i].dst + lo * io[i].bytes : nullptr, io[i].bytes};
+    return host_chunked(dev, hi - lo, sh, nio, fn, arg);
+  });
+}
+
 int host_step_one_device(const uint64_t *in, uint64_t *out, size_t n, uint32_t gens, int dev) {
   const HostIO io[1] = {{in, out, 512}};
   return host_chunked(dev, n, io, 1,
@@ -389,10 +407,8 @@ int lifeapi_host_unregister(void *p) {
 int lifeapi_pop_batch(const uint64_t *states, uint32_t *pop, size_t n, int device) {
   if (n == 0) return LIFEAPI_OK;
   if (!states || !pop || !aligned8(states)) return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_pop_batch%s");
-  const int dev = host_device(device);
-  if (dev < 0) return dev;
   const HostIO io[2] = {{states, nullptr, 512}, {nullptr, pop, 4}};
-  return host_chunked(dev, n, io, 2,
+  return host_batch(n, device, io, 2,
                       [](void *const *d, size_t m, hipStream_t s, const void *) {
                         return lifeapi_pop_batch_dev((const uint64_t *)d[0], (uint32_t *)d[1], m, s);
                       },
@@ -402,10 +418,8 @@ int lifeapi_pop_batch(const uint64_t *states, uint32_t *pop, size_t n, int devic
 int lifeapi_weld_step_batch(uint64_t *welds, size_t n, uint32_t generations, int device) {
   if (n == 0) return LIFEAPI_OK;
   if (!welds || !aligned8(welds)) return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_weld_step_batch%s");
-  const int dev = host_device(device);
-  if (dev < 0) return dev;
   const HostIO io[1] = {{welds, welds, 4 * 512}};
-  return host_chunked(dev, n, io, 1,
+  return host_batch(n, device, io, 1,
                       [](void *const *d, size_t m, hipStream_t s, const void *arg) {
                         return lifeapi_weld_step_batch_dev((uint64_t *)d[0], m, *(const uint32_t *)arg, s);
                       },
@@ -417,11 +431,9 @@ int lifeapi_stable_pass_batch(uint64_t *planes, uint8_t *flags, size_t n, int pa
   if (n == 0) return LIFEAPI_OK;
   if (!planes || !flags || !aligned8(planes) || pass < 0 || pass > 5)
     return fail(LIFEAPI_E_INVALID, "bad argument to lifeapi_stable_pass_batch%s");
-  const int dev = host_device(device);
-  if (dev < 0) return dev;
   const uint32_t arg[2] = {(uint32_t)pass, max_iters};
   const HostIO io[2] = {{planes, planes, 10 * 512}, {nullptr, flags, 1}};
-  return host_chunked(dev, n, io, 2,
+  return host_batch(n, device, io, 2,
                       [](void *const *d, size_t m, hipStream_t s, const void *a) {
                         const uint32_t *p = (const uint32_t *)a;
                         return lifeapi_stable_pass_batch_dev((uint64_t *)d[0], (uint8_t *)d[1], m,
@@ -434,10 +446,8 @@ int lifeapi_stable_vulnerable_batch(const uint64_t *planes, uint64_t *out, size_
   if (n == 0) return LIFEAPI_OK;
   if (!planes || !out || !aligned8(planes) || !aligned8(out))
     return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_stable_vulnerable_batch%s");
-  const int dev = host_device(device);
-  if (dev < 0) return dev;
   const HostIO io[2] = {{planes, nullptr, 10 * 512}, {nullptr, out, 512}};
-  return host_chunked(dev, n, io, 2,
+  return host_batch(n, device, io, 2,
                       [](void *const *d, size_t m, hipStream_t s, const void *) {
                         return lifeapi_stable_vulnerable_batch_dev((const uint64_t *)d[0], (uint64_t *)d[1],
                                                                    m, s);
@@ -449,10 +459,8 @@ int lifeapi_neighbour_count_batch(const uint64_t *in, uint64_t *out, size_t n, i
   if (n == 0) return LIFEAPI_OK;
   if (!in || !out || !aligned8(in) || !aligned8(out))
     return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_neighbour_count_batch%s");
-  const int dev = host_device(device);
-  if (dev < 0) return dev;
   const HostIO io[2] = {{in, nullptr, 512}, {nullptr, out, 4 * 512}};
-  return host_chunked(dev, n, io, 2,
+  return host_batch(n, device, io, 2,
                       [](void *const *d, size_t m, hipStream_t s, const void *) {
                         return lifeapi_neighbour_count_batch_dev((const uint64_t *)d[0], (uint64_t *)d[1], m, s);
                       },
@@ -464,10 +472,8 @@ int lifeapi_interaction_counts_batch(const uint64_t *in, uint64_t *out, size_t n
   if (n == 0) return LIFEAPI_OK;
   if (!in || !out || !aligned8(in) || !aligned8(out))
     return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_interaction_counts_batch%s");
-  const int dev = host_device(device);
-  if (dev < 0) return dev;
   const HostIO io[2] = {{in, nullptr, 512}, {nullptr, out, (with_next ? 4u : 3u) * 512}};
-  return host_chunked(dev, n, io, 2,
+  return host_batch(n, device, io, 2,
                       [](void *const *d, size_t m, hipStream_t s, const void *a) {
                         return lifeapi_interaction_counts_batch_dev((const uint64_t *)d[0], (uint64_t *)d[1],
                                                                     m, *(const int *)a, s);
@@ -479,23 +485,16 @@ int lifeapi_refined_step_batch(const uint64_t *in, uint64_t *out, size_t n, int 
   if (n == 0) return LIFEAPI_OK;
   if (!in || !out || !aligned8(in) || !aligned8(out))
     return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_refined_step_batch%s");
-  const int dev = host_device(device);
-  if (dev < 0) return dev;
   const HostIO io[2] = {{in, nullptr, 11 * 512}, {nullptr, out, 3 * 512}};
-  return host_chunked(dev, n, io, 2,
+  return host_batch(n, device, io, 2,
                       [](void *const *d, size_t m, hipStream_t s, const void *) {
                         return lifeapi_refined_step_batch_dev((const uint64_t *)d[0], (uint64_t *)d[1], m, s);
                       },
                       nullptr);
 }
 
-int lifeapi_contains_batch(const uint64_t *states, const uint64_t *wanted, const uint64_t *unwanted,
-                           uint8_t *out, size_t n, int device) {
-  if (n == 0) return LIFEAPI_OK;
-  if (!states || !wanted || !unwanted || !out || !aligned8(states))
-    return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_contains_batch%s");
-  const int dev = host_device(device);
-  if (dev < 0) return dev;
+static int host_contains_one_device(const uint64_t *states, const uint64_t *wanted, const uint64_t *unwanted,
+                                    uint8_t *out, size_t n, int dev) {
   // the target rides along as a tiny device copy owned by this call
   DeviceGuard guard;
   hipError_t e = hipSetDevice(dev);
@@ -518,6 +517,17 @@ int lifeapi_contains_batch(const uint64_t *states, const uint64_t *wanted, const
   }
   (void)hipFree(dt);
   return rc;
+}
+
+int lifeapi_contains_batch(const uint64_t *states, const uint64_t *wanted, const uint64_t *unwanted,
+                           uint8_t *out, size_t n, int device) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!states || !wanted || !unwanted || !out || !aligned8(states))
+    return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_contains_batch%s");
+  const std::pair<const void *, size_t> ranges[2] = {{states, n * 512}, {out, n}};
+  return over_devices(n, device, ranges, 2, [&](size_t lo, size_t hi, int dev) {
+    return host_contains_one_device(states + lo * 64, wanted, unwanted, out + lo, hi - lo, dev);
+  });
 }
 
 static int host_step_contains_one_device(const uint64_t *in, uint64_t *final_states, const uint64_t *wanted,

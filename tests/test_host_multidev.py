@@ -80,6 +80,71 @@ def test_sharded_host_search_loop(hip, shards, k, n, gens, keep):
         assert (fin == want_fin).all()
 
 
+@pytest.mark.parametrize("k", [2, 3])
+def test_sharded_host_forms(hip, shards, k):
+    """every other host form (pop, contains, counts, weld, refined, LifeStable
+    pass and Vulnerable) sharded the same way equals its one-device result"""
+    from oracle.oracle import Port
+    P = Port()
+    n = 3001
+    x = P.fill(n, seed=77) & P.fill(n, seed=78)
+    w = x[5].copy()
+    one = {"pop": hip.pop_host(x, device=0)}
+    shards(k)
+    assert (hip.pop_host(x, device=-1) == one["pop"]).all()
+    lib, c = hip.lib, __import__("ctypes")
+
+    def call(name, *args):
+        hip._check(getattr(lib, name)(*args))
+
+    def host_twice(fn):
+        a, b = fn(0), fn(-1)
+        assert all((p == q).all() for p, q in zip(a, b))
+        return a
+
+    def contains(dev):
+        out = np.zeros(n, np.uint8)
+        call("lifeapi_contains_batch", x.ctypes.data, w.ctypes.data, w.ctypes.data, out.ctypes.data, n, dev)
+        return (out,)
+    assert host_twice(contains)[0][5] == 1
+
+    def counts(dev):
+        out = np.zeros((n, 4, 64), np.uint64)
+        call("lifeapi_neighbour_count_batch", x.ctypes.data, out.ctypes.data, n, dev)
+        out3 = np.zeros((n, 3, 64), np.uint64)
+        call("lifeapi_interaction_counts_batch", x.ctypes.data, out3.ctypes.data, n, 0, dev)
+        return out, out3
+    host_twice(counts)
+
+    welds0 = P.fill(n * 4, seed=79).reshape(n, 256)
+
+    def weld(dev):
+        wd = welds0.copy()
+        call("lifeapi_weld_step_batch", wd.ctypes.data, n, 3, dev)
+        return (wd,)
+    host_twice(weld)
+
+    planes11 = P.fill(n * 11, seed=80).reshape(n, 11 * 64)
+
+    def refined(dev):
+        out = np.zeros((n, 3 * 64), np.uint64)
+        call("lifeapi_refined_step_batch", planes11.ctypes.data, out.ctypes.data, n, dev)
+        return (out,)
+    host_twice(refined)
+
+    st0 = P.fill(n * 10, seed=81).reshape(n, 640)
+    st0[:, 128:] &= P.fill(n * 8, seed=82).reshape(n, 512)
+
+    def stable(dev):
+        st = st0.copy()
+        flags = np.zeros(n, np.uint8)
+        call("lifeapi_stable_pass_batch", st.ctypes.data, flags.ctypes.data, n, 3, 0, dev)
+        vul = np.zeros((n, 64), np.uint64)
+        call("lifeapi_stable_vulnerable_batch", st0.ctypes.data, vul.ctypes.data, n, dev)
+        return st, flags, vul
+    host_twice(stable)
+
+
 def test_bad_device_index(hip):
     x = np.zeros((2, 64), np.uint64)
     with pytest.raises(hip.LifeApiError) as e:
