@@ -222,3 +222,30 @@ def test_eater_pairs_vs_reference(hip, R):
     _check(to_host(hip.step(to_dev(x), generations=1)), want, "eater pairs, Step()")
     nxt = hip.interaction_counts(to_dev(x), with_next=True)[:, 3].cpu().numpy().view(np.uint64)
     _check(nxt, want, "eater pairs, InteractionCountsAndNext next")
+
+
+@pytest.mark.parametrize("gens", [1, 5])
+def test_search_loop_beyond_2_32_words(hip, R, port, gens):
+    """the fused search loop on 2^26 + 5 universes (2^32 + 320 words): the
+    filter (1 generation) and the split-layout pair (5) index 64-bit; the
+    universes on both sides of the 2^32-word boundary and the ragged tail
+    against the reference's loop (the fill is indexable)"""
+    # two care cells (one alive, one dead): random universes hit it at varying
+    # generations, so a universe read from the wrong place would show
+    w, u = np.zeros(64, np.uint64), np.zeros(64, np.uint64)
+    w[10] = np.uint64(1 << 40)
+    u[11] = np.uint64(1 << 40)
+    n = (1 << 26) + 5
+    d = hip.fill_random(n, seed=78)
+    first, _ = hip.step_contains(d, to_dev(w[None]), to_dev(u[None]), gens)
+    torch.cuda.synchronize()
+    seen = set()
+    for lo in (0, (1 << 26) - 20, n - 40):   # the 2^32-word boundary is at universe 2^26
+        k = min(40, n - lo)
+        x = port.fill(k, seed=78, first_universe=lo)
+        want, _ = R.step_contains_batch(x, w, u, gens)
+        assert (first[lo:lo + k].cpu().numpy().astype(np.uint32) == want).all(), lo
+        seen |= set(want.tolist())
+    assert len(seen) >= 2, seen
+    del d, first
+    torch.cuda.empty_cache()
