@@ -14,6 +14,7 @@
 // return value, see lifeapi_hip.h).  Link with -llifeapi_hip.
 #pragma once
 
+#include <bit>
 #include <cstdint>
 #include <span>
 #include <stdexcept>
@@ -142,6 +143,36 @@ std::vector<uint8_t> ContainsBatch(std::span<const S> in, const T &target, int d
   return r;
 }
 
+// The target as the offset forms of the reference test it:
+//     s.Contains(target, dx, dy) = s.Contains(target.wanted, dx, dy) && s.AreDisjoint(target.unwanted, dx, dy)
+// (LifeTarget.hpp:38-42) reads s at column i+dx rotated right by dy against
+// target column i (LifeAPI.hpp:399-421): on the torus that is the unshifted
+// test against the target Moved(dx, dy) (LifeAPI.hpp:682-696).  Returns false
+// when some cell is both wanted and unwanted: no state passes the offset form
+// then, where the unshifted Contains(target) asks such a cell to be alive.
+namespace detail {
+inline bool moved_target(const uint64_t *t, int dx, int dy, uint64_t *out) {
+  const unsigned x = (unsigned)dx & 63u, y = (unsigned)dy & 63u;
+  uint64_t clash = 0;
+  for (unsigned i = 0; i < 64; ++i) {
+    clash |= t[i] & t[64 + i];
+    out[(i + x) & 63u] = std::rotl(t[i], (int)y);
+    out[64 + ((i + x) & 63u)] = std::rotl(t[64 + i], (int)y);
+  }
+  return clash == 0;
+}
+}  // namespace detail
+
+// r[i] = in[i].Contains(target, dx, dy)  (LifeTarget.hpp:38-42)
+template <LifeStateLayout S, LifeTargetLayout T>
+std::vector<uint8_t> ContainsBatch(std::span<const S> in, const T &target, int dx, int dy, int device = 0) {
+  uint64_t t[128];
+  if (!detail::moved_target(words(&target), dx, dy, t)) return std::vector<uint8_t>(in.size(), 0);
+  std::vector<uint8_t> r(in.size());
+  check(lifeapi_contains_batch(words(in.data()), t, t + 64, r.data(), in.size(), device));
+  return r;
+}
+
 // The search-loop idiom over a batch, in place (LifeAPI.hpp:1196-1216,
 // LifeTarget.hpp:44-51):
 //     for (unsigned g = 1; g <= gens; ++g) { s.Step(); if (!first && s.Contains(target)) first = g; }
@@ -150,6 +181,22 @@ template <LifeStateLayout S, LifeTargetLayout T>
 std::vector<uint32_t> StepContainsBatch(std::span<S> states, const T &target, unsigned gens, int device = 0) {
   std::vector<uint32_t> first(states.size());
   const uint64_t *t = words(&target);
+  check(lifeapi_step_contains_batch(words(states.data()), words(states.data()), t, t + 64, first.data(),
+                                    states.size(), gens, device));
+  return first;
+}
+
+// The search loop with the offset test s.Contains(target, dx, dy)
+// (LifeTarget.hpp:38-42) in place of s.Contains(target).
+template <LifeStateLayout S, LifeTargetLayout T>
+std::vector<uint32_t> StepContainsBatch(std::span<S> states, const T &target, int dx, int dy, unsigned gens,
+                                        int device = 0) {
+  uint64_t t[128];
+  std::vector<uint32_t> first(states.size());
+  if (!detail::moved_target(words(&target), dx, dy, t)) {  // never contained: step only
+    check(lifeapi_step_batch(words(states.data()), words(states.data()), states.size(), gens, device));
+    return first;
+  }
   check(lifeapi_step_contains_batch(words(states.data()), words(states.data()), t, t + 64, first.data(),
                                     states.size(), gens, device));
   return first;

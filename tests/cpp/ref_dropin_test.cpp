@@ -92,6 +92,69 @@ static void Contains_Target() {
   EXPECT_TRUE(hits >= 600);
 }
 
+// LifeState::Contains(const LifeTarget&, dx, dy) (LifeTarget.hpp:38-42):
+// offsets on both sides of the torus seam and beyond +-64, and a target with
+// a cell both wanted and unwanted (never contained by the offset form)
+static void Contains_TargetOffset() {
+  const LifeState loaf = LifeState::Parse("b2o$o2bo$bobo$2bo!");
+  const LifeTarget target(loaf, loaf.ZOI() & ~loaf);
+  LifeTarget clash = target;
+  clash.unwanted.Set(1, 0);  // (1, 0) is alive in the loaf
+  const int offs[][2] = {{0, 0}, {5, -3}, {-7, 60}, {63, 63}, {-64, 1}, {130, -200}};
+  for (const auto &o : offs) {
+    const int dx = o[0], dy = o[1];
+    std::vector<LifeState> s(1500);
+    for (size_t i = 0; i < s.size(); ++i) {
+      s[i] = LifeState::RandomState();
+      // plant the loaf where the offset test looks for it: state column
+      // i + dx rotated right by dy is matched against target column i
+      const LifeState at = loaf.Moved(dx, dy), zoi = loaf.ZOI().Moved(dx, dy);
+      if (i % 3 == 0) s[i] = (s[i] & ~zoi) | at;
+    }
+    const std::vector<uint8_t> hit = lifeapi::ContainsBatch(std::span<const LifeState>(s), target, dx, dy);
+    const std::vector<uint8_t> none = lifeapi::ContainsBatch(std::span<const LifeState>(s), clash, dx, dy);
+    int hits = 0;
+    for (size_t i = 0; i < s.size(); ++i) {
+      EXPECT_TRUE((hit[i] != 0) == s[i].Contains(target, dx, dy));
+      EXPECT_TRUE((none[i] != 0) == s[i].Contains(clash, dx, dy));
+      hits += hit[i] != 0;
+    }
+    EXPECT_TRUE(hits >= 400);
+  }
+}
+
+// the search loop with the offset test
+static void StepContains_Offset() {
+  const LifeState block = LifeState::Parse("2o$2o!");
+  const LifeTarget target(block, block.ZOI() & ~block);
+  const int dx = -20, dy = 45;
+  std::vector<LifeState> s(2000);
+  for (size_t i = 0; i < s.size(); ++i) {
+    s[i] = LifeState::RandomState() & LifeState::RandomState();
+    if (i % 4 == 0) s[i] = (s[i] & ~block.ZOI().Moved(dx, dy)) | block.Moved(dx, dy);
+  }
+  std::vector<LifeState> cpu = s, s2 = s;
+  std::vector<uint32_t> want(s.size(), 0);
+  for (size_t i = 0; i < s.size(); ++i)
+    for (unsigned g = 1; g <= 12; ++g) {
+      cpu[i].Step();
+      if (!want[i] && cpu[i].Contains(target, dx, dy)) want[i] = g;
+    }
+  const std::vector<uint32_t> got = lifeapi::StepContainsBatch(std::span(s), target, dx, dy, 12);
+  LifeTarget clash = target;
+  clash.wanted.Set(7, 7);
+  clash.unwanted.Set(7, 7);
+  const std::vector<uint32_t> none = lifeapi::StepContainsBatch(std::span(s2), clash, dx, dy, 12);
+  int hits = 0;
+  for (size_t i = 0; i < s.size(); ++i) {
+    EXPECT_TRUE(got[i] == want[i]);
+    EXPECT_TRUE(none[i] == 0);
+    EXPECT_TRUE(s[i] == cpu[i] && s2[i] == cpu[i]);
+    hits += want[i] != 0;
+  }
+  EXPECT_TRUE(hits > 0);
+}
+
 // the search-loop idiom: step, then Contains(target), first hit per state
 static void StepContains_SearchLoop() {
   const LifeState block = LifeState::Parse("2o$2o!").Moved(30, 30);
@@ -215,6 +278,8 @@ int main() {
   Stepped_And_Pop();
   RPentomino();
   Contains_Target();
+  Contains_TargetOffset();
+  StepContains_Offset();
   StepContains_SearchLoop();
   NeighbourCount_Planes();
   LifeWeld_Step();
