@@ -4,6 +4,8 @@
 // The kernels are in step_kernels.hpp; the measured alternatives (other
 // networks, exchanges, layouts and schedules) live in the tuning build,
 // tools/tune/tune_step.hip, and are not part of this library.
+#include <atomic>
+
 #include "step_kernels.hpp"
 
 using namespace lifeapi_impl;
@@ -14,8 +16,8 @@ using StepFn = void (*)(const uint64_t *, uint64_t *, uint64_t, uint32_t);
 
 // The shipped configurations (profiles/r01/tune_*.jsonl):
 // * gens <= 2 -- HBM-streaming: natural layout, DPP exchange, the 7-LUT
-//   network, 4 universes in flight per wave, nontemporal loads/stores (no
-//   layout change to pay for);
+//   network, 4 universes in flight per wave, nontemporal loads (no layout
+//   change to pay for);
 // * gens > 2 -- VALU-bound: 8-way row split with 4 universes interleaved bit
 //   by bit, LDS exchange, the 6-LUT tail, state resident in VGPRs for all
 //   generations, as the hand-allocated loop of split_asm.inc; nontemporal
@@ -27,26 +29,53 @@ using StepFn = void (*)(const uint64_t *, uint64_t *, uint64_t, uint32_t);
 // profiles/r02/step_occupancy.jsonl, same process: +2 % at 1M universes,
 // +2.4 % at 2M, +4.7 % at 4M, +7 % at 16M; 4 and 5 resident blocks nearly
 // as good, 7 and 8 not, 2-3 far worse, and grid-stride caps 7-19 % slower).
+// Batches of at most kCachedUniverses (1 GiB per buffer) store with plain
+// stores and alternate the group order between launches: a launch over the
+// batch the previous one wrote then starts on what that one wrote last, and
+// the plain stores leave it in the 256 MB memory-side Infinity Cache
+// (tools/order_ab.py, profiles/r02/order_ab.jsonl, same process, ping-pong
+// as the bench: +3.0 % at 1M universes, +1.5 % at 512K, equal at 2M); larger
+// batches keep nontemporal stores and one order (plain stores cost 1-2 %
+// there, alternating nothing).
+constexpr uint64_t kCachedUniverses = 1ull << 21;
+constexpr const char *kStreamName =
+    "k_step<dpp, 4 universes/wave, nt loads, 7-LUT network; up to 2M universes plain stores and alternating "
+    "order, above nt stores>";
 struct StepLaunch {
   StepFn fn;
   uint64_t universes_per_wave;
   int resident_blocks;  // per CU, 0 = as many as fit
+  bool alternate;       // alternate the group order between launches
   const char *name;
 };
-StepLaunch shipped_step(uint32_t gens) {
-  if (gens <= 2) return {k_step<XDPP, 4, true, 3>, 4, 6, "k_step<dpp, 4 universes/wave, nt, 7-LUT network>"};
+StepLaunch shipped_step(uint32_t gens, uint64_t n) {
+  if (gens <= 2) {
+    if (n <= kCachedUniverses)
+      return {k_step<XDPP, 4, true, 3, false>, 4, 6, true, kStreamName};
+    return {k_step<XDPP, 4, true, 3, true>, 4, 6, false, kStreamName};
+  }
   if (gens < 32)
-    return {k_step_split<8, 1, true, 6, kAsmLoop>, 4, 0,
+    return {k_step_split<8, 1, true, 6, kAsmLoop>, 4, 0, false,
             "k_step_split<8-way split, 4 universes/wave, nt, 6-LUT tail, assembly loop>"};
-  return {k_step_split<8, 1, false, 6, kAsmLoop>, 4, 0,
+  return {k_step_split<8, 1, false, 6, kAsmLoop>, 4, 0, false,
           "k_step_split<8-way split, 4 universes/wave, 6-LUT tail, assembly loop>"};
+}
+
+// Group order of the alternating launches, per device: the order never
+// changes a result (k_step kReverse).
+constexpr int kMaxDevices = 64;
+std::atomic<uint32_t> g_step_launches[kMaxDevices];
+uint32_t next_order() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return 0;
+  return (g_step_launches[dev].fetch_add(1, std::memory_order_relaxed) & 1u) ? kReverse : 0u;
 }
 
 }  // namespace
 
 extern "C" {
 
-const char *lifeapi_step_kernel_name(uint32_t generations) { return shipped_step(generations).name; }
+const char *lifeapi_step_kernel_name(uint32_t generations) { return shipped_step(generations, 1).name; }
 
 int lifeapi_step_batch_dev(const uint64_t *d_in, uint64_t *d_out, size_t n, uint32_t generations,
                            void *stream) {
@@ -55,7 +84,7 @@ int lifeapi_step_batch_dev(const uint64_t *d_in, uint64_t *d_out, size_t n, uint
   int cus = 0;
   rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
-  const StepLaunch l = shipped_step(generations);
+  const StepLaunch l = shipped_step(generations, n);
   const uint64_t waves = (n + l.universes_per_wave - 1) / l.universes_per_wave;
   unsigned lds = 0;
   if (l.resident_blocks) {
@@ -63,7 +92,7 @@ int lifeapi_step_batch_dev(const uint64_t *d_in, uint64_t *d_out, size_t n, uint
     if (rc != LIFEAPI_OK) return rc;
   }
   hipLaunchKernelGGL(l.fn, dim3(grid_for(waves, cus, 0)), dim3(kBlock), lds, (hipStream_t)stream, d_in,
-                     d_out, (uint64_t)n, generations);
+                     d_out, (uint64_t)n, generations | (l.alternate ? next_order() : 0u));
   return launched("k_step launch");
 }
 

@@ -106,7 +106,13 @@ __device__ __forceinline__ W life_gen(W a, uint64_t *slot, int lane) {
 // in == out is allowed (Step() in place), so neither pointer is
 // __restrict__: each wave loads its universes before it stores them and no
 // wave touches another's (the same holds for k_step_split).
-template <int X, int U, bool NT, int RULE>
+// Bit 31 of `gens` (kReverse) reverses the order in which waves take the
+// groups: alternated between launches, each launch first reads what the one
+// before it wrote last, part of which the memory-side Infinity Cache still
+// holds.  The launcher sets it only for gens <= 2.
+constexpr uint32_t kReverse = 1u << 31;
+// NTS: nontemporal stores (default: as the loads).
+template <int X, int U, bool NT, int RULE, bool NTS = NT>
 __global__ __launch_bounds__(kBlock) void k_step(const uint64_t *in, uint64_t *out, uint64_t n,
                                                  uint32_t gens) {
   __shared__ uint64_t lds[uses_lds(X) ? kWavesPerBlock * U * 2 * kWave : 1];
@@ -114,8 +120,11 @@ __global__ __launch_bounds__(kBlock) void k_step(const uint64_t *in, uint64_t *o
   // wave index in the block, made provably wave-uniform so that the tail
   // tests below are scalar branches
   const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock * U;
-  for (uint64_t u0 = ((uint64_t)blockIdx.x * kWavesPerBlock + wib) * U; u0 < n; u0 += stride) {
+  const bool rev = (gens & kReverse) != 0;
+  gens &= ~kReverse;
+  const uint64_t groups = (n + U - 1) / U, wstride = (uint64_t)gridDim.x * kWavesPerBlock;
+  for (uint64_t grp = (uint64_t)blockIdx.x * kWavesPerBlock + wib; grp < groups; grp += wstride) {
+    const uint64_t u0 = (rev ? groups - 1 - grp : grp) * U;
     W a[U];
 #pragma unroll
     for (int k = 0; k < U; ++k)
@@ -135,7 +144,7 @@ __global__ __launch_bounds__(kBlock) void k_step(const uint64_t *in, uint64_t *o
     }
 #pragma unroll
     for (int k = 0; k < U; ++k)
-      if (u0 + k < n) st<NT>(out + (u0 + k) * kWave + lane, a[k]);
+      if (u0 + k < n) st<NTS>(out + (u0 + k) * kWave + lane, a[k]);
   }
 }
 

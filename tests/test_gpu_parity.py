@@ -53,6 +53,27 @@ def test_ragged_default(hip, port, n):
         assert (got == port.step_batch(x, gens)).all()
 
 
+@pytest.mark.parametrize("n", [1, 3, 5, 4097, (1 << 21) - 1, (1 << 21) + 1])
+def test_alternating_order_launches(hip, port, n):
+    """Batches of up to 2M universes run the streaming step in the reverse
+    group order on every other launch (step.hip kCachedUniverses): four
+    launches in a row, ping-pong and in place, each equal to the oracle
+    whichever order it ran in; above 2M one order (the n = 2M + 1 case)."""
+    x = port.fill(n, seed=n + 11)
+    want = [x]
+    for _ in range(4):
+        want.append(port.step_batch(want[-1], 1, nthreads=16))
+    a, b = to_dev(x), torch.empty((n, 64), dtype=torch.int64, device="cuda")
+    for k in range(1, 5):
+        hip.step(a, out=b, generations=1)
+        assert (to_host(b) == want[k]).all(), k
+        a, b = b, a
+    d = to_dev(x)
+    for k in range(1, 3):
+        hip.step(d, out=d, generations=1)
+        assert (to_host(d) == want[k]).all(), k
+
+
 def test_zero_gens_and_empty(hip, port):
     x = port.fill(17, seed=5)
     assert (to_host(hip.step(to_dev(x), generations=0)) == x).all()

@@ -65,6 +65,21 @@ def test_step_all_cfgs(tune, port, xchg, upw, nt, rule):
 
 
 
+@pytest.mark.parametrize("nts", [False, True])
+@pytest.mark.parametrize("reverse", [False, True])
+def test_step_order(tune, port, nts, reverse):
+    """The streaming step in either group order, plain or nontemporal
+    stores (tools/order_ab.py), ragged against U = 4, 1 and 2 generations."""
+    import torch
+    n = 4096 + 3
+    x = np.concatenate([seam_cases(port), port.fill(n, seed=4242)])
+    d = to_dev(x)
+    out = torch.empty_like(d)
+    for gens in (1, 2):
+        tune.step_order(d, out, gens, reverse=reverse, nts=nts)
+        assert (to_host(out) == port.step_batch(x, gens)).all(), gens
+
+
 def test_bad_cfgs_rejected(tune, hip):
     import torch
     d = torch.zeros((4, 64), dtype=torch.int64, device="cuda")

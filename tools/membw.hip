@@ -13,6 +13,10 @@
 //                 footprint, partly served from the 256 MB Infinity Cache;
 //                 16M: 16 GiB, not); with as many blocks resident per CU
 //                 as fit and with at most 4, 5, 6 (unused dynamic LDS)
+//   membw snake <universes>
+//                 the same ping-pong with the group order reversed on every
+//                 other launch (each launch first reads what the last one
+//                 wrote last), against the same order, per nontemporal mode
 //   membw inplace <objects> <planes>
 //                 the LifeStable kernels' shape: one wave per object reads
 //                 its <planes> x 512 B (contiguous) and writes them back in
@@ -205,8 +209,93 @@ int pingpong(u64 universes) {
   return 0;
 }
 
+// One-shot copy (each wave one group of U rows) whose group order is reversed
+// when `rev` is set: alternating it between ping-pong launches makes each
+// launch read first what the previous one wrote last (the memory-side
+// Infinity Cache may still hold it).
+template <int U, int MODE>
+__global__ __launch_bounds__(256) void k_copy_dir(const u32x2 *in, u32x2 *out, u64 groups, int rev) {
+  const int lane = threadIdx.x & 63;
+  u64 g = (u64)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (g >= groups) return;
+  if (rev) g = groups - 1 - g;
+  const u32x2 *p = in + g * U * 64 + lane;
+  u32x2 *q = out + g * U * 64 + lane;
+  u32x2 v[U];
+#pragma unroll
+  for (int k = 0; k < U; ++k) v[k] = (MODE & 1) ? __builtin_nontemporal_load(p + k * 64) : p[k * 64];
+#pragma unroll
+  for (int k = 0; k < U; ++k) {
+    if (MODE & 2) __builtin_nontemporal_store(v[k] ^ u32x2{1u, 0u}, q + k * 64);
+    else q[k * 64] = v[k] ^ u32x2{1u, 0u};
+  }
+}
+
+// ping-pong copies as the bench's step launches (1 KiB per universe per
+// launch), same direction every launch vs alternating direction ("snake"),
+// for each nontemporal mode, at most 6 blocks resident per CU or all
+template <int MODE>
+int snake_mode(void *a, void *b, u64 universes, const hipDeviceProp_t &p) {
+  const size_t bytes = universes * 512;
+  const u64 groups = universes / 4;  // a row of 64 x 8 B is one universe; 4 per wave
+  const u64 blocks = (groups + 3) / 4;
+  hipEvent_t ev[41];
+  for (auto &e : ev) CHECK(hipEventCreate(&e));
+  for (int resident : {0, 6}) {
+    const unsigned lds = resident ? (unsigned)((p.maxSharedMemoryPerMultiProcessor / resident + 511) & ~511ull) : 0u;
+    for (int snake : {0, 1, 0, 1}) {
+      for (int rep = 0; rep < 10; ++rep)  // warm
+        hipLaunchKernelGGL((k_copy_dir<4, MODE>), dim3(blocks), dim3(256), lds, 0, (const u32x2 *)(rep & 1 ? b : a),
+                           (u32x2 *)(rep & 1 ? a : b), groups, snake ? (rep & 1) : 0);
+      CHECK(hipEventRecord(ev[0], 0));
+      for (int rep = 0; rep < 40; ++rep) {
+        hipLaunchKernelGGL((k_copy_dir<4, MODE>), dim3(blocks), dim3(256), lds, 0, (const u32x2 *)(rep & 1 ? b : a),
+                           (u32x2 *)(rep & 1 ? a : b), groups, snake ? (rep & 1) : 0);
+        CHECK(hipEventRecord(ev[rep + 1], 0));
+      }
+      CHECK(hipEventSynchronize(ev[40]));
+      std::vector<float> ms;
+      for (int rep = 0; rep < 40; ++rep) {
+        float t;
+        CHECK(hipEventElapsedTime(&t, ev[rep], ev[rep + 1]));
+        ms.push_back(t);
+      }
+      float tot;
+      CHECK(hipEventElapsedTime(&tot, ev[0], ev[40]));
+      std::sort(ms.begin(), ms.end());
+      std::printf("{\"variant\": \"dwordx2 pingpong snake\", \"mode\": %d, \"snake\": %d, \"universes\": %llu, "
+                  "\"resident_blocks\": %d, \"ms_mean\": %.4f, \"ms_median\": %.4f, \"GBps_mean\": %.1f, "
+                  "\"GBps_median\": %.1f}\n",
+                  MODE, snake, universes, resident, tot / 40, ms[20], 2.0 * bytes / (tot / 40 * 1e-3) / 1e9,
+                  2.0 * bytes / (ms[20] * 1e-3) / 1e9);
+      std::fflush(stdout);
+    }
+  }
+  for (auto &e : ev) CHECK(hipEventDestroy(e));
+  return 0;
+}
+
+int snake(u64 universes) {
+  if (universes % 4) return 1;
+  const size_t bytes = universes * 512;
+  void *a, *b;
+  CHECK(hipMalloc(&a, bytes));
+  CHECK(hipMalloc(&b, bytes));
+  CHECK(hipMemset(a, 0x5a, bytes));
+  CHECK(hipMemset(b, 0x3c, bytes));
+  hipDeviceProp_t p;
+  CHECK(hipGetDeviceProperties(&p, 0));
+  if (snake_mode<3>(a, b, universes, p) || snake_mode<1>(a, b, universes, p) ||
+      snake_mode<0>(a, b, universes, p) || snake_mode<2>(a, b, universes, p))
+    return 1;
+  CHECK(hipFree(a));
+  CHECK(hipFree(b));
+  return 0;
+}
+
 int main(int argc, char **argv) {
   if (argc > 2 && std::string(argv[1]) == "pingpong") return pingpong(std::stoull(argv[2]));
+  if (argc > 2 && std::string(argv[1]) == "snake") return snake(std::stoull(argv[2]));
   if (argc > 3 && std::string(argv[1]) == "inplace") {
     hipDeviceProp_t p;
     CHECK(hipGetDeviceProperties(&p, 0));

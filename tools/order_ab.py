@@ -1,0 +1,64 @@
+#!/usr/bin/env python3
+"""Group-order and store-policy A/B of the one-generation step (config 2 /
+config 4 shapes), ping-ponged between two buffers as bench.py does: every
+launch in the same order ("fixed") against the order reversed on every other
+launch ("alternate", k_step kReverse), so that each launch first reads what
+the previous one wrote last, each with nontemporal ("nts") or plain stores.
+The tuning build's launch of the streaming kernel (at most 6 blocks resident
+per CU); runs of 40 back-to-back launches between one pair of events, the
+modes interleaved, 6 runs each.  Results must equal the shipped entry
+point's in every mode.  Also times the shipped entry point itself.
+usage: python tools/order_ab.py [universes ...]"""
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools", "tune"))
+import lifeapi_amd.hip as hip  # noqa: E402
+import tune_hip  # noqa: E402
+
+REV = 1 << 31
+RUN = 40
+
+
+def run(bufs, launch):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for i in range(RUN):
+        launch(bufs[i & 1], bufs[(i + 1) & 1], i)
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / RUN
+
+
+for n in [int(a) for a in sys.argv[1:]] or [1 << 18, 1 << 19, 1 << 20, 1 << 21, 1 << 22, 1 << 24]:
+    a = hip.fill_random(n, seed=2)
+    b = torch.empty_like(a)
+    ref = hip.step(a, generations=1)
+    modes = {"shipped": lambda s, d, i: hip.step(s, out=d, generations=1)}
+    for nts in (True, False):
+        for alt in (False, True):
+            def f(s, d, i, nts=nts, alt=alt):
+                tune_hip.step_order(s, d, 1, reverse=alt and bool(i & 1), nts=nts)
+            modes[f"{'nts' if nts else 'plain'}-{'alternate' if alt else 'fixed'}"] = f
+            for rev in (False, True):
+                tune_hip.step_order(a, b, 1, reverse=rev, nts=nts)
+                assert torch.equal(b, ref), (nts, rev)
+    ms = {k: [] for k in modes}
+    bufs = [a, b]
+    for k in modes:  # warm
+        run(bufs, modes[k])
+    for rep in range(6):
+        for k in (list(modes) if rep % 2 == 0 else list(modes)[::-1]):
+            ms[k].append(run(bufs, modes[k]))
+    for k in modes:
+        med = statistics.median(ms[k])
+        print(json.dumps({"universes": n, "order": k, "ms_per_launch_median": med, "ms_all": ms[k],
+                          "GBps": n * 1024 / (med * 1e-3) / 1e9}), flush=True)
+    del a, b, ref
+    torch.cuda.empty_cache()

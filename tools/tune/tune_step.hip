@@ -550,6 +550,28 @@ int lifeapi_tune_step_pair(const uint64_t *d_in, uint64_t *d_out, size_t n, uint
   return launched("k_step_pair launch");
 }
 
+/* the shipped gens <= 2 kernel (k_step<dpp, 4, nt loads, rule 3>) with
+ * nontemporal (nts = 1) or plain stores, at most `resident` blocks per CU
+ * (0 = as many as fit); bit 31 of `generations` reverses the group order    */
+int lifeapi_tune_step_order(const uint64_t *d_in, uint64_t *d_out, size_t n, uint32_t generations, void *stream,
+                            int nts, int resident) {
+  int rc = check_batch(d_in, d_out, n);
+  if (rc != LIFEAPI_OK || n == 0) return rc;
+  if ((generations & ~kReverse) > 2) return fail(LIFEAPI_E_INVALID, "streaming step: generations <= 2%s");
+  int cus = 0;
+  rc = device_cus(cus);
+  if (rc != LIFEAPI_OK) return rc;
+  unsigned lds = 0;
+  if (resident > 0) {
+    rc = occupancy_lds(resident, lds);
+    if (rc != LIFEAPI_OK) return rc;
+  }
+  hipLaunchKernelGGL((nts ? k_step<XDPP, 4, true, 3, true> : k_step<XDPP, 4, true, 3, false>),
+                     dim3(grid_for((n + 3) / 4, cus, 0)), dim3(kBlock), lds, (hipStream_t)stream, d_in, d_out,
+                     (uint64_t)n, generations);
+  return launched("k_step (order) launch");
+}
+
 /* the shipped gens > 2 kernel with clock stamps (see k_step_split_clock);
  * d_stamps: 4 words per wave, one wave per 4 universes, one-shot grid      */
 int lifeapi_tune_step_clock(const uint64_t *d_in, uint64_t *d_out, size_t n, uint32_t generations,
