@@ -34,13 +34,15 @@ using StepFn = void (*)(const uint64_t *, uint64_t *, uint64_t, uint32_t);
 // batch the previous one wrote then starts on what that one wrote last, and
 // the plain stores leave it in the 256 MB memory-side Infinity Cache
 // (tools/order_ab.py, profiles/r02/order_ab.jsonl, same process, ping-pong
-// as the bench: +3.0 % at 1M universes, +1.5 % at 512K, equal at 2M); larger
-// batches keep nontemporal stores and one order (plain stores cost 1-2 %
-// there, alternating nothing).
+// as the bench: +3.0 % at 1M universes, +1.5 % at 512K, equal at 2M), and
+// with every block slot used (not the cap of 6 above: +2.8 % more at 1M,
+// profiles/r02/order_occupancy.jsonl); larger batches keep nontemporal
+// stores, one order and the cap (plain stores cost 1-2 % there, alternating
+// nothing).
 constexpr uint64_t kCachedUniverses = 1ull << 21;
 constexpr const char *kStreamName =
-    "k_step<dpp, 4 universes/wave, nt loads, 7-LUT network; up to 2M universes plain stores and alternating "
-    "order, above nt stores>";
+    "k_step<dpp, 4 universes/wave, nt loads, 7-LUT network; up to 2M universes plain stores, alternating "
+    "order, all block slots; above nt stores, 6 blocks per CU>";
 struct StepLaunch {
   StepFn fn;
   uint64_t universes_per_wave;
@@ -51,7 +53,7 @@ struct StepLaunch {
 StepLaunch shipped_step(uint32_t gens, uint64_t n) {
   if (gens <= 2) {
     if (n <= kCachedUniverses)
-      return {k_step<XDPP, 4, true, 3, false>, 4, 6, true, kStreamName};
+      return {k_step<XDPP, 4, true, 3, false>, 4, 0, true, kStreamName};
     return {k_step<XDPP, 4, true, 3, true>, 4, 6, false, kStreamName};
   }
   if (gens < 32)

@@ -8,7 +8,8 @@ The tuning build's launch of the streaming kernel (at most 6 blocks resident
 per CU); runs of 40 back-to-back launches between one pair of events, the
 modes interleaved, 6 runs each.  Results must equal the shipped entry
 point's in every mode.  Also times the shipped entry point itself.
-usage: python tools/order_ab.py [universes ...]"""
+usage: [RESIDENT=0,4,5,8] python tools/order_ab.py [universes ...]
+(RESIDENT: also the alternating plain-store launch with those occupancy caps)"""
 import json
 import os
 import statistics
@@ -24,6 +25,7 @@ import tune_hip  # noqa: E402
 
 REV = 1 << 31
 RUN = 40
+RESIDENT = [int(r) for r in os.environ.get("RESIDENT", "").split(",") if r]  # e.g. 0,4,5,8
 
 
 def run(bufs, launch):
@@ -49,6 +51,9 @@ for n in [int(a) for a in sys.argv[1:]] or [1 << 18, 1 << 19, 1 << 20, 1 << 21, 
             for rev in (False, True):
                 tune_hip.step_order(a, b, 1, reverse=rev, nts=nts)
                 assert torch.equal(b, ref), (nts, rev)
+    for r in RESIDENT:  # other occupancy caps for the alternating plain-store launch
+        modes[f"plain-alternate-r{r}"] = lambda s, d, i, r=r: tune_hip.step_order(s, d, 1, reverse=bool(i & 1),
+                                                                                   nts=False, resident=r)
     ms = {k: [] for k in modes}
     bufs = [a, b]
     for k in modes:  # warm
