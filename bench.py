@@ -174,26 +174,33 @@ def copy_ceiling(n: int):
     (tools/membw.hip `pingpong`, measured on MI355X and committed under
     profiles/): the streaming ceiling for this footprint, context for the
     roofline.  The nearest measured footprint is used, and the best of the
-    occupancy settings measured there."""
-    path = os.path.join(ROOT, "profiles", "r02", "membw_pingpong.jsonl")
+    occupancy settings, store policies and launch orders measured there
+    (`membw snake`: the group order alternated between launches, as the
+    step kernel runs batches of up to 2M universes)."""
     rows = []
-    try:
-        with open(path) as f:
-            for line in f:
-                try:
-                    d = json.loads(line)
-                except ValueError:
-                    continue
-                if "universes" in d and "GBps_median" in d:
-                    rows.append(d)
-    except OSError:
-        return None, None
+    for name in ("membw_pingpong.jsonl", "membw_snake.jsonl"):
+        path = os.path.join(ROOT, "profiles", "r02", name)
+        try:
+            with open(path) as f:
+                for line in f:
+                    try:
+                        d = json.loads(line)
+                    except ValueError:
+                        continue
+                    if "universes" in d and "GBps_median" in d:
+                        rows.append((d, os.path.relpath(path, ROOT)))
+        except OSError:
+            continue
     if not rows:
         return None, None
-    near = min(rows, key=lambda d: abs(np.log2(d["universes"]) - np.log2(max(n, 1))))["universes"]
-    best = max((d for d in rows if d["universes"] == near), key=lambda d: d["GBps_median"])
-    return best["GBps_median"], (f"{os.path.relpath(path, ROOT)} ({near} universes, "
-                                 f"{best.get('resident_blocks', 0) or 'all'} blocks resident per CU)")
+    near = min(rows, key=lambda r: abs(np.log2(r[0]["universes"]) - np.log2(max(n, 1))))[0]["universes"]
+    best, src = max((r for r in rows if r[0]["universes"] == near), key=lambda r: r[0]["GBps_median"])
+    shape = ""
+    if "snake" in best:
+        shape = (f", {'nt' if best['mode'] & 2 else 'plain'} stores, "
+                 f"{'alternating' if best['snake'] else 'one'} order")
+    return best["GBps_median"], (f"{src} ({near} universes, "
+                                 f"{best.get('resident_blocks', 0) or 'all'} blocks resident per CU{shape})")
 
 
 def load_pmc_traffic(n: int):
