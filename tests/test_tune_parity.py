@@ -69,15 +69,17 @@ def test_step_all_cfgs(tune, port, xchg, upw, nt, rule):
 @pytest.mark.parametrize("reverse", [False, True])
 def test_step_order(tune, port, nts, reverse):
     """The streaming step in either group order, plain or nontemporal
-    stores (tools/order_ab.py), ragged against U = 4, 1 and 2 generations."""
+    stores (tools/order_ab.py), 2, 4 or 8 universes per wave, ragged against
+    each, 1 and 2 generations."""
     import torch
     n = 4096 + 3
     x = np.concatenate([seam_cases(port), port.fill(n, seed=4242)])
     d = to_dev(x)
     out = torch.empty_like(d)
     for gens in (1, 2):
-        tune.step_order(d, out, gens, reverse=reverse, nts=nts)
-        assert (to_host(out) == port.step_batch(x, gens)).all(), gens
+        for upw in (2, 4, 8):
+            tune.step_order(d, out, gens, reverse=reverse, nts=nts, upw=upw)
+            assert (to_host(out) == port.step_batch(x, gens)).all(), (gens, upw)
 
 
 def test_bad_cfgs_rejected(tune, hip):

@@ -8,8 +8,9 @@ The tuning build's launch of the streaming kernel (at most 6 blocks resident
 per CU); runs of 40 back-to-back launches between one pair of events, the
 modes interleaved, 6 runs each.  Results must equal the shipped entry
 point's in every mode.  Also times the shipped entry point itself.
-usage: [RESIDENT=0,4,5,8] python tools/order_ab.py [universes ...]
-(RESIDENT: also the alternating plain-store launch with those occupancy caps)"""
+usage: [RESIDENT=0,4,5,8] [UPW=2,4,8] python tools/order_ab.py [universes ...]
+(RESIDENT: also the alternating plain-store launch with those occupancy caps,
+for each UPW universes per wave)"""
 import json
 import os
 import statistics
@@ -26,6 +27,7 @@ import tune_hip  # noqa: E402
 REV = 1 << 31
 RUN = 40
 RESIDENT = [int(r) for r in os.environ.get("RESIDENT", "").split(",") if r]  # e.g. 0,4,5,8
+UPW = [int(u) for u in os.environ.get("UPW", "4").split(",") if u]  # universes per wave for RESIDENT
 
 
 def run(bufs, launch):
@@ -52,8 +54,13 @@ for n in [int(a) for a in sys.argv[1:]] or [1 << 18, 1 << 19, 1 << 20, 1 << 21, 
                 tune_hip.step_order(a, b, 1, reverse=rev, nts=nts)
                 assert torch.equal(b, ref), (nts, rev)
     for r in RESIDENT:  # other occupancy caps for the alternating plain-store launch
-        modes[f"plain-alternate-r{r}"] = lambda s, d, i, r=r: tune_hip.step_order(s, d, 1, reverse=bool(i & 1),
-                                                                                   nts=False, resident=r)
+        for u in UPW:
+            modes[f"plain-alternate-r{r}-u{u}"] = (
+                lambda s, d, i, r=r, u=u: tune_hip.step_order(s, d, 1, reverse=bool(i & 1), nts=False, resident=r,
+                                                              upw=u))
+            for rev in (False, True):
+                tune_hip.step_order(a, b, 1, reverse=rev, nts=False, resident=r, upw=u)
+                assert torch.equal(b, ref), (r, u, rev)
     ms = {k: [] for k in modes}
     bufs = [a, b]
     for k in modes:  # warm

@@ -550,14 +550,22 @@ int lifeapi_tune_step_pair(const uint64_t *d_in, uint64_t *d_out, size_t n, uint
   return launched("k_step_pair launch");
 }
 
-/* the shipped gens <= 2 kernel (k_step<dpp, 4, nt loads, rule 3>) with
+/* the shipped gens <= 2 kernel (k_step<dpp, U, nt loads, rule 3>) with
  * nontemporal (nts = 1) or plain stores, at most `resident` blocks per CU
- * (0 = as many as fit); bit 31 of `generations` reverses the group order    */
+ * (0 = as many as fit), U = upw universes per wave (2, 4 or 8; shipped 4);
+ * bit 31 of `generations` reverses the group order                         */
+extern "C++" {
+template <int U>
+StepFn order_fn(int nts) { return nts ? k_step<XDPP, U, true, 3, true> : k_step<XDPP, U, true, 3, false>; }
+}
+
 int lifeapi_tune_step_order(const uint64_t *d_in, uint64_t *d_out, size_t n, uint32_t generations, void *stream,
-                            int nts, int resident) {
+                            int nts, int resident, int upw) {
   int rc = check_batch(d_in, d_out, n);
   if (rc != LIFEAPI_OK || n == 0) return rc;
   if ((generations & ~kReverse) > 2) return fail(LIFEAPI_E_INVALID, "streaming step: generations <= 2%s");
+  const StepFn fn = upw == 2 ? order_fn<2>(nts) : upw == 4 ? order_fn<4>(nts) : upw == 8 ? order_fn<8>(nts) : nullptr;
+  if (!fn) return fail(LIFEAPI_E_INVALID, "universes per wave: 2, 4 or 8%s");
   int cus = 0;
   rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
@@ -566,9 +574,8 @@ int lifeapi_tune_step_order(const uint64_t *d_in, uint64_t *d_out, size_t n, uin
     rc = occupancy_lds(resident, lds);
     if (rc != LIFEAPI_OK) return rc;
   }
-  hipLaunchKernelGGL((nts ? k_step<XDPP, 4, true, 3, true> : k_step<XDPP, 4, true, 3, false>),
-                     dim3(grid_for((n + 3) / 4, cus, 0)), dim3(kBlock), lds, (hipStream_t)stream, d_in, d_out,
-                     (uint64_t)n, generations);
+  hipLaunchKernelGGL(fn, dim3(grid_for((n + upw - 1) / upw, cus, 0)), dim3(kBlock), lds, (hipStream_t)stream, d_in,
+                     d_out, (uint64_t)n, generations);
   return launched("k_step (order) launch");
 }
 
