@@ -62,7 +62,11 @@ const char *lifeapi_step_kernel_name(uint32_t generations);
 
 /* ---- device-resident, stream-ordered (the hot path) -------------------- */
 
-/* out[u] = in[u] stepped `generations` times (0 = copy), for u < n.       */
+/* out[u] = in[u] stepped `generations` times (0 = copy), for u < n.  For
+ * 1-2 generations and n <= 2M the library alternates, per device, the order
+ * in which it walks the batch from one call to the next (a cache-locality
+ * choice for back-to-back calls on the batch just written);
+ * results never depend on it, and calls from several threads are safe.    */
 int lifeapi_step_batch_dev(const uint64_t *d_in, uint64_t *d_out, size_t n,
                            uint32_t generations, void *stream);
 /* d_pop[u] = population of universe u                                     */
