@@ -4,6 +4,7 @@
 // The kernels are in step_kernels.hpp; the measured alternatives (other
 // networks, exchanges, layouts and schedules) live in the tuning build,
 // tools/tune/tune_step.hip, and are not part of this library.
+#include <algorithm>
 #include <atomic>
 
 #include "step_kernels.hpp"
@@ -12,7 +13,7 @@ using namespace lifeapi_impl;
 
 namespace {
 
-using StepFn = void (*)(const uint64_t *, uint64_t *, uint64_t, uint32_t);
+using StepFn = void (*)(const uint64_t *, uint64_t *, uint64_t, uint32_t, uint64_t);
 
 // The shipped configurations (profiles/r01/tune_*.jsonl):
 // * gens <= 2 -- HBM-streaming: natural layout, DPP exchange, the 7-LUT
@@ -29,37 +30,36 @@ using StepFn = void (*)(const uint64_t *, uint64_t *, uint64_t, uint32_t);
 // profiles/r02/step_occupancy.jsonl, same process: +2 % at 1M universes,
 // +2.4 % at 2M, +4.7 % at 4M, +7 % at 16M; 4 and 5 resident blocks nearly
 // as good, 7 and 8 not, 2-3 far worse, and grid-stride caps 7-19 % slower).
-// Batches of at most kCachedUniverses (1 GiB per buffer) store with plain
-// stores and alternate the group order between launches: a launch over the
-// batch the previous one wrote then starts on what that one wrote last, and
-// the plain stores leave it in the 256 MB memory-side Infinity Cache
-// (tools/order_ab.py, profiles/r02/order_ab.jsonl, same process, ping-pong
-// as the bench: +3.0 % at 1M universes, +1.5 % at 512K, equal at 2M), and
-// with every block slot used (not the cap of 6 above: +2.8 % more at 1M,
-// profiles/r02/order_occupancy.jsonl); larger batches keep nontemporal
-// stores, one order and the cap (plain stores cost 1-2 % there, alternating
-// nothing).
-constexpr uint64_t kCachedUniverses = 1ull << 21;
+// Launch order and store policy (tools/order_ab.py, profiles/r02/order_*.jsonl,
+// same process, ping-pong as the bench): every launch takes the groups in
+// the reverse order of the launch before it (per device), so it starts on
+// what that one wrote last; the groups that store the last min(256 MiB, half
+// the batch) of a launch use plain stores, which leave that part in the 256 MB
+// memory-side Infinity Cache, and the rest nontemporal ones, which do not
+// evict it.  Batches of up to kCachedUniverses use every block slot, larger
+// ones the cap.  Against round 2's launch (nontemporal, one order, capped):
+// +12 % at 1M universes, +10 % at 2M, +3-5 % at 512K and 4M, equal at 8M-16M.
+constexpr uint64_t kCachedUniverses = 1ull << 22;
+constexpr uint64_t kPlainBytes = 256ull << 20;
 constexpr const char *kStreamName =
-    "k_step<dpp, 4 universes/wave, nt loads, 7-LUT network; up to 2M universes plain stores, alternating "
-    "order, all block slots; above nt stores, 6 blocks per CU>";
+    "k_step<dpp, 4 universes/wave, nt loads, 7-LUT network; alternating order, the last min(256 MiB, half) of "
+    "each launch stored plain, the rest nt>";
 struct StepLaunch {
   StepFn fn;
   uint64_t universes_per_wave;
-  int resident_blocks;  // per CU, 0 = as many as fit
-  bool alternate;       // alternate the group order between launches
+  int resident_blocks;   // per CU, 0 = as many as fit
+  bool alternate;        // alternate the group order between launches
+  uint64_t plain_bytes;  // the last bytes of a launch stored plain
   const char *name;
 };
 StepLaunch shipped_step(uint32_t gens, uint64_t n) {
-  if (gens <= 2) {
-    if (n <= kCachedUniverses)
-      return {k_step<XDPP, 4, true, 3, false>, 4, 0, true, kStreamName};
-    return {k_step<XDPP, 4, true, 3, true>, 4, 6, false, kStreamName};
-  }
+  if (gens <= 2)
+    return {k_step<XDPP, 4, true, 3, true>, 4, n <= kCachedUniverses ? 0 : 6, true,
+            std::min<uint64_t>(kPlainBytes, n * 512 / 2), kStreamName};
   if (gens < 32)
-    return {k_step_split<8, 1, true, 6, kAsmLoop>, 4, 0, false,
+    return {k_step_split<8, 1, true, 6, kAsmLoop>, 4, 0, false, 0,
             "k_step_split<8-way split, 4 universes/wave, nt, 6-LUT tail, assembly loop>"};
-  return {k_step_split<8, 1, false, 6, kAsmLoop>, 4, 0, false,
+  return {k_step_split<8, 1, false, 6, kAsmLoop>, 4, 0, false, 0,
           "k_step_split<8-way split, 4 universes/wave, 6-LUT tail, assembly loop>"};
 }
 
@@ -93,8 +93,10 @@ int lifeapi_step_batch_dev(const uint64_t *d_in, uint64_t *d_out, size_t n, uint
     rc = occupancy_lds(l.resident_blocks, lds);
     if (rc != LIFEAPI_OK) return rc;
   }
+  const uint64_t plain = (l.plain_bytes + l.universes_per_wave * 512 - 1) / (l.universes_per_wave * 512);
   hipLaunchKernelGGL(l.fn, dim3(grid_for(waves, cus, 0)), dim3(kBlock), lds, (hipStream_t)stream, d_in,
-                     d_out, (uint64_t)n, generations | (l.alternate ? next_order() : 0u));
+                     d_out, (uint64_t)n, generations | (l.alternate ? next_order() : 0u),
+                     plain < waves ? waves - plain : (uint64_t)0);
   return launched("k_step launch");
 }
 

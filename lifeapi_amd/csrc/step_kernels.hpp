@@ -108,13 +108,16 @@ __device__ __forceinline__ W life_gen(W a, uint64_t *slot, int lane) {
 // wave touches another's (the same holds for k_step_split).
 // Bit 31 of `gens` (kReverse) reverses the order in which waves take the
 // groups: alternated between launches, each launch first reads what the one
-// before it wrote last, part of which the memory-side Infinity Cache still
-// holds.  The launcher sets it only for gens <= 2.
+// before it wrote last.  The groups taken from position `plain_from` on (in
+// the launch's order) store with plain stores, the rest as NTS says: the
+// last-written part then stays in the memory-side Infinity Cache for the next
+// launch to read first, and the nontemporal rest does not evict it
+// (DESIGN.md 3.1).  The launcher sets both only for gens <= 2.
 constexpr uint32_t kReverse = 1u << 31;
-// NTS: nontemporal stores (default: as the loads).
+// NTS: nontemporal stores (default: as the loads) before `plain_from`.
 template <int X, int U, bool NT, int RULE, bool NTS = NT>
 __global__ __launch_bounds__(kBlock) void k_step(const uint64_t *in, uint64_t *out, uint64_t n,
-                                                 uint32_t gens) {
+                                                 uint32_t gens, uint64_t plain_from) {
   __shared__ uint64_t lds[uses_lds(X) ? kWavesPerBlock * U * 2 * kWave : 1];
   const int lane = threadIdx.x & (kWave - 1);
   // wave index in the block, made provably wave-uniform so that the tail
@@ -142,9 +145,15 @@ __global__ __launch_bounds__(kBlock) void k_step(const uint64_t *in, uint64_t *o
 #pragma unroll
       for (int k = 0; k < U; ++k) a[k] = from_eo(a[k]);
     }
+    if (grp < plain_from) {
 #pragma unroll
-    for (int k = 0; k < U; ++k)
-      if (u0 + k < n) st<NTS>(out + (u0 + k) * kWave + lane, a[k]);
+      for (int k = 0; k < U; ++k)
+        if (u0 + k < n) st<NTS>(out + (u0 + k) * kWave + lane, a[k]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < U; ++k)
+        if (u0 + k < n) st<false>(out + (u0 + k) * kWave + lane, a[k]);
+    }
   }
 }
 
@@ -157,7 +166,7 @@ constexpr int kPipe = -1;
 constexpr int kAsmLoop = -3;  // the hand-allocated rule-11 loop (split_asm.inc)
 template <int S, int G, bool NT, int NET, int D = 0, int V = 0>
 __global__ __launch_bounds__(kBlock) void k_step_split(const uint64_t *in, uint64_t *out, uint64_t n,
-                                                       uint32_t gens) {
+                                                       uint32_t gens, uint64_t /* plain_from: k_step's */) {
   constexpr int P = S / 2;
   __shared__ uint32_t lds[kWavesPerBlock * G * S * kWave];
   const int lane = threadIdx.x & (kWave - 1);

@@ -55,10 +55,11 @@ def test_ragged_default(hip, port, n):
 
 @pytest.mark.parametrize("n", [1, 3, 5, 4097, (1 << 21) - 1, (1 << 21) + 1])
 def test_alternating_order_launches(hip, port, n):
-    """Batches of up to 2M universes run the streaming step in the reverse
-    group order on every other launch (step.hip kCachedUniverses): four
-    launches in a row, ping-pong and in place, each equal to the oracle
-    whichever order it ran in; above 2M one order (the n = 2M + 1 case)."""
+    """The streaming step takes the groups in the reverse order on every
+    other launch and stores the last min(256 MiB, half the batch) of each
+    launch with plain stores (step.hip): four launches in a row, ping-pong
+    and in place, each equal to the oracle whichever order it ran in, with
+    the plain/nontemporal boundary inside the batch."""
     x = port.fill(n, seed=n + 11)
     want = [x]
     for _ in range(4):

@@ -78,8 +78,9 @@ def test_step_order(tune, port, nts, reverse):
     out = torch.empty_like(d)
     for gens in (1, 2):
         for upw in (2, 4, 8):
-            tune.step_order(d, out, gens, reverse=reverse, nts=nts, upw=upw)
-            assert (to_host(out) == port.step_batch(x, gens)).all(), (gens, upw)
+            for plain in (0, 1, 300 * 512, 1 << 40):  # no, one, some and all groups store plain
+                tune.step_order(d, out, gens, reverse=reverse, nts=nts, upw=upw, plain_bytes=plain)
+                assert (to_host(out) == port.step_batch(x, gens)).all(), (gens, upw, plain)
 
 
 def test_bad_cfgs_rejected(tune, hip):

@@ -48,7 +48,7 @@ def main(prof_dir: str, out_json: str, universes: int = 1 << 20):
                 "hbm_bytes_per_launch": fetch_b + write_b, "algorithmic_bytes_per_launch": algo,
                 "traffic_over_algorithmic": (fetch_b + write_b) / algo}
 
-    c2 = entry("k_step<0, 4, true, 3, false>", "k_step<DPP, U=4, nt loads, plain stores, rule 3> (config 2: 1M universes x 1 gen)",
+    c2 = entry("k_step<0, 4, true, 3, true>", "k_step<DPP, U=4, nt loads, nt stores but the last 256 MiB plain, alternating order, rule 3> (config 2: 1M universes x 1 gen)",
                universes * 1024)
     d = dict(c2)
     d["universes"] = universes

@@ -79,19 +79,21 @@ def step_clock(states: torch.Tensor, out: torch.Tensor, generations: int, stream
     return out, stamps
 
 
-lib.lifeapi_tune_step_order.argtypes = [_vp, _vp, _sz, _u32, _vp, _int, _int, _int]
+lib.lifeapi_tune_step_order.argtypes = [_vp, _vp, _sz, _u32, _vp, _int, _int, _int, ctypes.c_uint64]
 lib.lifeapi_tune_step_order.restype = _int
 
 
 def step_order(states: torch.Tensor, out: torch.Tensor, generations: int = 1, reverse: bool = False,
-               nts: bool = True, resident: int = 6, upw: int = 4, stream=None) -> torch.Tensor:
+               nts: bool = True, resident: int = 6, upw: int = 4, plain_bytes: int = 0,
+               stream=None) -> torch.Tensor:
     """The shipped gens <= 2 kernel with nontemporal or plain stores, at most
     `resident` blocks per CU, `upw` universes per wave, universes taken in
-    reverse order if asked."""
+    reverse order if asked; plain stores for the groups that store the last
+    `plain_bytes` of the launch's order whatever `nts` says."""
     n = hip._universes(states)
     hip._check(lib.lifeapi_tune_step_order(states.data_ptr(), out.data_ptr(), n,
                                            generations | ((1 << 31) if reverse else 0), hip._stream(stream),
-                                           1 if nts else 0, resident, upw))
+                                           1 if nts else 0, resident, upw, plain_bytes))
     return out
 
 

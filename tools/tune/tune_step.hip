@@ -89,7 +89,7 @@ __device__ __forceinline__ void gens_asm(W &a, uint32_t gens, uint32_t lds_self,
 template <int X, int U, bool NT, int RULE>
 __global__ __launch_bounds__(kBlock) void k_step_asm4(const uint64_t *__restrict__ in,
                                                  uint64_t *__restrict__ out, uint64_t n,
-                                                 uint32_t gens) {
+                                                 uint32_t gens, uint64_t /* plain_from */) {
   __shared__ uint64_t lds[uses_lds(X) ? kWavesPerBlock * U * 2 * kWave : 1];
   const int lane = threadIdx.x & (kWave - 1);
   // wave index in the block, made provably wave-uniform so that the tail
@@ -150,7 +150,7 @@ __device__ __forceinline__ void st2(uint64_t *p, u64x2 v) {
 template <int S, int C, int X, bool NT, int NET>
 __global__ __launch_bounds__(kBlock) void k_step_tile(const uint64_t *__restrict__ in,
                                                       uint64_t *__restrict__ out, uint64_t n,
-                                                      uint32_t gens) {
+                                                      uint32_t gens, uint64_t /* plain_from */) {
   constexpr int P = S / 2, LPG = kWave / C;
   static_assert(C % 2 == 0, "columns are moved in pairs");
   __shared__ uint32_t lds[X == XDPP ? 1 : kWavesPerBlock * 2 * S * kWave];  // 4 planes of 1 KiB per wave (S = 8)
@@ -221,7 +221,7 @@ __global__ __launch_bounds__(kBlock) void k_step_tile(const uint64_t *__restrict
   }
 }
 
-using StepFn = void (*)(const uint64_t *, uint64_t *, uint64_t, uint32_t);
+using StepFn = void (*)(const uint64_t *, uint64_t *, uint64_t, uint32_t, uint64_t);
 
 template <int X, int U, bool NT, int RULE>
 constexpr StepFn step_ptr() {
@@ -551,7 +551,8 @@ int lifeapi_tune_step_pair(const uint64_t *d_in, uint64_t *d_out, size_t n, uint
 }
 
 /* the shipped gens <= 2 kernel (k_step<dpp, U, nt loads, rule 3>) with
- * nontemporal (nts = 1) or plain stores, at most `resident` blocks per CU
+ * nontemporal (nts = 1) or plain stores (0), but plain for the groups that
+ * store the last `plain_bytes` of the launch's order, at most `resident` blocks per CU
  * (0 = as many as fit), U = upw universes per wave (2, 4 or 8; shipped 4);
  * bit 31 of `generations` reverses the group order                         */
 extern "C++" {
@@ -560,7 +561,7 @@ StepFn order_fn(int nts) { return nts ? k_step<XDPP, U, true, 3, true> : k_step<
 }
 
 int lifeapi_tune_step_order(const uint64_t *d_in, uint64_t *d_out, size_t n, uint32_t generations, void *stream,
-                            int nts, int resident, int upw) {
+                            int nts, int resident, int upw, uint64_t plain_bytes) {
   int rc = check_batch(d_in, d_out, n);
   if (rc != LIFEAPI_OK || n == 0) return rc;
   if ((generations & ~kReverse) > 2) return fail(LIFEAPI_E_INVALID, "streaming step: generations <= 2%s");
@@ -574,8 +575,9 @@ int lifeapi_tune_step_order(const uint64_t *d_in, uint64_t *d_out, size_t n, uin
     rc = occupancy_lds(resident, lds);
     if (rc != LIFEAPI_OK) return rc;
   }
-  hipLaunchKernelGGL(fn, dim3(grid_for((n + upw - 1) / upw, cus, 0)), dim3(kBlock), lds, (hipStream_t)stream, d_in,
-                     d_out, (uint64_t)n, generations);
+  const uint64_t groups = (n + upw - 1) / upw, plain = (plain_bytes + upw * 512 - 1) / (upw * 512);
+  hipLaunchKernelGGL(fn, dim3(grid_for(groups, cus, 0)), dim3(kBlock), lds, (hipStream_t)stream, d_in, d_out,
+                     (uint64_t)n, generations, plain < groups ? groups - plain : (uint64_t)0);
   return launched("k_step (order) launch");
 }
 
@@ -633,7 +635,7 @@ int lifeapi_tune_step_batch_dev_cfg(const uint64_t *d_in, uint64_t *d_out, size_
     if (rc != LIFEAPI_OK) return rc;
   }
   hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), lds, (hipStream_t)stream, d_in, d_out,
-                     (uint64_t)n, generations);
+                     (uint64_t)n, generations, ~(uint64_t)0);
   return launched("k_step (tuning) launch");
 }
 
