@@ -41,6 +41,7 @@ using StepFn = void (*)(const uint64_t *, uint64_t *, uint64_t, uint32_t, uint64
 // +12 % at 1M universes, +10 % at 2M, +3-5 % at 512K and 4M, equal at 8M-16M.
 constexpr uint64_t kCachedUniverses = 1ull << 22;
 constexpr uint64_t kPlainBytes = 256ull << 20;
+constexpr uint64_t kFilterOrderUniverses = 1ull << 21;  // the same for the 1-2 generation search filter
 constexpr const char *kStreamName =
     "k_step<dpp, 4 universes/wave, nt loads, 7-LUT network; alternating order, the last min(256 MiB, half) of "
     "each launch stored plain, the rest nt>";
@@ -136,10 +137,18 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
     // profiles/r02/filter_ab.jsonl, 1M universes x 1 generation, same
     // process): 0.087 ms = 6.25 TB/s on the 516 B per universe of the bare
     // filter, 0.181 ms with final states (5.96 TB/s on 1028 B); 4 per wave
-    // 0.107 / 0.179, with fewer blocks resident slower; one per wave 0.229
-    hipLaunchKernelGGL(k_step_contains<8>, dim3(grid_for((n + 7) / 8, cus, 0)), dim3(kBlock), 0,
-                       (hipStream_t)stream, d_in, d_final, d_wanted, d_unwanted, d_first_gen,
-                       (uint64_t)n, generations);
+    // 0.107 / 0.179, with fewer blocks resident slower; one per wave 0.229.
+    // With final states, the launch order and plain-stored tail of the step
+    // (above): a loop that filters the states the last call left gets them
+    // partly from the Infinity Cache (tools/filter_order_ab.py).
+    const uint64_t groups = (n + 7) / 8;
+    // Up to 2M universes: +3.4 % at 512K and 1M, +2 % at 2M, none at 4M
+    // (profiles/r02/filter_order_ab.jsonl).
+    const bool order = d_final && n <= kFilterOrderUniverses;
+    const uint64_t plain = order ? (std::min<uint64_t>(kPlainBytes, n * 512 / 2) + 8 * 512 - 1) / (8 * 512) : 0;
+    hipLaunchKernelGGL(k_step_contains<8>, dim3(grid_for(groups, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream,
+                       d_in, d_final, d_wanted, d_unwanted, d_first_gen, (uint64_t)n,
+                       generations | (order ? next_order() : 0u), plain < groups ? groups - plain : (uint64_t)0);
   }
   return launched("k_step_contains launch");
 }

@@ -226,17 +226,22 @@ __global__ __launch_bounds__(kBlock) void k_step_split(const uint64_t *in, uint6
 // universe.  `in` and `fin` may be the same array (the host form stages
 // through one buffer), so neither is __restrict__: each wave loads its
 // universes before it stores them, and no wave touches another's universes.
+// Group order (kReverse in `gens`) and the plain-stored tail of the final
+// states (`plain_from`) as k_step's.
 template <int U>
 __global__ __launch_bounds__(kBlock) void k_step_contains(const uint64_t *in, uint64_t *fin,
                                                           const uint64_t *__restrict__ wanted,
                                                           const uint64_t *__restrict__ unwanted,
                                                           uint32_t *__restrict__ first,
-                                                          uint64_t n, uint32_t gens) {
+                                                          uint64_t n, uint32_t gens, uint64_t plain_from) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const W w = split(wanted[lane]), uw = split(unwanted[lane]);
-  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock * U;
-  for (uint64_t u0 = ((uint64_t)blockIdx.x * kWavesPerBlock + wib) * U; u0 < n; u0 += stride) {
+  const bool rev = (gens & kReverse) != 0;
+  gens &= ~kReverse;
+  const uint64_t groups = (n + U - 1) / U, wstride = (uint64_t)gridDim.x * kWavesPerBlock;
+  for (uint64_t grp = (uint64_t)blockIdx.x * kWavesPerBlock + wib; grp < groups; grp += wstride) {
+    const uint64_t u0 = (rev ? groups - 1 - grp : grp) * U;
     W a[U];
 #pragma unroll
     for (int k = 0; k < U; ++k) a[k] = (u0 + k < n) ? ld<true>(in + (u0 + k) * kWave + lane) : W{0u, 0u};
@@ -250,10 +255,14 @@ __global__ __launch_bounds__(kBlock) void k_step_contains(const uint64_t *in, ui
         if (hit[k] == 0 && wave_contains(a[k], w, uw)) hit[k] = g;
       }
     }
-    if (fin) {
+    if (fin && grp < plain_from) {
 #pragma unroll
       for (int k = 0; k < U; ++k)
         if (u0 + k < n) st<true>(fin + (u0 + k) * kWave + lane, a[k]);
+    } else if (fin) {
+#pragma unroll
+      for (int k = 0; k < U; ++k)
+        if (u0 + k < n) st<false>(fin + (u0 + k) * kWave + lane, a[k]);
     }
     // lanes 0..U-1 write the U first-hit generations with one store
     uint32_t h = hit[0];

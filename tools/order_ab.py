@@ -12,7 +12,7 @@ usage: [RESIDENT=0,4,5,8] [UPW=2,4,8] [LATE=128,256] [LATE_RESIDENT=0,6] python 
 (RESIDENT: also the alternating plain-store launch with those occupancy caps,
 for each UPW universes per wave; LATE: nontemporal stores but plain for
 the groups that store the last LATE MiB of each launch, alternating, with
-each LATE_RESIDENT occupancy cap)"""
+each LATE_RESIDENT occupancy cap and LATE_UPW universes per wave)"""
 import json
 import os
 import statistics
@@ -32,6 +32,7 @@ RESIDENT = [int(r) for r in os.environ.get("RESIDENT", "").split(",") if r]  # e
 UPW = [int(u) for u in os.environ.get("UPW", "4").split(",") if u]  # universes per wave for RESIDENT
 LATE = [int(e) for e in os.environ.get("LATE", "").split(",") if e]  # MiB stored plain at each launch's end
 LATE_RESIDENT = [int(r) for r in os.environ.get("LATE_RESIDENT", "0").split(",") if r]
+LATE_UPW = [int(u) for u in os.environ.get("LATE_UPW", "4").split(",") if u]
 
 
 def run(bufs, launch):
@@ -67,12 +68,13 @@ for n in [int(a) for a in sys.argv[1:]] or [1 << 18, 1 << 19, 1 << 20, 1 << 21, 
                 assert torch.equal(b, ref), (r, u, rev)
     for mb in LATE:  # nontemporal stores but the last `mb` MiB plain, alternating, per occupancy
         for r in LATE_RESIDENT:
-            modes[f"late{mb}M-alternate-r{r}"] = (
-                lambda s, d, i, mb=mb, r=r: tune_hip.step_order(s, d, 1, reverse=bool(i & 1), resident=r,
-                                                                plain_bytes=mb << 20))
-            for rev in (False, True):
-                tune_hip.step_order(a, b, 1, reverse=rev, resident=r, plain_bytes=mb << 20)
-                assert torch.equal(b, ref), (mb, r, rev)
+            for u in LATE_UPW:
+                modes[f"late{mb}M-alternate-r{r}" + (f"-u{u}" if u != 4 else "")] = (
+                    lambda s, d, i, mb=mb, r=r, u=u: tune_hip.step_order(s, d, 1, reverse=bool(i & 1), resident=r,
+                                                                         upw=u, plain_bytes=mb << 20))
+                for rev in (False, True):
+                    tune_hip.step_order(a, b, 1, reverse=rev, resident=r, upw=u, plain_bytes=mb << 20)
+                    assert torch.equal(b, ref), (mb, r, u, rev)
     ms = {k: [] for k in modes}
     bufs = [a, b]
     for k in modes:  # warm

@@ -496,12 +496,14 @@ int lifeapi_tune_step_contains_nat(const uint64_t *d_in, uint64_t *d_final, cons
     rc = occupancy_lds(resident, lds);
     if (rc != LIFEAPI_OK) return rc;
   }
-  using Fn = void (*)(const uint64_t *, uint64_t *, const uint64_t *, const uint64_t *, uint32_t *, uint64_t, uint32_t);
+  using Fn = void (*)(const uint64_t *, uint64_t *, const uint64_t *, const uint64_t *, uint32_t *, uint64_t, uint32_t,
+                      uint64_t);
   Fn fn = upw == 1 ? (Fn)k_step_contains<1> : upw == 2 ? (Fn)k_step_contains<2> : upw == 4 ? (Fn)k_step_contains<4>
         : upw == 8 ? (Fn)k_step_contains<8> : nullptr;
   if (!fn) return fail(LIFEAPI_E_INVALID, "universes per wave: 1, 2, 4 or 8%s");
+  // one order, nontemporal stores (the launch before the product's order policy)
   hipLaunchKernelGGL(fn, dim3(grid_for((n + upw - 1) / upw, cus, cap)), dim3(kBlock), lds, (hipStream_t)stream, d_in,
-                     d_final, d_wanted, d_unwanted, d_first_gen, (uint64_t)n, generations);
+                     d_final, d_wanted, d_unwanted, d_first_gen, (uint64_t)n, generations, ~(uint64_t)0);
   return launched("k_step_contains (tuning) launch");
 }
 
