@@ -89,17 +89,34 @@ __device__ __forceinline__ W weld_gen(W s, W f2, W f1, W f0) {
   return W{p.lo & (s1.lo ^ s2.lo), p.hi & (s1.hi ^ s2.hi)};
 }
 
+// In place, one wave per LifeWeld.  Bit 31 of `gens` (kWeldReverse)
+// reverses the order in which waves take the welds, and the welds taken
+// from position `plain_from` on load and store with plain (not
+// nontemporal) accesses: alternated between launches, a launch on the batch
+// the last one stepped starts on the welds that launch touched last, part of
+// which the memory-side Infinity Cache still holds (as k_step).
+constexpr uint32_t kWeldReverse = 1u << 31;
 __global__ __launch_bounds__(kBlock) void k_weld(uint64_t *__restrict__ welds, uint64_t n,
-                                                 uint32_t gens) {
+                                                 uint32_t gens, uint64_t plain_from) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const bool rev = (gens & kWeldReverse) != 0;
+  gens &= ~kWeldReverse;
   const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock;
-  for (uint64_t u = (uint64_t)blockIdx.x * kWavesPerBlock + wib; u < n; u += stride) {
+  for (uint64_t k = (uint64_t)blockIdx.x * kWavesPerBlock + wib; k < n; k += stride) {
+    const uint64_t u = rev ? n - 1 - k : k;
     uint64_t *p = welds + u * 4 * kWave + lane;
-    W s = ld<true>(p);
-    const W f2 = ld<true>(p + kWave), f1 = ld<true>(p + 2 * kWave), f0 = ld<true>(p + 3 * kWave);
-    for (uint32_t g = 0; g < gens; ++g) s = weld_gen(s, f2, f1, f0);
-    st<true>(p, s);
+    if (k < plain_from) {
+      W s = ld<true>(p);
+      const W f2 = ld<true>(p + kWave), f1 = ld<true>(p + 2 * kWave), f0 = ld<true>(p + 3 * kWave);
+      for (uint32_t g = 0; g < gens; ++g) s = weld_gen(s, f2, f1, f0);
+      st<true>(p, s);
+    } else {
+      W s = ld<false>(p);
+      const W f2 = ld<false>(p + kWave), f1 = ld<false>(p + 2 * kWave), f0 = ld<false>(p + 3 * kWave);
+      for (uint32_t g = 0; g < gens; ++g) s = weld_gen(s, f2, f1, f0);
+      st<false>(p, s);
+    }
   }
 }
 

@@ -137,6 +137,18 @@ def reduce(kind: int, states, out, upw: int, blocks_per_cu: int, wanted=None, un
     return out
 
 
+lib.lifeapi_tune_weld_order.argtypes = [_vp, _sz, _int, ctypes.c_uint64, _vp]
+lib.lifeapi_tune_weld_order.restype = _int
+
+
+def weld_order(welds: torch.Tensor, reverse: bool = False, plain_welds: int = 0, stream=None):
+    """k_weld one generation in place, order reversed if asked, the last
+    `plain_welds` welds of the launch's order loaded and stored plain."""
+    hip._check(lib.lifeapi_tune_weld_order(welds.data_ptr(), welds.shape[0], 1 if reverse else 0, plain_welds,
+                                           hip._stream(stream)))
+    return welds
+
+
 lib.lifeapi_tune_stencil.argtypes = [_int, _vp, _vp, _sz, _int, _vp]
 lib.lifeapi_tune_stencil.restype = _int
 

@@ -64,12 +64,26 @@ int lifeapi_tune_stencil(int kind, const uint64_t *d_in, uint64_t *d_out, size_t
     case 1: hipLaunchKernelGGL(k_counts<1>, grid, dim3(kBlock), lds, (hipStream_t)stream, d_in, d_out, (uint64_t)n); break;
     case 2: hipLaunchKernelGGL(k_counts<2>, grid, dim3(kBlock), lds, (hipStream_t)stream, d_in, d_out, (uint64_t)n); break;
     case 3:
-      hipLaunchKernelGGL(k_weld, grid, dim3(kBlock), lds, (hipStream_t)stream, (uint64_t *)d_in, (uint64_t)n, 1u);
+      // one order, nontemporal throughout (the launch before the product's order policy)
+      hipLaunchKernelGGL(k_weld, grid, dim3(kBlock), lds, (hipStream_t)stream, (uint64_t *)d_in, (uint64_t)n, 1u,
+                         ~(uint64_t)0);
       break;
     default:
       hipLaunchKernelGGL((k_refined<1, 0>), grid, dim3(kBlock), lds, (hipStream_t)stream, d_in, d_out, (uint64_t)n);
   }
   return launched("stencil (tuning) launch");
+}
+
+/* k_weld one generation in place, the order reversed if `reverse`, the
+ * welds taken from position n - plain_welds on loaded and stored plain     */
+int lifeapi_tune_weld_order(uint64_t *d_welds, size_t n, int reverse, uint64_t plain_welds, void *stream) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!d_welds) return fail(LIFEAPI_E_INVALID, "bad argument to lifeapi_tune_weld_order%s");
+  int cus = 0, rc = device_cus(cus);
+  if (rc != LIFEAPI_OK) return rc;
+  hipLaunchKernelGGL(k_weld, dim3(grid_for(n, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream, d_welds, (uint64_t)n,
+                     1u | (reverse ? kWeldReverse : 0u), plain_welds < n ? (uint64_t)n - plain_welds : (uint64_t)0);
+  return launched("k_weld (order) launch");
 }
 
 }  // extern "C"
