@@ -56,7 +56,7 @@ int lifeapi_stable_pass_batch_dev(uint64_t *d_planes, uint8_t *d_flags, size_t n
   if (b < a + n * 10 * 512 && a < b + n) return fail(LIFEAPI_E_INVALID, "flags overlap planes%s");
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
-  using Fn = void (*)(uint64_t *, uint8_t *, uint64_t, uint32_t);
+  using Fn = void (*)(uint64_t *, uint8_t *, uint64_t, uint32_t, uint32_t);
   const Fn fns[6] = {k_stable<0>, k_stable<1>, k_stable<2>, k_stable<3>, k_stable<4>, k_stable<5>};
   // Launch shape (same-process A/Bs, tools/stable_grid_ab.py, on still lifes
   // around an unknown window with fresh options -- the state a search
@@ -79,8 +79,10 @@ int lifeapi_stable_pass_batch_dev(uint64_t *d_planes, uint8_t *d_flags, size_t n
     rc = occupancy_lds(kStableResidentBlocks, lds);
     if (rc != LIFEAPI_OK) return rc;
   }
+  // One order: alternating it, as k_weld does, was 1-2 % slower on repeated
+  // passes in place (tools/stable_order_ab.py, profiles/r02/stable_order_ab.jsonl).
   hipLaunchKernelGGL(fns[pass], dim3(grid_for(n, cus, 0)), dim3(kBlock), lds, (hipStream_t)stream,
-                     d_planes, d_flags, (uint64_t)n, max_iters ? max_iters : 1u << 20);
+                     d_planes, d_flags, (uint64_t)n, max_iters ? max_iters : 1u << 20, 0u);
   return launched("k_stable launch");
 }
 

@@ -110,17 +110,18 @@ def hash_variant(states: torch.Tensor, variant: int, blocks_per_cu: int = 0, out
     return out
 
 
-lib.lifeapi_tune_stable_pass.argtypes = [_vp, _vp, _sz, _int, _u32, _int, _vp]
+lib.lifeapi_tune_stable_pass.argtypes = [_vp, _vp, _sz, _int, _u32, _int, _vp, _int]
 lib.lifeapi_tune_stable_pass.restype = _int
 lib.lifeapi_tune_stable_vulnerable.argtypes = [_vp, _vp, _sz, _int, _vp]
 lib.lifeapi_tune_stable_vulnerable.restype = _int
 
 
-def stable_pass(planes: torch.Tensor, which: int, blocks_per_cu: int, max_iters: int = 0, stream=None):
+def stable_pass(planes: torch.Tensor, which: int, blocks_per_cu: int, max_iters: int = 0, stream=None,
+                reverse: bool = False):
     n = planes.numel() // (10 * 64)
     flags = torch.empty(n, dtype=torch.uint8, device=planes.device)
     hip._check(lib.lifeapi_tune_stable_pass(planes.data_ptr(), flags.data_ptr(), n, which, max_iters,
-                                            blocks_per_cu, hip._stream(stream)))
+                                            blocks_per_cu, hip._stream(stream), 1 if reverse else 0))
     return flags
 
 

@@ -13,19 +13,20 @@ using namespace lifeapi_impl;
 extern "C" {
 
 int lifeapi_tune_stable_pass(uint64_t *d_planes, uint8_t *d_flags, size_t n, int pass, uint32_t max_iters,
-                             int blocks_per_cu, void *stream) {
+                             int blocks_per_cu, void *stream, int reverse) {
   if (n == 0) return LIFEAPI_OK;
   if (!d_planes || !d_flags || !aligned8(d_planes) || pass < 0 || pass > 5)
     return fail(LIFEAPI_E_INVALID, "bad argument to lifeapi_tune_stable_pass%s");
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
-  using Fn = void (*)(uint64_t *, uint8_t *, uint64_t, uint32_t);
+  using Fn = void (*)(uint64_t *, uint8_t *, uint64_t, uint32_t, uint32_t);
   const Fn fns[6] = {k_stable<0>, k_stable<1>, k_stable<2>, k_stable<3>, k_stable<4>, k_stable<5>};
   // blocks_per_cu < 0: uncapped grid, at most -blocks_per_cu blocks resident
   // per CU (unused dynamic LDS out of the CU's 160 KiB)
   const unsigned lds = blocks_per_cu < 0 ? ((160u << 10) / (unsigned)-blocks_per_cu + 511u) & ~511u : 0u;
   hipLaunchKernelGGL(fns[pass], dim3(grid_for(n, cus, blocks_per_cu > 0 ? blocks_per_cu : 0)), dim3(kBlock), lds,
-                     (hipStream_t)stream, d_planes, d_flags, (uint64_t)n, max_iters ? max_iters : 1u << 20);
+                     (hipStream_t)stream, d_planes, d_flags, (uint64_t)n, max_iters ? max_iters : 1u << 20,
+                     reverse ? 1u : 0u);
   return launched("k_stable (tuning) launch");
 }
 
