@@ -643,6 +643,9 @@ def main(argv=None):
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                          "traffic": traffic, "traffic_source": tsrc,
+                         "traffic_note": "FETCH_SIZE/WRITE_SIZE count L2-to-fabric bytes, so reads the "
+                                         "memory-side Infinity Cache serves (the alternating launch order, "
+                                         "DESIGN.md 3.1) count as HBM bytes; achieved is algorithmic bytes / time",
                          "algorithmic_bytes_per_launch": bpl,
                          "aggregate_GBps": agg,
                          "aggregate_frac": (agg / (world * HBM_PEAK_GBS)) if agg else None,
