@@ -71,12 +71,84 @@ int device_cus(int &cus) {
   return rc;
 }
 
-int occupancy_lds(int blocks_per_cu, unsigned &bytes) {
+int occupancy_lds(const void *kernel, int blocks_per_cu, unsigned &bytes) {
   DevInfo d;
-  const int rc = device_info(d);
+  int rc = device_info(d);
   if (rc != LIFEAPI_OK) return rc;
-  bytes = (unsigned)((d.lds_per_cu / (size_t)blocks_per_cu + 511) & ~(size_t)511);
+  if (blocks_per_cu < 1) return fail(LIFEAPI_E_INVALID, "occupancy cap below one block per CU%s");
+  hipFuncAttributes fa;
+  hipError_t e = hipFuncGetAttributes(&fa, kernel);
+  if (e != hipSuccess) return fail_hip(e, "hipFuncGetAttributes");
+  int free_blocks = 0;  // what the kernel's registers and static LDS allow
+  e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&free_blocks, kernel, kBlock, 0);
+  if (e != hipSuccess) return fail_hip(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor");
+  if (free_blocks < 1) return fail(LIFEAPI_E_INVALID, "kernel cannot be resident%s");
+  const int want = std::min(blocks_per_cu, free_blocks);
+  // round DOWN: k blocks of (static + dynamic) LDS must fit in the CU's LDS
+  // (rounding up to the granule allowed one block fewer whenever k does not
+  // divide it: 6 -> 5, 3 -> 2)
+  const size_t per_block = d.lds_per_cu / (size_t)want;
+  size_t dyn = per_block > fa.sharedSizeBytes ? (per_block - fa.sharedSizeBytes) & ~(size_t)255 : 0;
+  for (;; dyn -= 256) {
+    int got = 0;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&got, kernel, kBlock, dyn);
+    if (e != hipSuccess) return fail_hip(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor");
+    if (got >= want) break;  // the granule rounded us above the share: shrink
+    if (dyn < 256) return fail(LIFEAPI_E_INVALID, "cannot set the occupancy cap%s");
+  }
+  bytes = (unsigned)dyn;
   return LIFEAPI_OK;
+}
+
+// ---- launch order keyed on the batch (host.hpp launch_reverse) ----
+namespace {
+constexpr int kOrderDevices = 64, kOrderSlots = 8;
+struct OrderSlot {
+  uintptr_t ptr = 0;
+  uint64_t bytes = 0, tick = 0;
+  bool reverse = false;
+};
+struct OrderBook {
+  std::mutex mu;
+  OrderSlot slot[kOrderSlots];
+  uint64_t tick = 0;
+};
+OrderBook g_order[kOrderDevices];
+
+OrderBook *order_book() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kOrderDevices) return nullptr;
+  return &g_order[dev];
+}
+
+// forget every batch overlapping [p, p + bytes), then remember it written in
+// order `rev` (the least recently written slot makes room); mu held
+void order_record(OrderBook &b, uintptr_t p, uint64_t bytes, bool rev) {
+  OrderSlot *victim = &b.slot[0];
+  for (OrderSlot &s : b.slot) {
+    if (s.bytes && s.ptr < p + bytes && p < s.ptr + s.bytes) s = OrderSlot{};
+    if (!s.bytes || (victim->bytes && s.tick < victim->tick)) victim = &s;
+  }
+  *victim = OrderSlot{p, bytes, ++b.tick, rev};
+}
+}  // namespace
+
+bool launch_reverse(const void *d_in, const void *d_out, uint64_t bytes) {
+  OrderBook *b = order_book();
+  if (!b || bytes == 0) return false;
+  std::lock_guard<std::mutex> lk(b->mu);
+  bool rev = false;
+  for (const OrderSlot &s : b->slot)
+    if (s.bytes == bytes && s.ptr == (uintptr_t)d_in) rev = !s.reverse;
+  order_record(*b, (uintptr_t)d_out, bytes, rev);
+  return rev;
+}
+
+void note_forward_write(const void *d_out, uint64_t bytes) {
+  OrderBook *b = order_book();
+  if (!b || bytes == 0) return;
+  std::lock_guard<std::mutex> lk(b->mu);
+  order_record(*b, (uintptr_t)d_out, bytes, false);
 }
 
 bool aligned8(const void *p) { return ((uintptr_t)p & 7u) == 0; }
@@ -297,10 +369,12 @@ int host_device(int device) {
 // device >= 0: fn(0, n, device) on that device.  device -1: one contiguous
 // shard per visible device, fn(lo, hi, dev) on one host thread each, with the
 // given host ranges page-locked once for all shards (shard boundaries share
-// pages).  LIFEAPI_HOST_SHARDS=k (k >= 1) overrides the shard count, shard s
+// pages).  LIFEAPI_HOST_SHARDS=k (1 <= k <= 64, else LIFEAPI_E_INVALID)
+// overrides the shard count (at most n shards), shard s
 // running on device s mod ndev: a rehearsal knob that runs the threaded path
 // on a machine with fewer GPUs (tests/test_host_multidev.py).  The first
 // failing shard's code and message are returned.
+constexpr long kMaxHostShards = 64;
 template <class F>
 int over_devices(size_t n, int device, const std::pair<const void *, size_t> *ranges, int nranges, F &&fn) {
   const int ndev = lifeapi_device_count();
@@ -309,9 +383,13 @@ int over_devices(size_t n, int device, const std::pair<const void *, size_t> *ra
   int shards = ndev;
   if (device < 0) {
     if (const char *e = std::getenv("LIFEAPI_HOST_SHARDS")) {
-      const int k = std::atoi(e);
-      if (k >= 1) shards = k;
+      char *end = nullptr;
+      const long k = std::strtol(e, &end, 10);
+      if (end == e || *end != '\0' || k < 1 || k > kMaxHostShards)
+        return fail(LIFEAPI_E_INVALID, "LIFEAPI_HOST_SHARDS must be an integer in 1..64, not '%s'", e);
+      shards = (int)k;
     }
+    shards = (int)std::min<size_t>((size_t)shards, std::max<size_t>(n, 1));  // no empty shards
   }
   if (device >= 0 || shards == 1) return fn(0, n, device < 0 ? 0 : device);
   CallPins pins;

@@ -20,9 +20,22 @@ int fail(int code, const char *fmt, const char *arg = nullptr);
 int fail_hip(hipError_t e, const char *what);
 // CUs of the current device, which must be a gfx950
 int device_cus(int &cus);
-// unused dynamic LDS per block that leaves room for at most blocks_per_cu
-// resident blocks on a CU of the current device (an occupancy cap)
-int occupancy_lds(int blocks_per_cu, unsigned &bytes);
+// unused dynamic LDS per block that leaves exactly min(blocks_per_cu, what
+// the kernel's registers allow) blocks of `kernel` resident per CU of the
+// current device (an occupancy cap), checked against the occupancy API
+int occupancy_lds(const void *kernel, int blocks_per_cu, unsigned &bytes);
+// Launch order keyed on the batch (the order never changes a result): true
+// = take the groups in reverse.  Reverse exactly when d_in is a batch of
+// `bytes` that an earlier order-keyed launch on this device wrote in forward
+// order (and forward when it wrote it in reverse), so that each launch starts
+// on what the launch that wrote its input wrote last, which the memory-side
+// Infinity Cache may still hold; any other input runs forward.  Records d_out
+// as written in the order returned.  A few batches are remembered per device,
+// so interleaved loops over several batches keep the alternation.
+bool launch_reverse(const void *d_in, const void *d_out, uint64_t bytes);
+// Records d_out (bytes) as written in forward order by a launch that does not
+// alternate (so a stale entry for that range cannot reverse a later reader).
+void note_forward_write(const void *d_out, uint64_t bytes);
 bool aligned8(const void *p);
 // n universes in / out: non-null, 8-byte aligned, equal or disjoint
 int check_batch(const void *in, const void *out, size_t n);

@@ -2,8 +2,6 @@
 // NeighbourCount / InteractionCounts (LifeAPI.hpp:909-1040), LifeWeld::Step
 // (LifeWeld.hpp:169-186), the LifeStable propagation passes
 // (LifeStable.hpp:526-729) and the config-5 unknown_step_refined step.
-#include <atomic>
-
 #include "device.hpp"
 #include "host.hpp"
 #include "split_layout.hpp"
@@ -11,18 +9,6 @@
 #include "stencil_kernels.hpp"
 
 using namespace lifeapi_impl;
-
-namespace {
-// Launch order of k_weld, alternated per device (the order never changes a
-// result).
-constexpr int kMaxWeldDevices = 64;
-std::atomic<uint32_t> g_weld_launches[kMaxWeldDevices];
-uint32_t next_weld_order() {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxWeldDevices) return 0;
-  return (g_weld_launches[dev].fetch_add(1, std::memory_order_relaxed) & 1u) ? kWeldReverse : 0u;
-}
-}  // namespace
 
 extern "C" {
 
@@ -76,7 +62,7 @@ int lifeapi_stable_pass_batch_dev(uint64_t *d_planes, uint8_t *d_flags, size_t n
   // random planes, whose fixpoints take more steps).
   unsigned lds = 0;
   if (pass != 4) {
-    rc = occupancy_lds(kStableResidentBlocks, lds);
+    rc = occupancy_lds(reinterpret_cast<const void *>(fns[pass]), kStableResidentBlocks, lds);
     if (rc != LIFEAPI_OK) return rc;
   }
   // One order: alternating it, as k_weld does, was 1-2 % slower on repeated
@@ -98,7 +84,7 @@ int lifeapi_stable_vulnerable_batch_dev(const uint64_t *d_planes, uint64_t *d_ou
   // CU (0.96-0.97 ms at 1M against 0.97-1.00 unlimited and 1.02-1.04 on a
   // looping grid; profiles/r02/stable_occupancy_*.jsonl)
   unsigned lds = 0;
-  rc = occupancy_lds(kStableResidentBlocks, lds);
+  rc = occupancy_lds(reinterpret_cast<const void *>(k_stable_vulnerable), kStableResidentBlocks, lds);
   if (rc != LIFEAPI_OK) return rc;
   hipLaunchKernelGGL(k_stable_vulnerable, dim3(grid_for(n, cus, 0)), dim3(kBlock), lds, (hipStream_t)stream,
                      d_planes, d_out, (uint64_t)n);
@@ -116,12 +102,14 @@ int lifeapi_weld_step_batch_dev(uint64_t *d_welds, size_t n, uint32_t generation
                        dim3(grid_for((n + 3) / 4, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream,
                        d_welds, (uint64_t)n, generations);
   else {
-    // the order alternated per device, nontemporal throughout: in a loop
-    // stepping the batch in place, +15 % at 256K welds, +7 % at 512K,
-    // +3.5 % at 1M, +1.5 % at 2M; a plain-stored tail adds nothing here
-    // (tools/weld_order_ab.py, profiles/r02/weld_order_ab.jsonl)
+    // the order keyed on the batch (host.hpp launch_reverse: in place, so
+    // it alternates between calls on the same welds), nontemporal
+    // throughout: in a loop stepping the batch in place, +15 % at 256K
+    // welds, +7 % at 512K, +3.5 % at 1M, +1.5 % at 2M; a plain-stored tail
+    // adds nothing here (tools/weld_order_ab.py, profiles/r02/weld_order_ab.jsonl)
+    const uint32_t rev = launch_reverse(d_welds, d_welds, (uint64_t)n * 2048) ? kWeldReverse : 0u;
     hipLaunchKernelGGL(k_weld, dim3(grid_for(n, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream, d_welds,
-                       (uint64_t)n, generations | next_weld_order(), (uint64_t)n);
+                       (uint64_t)n, generations | rev, (uint64_t)n);
   }
   return launched("k_weld launch");
 }

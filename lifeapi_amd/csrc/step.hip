@@ -5,7 +5,6 @@
 // networks, exchanges, layouts and schedules) live in the tuning build,
 // tools/tune/tune_step.hip, and are not part of this library.
 #include <algorithm>
-#include <atomic>
 
 #include "step_kernels.hpp"
 
@@ -24,22 +23,28 @@ using StepFn = void (*)(const uint64_t *, uint64_t *, uint64_t, uint32_t, uint64
 //   generations, as the hand-allocated loop of split_asm.inc; nontemporal
 //   below 32 generations.  One-shot grids: every capped grid-stride grid
 //   measured slower.
-// The streaming kernel runs with at most 6 blocks (24 waves) resident per CU
+// The streaming kernel runs with at most 5 blocks (20 waves) resident per CU
 // instead of the 8 its registers allow, set by unused dynamic LDS: fewer
 // concurrent streams per CU, better served by HBM (tools/step_occupancy_ab.py,
 // profiles/r02/step_occupancy.jsonl, same process: +2 % at 1M universes,
-// +2.4 % at 2M, +4.7 % at 4M, +7 % at 16M; 4 and 5 resident blocks nearly
-// as good, 7 and 8 not, 2-3 far worse, and grid-stride caps 7-19 % slower).
+// +2.4 % at 2M, +4.7 % at 4M, +7 % at 16M over 8; 4 nearly as good, 6 and 8
+// not, 2 far worse, and grid-stride caps 7-19 % slower).  Round 2 recorded
+// that sweep as caps of 2..8, but its LDS arithmetic rounded up and gave one
+// block fewer whenever the cap did not divide the CU's LDS (6 -> 5, 7 -> 6,
+// 3 -> 2): its "6" was 5, the setting kept here; occupancy_lds now checks
+// the count against the occupancy API.
 // Launch order and store policy (tools/order_ab.py, profiles/r02/order_*.jsonl,
-// same process, ping-pong as the bench): every launch takes the groups in
-// the reverse order of the launch before it (per device), so it starts on
-// what that one wrote last; the groups that store the last min(256 MiB, half
+// same process, ping-pong as the bench): a launch whose input batch an
+// earlier launch wrote takes the groups in the reverse of that launch's order
+// (host.hpp launch_reverse, keyed on the batch), so it starts on what was
+// written last; the groups that store the last min(256 MiB, half
 // the batch) of a launch use plain stores, which leave that part in the 256 MB
 // memory-side Infinity Cache, and the rest nontemporal ones, which do not
 // evict it.  Batches of up to kCachedUniverses use every block slot, larger
 // ones the cap.  Against round 2's launch (nontemporal, one order, capped):
 // +12 % at 1M universes, +10 % at 2M, +3-5 % at 512K and 4M, equal at 8M-16M.
 constexpr uint64_t kCachedUniverses = 1ull << 22;
+constexpr int kStreamResidentBlocks = 5;
 constexpr uint64_t kPlainBytes = 256ull << 20;
 constexpr uint64_t kFilterOrderUniverses = 1ull << 21;  // the same for the 1-2 generation search filter
 constexpr const char *kStreamName =
@@ -55,23 +60,13 @@ struct StepLaunch {
 };
 StepLaunch shipped_step(uint32_t gens, uint64_t n) {
   if (gens <= 2)
-    return {k_step<XDPP, 4, true, 3, true>, 4, n <= kCachedUniverses ? 0 : 6, true,
+    return {k_step<XDPP, 4, true, 3, true>, 4, n <= kCachedUniverses ? 0 : kStreamResidentBlocks, true,
             std::min<uint64_t>(kPlainBytes, n * 512 / 2), kStreamName};
   if (gens < 32)
     return {k_step_split<8, 1, true, 6, kAsmLoop>, 4, 0, false, 0,
             "k_step_split<8-way split, 4 universes/wave, nt, 6-LUT tail, assembly loop>"};
   return {k_step_split<8, 1, false, 6, kAsmLoop>, 4, 0, false, 0,
           "k_step_split<8-way split, 4 universes/wave, 6-LUT tail, assembly loop>"};
-}
-
-// Group order of the alternating launches, per device: the order never
-// changes a result (k_step kReverse).
-constexpr int kMaxDevices = 64;
-std::atomic<uint32_t> g_step_launches[kMaxDevices];
-uint32_t next_order() {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return 0;
-  return (g_step_launches[dev].fetch_add(1, std::memory_order_relaxed) & 1u) ? kReverse : 0u;
 }
 
 }  // namespace
@@ -91,13 +86,15 @@ int lifeapi_step_batch_dev(const uint64_t *d_in, uint64_t *d_out, size_t n, uint
   const uint64_t waves = (n + l.universes_per_wave - 1) / l.universes_per_wave;
   unsigned lds = 0;
   if (l.resident_blocks) {
-    rc = occupancy_lds(l.resident_blocks, lds);
+    rc = occupancy_lds(reinterpret_cast<const void *>(l.fn), l.resident_blocks, lds);
     if (rc != LIFEAPI_OK) return rc;
   }
   const uint64_t plain = (l.plain_bytes + l.universes_per_wave * 512 - 1) / (l.universes_per_wave * 512);
+  uint32_t order = 0;
+  if (l.alternate) order = launch_reverse(d_in, d_out, (uint64_t)n * 512) ? kReverse : 0u;
+  else note_forward_write(d_out, (uint64_t)n * 512);
   hipLaunchKernelGGL(l.fn, dim3(grid_for(waves, cus, 0)), dim3(kBlock), lds, (hipStream_t)stream, d_in,
-                     d_out, (uint64_t)n, generations | (l.alternate ? next_order() : 0u),
-                     plain < waves ? waves - plain : (uint64_t)0);
+                     d_out, (uint64_t)n, generations | order, plain < waves ? waves - plain : (uint64_t)0);
   return launched("k_step launch");
 }
 
@@ -125,6 +122,7 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
     const Fn fns[2] = {k_step_contains_split<8, kContainsNet, kContainsLo>,
                        k_step_contains_split<8, kContainsNet, kContainsHi>};
     const dim3 grid(grid_for((n + 3) / 4, cus, 0));
+    if (d_final) note_forward_write(d_final, (uint64_t)n * 512);
     for (const Fn fn : fns) {
       hipLaunchKernelGGL(fn, grid, dim3(kBlock), 0, (hipStream_t)stream, d_in, d_final, d_wanted, d_unwanted,
                          d_first_gen, (uint64_t)n, generations);
@@ -146,9 +144,12 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
     // (profiles/r02/filter_order_ab.jsonl).
     const bool order = d_final && n <= kFilterOrderUniverses;
     const uint64_t plain = order ? (std::min<uint64_t>(kPlainBytes, n * 512 / 2) + 8 * 512 - 1) / (8 * 512) : 0;
+    uint32_t rev = 0;
+    if (order) rev = launch_reverse(d_in, d_final, (uint64_t)n * 512) ? kReverse : 0u;
+    else if (d_final) note_forward_write(d_final, (uint64_t)n * 512);
     hipLaunchKernelGGL(k_step_contains<8>, dim3(grid_for(groups, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream,
-                       d_in, d_final, d_wanted, d_unwanted, d_first_gen, (uint64_t)n,
-                       generations | (order ? next_order() : 0u), plain < groups ? groups - plain : (uint64_t)0);
+                       d_in, d_final, d_wanted, d_unwanted, d_first_gen, (uint64_t)n, generations | rev,
+                       plain < groups ? groups - plain : (uint64_t)0);
   }
   return launched("k_step_contains launch");
 }

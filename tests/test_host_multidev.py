@@ -152,3 +152,23 @@ def test_bad_device_index(hip):
     assert e.value.code == -2
     with pytest.raises(hip.LifeApiError):
         hip.step_host(x, 1, device=-2)
+
+
+@pytest.mark.parametrize("bad", ["0", "65", "100000", "-3", "4x", ""])
+def test_shard_override_rejects_bad_values(hip, shards, bad):
+    """LIFEAPI_HOST_SHARDS outside 1..64 (or not an integer) is a caller
+    error, not a request for that many threads (host.hip over_devices)"""
+    shards(bad)
+    from oracle.oracle import Port
+    x = Port().fill(5, seed=5)
+    with pytest.raises(hip.LifeApiError) as e:
+        hip.step_host(x, 1, device=-1)
+    assert e.value.code == -1 and "LIFEAPI_HOST_SHARDS" in str(e.value)  # LIFEAPI_E_INVALID
+
+
+def test_shard_override_capped_at_n(hip, stepper, shards):
+    """more shards than universes: one shard per universe, no empty shards"""
+    shards(64)
+    from oracle.oracle import Port
+    x = Port().fill(3, seed=33)
+    assert (hip.step_host(x, 2, device=-1) == stepper.step_batch(x, 2)).all()

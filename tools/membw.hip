@@ -184,7 +184,7 @@ int pingpong(u64 universes) {
   // as many blocks resident per CU as fit, then at most 4 / 5 / 6 (unused
   // dynamic LDS), as the step kernel can be launched
   for (int resident : {0, 4, 5, 6}) {
-    const unsigned lds = resident ? (unsigned)((p.maxSharedMemoryPerMultiProcessor / resident + 511) & ~511ull) : 0u;
+    const unsigned lds = resident ? (unsigned)((p.maxSharedMemoryPerMultiProcessor / resident) & ~255ull)  /* round down: k blocks fit */ : 0u;
     std::vector<float> ms;
     for (int rep = 0; rep < 30; ++rep) {
       void *src = rep & 1 ? b : a, *dst = rep & 1 ? a : b;
@@ -242,7 +242,7 @@ int snake_mode(void *a, void *b, u64 universes, const hipDeviceProp_t &p) {
   hipEvent_t ev[41];
   for (auto &e : ev) CHECK(hipEventCreate(&e));
   for (int resident : {0, 6}) {
-    const unsigned lds = resident ? (unsigned)((p.maxSharedMemoryPerMultiProcessor / resident + 511) & ~511ull) : 0u;
+    const unsigned lds = resident ? (unsigned)((p.maxSharedMemoryPerMultiProcessor / resident) & ~255ull)  /* round down: k blocks fit */ : 0u;
     for (int snake : {0, 1, 0, 1}) {
       for (int rep = 0; rep < 10; ++rep)  // warm
         hipLaunchKernelGGL((k_copy_dir<4, MODE>), dim3(blocks), dim3(256), lds, 0, (const u32x2 *)(rep & 1 ? b : a),

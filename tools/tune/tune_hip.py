@@ -219,3 +219,35 @@ def step_contains_pair(states, wanted, unwanted, generations, cap_lo, cap_hi, fi
         states.data_ptr(), None if final is None else final.data_ptr(), wanted.data_ptr(), unwanted.data_ptr(),
         first.data_ptr(), n, generations, cap_lo, cap_hi, hip._stream(stream)))
     return first
+
+
+lib.lifeapi_tune_capped_occupancy.argtypes = [_int, _int, ctypes.POINTER(_int)]
+lib.lifeapi_tune_capped_occupancy.restype = _int
+
+
+def capped_occupancy(which: int, want: int) -> int:
+    """resident blocks per CU (occupancy API) of a shipped kernel under the
+    cap the product sets for `want`: which 0 = the streaming k_step, 1..6 =
+    k_stable<which-1>, 7 = k_stable_vulnerable"""
+    got = _int(0)
+    hip._check(lib.lifeapi_tune_capped_occupancy(which, want, ctypes.byref(got)))
+    return got.value
+
+
+lib.lifeapi_tune_order_probe.argtypes = [_vp, _vp, ctypes.c_uint64]
+lib.lifeapi_tune_order_probe.restype = _int
+
+
+def order_probe(d_in: int, d_out: int, nbytes: int) -> bool:
+    """the product's launch-order book: would a launch reading d_in and
+    writing d_out run in reverse?  (records d_out as such a launch does)"""
+    return bool(lib.lifeapi_tune_order_probe(d_in, d_out, nbytes))
+
+
+lib.lifeapi_tune_order_note.argtypes = [_vp, ctypes.c_uint64]
+lib.lifeapi_tune_order_note.restype = None
+
+
+def order_note(d_out: int, nbytes: int) -> None:
+    """record d_out (nbytes) in the product's order book as written forward"""
+    lib.lifeapi_tune_order_note(d_out, nbytes)

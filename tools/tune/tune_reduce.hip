@@ -146,22 +146,20 @@ int lifeapi_tune_reduce(int kind, const uint64_t *d_states, const uint64_t *d_w,
     return fail(LIFEAPI_E_INVALID, "bad argument to lifeapi_tune_reduce%s");
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
-  unsigned lds = 0;
-  if (blocks_per_cu < 0) {
-    rc = occupancy_lds(-blocks_per_cu, lds);
-    if (rc != LIFEAPI_OK) return rc;
-  }
   const dim3 grid(grid_for((n + upw - 1) / upw, cus, blocks_per_cu > 0 ? blocks_per_cu : 0));
   const hipStream_t st = (hipStream_t)stream;
+  unsigned lds = 0;
   if (kind == 0) {
     using Fn = void (*)(const uint64_t *, uint32_t *, uint64_t);
     Fn fn = upw == 2 ? (Fn)k_pop<2> : upw == 4 ? (Fn)k_pop<4> : upw == 8 ? (Fn)k_pop<8> : nullptr;
     if (!fn) return fail(LIFEAPI_E_INVALID, "universes per wave: 2, 4 or 8%s");
+    if (blocks_per_cu < 0 && (rc = occupancy_lds((const void *)fn, -blocks_per_cu, lds)) != LIFEAPI_OK) return rc;
     hipLaunchKernelGGL(fn, grid, dim3(kBlock), lds, st, d_states, (uint32_t *)d_out, (uint64_t)n);
   } else {
     using Fn = void (*)(const uint64_t *, const uint64_t *, const uint64_t *, uint8_t *, uint64_t);
     Fn fn = upw == 2 ? (Fn)k_contains<2> : upw == 4 ? (Fn)k_contains<4> : upw == 8 ? (Fn)k_contains<8> : nullptr;
     if (!fn) return fail(LIFEAPI_E_INVALID, "universes per wave: 2, 4 or 8%s");
+    if (blocks_per_cu < 0 && (rc = occupancy_lds((const void *)fn, -blocks_per_cu, lds)) != LIFEAPI_OK) return rc;
     hipLaunchKernelGGL(fn, grid, dim3(kBlock), lds, st, d_states, d_w, d_u, (uint8_t *)d_out, (uint64_t)n);
   }
   return launched("reduce (tuning) launch");

@@ -7,6 +7,7 @@
 #include "host.hpp"
 #include "stable_kernels.hpp"
 #include "stencil_kernels.hpp"
+#include "step_kernels.hpp"
 
 using namespace lifeapi_impl;
 
@@ -23,7 +24,8 @@ int lifeapi_tune_stable_pass(uint64_t *d_planes, uint8_t *d_flags, size_t n, int
   const Fn fns[6] = {k_stable<0>, k_stable<1>, k_stable<2>, k_stable<3>, k_stable<4>, k_stable<5>};
   // blocks_per_cu < 0: uncapped grid, at most -blocks_per_cu blocks resident
   // per CU (unused dynamic LDS out of the CU's 160 KiB)
-  const unsigned lds = blocks_per_cu < 0 ? ((160u << 10) / (unsigned)-blocks_per_cu + 511u) & ~511u : 0u;
+  unsigned lds = 0;
+  if (blocks_per_cu < 0 && (rc = occupancy_lds((const void *)fns[pass], -blocks_per_cu, lds)) != LIFEAPI_OK) return rc;
   hipLaunchKernelGGL(fns[pass], dim3(grid_for(n, cus, blocks_per_cu > 0 ? blocks_per_cu : 0)), dim3(kBlock), lds,
                      (hipStream_t)stream, d_planes, d_flags, (uint64_t)n, max_iters ? max_iters : 1u << 20,
                      reverse ? 1u : 0u);
@@ -37,7 +39,10 @@ int lifeapi_tune_stable_vulnerable(const uint64_t *d_planes, uint64_t *d_out, si
     return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_tune_stable_vulnerable%s");
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
-  const unsigned lds = blocks_per_cu < 0 ? ((160u << 10) / (unsigned)-blocks_per_cu + 511u) & ~511u : 0u;
+  unsigned lds = 0;
+  if (blocks_per_cu < 0 &&
+      (rc = occupancy_lds((const void *)k_stable_vulnerable, -blocks_per_cu, lds)) != LIFEAPI_OK)
+    return rc;
   hipLaunchKernelGGL(k_stable_vulnerable, dim3(grid_for(n, cus, blocks_per_cu > 0 ? blocks_per_cu : 0)),
                      dim3(kBlock), lds, (hipStream_t)stream, d_planes, d_out, (uint64_t)n);
   return launched("k_stable_vulnerable (tuning) launch");
@@ -56,7 +61,9 @@ int lifeapi_tune_stencil(int kind, const uint64_t *d_in, uint64_t *d_out, size_t
   if (rc != LIFEAPI_OK) return rc;
   unsigned lds = 0;
   if (resident) {
-    rc = occupancy_lds(resident, lds);
+    const void *fns[5] = {(const void *)k_counts<0>, (const void *)k_counts<1>, (const void *)k_counts<2>,
+                          (const void *)k_weld, (const void *)k_refined<1, 0>};
+    rc = occupancy_lds(fns[kind], resident, lds);
     if (rc != LIFEAPI_OK) return rc;
   }
   const dim3 grid(grid_for(n, cus, 0));
@@ -74,6 +81,32 @@ int lifeapi_tune_stencil(int kind, const uint64_t *d_in, uint64_t *d_out, size_t
   }
   return launched("stencil (tuning) launch");
 }
+
+/* resident blocks per CU of a shipped kernel under the occupancy cap
+ * occupancy_lds sets for `want` (which: 0 = the streaming k_step, 1..6 =
+ * k_stable<which-1>, 7 = k_stable_vulnerable): *got from the occupancy API */
+int lifeapi_tune_capped_occupancy(int which, int want, int *got) {
+  if (!got || which < 0 || which > 7 || want < 1) return fail(LIFEAPI_E_INVALID, "bad argument%s");
+  const void *fns[8] = {(const void *)k_step<XDPP, 4, true, 3, true>,
+                        (const void *)k_stable<0>, (const void *)k_stable<1>, (const void *)k_stable<2>,
+                        (const void *)k_stable<3>, (const void *)k_stable<4>, (const void *)k_stable<5>,
+                        (const void *)k_stable_vulnerable};
+  unsigned lds = 0;
+  int rc = occupancy_lds(fns[which], want, lds);
+  if (rc != LIFEAPI_OK) return rc;
+  const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(got, fns[which], kBlock, lds);
+  return e == hipSuccess ? LIFEAPI_OK : fail_hip(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor");
+}
+
+/* the product's launch-order book (host.hpp launch_reverse): 1 = a launch
+ * reading d_in (bytes) and writing d_out on the current device would take
+ * the reverse order; records d_out, as the product's launchers do        */
+int lifeapi_tune_order_probe(const void *d_in, const void *d_out, uint64_t bytes) {
+  return launch_reverse(d_in, d_out, bytes) ? 1 : 0;
+}
+
+/* the book's note_forward_write: d_out (bytes) recorded as written forward */
+void lifeapi_tune_order_note(const void *d_out, uint64_t bytes) { note_forward_write(d_out, bytes); }
 
 /* k_weld one generation in place, the order reversed if `reverse`, the
  * welds taken from position n - plain_welds on loaded and stored plain     */

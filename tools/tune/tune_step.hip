@@ -492,15 +492,15 @@ int lifeapi_tune_step_contains_nat(const uint64_t *d_in, uint64_t *d_final, cons
   if (rc != LIFEAPI_OK) return rc;
   unsigned lds = 0;
   const int cap = resident < 0 ? -resident : 0;  // resident < 0: a grid-stride grid of -resident blocks per CU
-  if (resident > 0) {
-    rc = occupancy_lds(resident, lds);
-    if (rc != LIFEAPI_OK) return rc;
-  }
   using Fn = void (*)(const uint64_t *, uint64_t *, const uint64_t *, const uint64_t *, uint32_t *, uint64_t, uint32_t,
                       uint64_t);
   Fn fn = upw == 1 ? (Fn)k_step_contains<1> : upw == 2 ? (Fn)k_step_contains<2> : upw == 4 ? (Fn)k_step_contains<4>
         : upw == 8 ? (Fn)k_step_contains<8> : nullptr;
   if (!fn) return fail(LIFEAPI_E_INVALID, "universes per wave: 1, 2, 4 or 8%s");
+  if (resident > 0) {
+    rc = occupancy_lds((const void *)fn, resident, lds);
+    if (rc != LIFEAPI_OK) return rc;
+  }
   // one order, nontemporal stores (the launch before the product's order policy)
   hipLaunchKernelGGL(fn, dim3(grid_for((n + upw - 1) / upw, cus, cap)), dim3(kBlock), lds, (hipStream_t)stream, d_in,
                      d_final, d_wanted, d_unwanted, d_first_gen, (uint64_t)n, generations, ~(uint64_t)0);
@@ -574,7 +574,7 @@ int lifeapi_tune_step_order(const uint64_t *d_in, uint64_t *d_out, size_t n, uin
   if (rc != LIFEAPI_OK) return rc;
   unsigned lds = 0;
   if (resident > 0) {
-    rc = occupancy_lds(resident, lds);
+    rc = occupancy_lds((const void *)fn, resident, lds);
     if (rc != LIFEAPI_OK) return rc;
   }
   const uint64_t groups = (n + upw - 1) / upw, plain = (plain_bytes + upw * 512 - 1) / (upw * 512);
@@ -633,7 +633,7 @@ int lifeapi_tune_step_batch_dev_cfg(const uint64_t *d_in, uint64_t *d_out, size_
   // per CU (unused dynamic LDS on top of the kernel's own)
   unsigned lds = 0;
   if (c.blocks_per_cu < 0) {
-    rc = occupancy_lds(-c.blocks_per_cu, lds);
+    rc = occupancy_lds((const void *)fn, -c.blocks_per_cu, lds);
     if (rc != LIFEAPI_OK) return rc;
   }
   hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), lds, (hipStream_t)stream, d_in, d_out,
