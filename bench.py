@@ -123,6 +123,13 @@ class HipRuntime:
         self.device = torch.device("cuda", local_rank % ndev)
         torch.cuda.set_device(self.device)
         self.stream = torch.cuda.current_stream(self.device)
+        self.neutral, self.neutral_error = None, None
+        try:  # the tuning build's streaming-step launcher (fixed order, explicit store policy)
+            sys.path.insert(0, os.path.join(ROOT, "tools", "tune"))
+            import tune_hip
+            self.neutral = tune_hip.step_order
+        except (ImportError, OSError) as e:
+            self.neutral_error = str(e)
 
     def sync(self):
         torch.cuda.synchronize(self.device)
@@ -166,6 +173,56 @@ def median_launch_ms(hip, rt, a, b, gens, reps=10):
         e1.synchronize()
         ms.append(e0.elapsed_time(e1))
     return sorted(ms)[len(ms) // 2], ms
+
+
+def pingpong_ms(rt, fn, a, b, reps=20, warm=5):
+    """per-launch ms of fn(src, dst) ping-ponged between a and b: `warm`
+    untimed launches, then `reps` launches each between a pair of events on
+    the rank's stream.  Returns (median, min, all)."""
+    bufs = [a, b]
+    for k in range(warm):
+        fn(bufs[k % 2], bufs[1 - k % 2])
+    ms = []
+    for k in range(reps):
+        e0, e1 = rt.event(), rt.event()
+        e0.record(rt.stream)
+        fn(bufs[(warm + k) % 2], bufs[1 - (warm + k) % 2])
+        e1.record(rt.stream)
+        e1.synchronize()
+        ms.append(e0.elapsed_time(e1))
+    return float(np.median(ms)), float(min(ms)), ms
+
+
+def neutral_fn(hip, rt, gens):
+    """The cache-neutral form of the shipped streaming launch: the same
+    kernel (k_step, 4 universes per wave, nontemporal loads) in ONE fixed
+    order with every store nontemporal, so no launch reads what the one
+    before it left in the 256 MB Infinity Cache (tools/tune step_order);
+    None without the tuning build."""
+    if rt.neutral is None:
+        return None
+
+    def fn(src, dst):
+        n = src.shape[0]
+        rt.neutral(src, dst, generations=gens, reverse=False, nts=True,
+                   resident=0 if n <= (1 << 22) else 5, upw=4, plain_bytes=0, stream=rt.stream)
+    return fn
+
+
+def stream_figures(hip, rt, a, b, gens, reps=20):
+    """Per-rank side measurements of the streaming launch on the rank's own
+    buffers, after the timed region: the cache-neutral step, and copy
+    ceilings of the same access shape -- the product kernel with 0
+    generations (the step's exact loads, stores, store policy and
+    batch-keyed order: a copy) and its cache-neutral form.  ms per launch."""
+    n = a.shape[0]
+    out = {"copy_ms": pingpong_ms(rt, lambda x, y: hip.step(x, out=y, generations=0, stream=rt.stream),
+                                  a, b, reps)[0]}
+    for key, g in (("neutral_ms", gens), ("copy_neutral_ms", 0)):
+        fn = neutral_fn(hip, rt, g)
+        out[key] = pingpong_ms(rt, fn, a, b, reps)[0] if fn is not None else None
+    out["bytes"] = n * BYTES_PER_UNIVERSE_GEN
+    return out
 
 
 def copy_ceiling(n: int):
@@ -354,6 +411,16 @@ def expected_digests(cfg: int, seed: int, gens: int, world: int, n_rank: int, n_
     return [None] * world, None, None
 
 
+def golden_digest(key: str):
+    """the reference-generated output digest of a full-size config
+    (tests/golden/golden.json, tests/golden/make_golden.py via oracle/_ref)"""
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "golden.json")) as f:
+            return json.load(f)["digests"][key]["output_digest"]
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def _i64(u: int) -> int:
     return u - (1 << 64) if u >= 1 << 63 else u
 
@@ -403,11 +470,14 @@ def secondary_config3(hip, rt, cpu_seconds=0.0):
     if cpu_seconds > 0:
         cpu = cpu_baseline_config3(a.cpu().numpy().view(np.uint64), cpu_seconds)
     achieved = gps * C3_SLOTS_PER_UNIVERSE_GEN
+    want = golden_digest("config3")
     return {"workload": "config3: 64K universes x 1024 generations (one launch)",
             "value": gps, "unit": "universe-gen/s", "cell_updates_per_s": gps * 4096,
             "kernel_ms": med, "kernel_ms_min": min(ms), "kernel_ms_all": ms,
             "kernel": hip.step_kernel_name(gens),
-            "output_digest": digest, "output_digest_expected": "76acdc1ac3d9fbc7",
+            "output_digest": digest, "output_digest_expected": want,
+            "verified": (digest == want) if want else None,
+            "verified_against": "tests/golden/golden.json digests.config3 (reference Step(1024) via oracle/_ref)",
             "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_SLOTS / 1e12,
                          "unit": "T wave64-VALU slots/s", "frac": achieved / VALU_PEAK_SLOTS,
                          "algorithmic_slots_per_universe_gen": C3_SLOTS_PER_UNIVERSE_GEN,
@@ -457,25 +527,40 @@ def config3_search_loop(hip, rt, a, step_ms):
             "verified": fd == gold["first_digest"] and hits == gold["hits"] and od == gold["output_digest"]}
 
 
-def secondary_config4_1gpu(hip, rt, steps=10):
+def secondary_config4_1gpu(hip, rt, steps=20, warm=20):
     """Config 4's fixed 16M-universe problem on ONE GPU: the same-problem
-    denominator of the 8-vs-1 strong-scaling ratio."""
+    denominator of the 8-vs-1 strong-scaling ratio.  Warmed like config 3
+    (`warm` back-to-back launches first, so the clock has settled), then
+    `steps` ping-pong launches timed one by one; min and median, and the
+    cache-neutral form (one fixed order, all stores nontemporal) and copy
+    ceilings at the same size, so the ratio can be read both ways."""
     n = 1 << 24
     a = hip.fill_random(n, seed=4, device=rt.device, stream=rt.stream)
     b = torch.empty_like(a)
     hip.step(a, out=b, generations=1, stream=rt.stream)
     digest = f"{batch_digest(hip.hashes(b, stream=rt.stream).cpu().numpy()):016x}"
-    med, ms = median_launch_ms(hip, rt, a, b, 1, reps=steps)
-    gps = n / (med / 1e3)
-    achieved = n * BYTES_PER_UNIVERSE_GEN / (med / 1e3) / 1e9
+    med, mn, ms = pingpong_ms(rt, lambda x, y: hip.step(x, out=y, generations=1, stream=rt.stream), b, a,
+                              reps=steps, warm=warm)
+    figs = stream_figures(hip, rt, a, b, 1, reps=steps)
     del a, b
     torch.cuda.empty_cache()
+    gb = lambda t: n * BYTES_PER_UNIVERSE_GEN / (t / 1e3) / 1e9 if t else None  # noqa: E731
+    spread = (max(ms) - min(ms)) / med
     return {"workload": "config4 on 1 GPU: 16777216 universes x 1 generation per launch",
-            "value": gps, "unit": "universe-gen/s", "kernel_ms_median": med, "kernel_ms_all": ms,
-            "output_digest": digest, "output_digest_expected": "3f1b0a5bcd971521",
-            "verified": digest == "3f1b0a5bcd971521",
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS}}
+            "value": n / (med / 1e3), "value_best": n / (mn / 1e3), "unit": "universe-gen/s",
+            "kernel_ms_median": med, "kernel_ms_min": mn, "kernel_ms_all": ms,
+            "kernel_ms_spread": spread, "flat_within_3pct": spread <= 0.03,
+            "timing": f"{warm} warm launches, then {steps} ping-pong launches, each between events on the stream",
+            "output_digest": digest, "output_digest_expected": golden_digest("config4"),
+            "verified": digest == golden_digest("config4"),
+            "roofline": {"bound": "hbm", "achieved": gb(med), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": gb(med) / HBM_PEAK_GBS,
+                         "cache_neutral": {"achieved": gb(figs["neutral_ms"]),
+                                           "frac": gb(figs["neutral_ms"]) / HBM_PEAK_GBS
+                                           if figs["neutral_ms"] else None,
+                                           "kernel_ms": figs["neutral_ms"]},
+                         "copy_ceiling_GBps": gb(figs["copy_ms"]),
+                         "copy_ceiling_cache_neutral_GBps": gb(figs["copy_neutral_ms"])}}
 
 
 def secondary_config5(hip, rt):
@@ -582,6 +667,18 @@ def main(argv=None):
     # result collection (not in the timed region): all-gather per-universe hashes
     h = hip.hashes(final, stream=rt.stream)
     rt.sync()
+    # side figures on the rank's own buffers (after the hashes: they overwrite
+    # both): cache-neutral step and live copy ceilings, gathered per rank
+    figs = stream_figures(hip, rt, final, bufs[1 - cur], gens) if gens <= 2 else None
+    fig_keys = ("neutral_ms", "copy_ms", "copy_neutral_ms")
+    fv = [(-1.0 if figs is None or figs[k] is None else figs[k]) for k in fig_keys]
+    if world > 1:
+        ft = torch.tensor(fv, dtype=torch.float64, device=COLL_DEV)
+        fparts = [torch.empty_like(ft) for _ in range(world)]
+        dist.all_gather(fparts, ft)
+        rank_figs = [[(None if x < 0 else float(x)) for x in fp.tolist()] for fp in fparts]
+    else:
+        rank_figs = [[(None if x < 0 else x) for x in fv]]
     collect = None
     if world > 1:
         dist.barrier()
@@ -621,6 +718,19 @@ def main(argv=None):
         achieved = bpl / (avg_launch / 1e3) / 1e9 if gens == 1 else None
         agg = sum(c * gens * BYTES_PER_UNIVERSE_GEN / (ms / 1e3) / 1e9 for ms, c in per_rank) if gens == 1 else None
         traffic, tsrc = load_pmc_traffic(n)
+
+        def gbps(ms, c):
+            return c * max(gens, 1) * BYTES_PER_UNIVERSE_GEN / (ms / 1e3) / 1e9 if ms else None
+
+        def copy_gbps(ms, c):
+            return c * BYTES_PER_UNIVERSE_GEN / (ms / 1e3) / 1e9 if ms else None
+
+        neu = [gbps(f[0], c) for f, (_, c) in zip(rank_figs, per_rank)]
+        cpy = [copy_gbps(f[1], c) for f, (_, c) in zip(rank_figs, per_rank)]
+        cpy_neu = [copy_gbps(f[2], c) for f, (_, c) in zip(rank_figs, per_rank)]
+        agg_neu = sum(neu) if all(v is not None for v in neu) else None
+        val_neu = (sum(c * gens / (f[0] / 1e3) for f, (_, c) in zip(rank_figs, per_rank))
+                   if all(f[0] for f in rank_figs) else None)
         line = {
             "metric": METRIC, "value": value, "unit": "universe-gen/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
@@ -637,11 +747,30 @@ def main(argv=None):
             "kernel_ms_avg": avg_launch,
             "kernel_timing": "HIP events on the launch stream around the K timed launches / K",
             "per_rank": [{"rank": r, "universes": c, "kernel_ms_avg": ms,
-                          "GBps": c * gens * BYTES_PER_UNIVERSE_GEN / (ms / 1e3) / 1e9 if gens == 1 else None}
+                          "GBps": c * gens * BYTES_PER_UNIVERSE_GEN / (ms / 1e3) / 1e9 if gens == 1 else None,
+                          "kernel_ms_cache_neutral": rank_figs[r][0], "GBps_cache_neutral": neu[r],
+                          "copy_GBps": cpy[r], "copy_GBps_cache_neutral": cpy_neu[r]}
                          for r, (ms, c) in enumerate(per_rank)],
+            "value_cache_neutral": val_neu,
+            "value_cache_neutral_note": ("universe-gen/s if every rank ran its shard at its cache-neutral rate "
+                                         "(the same kernel in one fixed order with all stores nontemporal, "
+                                         "timed per rank after the timed region): the 8-vs-1 ratio without "
+                                         "Infinity Cache reuse on either side"),
             "collective_world_size": coll_world,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                         "frac_kind": "effective: algorithmic bytes / launch time; with the batch-keyed "
+                                      "launch order and the plain-stored tail part of each launch's reads are "
+                                      "served by the 256 MB memory-side Infinity Cache (DESIGN.md 3.1, 5.2); "
+                                      "cache_neutral is the HBM-only figure",
+                         "cache_neutral": ({"achieved": neu[0], "frac": neu[0] / HBM_PEAK_GBS,
+                                            "kernel_ms": rank_figs[0][0],
+                                            "method": "same kernel, same size, same process, rank 0: one fixed "
+                                                      "group order, every store nontemporal, no plain-stored "
+                                                      "tail (tools/tune step_order), 20 ping-pong launches "
+                                                      "after 5 warm ones, median"}
+                                           if neu[0] else None),
+                         "cache_gain": (achieved / neu[0] - 1) if (achieved and neu[0]) else None,
                          "traffic": traffic, "traffic_source": tsrc,
                          "traffic_note": "FETCH_SIZE/WRITE_SIZE count L2-to-fabric bytes, so reads the "
                                          "memory-side Infinity Cache serves (the alternating launch order, "
@@ -649,9 +778,18 @@ def main(argv=None):
                          "algorithmic_bytes_per_launch": bpl,
                          "aggregate_GBps": agg,
                          "aggregate_frac": (agg / (world * HBM_PEAK_GBS)) if agg else None,
+                         "aggregate_GBps_cache_neutral": agg_neu,
+                         "aggregate_frac_cache_neutral": (agg_neu / (world * HBM_PEAK_GBS)) if agg_neu else None,
                          "read_only_GBps": achieved / 2 if achieved else None,
-                         "copy_ceiling_GBps": ceiling, "copy_ceiling_source": ceiling_src,
-                         "frac_of_copy_ceiling": (achieved / ceiling) if (achieved and ceiling) else None},
+                         "copy_ceiling_GBps": cpy[0],
+                         "copy_ceiling_source": "live, rank 0: the product step kernel with 0 generations "
+                                                "(a copy with the step's exact loads, stores, store policy and "
+                                                "batch-keyed order), 20 ping-pong launches, median",
+                         "frac_of_copy_ceiling": (achieved / cpy[0]) if (achieved and cpy[0]) else None,
+                         "copy_ceiling_cache_neutral_GBps": cpy_neu[0],
+                         "frac_of_copy_ceiling_cache_neutral": (neu[0] / cpy_neu[0])
+                         if (neu[0] and cpy_neu[0]) else None,
+                         "copy_ceiling_recorded_GBps": ceiling, "copy_ceiling_recorded_source": ceiling_src},
             "cpu_baseline": cpu,
             "verified": verified,
             "collect": collect,

@@ -36,6 +36,13 @@ class Runtime:
     def __init__(self, local_rank: int):
         self.device = torch.device("cpu")
         self.stream = None
+        self.neutral_error = None
+
+    @staticmethod
+    def neutral(states, out, generations=1, reverse=False, nts=True, resident=0, upw=4, plain_bytes=0,
+                stream=None):
+        """stand-in for the tuning build's fixed-order launcher (same result)"""
+        return step(states, out=out, generations=generations)
 
     def sync(self):
         pass

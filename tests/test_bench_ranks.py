@@ -54,6 +54,15 @@ def test_bench_gpus2_strong_config4_spawns_two_ranks():
     assert "config4_small" in v["against"]
     assert line["value"] > 0 and line["ms_per_step"] > 0
     assert "STUB" in line["kernel_backend"]
+    # per rank: the shipped figure and the cache-neutral one (same kernel,
+    # fixed order, all stores nontemporal), and live copy ceilings
+    for p in line["per_rank"]:
+        assert p["GBps"] > 0 and p["GBps_cache_neutral"] > 0
+        assert p["kernel_ms_cache_neutral"] > 0 and p["copy_GBps"] > 0 and p["copy_GBps_cache_neutral"] > 0
+    r = line["roofline"]
+    assert r["aggregate_GBps_cache_neutral"] > 0 and r["cache_neutral"]["achieved"] > 0
+    assert r["frac_kind"].startswith("effective") and r["copy_ceiling_GBps"] > 0
+    assert line["value_cache_neutral"] > 0
     # result collection: 1 warmup launch + (warmup-1) + steps generations in all
     c = line["collect"]
     assert c["universes_gathered"] == 1 << 14
@@ -83,6 +92,8 @@ def test_bench_gpus4_ragged_strong_split():
     P = Port()
     x = P.fill((1 << 14) + 4, seed=4)
     assert line["verified"]["global_digest"] == f"{batch_digest(P.hashes(P.step_batch(x, 1)).view(np.int64)):016x}"
+    assert len(line["per_rank"]) == 4 and all(p["GBps_cache_neutral"] > 0 for p in line["per_rank"])
+    assert line["roofline"]["aggregate_GBps_cache_neutral"] > 0
     assert line["collect"]["final_digest"] == _expected_collect((1 << 14) + 4, 4, 2)
 
 

@@ -52,6 +52,13 @@ __global__ __launch_bounds__(kBlock) void k_diag(const uint64_t *in, uint64_t *o
   if constexpr (CUT == 6) diag_half_read(r, gens, self, prev, next);
   if constexpr (CUT == 7) diag_no_write(r, gens, self, prev, next);
   if constexpr (CUT == 8) diag_no_read(r, gens, self, prev, next);
+  if constexpr (CUT == 9) diag_b64(r, gens, self, prev, next);
+  if constexpr (CUT == 10) diag_prio1(r, gens, self, prev, next);
+  if constexpr (CUT == 11) diag_prio_e(r, gens, self, prev, next);
+  if constexpr (CUT == 12) {  // odd blocks one priority class higher (static, guide "Two waves per SIMD" item 4)
+    if (blockIdx.x & 1) diag_hi(r, gens, self, prev, next);
+    else diag_full(r, gens, self, prev, next);
+  }
   const uint64_t t1 = __builtin_amdgcn_s_memtime(), q1 = __builtin_amdgcn_s_memrealtime();
   Split<S>::store(r, c);
 #pragma unroll
@@ -75,7 +82,9 @@ struct Cut {
 };
 const Cut kCuts[] = {{"full", k_diag<0>, 4},      {"nolds", k_diag<1>, 4},      {"norot", k_diag<2>, 4},
                      {"valu_only", k_diag<3>, 4}, {"lds_only", k_diag<4>, 4},   {"half_write", k_diag<5>, 4},
-                     {"half_read", k_diag<6>, 4}, {"no_write", k_diag<7>, 4},   {"no_read", k_diag<8>, 4}};
+                     {"half_read", k_diag<6>, 4}, {"no_write", k_diag<7>, 4},   {"no_read", k_diag<8>, 4},
+                     {"b64", k_diag<9>, 4},       {"prio1", k_diag<10>, 4},     {"prio_e", k_diag<11>, 4},
+                     {"odd_blocks_hi", k_diag<12>, 4}};
 constexpr int kNCuts = sizeof(kCuts) / sizeof(kCuts[0]);
 
 struct Run {
