@@ -207,6 +207,9 @@ __device__ __forceinline__ uint32_t life_tail(uint32_t h0u, uint32_t h0, uint32_
   else return life_tail7(h0u, h0, h0d, h1u, h1, h1d, a);
 }
 
+// two adjacent 64-bit words: the unit of a 16-byte (dwordx4) access
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+
 template <bool NT>
 __device__ __forceinline__ W ld(const uint64_t *p) {
   if constexpr (NT) return split(__builtin_nontemporal_load(p));

@@ -37,6 +37,7 @@ bool launch_reverse(const void *d_in, const void *d_out, uint64_t bytes);
 // alternate (so a stale entry for that range cannot reverse a later reader).
 void note_forward_write(const void *d_out, uint64_t bytes);
 bool aligned8(const void *p);
+inline bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
 // n universes in / out: non-null, 8-byte aligned, equal or disjoint
 int check_batch(const void *in, const void *out, size_t n);
 // blocks for `waves_needed` waves, capped at cus * blocks_per_cu (0 = no cap)

@@ -57,6 +57,20 @@ __global__ __launch_bounds__(kBlock) void k_fill(uint64_t *__restrict__ out, uin
   }
 }
 
+// the same words with 16-byte stores: two consecutive words per lane
+__global__ __launch_bounds__(kBlock) void k_fill16(uint64_t *__restrict__ out, uint64_t nwords, uint64_t seed,
+                                                   uint64_t first_word, int mode) {
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock * 2;
+  for (uint64_t i = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) * 2; i < nwords; i += stride) {
+    uint64_t v0 = mix64(seed + (first_word + i + 1) * kGolden), v1 = mix64(seed + (first_word + i + 2) * kGolden);
+    if (mode == 1) {
+      v0 = (v0 & ((1ULL << 61) - 1)) | (1ULL << 61);
+      v1 = (v1 & ((1ULL << 61) - 1)) | (1ULL << 61);
+    }
+    __builtin_nontemporal_store(u64x2{v0, v1}, reinterpret_cast<u64x2 *>(out + i));
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -67,8 +81,17 @@ int lifeapi_pop_batch_dev(const uint64_t *d_states, uint32_t *d_pop, size_t n, v
     return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_pop_batch_dev%s");
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
-  hipLaunchKernelGGL(k_pop<kRedU>, dim3(grid_for((n + kRedU - 1) / kRedU, cus, kRedBlocksPerCU)), dim3(kBlock), 0,
-                     (hipStream_t)stream, d_states, d_pop, (uint64_t)n);
+  // 16-byte loads (two universes per wave-instruction), 8 universes per
+  // wave, one-shot grid: 0.0820 ms on 1M against 0.0918 for the 8-byte
+  // k_pop<4> on the 32-blocks-per-CU grid, same process (tools/rows_ab.py,
+  // profiles/r03/rows_ab.jsonl); batches that are only 8-byte aligned keep
+  // the 8-byte kernel
+  if (aligned16(d_states))
+    hipLaunchKernelGGL(k_pop16<8>, dim3(grid_for((n + 7) / 8, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream,
+                       d_states, d_pop, (uint64_t)n);
+  else
+    hipLaunchKernelGGL(k_pop<kRedU>, dim3(grid_for((n + kRedU - 1) / kRedU, cus, kRedBlocksPerCU)), dim3(kBlock),
+                       0, (hipStream_t)stream, d_states, d_pop, (uint64_t)n);
   return launched("k_pop launch");
 }
 
@@ -92,11 +115,17 @@ int lifeapi_contains_batch_dev(const uint64_t *d_states, const uint64_t *d_wante
     return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_contains_batch_dev%s");
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
-  // 8 universes per wave, one-shot grid: 0.0867 ms on 1M against 0.0892 for
-  // 4 per wave on the capped grid (tools/reduce_ab.py, profiles/r02/reduce_ab.jsonl;
-  // GetPop keeps 4 on the capped grid, which measured best for it)
-  hipLaunchKernelGGL(k_contains<8>, dim3(grid_for((n + 7) / 8, cus, 0)), dim3(kBlock), 0,
-                     (hipStream_t)stream, d_states, d_wanted, d_unwanted, d_out, (uint64_t)n);
+  // 8 universes per wave, one-shot grid (0.0867 ms on 1M against 0.0892 for
+  // 4 per wave on the capped grid, profiles/r02/reduce_ab.jsonl), with
+  // 16-byte loads: 0.0827 against 0.0884 for 8-byte ones, same process
+  // (tools/rows_ab.py, profiles/r03/rows_ab.jsonl); 8-byte-aligned batches
+  // keep the 8-byte kernel
+  if (aligned16(d_states))
+    hipLaunchKernelGGL(k_contains16<8>, dim3(grid_for((n + 7) / 8, cus, 0)), dim3(kBlock), 0,
+                       (hipStream_t)stream, d_states, d_wanted, d_unwanted, d_out, (uint64_t)n);
+  else
+    hipLaunchKernelGGL(k_contains<8>, dim3(grid_for((n + 7) / 8, cus, 0)), dim3(kBlock), 0,
+                       (hipStream_t)stream, d_states, d_wanted, d_unwanted, d_out, (uint64_t)n);
   return launched("k_contains launch");
 }
 
@@ -108,8 +137,14 @@ int lifeapi_fill_random_dev(uint64_t *d_out, size_t n, uint64_t seed, uint64_t f
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
   const uint64_t words = (uint64_t)n * kWave;
-  hipLaunchKernelGGL(k_fill, dim3(grid_for(words / kWave, cus, 0)), dim3(kBlock), 0,
-                     (hipStream_t)stream, d_out, words, seed, first_universe * kWave, mode);
+  // 16-byte stores (two words per lane): 0.0836 ms on 1M against 0.0862 for
+  // 8-byte ones (tools/rows_ab.py, profiles/r03/rows_ab.jsonl)
+  if (aligned16(d_out))
+    hipLaunchKernelGGL(k_fill16, dim3(grid_for(words / (2 * kWave), cus, 0)), dim3(kBlock), 0,
+                       (hipStream_t)stream, d_out, words, seed, first_universe * kWave, mode);
+  else
+    hipLaunchKernelGGL(k_fill, dim3(grid_for(words / kWave, cus, 0)), dim3(kBlock), 0,
+                       (hipStream_t)stream, d_out, words, seed, first_universe * kWave, mode);
   return launched("k_fill launch");
 }
 

@@ -65,5 +65,73 @@ __global__ __launch_bounds__(kBlock) void k_contains(const uint64_t *__restrict_
   }
 }
 
+// The same two reductions with 16-byte loads: lane l reads words 2(l%32),
+// 2(l%32)+1 of universe u0 + 2k + l/32 (one dwordx4 per lane = two universes
+// per wave-instruction, against one with lane = column), so half the load
+// instructions move the same bytes.  U (even) universes per wave.
+
+template <int U>
+__global__ __launch_bounds__(kBlock) void k_pop16(const uint64_t *__restrict__ s,
+                                                  uint32_t *__restrict__ pop, uint64_t n) {
+  static_assert(U % 2 == 0, "universes come in pairs");
+  const int lane = threadIdx.x & (kWave - 1);
+  const int half = lane >> 5, col = (lane & 31) * 2;
+  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock * U;
+  for (uint64_t u0 = ((uint64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave) * U; u0 < n;
+       u0 += stride) {
+    uint32_t c[U / 2];
+#pragma unroll
+    for (int k = 0; k < U / 2; ++k) {
+      const uint64_t u = u0 + 2 * k + half;
+      if (u < n) {
+        const u64x2 v = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(s + u * kWave + col));
+        c[k] = (uint32_t)(__popcll(v[0]) + __popcll(v[1])) << (16 * half);
+      } else {
+        c[k] = 0u;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < U / 2; ++k) {
+      const uint32_t t = wave_sum_u32_dpp(c[k]);  // universe 2k in the low half, 2k+1 in the high
+      if (lane == 0) {
+        if (u0 + 2 * k < n) pop[u0 + 2 * k] = t & 0xFFFF;
+        if (u0 + 2 * k + 1 < n) pop[u0 + 2 * k + 1] = t >> 16;
+      }
+    }
+  }
+}
+
+template <int U>
+__global__ __launch_bounds__(kBlock) void k_contains16(const uint64_t *__restrict__ s,
+                                                       const uint64_t *__restrict__ wanted,
+                                                       const uint64_t *__restrict__ unwanted,
+                                                       uint8_t *__restrict__ out, uint64_t n) {
+  static_assert(U % 2 == 0, "universes come in pairs");
+  const int lane = threadIdx.x & (kWave - 1);
+  const int half = lane >> 5, col = (lane & 31) * 2;
+  const uint64_t w0 = wanted[col], w1 = wanted[col + 1];
+  const uint64_t m0 = w0 | unwanted[col], m1 = w1 | unwanted[col + 1];
+  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock * U;
+  for (uint64_t u0 = ((uint64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave) * U; u0 < n;
+       u0 += stride) {
+    u64x2 v[U / 2];
+#pragma unroll
+    for (int k = 0; k < U / 2; ++k) {
+      const uint64_t u = u0 + 2 * k + half;
+      v[k] = u < n ? __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(s + u * kWave + col))
+                   : u64x2{w0, w1};
+    }
+#pragma unroll
+    for (int k = 0; k < U / 2; ++k) {
+      const uint64_t d = ((v[k][0] ^ w0) & m0) | ((v[k][1] ^ w1) & m1);
+      const uint64_t bad = __ballot(d != 0ull);  // lanes 0-31: universe 2k, 32-63: 2k+1
+      if (lane == 0) {
+        if (u0 + 2 * k < n) out[u0 + 2 * k] = (uint32_t)bad == 0u ? 1 : 0;
+        if (u0 + 2 * k + 1 < n) out[u0 + 2 * k + 1] = (uint32_t)(bad >> 32) == 0u ? 1 : 0;
+      }
+    }
+  }
+}
+
 }  // namespace
 }  // namespace lifeapi_impl

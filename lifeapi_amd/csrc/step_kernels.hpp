@@ -228,23 +228,48 @@ __global__ __launch_bounds__(kBlock) void k_step_split(const uint64_t *in, uint6
 // universes before it stores them, and no wave touches another's universes.
 // Group order (kReverse in `gens`) and the plain-stored tail of the final
 // states (`plain_from`) as k_step's.
-template <int U>
+template <int U, bool WIDE = false>
 __global__ __launch_bounds__(kBlock) void k_step_contains(const uint64_t *in, uint64_t *fin,
                                                           const uint64_t *__restrict__ wanted,
                                                           const uint64_t *__restrict__ unwanted,
                                                           uint32_t *__restrict__ first,
                                                           uint64_t n, uint32_t gens, uint64_t plain_from) {
+  // WIDE: the states move as 16-byte accesses (two adjacent columns per
+  // lane, two universes per wave-instruction) staged through the wave's own
+  // U x 512 B of LDS, which turns them into lane = column (and back for the
+  // final states); the batch must be 16-byte aligned
+  __shared__ uint64_t stage[WIDE ? kWavesPerBlock * U * kWave : 1];
   const int lane = threadIdx.x & (kWave - 1);
   const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const W w = split(wanted[lane]), uw = split(unwanted[lane]);
   const bool rev = (gens & kReverse) != 0;
   gens &= ~kReverse;
   const uint64_t groups = (n + U - 1) / U, wstride = (uint64_t)gridDim.x * kWavesPerBlock;
+  uint64_t *st_w = stage + (WIDE ? wib * U * kWave : 0);
+  const int half = lane >> 5, col = (lane & 31) * 2;
   for (uint64_t grp = (uint64_t)blockIdx.x * kWavesPerBlock + wib; grp < groups; grp += wstride) {
     const uint64_t u0 = (rev ? groups - 1 - grp : grp) * U;
     W a[U];
+    if constexpr (WIDE) {
+      static_assert(U % 2 == 0, "universes come in pairs");
+      u64x2 v[U / 2];
 #pragma unroll
-    for (int k = 0; k < U; ++k) a[k] = (u0 + k < n) ? ld<true>(in + (u0 + k) * kWave + lane) : W{0u, 0u};
+      for (int k = 0; k < U / 2; ++k) {
+        const uint64_t u = u0 + 2 * k + half;
+        v[k] = u < n ? __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(in + u * kWave + col))
+                     : u64x2{0ull, 0ull};
+      }
+#pragma unroll
+      for (int k = 0; k < U / 2; ++k)
+        *reinterpret_cast<u64x2 *>(st_w + (2 * k + half) * kWave + col) = v[k];
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int k = 0; k < U; ++k) a[k] = split(st_w[k * kWave + lane]);
+      __builtin_amdgcn_wave_barrier();  // (the final states reuse the stage below)
+    } else {
+#pragma unroll
+      for (int k = 0; k < U; ++k) a[k] = (u0 + k < n) ? ld<true>(in + (u0 + k) * kWave + lane) : W{0u, 0u};
+    }
     uint32_t hit[U];
 #pragma unroll
     for (int k = 0; k < U; ++k) hit[k] = 0;
@@ -255,7 +280,25 @@ __global__ __launch_bounds__(kBlock) void k_step_contains(const uint64_t *in, ui
         if (hit[k] == 0 && wave_contains(a[k], w, uw)) hit[k] = g;
       }
     }
-    if (fin && grp < plain_from) {
+    if constexpr (WIDE) {
+      if (fin) {
+#pragma unroll
+        for (int k = 0; k < U; ++k) st_w[k * kWave + lane] = join(a[k]);
+        __builtin_amdgcn_wave_barrier();
+        const bool nt = grp < plain_from;
+#pragma unroll
+        for (int k = 0; k < U / 2; ++k) {
+          const uint64_t u = u0 + 2 * k + half;
+          const u64x2 v = *reinterpret_cast<const u64x2 *>(st_w + (2 * k + half) * kWave + col);
+          u64x2 *dst = reinterpret_cast<u64x2 *>(fin + u * kWave + col);
+          if (u < n) {
+            if (nt) __builtin_nontemporal_store(v, dst);
+            else *dst = v;
+          }
+        }
+        __builtin_amdgcn_wave_barrier();  // (the next group's loads reuse the stage)
+      }
+    } else if (fin && grp < plain_from) {
 #pragma unroll
       for (int k = 0; k < U; ++k)
         if (u0 + k < n) st<true>(fin + (u0 + k) * kWave + lane, a[k]);

@@ -143,6 +143,35 @@ def test_contains(hip, port):
     assert (got.astype(bool) == want).all() and want[:100].all() and not want[100:200].any()
 
 
+def _off8(a: np.ndarray) -> torch.Tensor:
+    """a on the device at an address that is 8 mod 16 (8-byte aligned only)"""
+    t = torch.zeros(a.size + 1, dtype=torch.int64, device="cuda")
+    v = t[1:].view(a.shape)
+    v.copy_(to_dev(a))
+    assert v.data_ptr() % 16 == 8
+    return v
+
+
+@pytest.mark.parametrize("n", [1, 7, 4099])
+def test_reductions_on_8_byte_aligned_batches(hip, port, n):
+    """GetPop, Contains and the fill take 16-byte accesses on 16-byte
+    aligned batches (reduce.hip) and fall back to 8-byte ones otherwise;
+    both equal the oracle, ragged n included"""
+    x = port.fill(n, seed=n + 900)
+    w, u = x[0].copy(), np.zeros(64, np.uint64)
+    u[5] = np.uint64(0xFF)
+    u &= ~w
+    want_c = np.array([port.contains(x[k], w, u) for k in range(n)])
+    for d in (to_dev(x), _off8(x)):
+        assert (hip.pop(d).cpu().numpy().astype(np.uint32) == port.pop(x)).all()
+        got = hip.contains(d, to_dev(w[None]), to_dev(u[None])).cpu().numpy().astype(bool)
+        assert (got == want_c).all() and got[0]
+    out = _off8(np.zeros((n, 64), np.uint64))
+    for mode in (0, 1):
+        hip.fill_random(n, seed=3, first_universe=77, mode=mode, out=out)
+        assert (to_host(out) == port.fill(n, 3, 77, mode)).all()
+
+
 def test_step_contains(hip, port):
     # blinkers: contained every second generation
     b = np.zeros(64, np.uint64)
@@ -516,6 +545,30 @@ def test_stable_passes_vs_oracle(hip, port):
         exp = port.stable_vulnerable(planes)
         assert (to_host(got) == exp).all()
     assert exp.any()
+
+
+@pytest.mark.parametrize("density", [0.2, 0.5, 0.8])
+def test_stable_step_and_propagate_dense_counts(hip, port, density):
+    """PropagateStep counts the state once and derives NeighbourCount(state |
+    unknown) as 9 - NeighbourCount(~(state | unknown)) (stable_kernels.hpp
+    StableCounts): random state / unknown planes of every density, so the
+    counts cover 0..9, and options mostly open, against the oracle's
+    four-count restatement of LifeStable.hpp:526-729"""
+    rng = np.random.default_rng(int(density * 100))
+    n = 512
+    bits = lambda p: np.packbits(rng.random((n, 64, 64)) < p, axis=2, bitorder="little").view(np.uint64)[..., 0]  # noqa: E731
+    x = np.zeros((n, 10, 64), np.uint64)
+    x[:, 0] = bits(density)
+    x[:, 1] = bits(density) & ~x[:, 0]
+    for k in range(2, 10):
+        x[:, k] = bits(0.1)
+    x = x.reshape(n, 640)
+    for w, name in ((3, "step"), (4, "propagate")):
+        d = to_dev(x).reshape(n, 640)
+        fl = hip.stable_pass(d, name).cpu().numpy()
+        want, wfl = port.stable_pass(x, w)
+        assert (d.cpu().numpy().view(np.uint64) == want).all(), name
+        assert (fl == wfl).all(), name
 
 
 def test_stable_vulnerable_golden_gpu(hip):

@@ -251,3 +251,15 @@ lib.lifeapi_tune_order_note.restype = None
 def order_note(d_out: int, nbytes: int) -> None:
     """record d_out (nbytes) in the product's order book as written forward"""
     lib.lifeapi_tune_order_note(d_out, nbytes)
+
+
+lib.lifeapi_tune_fill16.argtypes = [_vp, _sz, ctypes.c_uint64, ctypes.c_uint64, _int, _int, _vp]
+lib.lifeapi_tune_fill16.restype = _int
+
+
+def fill16(out: torch.Tensor, seed: int, first_universe: int = 0, mode: int = 0, blocks_per_cu: int = 0,
+           stream=None) -> torch.Tensor:
+    """the seeded fill with 16-byte stores into out (n, 64)"""
+    hip._check(lib.lifeapi_tune_fill16(out.data_ptr(), hip._universes(out), seed, first_universe, mode,
+                                       blocks_per_cu, hip._stream(stream)))
+    return out

@@ -40,7 +40,6 @@ __global__ __launch_bounds__(kBlock) void k_hash_lanecol(const uint64_t *__restr
   }
 }
 
-typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
 // lane = universe: 64 universes per wave, each lane streams its own 512 B
 template <bool NT>
@@ -95,9 +94,40 @@ __global__ __launch_bounds__(kBlock) void k_hash_lds(const uint64_t *__restrict_
   }
 }
 
+// the seeded fill with 16-byte stores: two consecutive words per lane
+__global__ __launch_bounds__(kBlock) void k_fill16(uint64_t *__restrict__ out, uint64_t nwords, uint64_t seed,
+                                                   uint64_t first_word, int mode) {
+  typedef uint64_t u64x2v __attribute__((ext_vector_type(2)));
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock * 2;
+  for (uint64_t i = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) * 2; i < nwords; i += stride) {
+    uint64_t v0 = mix64(seed + (first_word + i + 1) * kGolden), v1 = mix64(seed + (first_word + i + 2) * kGolden);
+    if (mode == 1) {
+      v0 = (v0 & ((1ULL << 61) - 1)) | (1ULL << 61);
+      v1 = (v1 & ((1ULL << 61) - 1)) | (1ULL << 61);
+    }
+    __builtin_nontemporal_store(u64x2v{v0, v1}, reinterpret_cast<u64x2v *>(out + i));
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+/* the seeded fill (lifeapi_fill_random_dev's definition) with 16-byte
+ * stores; grid of one block per 512 words, capped at blocks_per_cu if > 0 */
+int lifeapi_tune_fill16(uint64_t *d_out, size_t n, uint64_t seed, uint64_t first_universe, int mode,
+                        int blocks_per_cu, void *stream) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!d_out || ((uintptr_t)d_out & 15u) || (mode != 0 && mode != 1))
+    return fail(LIFEAPI_E_INVALID, "bad argument to lifeapi_tune_fill16%s");
+  int cus = 0, rc = device_cus(cus);
+  if (rc != LIFEAPI_OK) return rc;
+  const uint64_t words = (uint64_t)n * kWave;
+  hipLaunchKernelGGL(k_fill16, dim3(grid_for(words / (2 * kWave), cus, blocks_per_cu)), dim3(kBlock), 0,
+                     (hipStream_t)stream, d_out, words, seed, first_universe * kWave, mode);
+  return launched("k_fill16 launch");
+}
+
 
 int lifeapi_tune_hash(const uint64_t *d_states, uint64_t *d_hash, size_t n, int variant, int blocks_per_cu,
                       void *stream) {
@@ -142,22 +172,27 @@ int lifeapi_tune_hash(const uint64_t *d_states, uint64_t *d_hash, size_t n, int 
 int lifeapi_tune_reduce(int kind, const uint64_t *d_states, const uint64_t *d_w, const uint64_t *d_u, void *d_out,
                         size_t n, int upw, int blocks_per_cu, void *stream) {
   if (n == 0) return LIFEAPI_OK;
-  if (!d_states || !d_out || (kind == 1 && (!d_w || !d_u)) || kind < 0 || kind > 1)
+  if (!d_states || !d_out || ((kind & 1) && (!d_w || !d_u)) || kind < 0 || kind > 3)
     return fail(LIFEAPI_E_INVALID, "bad argument to lifeapi_tune_reduce%s");
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
   const dim3 grid(grid_for((n + upw - 1) / upw, cus, blocks_per_cu > 0 ? blocks_per_cu : 0));
   const hipStream_t st = (hipStream_t)stream;
   unsigned lds = 0;
-  if (kind == 0) {
+  if (kind == 0 || kind == 2) {
     using Fn = void (*)(const uint64_t *, uint32_t *, uint64_t);
-    Fn fn = upw == 2 ? (Fn)k_pop<2> : upw == 4 ? (Fn)k_pop<4> : upw == 8 ? (Fn)k_pop<8> : nullptr;
+    Fn fn = kind == 2 ? (upw == 2 ? (Fn)k_pop16<2> : upw == 4 ? (Fn)k_pop16<4> : upw == 8 ? (Fn)k_pop16<8> : nullptr)
+                      : (upw == 2 ? (Fn)k_pop<2> : upw == 4 ? (Fn)k_pop<4> : upw == 8 ? (Fn)k_pop<8> : nullptr);
     if (!fn) return fail(LIFEAPI_E_INVALID, "universes per wave: 2, 4 or 8%s");
     if (blocks_per_cu < 0 && (rc = occupancy_lds((const void *)fn, -blocks_per_cu, lds)) != LIFEAPI_OK) return rc;
     hipLaunchKernelGGL(fn, grid, dim3(kBlock), lds, st, d_states, (uint32_t *)d_out, (uint64_t)n);
   } else {
     using Fn = void (*)(const uint64_t *, const uint64_t *, const uint64_t *, uint8_t *, uint64_t);
-    Fn fn = upw == 2 ? (Fn)k_contains<2> : upw == 4 ? (Fn)k_contains<4> : upw == 8 ? (Fn)k_contains<8> : nullptr;
+    Fn fn = kind == 3
+                ? (upw == 2 ? (Fn)k_contains16<2> : upw == 4 ? (Fn)k_contains16<4> : upw == 8 ? (Fn)k_contains16<8>
+                                                                                          : nullptr)
+                : (upw == 2 ? (Fn)k_contains<2> : upw == 4 ? (Fn)k_contains<4> : upw == 8 ? (Fn)k_contains<8>
+                                                                                    : nullptr);
     if (!fn) return fail(LIFEAPI_E_INVALID, "universes per wave: 2, 4 or 8%s");
     if (blocks_per_cu < 0 && (rc = occupancy_lds((const void *)fn, -blocks_per_cu, lds)) != LIFEAPI_OK) return rc;
     hipLaunchKernelGGL(fn, grid, dim3(kBlock), lds, st, d_states, d_w, d_u, (uint8_t *)d_out, (uint64_t)n);

@@ -135,7 +135,6 @@ __global__ __launch_bounds__(kBlock) void k_step_asm4(const uint64_t *__restrict
 // k_step for the tile layouts (gen_tile): a wave holds C groups of P = S/2
 // universes, lane i of group g columns C*i .. C*i+C-1 of each (C*8
 // contiguous bytes per universe: two dwordx4 loads for C = 4).
-typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 template <bool NT>
 __device__ __forceinline__ u64x2 ld2(const uint64_t *p) {
   if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(p));
@@ -494,9 +493,14 @@ int lifeapi_tune_step_contains_nat(const uint64_t *d_in, uint64_t *d_final, cons
   const int cap = resident < 0 ? -resident : 0;  // resident < 0: a grid-stride grid of -resident blocks per CU
   using Fn = void (*)(const uint64_t *, uint64_t *, const uint64_t *, const uint64_t *, uint32_t *, uint64_t, uint32_t,
                       uint64_t);
+  // upw 16 + U: the 16-byte staged form (k_step_contains<U, true>), U = 2, 4, 8
   Fn fn = upw == 1 ? (Fn)k_step_contains<1> : upw == 2 ? (Fn)k_step_contains<2> : upw == 4 ? (Fn)k_step_contains<4>
-        : upw == 8 ? (Fn)k_step_contains<8> : nullptr;
-  if (!fn) return fail(LIFEAPI_E_INVALID, "universes per wave: 1, 2, 4 or 8%s");
+        : upw == 8 ? (Fn)k_step_contains<8> : upw == 18 ? (Fn)k_step_contains<2, true>
+        : upw == 20 ? (Fn)k_step_contains<4, true> : upw == 24 ? (Fn)k_step_contains<8, true> : nullptr;
+  if (!fn) return fail(LIFEAPI_E_INVALID, "universes per wave: 1, 2, 4 or 8 (16 + 2, 4, 8: 16-byte form)%s");
+  if (upw > 16 && (((uintptr_t)d_in | (uintptr_t)d_final) & 15u))
+    return fail(LIFEAPI_E_INVALID, "the 16-byte form needs 16-byte aligned batches%s");
+  upw &= 15;
   if (resident > 0) {
     rc = occupancy_lds((const void *)fn, resident, lds);
     if (rc != LIFEAPI_OK) return rc;
