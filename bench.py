@@ -205,7 +205,7 @@ def neutral_fn(hip, rt, gens):
     def fn(src, dst):
         n = src.shape[0]
         rt.neutral(src, dst, generations=gens, reverse=False, nts=True,
-                   resident=0 if n <= (1 << 22) else 5, upw=4, plain_bytes=0, stream=rt.stream)
+                   resident=0 if n <= (1 << 22) else 7, upw=4, plain_bytes=0, stream=rt.stream)
     return fn
 
 

@@ -15,6 +15,15 @@ extern "C" {
 // LifeStable kernels: one wave per LifeStable, at most this many blocks (of
 // kWavesPerBlock waves) resident per CU (see lifeapi_stable_pass_batch_dev)
 constexpr int kStableResidentBlocks = 4;
+// per pass (sync, options, signal, step, propagate, stabilise): 0 = every
+// slot.  Round 3, exact caps, 1M LifeStables of three families, same process
+// (tools/stable_grid_ab.py, profiles/r03/stable_caps_1m.jsonl): the single
+// passes 2-5 % faster with 3 resident blocks than with 4 (sync 1.79-1.81
+// against 1.86 ms, signal 1.80-1.82 against 1.83-1.87); Propagate keeps
+// every slot (3 blocks: +25 % on still lifes; 4-6 within 3 % of it) and
+// StabiliseOptions 4 (3 and 4 within 1 %).  Round 2's "3" had been 2 (its
+// LDS share was rounded up).
+constexpr int kStablePassResident[6] = {3, 3, 3, 3, 0, kStableResidentBlocks};
 
 static int counts_launch(const uint64_t *d_in, uint64_t *d_out, size_t n, int mode, void *stream) {
   if (n == 0) return LIFEAPI_OK;
@@ -48,8 +57,9 @@ int lifeapi_stable_pass_batch_dev(uint64_t *d_planes, uint8_t *d_flags, size_t n
   // around an unknown window with fresh options -- the state a search
   // propagates from --, sparse soups and random planes, 64K and 1M
   // LifeStables; profiles/r02/stable_occupancy_*.jsonl): one wave per
-  // LifeStable with at most 4 blocks resident per CU, set by unused dynamic
-  // LDS, for every pass but Propagate (below).  Every pass reads and writes its 5 KiB in place; fewer concurrent
+  // LifeStable with at most kStablePassResident[pass] blocks resident per
+  // CU (round 3's exact caps, above), set by unused dynamic LDS; round 2's
+  // measurements below were of 4 (and its "3" of 2).  Every pass reads and writes its 5 KiB in place; fewer concurrent
   // streams per CU serve that better (the in-place copy of the same shape,
   // build/membw inplace: 5.73 TB/s uncapped, 5.87 at 2 blocks per CU).  At
   // 1M: 5-10 % faster than one wave per LifeStable unlimited or a
@@ -61,8 +71,8 @@ int lifeapi_stable_pass_batch_dev(uint64_t *d_planes, uint8_t *d_flags, size_t n
   // resident: +1.4 % on still lifes at 1M, and 8 % slower on tools/rows_bench.py's
   // random planes, whose fixpoints take more steps).
   unsigned lds = 0;
-  if (pass != 4) {
-    rc = occupancy_lds(reinterpret_cast<const void *>(fns[pass]), kStableResidentBlocks, lds);
+  if (kStablePassResident[pass]) {
+    rc = occupancy_lds(reinterpret_cast<const void *>(fns[pass]), kStablePassResident[pass], lds);
     if (rc != LIFEAPI_OK) return rc;
   }
   // One order: alternating it, as k_weld does, was 1-2 % slower on repeated

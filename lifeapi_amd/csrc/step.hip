@@ -23,16 +23,20 @@ using StepFn = void (*)(const uint64_t *, uint64_t *, uint64_t, uint32_t, uint64
 //   generations, as the hand-allocated loop of split_asm.inc; nontemporal
 //   below 32 generations.  One-shot grids: every capped grid-stride grid
 //   measured slower.
-// The streaming kernel runs with at most 5 blocks (20 waves) resident per CU
-// instead of the 8 its registers allow, set by unused dynamic LDS: fewer
-// concurrent streams per CU, better served by HBM (tools/step_occupancy_ab.py,
-// profiles/r02/step_occupancy.jsonl, same process: +2 % at 1M universes,
-// +2.4 % at 2M, +4.7 % at 4M, +7 % at 16M over 8; 4 nearly as good, 6 and 8
-// not, 2 far worse, and grid-stride caps 7-19 % slower).  Round 2 recorded
-// that sweep as caps of 2..8, but its LDS arithmetic rounded up and gave one
-// block fewer whenever the cap did not divide the CU's LDS (6 -> 5, 7 -> 6,
-// 3 -> 2): its "6" was 5, the setting kept here; occupancy_lds now checks
-// the count against the occupancy API.
+// Batches above kCachedUniverses run with at most 7 blocks (28 waves)
+// resident per CU instead of the 8 its registers allow, set by unused dynamic
+// LDS: fewer concurrent streams per CU, better served by HBM.  Round 3,
+// exact caps (host.hip occupancy_lds), same process, ping-pong with the
+// batch-keyed order (tools/order_interleave_ab.py --caps,
+// profiles/r03/order_caps.jsonl): 8M universes 6.25 TB/s with 7 and 6.22
+// with 6 against 6.09 uncapped and 5.76 with 5; 16M 6.13 with 6 or 7 against
+// 5.95 uncapped and 5.71 with 5; at 4M 7 and uncapped equal (6.44 / 6.39),
+// at 1M-3M uncapped best (7 is 3-4 % slower, 6 up to 7 %).  The fixed-order
+// sweep agrees (tools/step_occupancy_ab.py, profiles/r03/step_occupancy.jsonl:
+// 16M 6.09 / 6.07 TB/s with 6 / 7 against 5.78 uncapped and 5.67 with 5).
+// Round 2 shipped "6", but its LDS arithmetic rounded the share up and gave
+// one block fewer whenever the cap did not divide 160 KiB (6 -> 5, 7 -> 6):
+// it ran 5; occupancy_lds now checks the count on the occupancy API.
 // Launch order and store policy (tools/order_ab.py, profiles/r02/order_*.jsonl,
 // same process, ping-pong as the bench): a launch whose input batch an
 // earlier launch wrote takes the groups in the reverse of that launch's order
@@ -44,7 +48,14 @@ using StepFn = void (*)(const uint64_t *, uint64_t *, uint64_t, uint32_t, uint64
 // ones the cap.  Against round 2's launch (nontemporal, one order, capped):
 // +12 % at 1M universes, +10 % at 2M, +3-5 % at 512K and 4M, equal at 8M-16M.
 constexpr uint64_t kCachedUniverses = 1ull << 22;
-constexpr int kStreamResidentBlocks = 5;
+constexpr int kStreamResidentBlocks = 7;
+// Below this batch size the order stays fixed: at 64K universes (64 MiB per
+// launch) the fixed order was 4 % faster, single batch and two interleaved,
+// and at 128K the two boxes disagreed (-4 / +1 %); from 192K on the
+// batch-keyed order is as fast or faster (+1-3 % at 192K-384K, +7-8 % for two
+// interleaved 512K batches, +16 % for one 1M batch; tools/order_interleave_ab.py,
+// profiles/r03/order_interleave*.jsonl)
+constexpr uint64_t kOrderMinUniverses = 3ull << 16;
 constexpr uint64_t kPlainBytes = 256ull << 20;
 constexpr uint64_t kFilterOrderUniverses = 1ull << 21;  // the same for the 1-2 generation search filter
 constexpr const char *kStreamName =
@@ -91,7 +102,7 @@ int lifeapi_step_batch_dev(const uint64_t *d_in, uint64_t *d_out, size_t n, uint
   }
   const uint64_t plain = (l.plain_bytes + l.universes_per_wave * 512 - 1) / (l.universes_per_wave * 512);
   uint32_t order = 0;
-  if (l.alternate) order = launch_reverse(d_in, d_out, (uint64_t)n * 512) ? kReverse : 0u;
+  if (l.alternate && n >= kOrderMinUniverses) order = launch_reverse(d_in, d_out, (uint64_t)n * 512) ? kReverse : 0u;
   else note_forward_write(d_out, (uint64_t)n * 512);
   hipLaunchKernelGGL(l.fn, dim3(grid_for(waves, cus, 0)), dim3(kBlock), lds, (hipStream_t)stream, d_in,
                      d_out, (uint64_t)n, generations | order, plain < waves ? waves - plain : (uint64_t)0);
@@ -142,7 +153,7 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
     const uint64_t groups = (n + 7) / 8;
     // Up to 2M universes: +3.4 % at 512K and 1M, +2 % at 2M, none at 4M
     // (profiles/r02/filter_order_ab.jsonl).
-    const bool order = d_final && n <= kFilterOrderUniverses;
+    const bool order = d_final && n <= kFilterOrderUniverses && n >= kOrderMinUniverses;
     const uint64_t plain = order ? (std::min<uint64_t>(kPlainBytes, n * 512 / 2) + 8 * 512 - 1) / (8 * 512) : 0;
     uint32_t rev = 0;
     if (order) rev = launch_reverse(d_in, d_final, (uint64_t)n * 512) ? kReverse : 0u;

@@ -34,11 +34,13 @@ def stepper():
 
 
 def test_shipped_occupancy_caps_are_exact(tune):
-    """the streaming k_step's cap (5 blocks, step.hip kStreamResidentBlocks)
-    and the LifeStable kernels' (4, stencils.hip kStableResidentBlocks)"""
-    assert tune.capped_occupancy(0, 5) == 5
+    """the streaming k_step's cap (7 blocks, step.hip kStreamResidentBlocks)
+    and the LifeStable kernels' (3 for the single passes and 4 for
+    StabiliseOptions and Vulnerable, stencils.hip kStablePassResident)"""
+    assert tune.capped_occupancy(0, 7) == 7
     for which in range(1, 8):
-        assert tune.capped_occupancy(which, 4) == 4, which
+        for want in (3, 4):
+            assert tune.capped_occupancy(which, want) == want, (which, want)
 
 
 @pytest.mark.parametrize("want", [2, 3, 4, 5, 6, 7, 8])

@@ -157,18 +157,20 @@ def _target(kind):
     return w, u
 
 
-@pytest.mark.parametrize("kind", ["seam", "tall", "row", "empty", "six"])
+# the windows each variant takes: 3..5 any; 6 and 7 (<= 4 rows) the seam,
+# one-row and empty targets; 8 (the wider windows) the tall and six-row ones
+_WINDOW_CASES = [(k, v) for v in (3, 4, 5) for k in ("seam", "tall", "row", "empty", "six")]
+_WINDOW_CASES += [(k, v) for v in (6, 7) for k in ("seam", "row", "empty")] + [(k, 8) for k in ("tall", "six")]
+
+
+@pytest.mark.parametrize("kind,variant", _WINDOW_CASES)
 @pytest.mark.parametrize("with_final", [False, True])
-@pytest.mark.parametrize("variant", [3, 4, 5, 6, 7, 8])
 def test_step_contains_row_window(tune, hip, port, kind, with_final, variant):
     """variants 3..8 (the target's row window, universes rotated into it
     and back) against the oracle and against the shipped kernels, for
     targets whose window wraps the row seam, exceeds 8 rows, is one row, is
     empty, or is six rows (batched in the full layout)."""
     import torch
-    own = {6: ("seam", "row", "empty"), 7: ("seam", "row", "empty"), 8: ("tall", "six")}
-    if variant in own and kind not in own[variant]:
-        pytest.skip(f"variant {variant} does not take this window")
     n, gens = 2001, 9
     w, u = _target(kind)
     x = port.fill(n, seed=501) & port.fill(n, seed=502)
