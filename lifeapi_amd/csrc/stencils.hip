@@ -15,6 +15,7 @@ extern "C" {
 // LifeStable kernels: one wave per LifeStable, at most this many blocks (of
 // kWavesPerBlock waves) resident per CU (see lifeapi_stable_pass_batch_dev)
 constexpr int kStableResidentBlocks = 4;
+constexpr int kWeldResidentBlocks = 7;  // k_weld (below 12 generations)
 // per pass (sync, options, signal, step, propagate, stabilise): 0 = every
 // slot.  Round 3, exact caps, 1M LifeStables of three families, same process
 // (tools/stable_grid_ab.py, profiles/r03/stable_caps_1m.jsonl): the single
@@ -117,8 +118,14 @@ int lifeapi_weld_step_batch_dev(uint64_t *d_welds, size_t n, uint32_t generation
     // throughout: in a loop stepping the batch in place, +15 % at 256K
     // welds, +7 % at 512K, +3.5 % at 1M, +1.5 % at 2M; a plain-stored tail
     // adds nothing here (tools/weld_order_ab.py, profiles/r02/weld_order_ab.jsonl)
+    // At most 7 blocks resident per CU: 0.459 against 0.484 ms for 1M welds
+    // with every slot (6: 0.458; 5: 0.472), same process, exact caps
+    // (tools/stencil_occupancy_ab.py, profiles/r03/stencil_caps.jsonl).
+    unsigned lds = 0;
+    rc = occupancy_lds(reinterpret_cast<const void *>(k_weld), kWeldResidentBlocks, lds);
+    if (rc != LIFEAPI_OK) return rc;
     const uint32_t rev = launch_reverse(d_welds, d_welds, (uint64_t)n * 2048) ? kWeldReverse : 0u;
-    hipLaunchKernelGGL(k_weld, dim3(grid_for(n, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream, d_welds,
+    hipLaunchKernelGGL(k_weld, dim3(grid_for(n, cus, 0)), dim3(kBlock), lds, (hipStream_t)stream, d_welds,
                        (uint64_t)n, generations | rev, (uint64_t)n);
   }
   return launched("k_weld launch");
