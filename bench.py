@@ -193,33 +193,48 @@ def pingpong_ms(rt, fn, a, b, reps=20, warm=5):
     return float(np.median(ms)), float(min(ms)), ms
 
 
-def neutral_fn(hip, rt, gens):
-    """The cache-neutral form of the shipped streaming launch: the same
-    kernel (k_step, 4 universes per wave, nontemporal loads) in ONE fixed
-    order with every store nontemporal, so no launch reads what the one
-    before it left in the 256 MB Infinity Cache (tools/tune step_order);
-    None without the tuning build."""
+def side_fn(rt, gens, neutral):
+    """A side launch of the shipped streaming kernel's code through the
+    tuning build (tools/tune step_order, kernel k_step_ab: the same code as
+    the product's k_step under another name, so that a rocprofv3 trace of
+    this bench tells side launches from the timed ones); None without the
+    tuning build.
+      neutral: the cache-neutral form -- ONE fixed group order, every store
+               nontemporal, no plain-stored tail, so no launch can read what
+               the one before it left in the 256 MB Infinity Cache;
+      else:    the product's policy (step.hip): the order reversed on every
+               launch of a ping-pong from 192K universes on (what the
+               batch-keyed order does there), the last min(256 MiB, half)
+               of each launch stored plain, at most 7 blocks per CU above 4M.
+    With gens = 0 the kernel is a copy of exactly that access shape."""
     if rt.neutral is None:
         return None
+    flip = [False]
 
     def fn(src, dst):
         n = src.shape[0]
-        rt.neutral(src, dst, generations=gens, reverse=False, nts=True,
-                   resident=0 if n <= (1 << 22) else 7, upw=4, plain_bytes=0, stream=rt.stream)
+        resident = 0 if n <= (1 << 22) else 7
+        if neutral:
+            rt.neutral(src, dst, generations=gens, reverse=False, nts=True, resident=resident, upw=4,
+                       plain_bytes=0, stream=rt.stream)
+        else:
+            rev = flip[0] and n >= 3 * (1 << 16)
+            flip[0] = not flip[0]
+            rt.neutral(src, dst, generations=gens, reverse=rev, nts=True, resident=resident, upw=4,
+                       plain_bytes=min(256 << 20, n * 512 // 2), stream=rt.stream)
     return fn
 
 
 def stream_figures(hip, rt, a, b, gens, reps=20):
     """Per-rank side measurements of the streaming launch on the rank's own
-    buffers, after the timed region: the cache-neutral step, and copy
-    ceilings of the same access shape -- the product kernel with 0
-    generations (the step's exact loads, stores, store policy and
-    batch-keyed order: a copy) and its cache-neutral form.  ms per launch."""
+    buffers, after the timed region (side_fn): the cache-neutral step, and
+    copy ceilings of the same access shape -- the kernel with 0 generations
+    under the product's store/order policy and in the neutral form.  ms per
+    launch, median of `reps` after 5 warm launches."""
     n = a.shape[0]
-    out = {"copy_ms": pingpong_ms(rt, lambda x, y: hip.step(x, out=y, generations=0, stream=rt.stream),
-                                  a, b, reps)[0]}
-    for key, g in (("neutral_ms", gens), ("copy_neutral_ms", 0)):
-        fn = neutral_fn(hip, rt, g)
+    out = {}
+    for key, g, neu in (("neutral_ms", gens, True), ("copy_ms", 0, False), ("copy_neutral_ms", 0, True)):
+        fn = side_fn(rt, g, neu)
         out[key] = pingpong_ms(rt, fn, a, b, reps)[0] if fn is not None else None
     out["bytes"] = n * BYTES_PER_UNIVERSE_GEN
     return out
@@ -765,10 +780,11 @@ def main(argv=None):
                                       "cache_neutral is the HBM-only figure",
                          "cache_neutral": ({"achieved": neu[0], "frac": neu[0] / HBM_PEAK_GBS,
                                             "kernel_ms": rank_figs[0][0],
-                                            "method": "same kernel, same size, same process, rank 0: one fixed "
-                                                      "group order, every store nontemporal, no plain-stored "
-                                                      "tail (tools/tune step_order), 20 ping-pong launches "
-                                                      "after 5 warm ones, median"}
+                                            "method": "the step kernel's code (k_step_ab), same size, same "
+                                                      "process, rank 0: one fixed group order, every store "
+                                                      "nontemporal, no plain-stored tail (tools/tune "
+                                                      "step_order), 20 ping-pong launches after 5 warm ones, "
+                                                      "median"}
                                            if neu[0] else None),
                          "cache_gain": (achieved / neu[0] - 1) if (achieved and neu[0]) else None,
                          "traffic": traffic, "traffic_source": tsrc,
@@ -782,9 +798,10 @@ def main(argv=None):
                          "aggregate_frac_cache_neutral": (agg_neu / (world * HBM_PEAK_GBS)) if agg_neu else None,
                          "read_only_GBps": achieved / 2 if achieved else None,
                          "copy_ceiling_GBps": cpy[0],
-                         "copy_ceiling_source": "live, rank 0: the product step kernel with 0 generations "
-                                                "(a copy with the step's exact loads, stores, store policy and "
-                                                "batch-keyed order), 20 ping-pong launches, median",
+                         "copy_ceiling_source": "live, rank 0: the step kernel's code with 0 generations (a copy "
+                                                "with the step's exact loads, stores, store policy and order), "
+                                                "20 ping-pong launches after 5 warm ones, median (bench.py "
+                                                "side_fn, kernel k_step_ab)",
                          "frac_of_copy_ceiling": (achieved / cpy[0]) if (achieved and cpy[0]) else None,
                          "copy_ceiling_cache_neutral_GBps": cpy_neu[0],
                          "frac_of_copy_ceiling_cache_neutral": (neu[0] / cpy_neu[0])

@@ -563,7 +563,7 @@ int lifeapi_tune_step_pair(const uint64_t *d_in, uint64_t *d_out, size_t n, uint
  * bit 31 of `generations` reverses the group order                         */
 extern "C++" {
 template <int U>
-StepFn order_fn(int nts) { return nts ? k_step<XDPP, U, true, 3, true> : k_step<XDPP, U, true, 3, false>; }
+StepFn order_fn(int nts) { return nts ? k_step_ab<XDPP, U, true, 3, true> : k_step_ab<XDPP, U, true, 3, false>; }
 }
 
 int lifeapi_tune_step_order(const uint64_t *d_in, uint64_t *d_out, size_t n, uint32_t generations, void *stream,
