@@ -46,6 +46,16 @@ __device__ __forceinline__ W life_gen(W a, uint64_t *slot, int lane) {
     const W t2 = lut3<kT2>(s2, a, t1);
     return lut3<kT3>(s1, s3, t2);
   }
+  if constexpr (RULE == 14) {
+    // RULE 3's exchange, h-layer and rotates with the 6-LUT tail
+    // (life_tail6) per 32-bit half: 24 VALU per generation plus the exchange
+    W L, R;
+    neighbour_cols<X>(a, L, R, slot, lane);
+    const W h0 = lut3<kXor3>(L, a, R), h1 = lut3<kMaj>(L, a, R);
+    const W h0u = rot_up(h0), h0d = rot_dn(h0), h1u = rot_up(h1), h1d = rot_dn(h1);
+    return W{life_tail6(h0u.lo, h0.lo, h0d.lo, h1u.lo, h1.lo, h1d.lo, a.lo),
+             life_tail6(h0u.hi, h0.hi, h0d.hi, h1u.hi, h1.hi, h1d.hi, a.hi)};
+  }
   if constexpr (RULE == 2) {
     // Row-first form of the same adder network.  A DPP move issues at half
     // the VALU rate on gfx950 (tools/valu_probe.hip: 8 DPP of 32 instructions
@@ -242,7 +252,8 @@ __global__ __launch_bounds__(kBlock) void k_step_split(const uint64_t *in, uint6
 // universes before it stores them, and no wave touches another's universes.
 // Group order (kReverse in `gens`) and the plain-stored tail of the final
 // states (`plain_from`) as k_step's.
-template <int U, bool WIDE = false>
+// X / RULE: the exchange and network of the generation (life_gen).
+template <int U, bool WIDE = false, int X = XDPP, int RULE = 3>
 __global__ __launch_bounds__(kBlock) void k_step_contains(const uint64_t *in, uint64_t *fin,
                                                           const uint64_t *__restrict__ wanted,
                                                           const uint64_t *__restrict__ unwanted,
@@ -252,14 +263,14 @@ __global__ __launch_bounds__(kBlock) void k_step_contains(const uint64_t *in, ui
   // lane, two universes per wave-instruction) staged through the wave's own
   // U x 512 B of LDS, which turns them into lane = column (and back for the
   // final states); the batch must be 16-byte aligned
-  __shared__ uint64_t stage[WIDE ? kWavesPerBlock * U * kWave : 1];
+  __shared__ uint64_t stage[WIDE || uses_lds(X) ? kWavesPerBlock * U * kWave : 1];
   const int lane = threadIdx.x & (kWave - 1);
   const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const W w = split(wanted[lane]), uw = split(unwanted[lane]);
   const bool rev = (gens & kReverse) != 0;
   gens &= ~kReverse;
   const uint64_t groups = (n + U - 1) / U, wstride = (uint64_t)gridDim.x * kWavesPerBlock;
-  uint64_t *st_w = stage + (WIDE ? wib * U * kWave : 0);
+  uint64_t *st_w = stage + (WIDE || uses_lds(X) ? wib * U * kWave : 0);
   const int half = lane >> 5, col = (lane & 31) * 2;
   for (uint64_t grp = (uint64_t)blockIdx.x * kWavesPerBlock + wib; grp < groups; grp += wstride) {
     const uint64_t u0 = (rev ? groups - 1 - grp : grp) * U;
@@ -290,7 +301,7 @@ __global__ __launch_bounds__(kBlock) void k_step_contains(const uint64_t *in, ui
     for (uint32_t g = 1; g <= gens; ++g) {
 #pragma unroll
       for (int k = 0; k < U; ++k) {
-        a[k] = life_gen<XDPP, 3>(a[k], nullptr, lane);
+        a[k] = life_gen<X, RULE>(a[k], uses_lds(X) ? st_w + k * kWave : nullptr, lane);
         if (hit[k] == 0 && wave_contains(a[k], w, uw)) hit[k] = g;
       }
     }

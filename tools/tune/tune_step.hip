@@ -251,6 +251,7 @@ StepFn pick_rule(int u, bool nt, int rule) {
       case 2: return pick_nt<X, 2>(u, nt);
       case 3: return pick_nt<X, 3>(u, nt);
       case 4: return pick_nt<X, 4>(u, nt);
+      case 14: return pick_nt<X, 14>(u, nt);
       default: return nullptr;
     }
   }
@@ -496,7 +497,12 @@ int lifeapi_tune_step_contains_nat(const uint64_t *d_in, uint64_t *d_final, cons
   // upw 16 + U: the 16-byte staged form (k_step_contains<U, true>), U = 2, 4, 8
   Fn fn = upw == 1 ? (Fn)k_step_contains<1> : upw == 2 ? (Fn)k_step_contains<2> : upw == 4 ? (Fn)k_step_contains<4>
         : upw == 8 ? (Fn)k_step_contains<8> : upw == 18 ? (Fn)k_step_contains<2, true>
-        : upw == 20 ? (Fn)k_step_contains<4, true> : upw == 24 ? (Fn)k_step_contains<8, true> : nullptr;
+        : upw == 20 ? (Fn)k_step_contains<4, true> : upw == 24 ? (Fn)k_step_contains<8, true>
+        // 32 + U: LDS exchange; 64 + U: the 6-LUT tail (RULE 14); 96 + U: both
+        : upw == 36 ? (Fn)k_step_contains<4, false, XLDS, 3> : upw == 40 ? (Fn)k_step_contains<8, false, XLDS, 3>
+        : upw == 68 ? (Fn)k_step_contains<4, false, XDPP, 14> : upw == 72 ? (Fn)k_step_contains<8, false, XDPP, 14>
+        : upw == 100 ? (Fn)k_step_contains<4, false, XLDS, 14> : upw == 104 ? (Fn)k_step_contains<8, false, XLDS, 14>
+        : nullptr;
   if (!fn) return fail(LIFEAPI_E_INVALID, "universes per wave: 1, 2, 4 or 8 (16 + 2, 4, 8: 16-byte form)%s");
   if (upw > 16 && (((uintptr_t)d_in | (uintptr_t)d_final) & 15u))
     return fail(LIFEAPI_E_INVALID, "the 16-byte form needs 16-byte aligned batches%s");
