@@ -252,8 +252,10 @@ __global__ __launch_bounds__(kBlock) void k_step_split(const uint64_t *in, uint6
 // universes before it stores them, and no wave touches another's universes.
 // Group order (kReverse in `gens`) and the plain-stored tail of the final
 // states (`plain_from`) as k_step's.
-// X / RULE: the exchange and network of the generation (life_gen).
-template <int U, bool WIDE = false, int X = XDPP, int RULE = 3>
+// X / RULE: the exchange and network of the generation (life_gen).  PF: each
+// wave loads the next group's states before it works on the current one (a
+// grid of at most the resident waves, looping over the batch).
+template <int U, bool WIDE = false, int X = XDPP, int RULE = 3, bool PF = false>
 __global__ __launch_bounds__(kBlock) void k_step_contains(const uint64_t *in, uint64_t *fin,
                                                           const uint64_t *__restrict__ wanted,
                                                           const uint64_t *__restrict__ unwanted,
@@ -272,10 +274,25 @@ __global__ __launch_bounds__(kBlock) void k_step_contains(const uint64_t *in, ui
   const uint64_t groups = (n + U - 1) / U, wstride = (uint64_t)gridDim.x * kWavesPerBlock;
   uint64_t *st_w = stage + (WIDE || uses_lds(X) ? wib * U * kWave : 0);
   const int half = lane >> 5, col = (lane & 31) * 2;
+  static_assert(!(PF && WIDE), "the prefetching loop is the 8-byte form's");
+  W an[U];
+  auto load_group = [&](uint64_t g, W (&dst)[U]) __attribute__((always_inline)) {
+    const uint64_t v0 = (rev ? groups - 1 - g : g) * U;
+#pragma unroll
+    for (int k = 0; k < U; ++k) dst[k] = (v0 + k < n) ? ld<true>(in + (v0 + k) * kWave + lane) : W{0u, 0u};
+  };
+  if constexpr (PF) {
+    const uint64_t g0 = (uint64_t)blockIdx.x * kWavesPerBlock + wib;
+    if (g0 < groups) load_group(g0, an);
+  }
   for (uint64_t grp = (uint64_t)blockIdx.x * kWavesPerBlock + wib; grp < groups; grp += wstride) {
     const uint64_t u0 = (rev ? groups - 1 - grp : grp) * U;
     W a[U];
-    if constexpr (WIDE) {
+    if constexpr (PF) {
+#pragma unroll
+      for (int k = 0; k < U; ++k) a[k] = an[k];
+      if (grp + wstride < groups) load_group(grp + wstride, an);
+    } else if constexpr (WIDE) {
       static_assert(U % 2 == 0, "universes come in pairs");
       u64x2 v[U / 2];
 #pragma unroll

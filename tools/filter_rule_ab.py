@@ -4,7 +4,9 @@ universes: RULE 3 (7-LUT tail, shipped) against RULE 14 (the 6-LUT tail,
 device.hpp life_tail6), each with the DPP or the LDS neighbour exchange, in
   - the 1-generation search filter, first hits only (k_step_contains, 516 B
     per universe) and with final states (1028 B);
-  - the streaming step (k_step, 1024 B), one fixed order, nt loads/stores.
+  - the streaming step (k_step, 1024 B), one fixed order, nt loads/stores;
+and the filter with the prefetching loop (k_step_contains<..., PF>: each wave
+loads its next group before working on the current one) on capped grids.
 Every variant's output is checked equal to the shipped kernel's.  Rounds
 interleave the variants; a timing is K back-to-back launches between two
 events (per launch: / K); one JSON line per variant, median over rounds.
@@ -57,6 +59,14 @@ def main():
              4: "dpp rule3 upw4", 36: "lds rule3 upw4", 68: "dpp rule14 upw4", 100: "lds rule14 upw4"}
     for code, nm in names.items():
         cases[f"filter {nm}"] = (516, lambda code=code: tune.step_contains_nat(x, w, w, 1, code, 0), None)
+    for code, nm in ((136, "dpp rule3 prefetch"), (200, "dpp rule14 prefetch"), (132, "dpp rule3 upw4 prefetch")):
+        for cap in (4, 6, 8):
+            cases[f"filter {nm} grid={cap}/CU"] = (
+                516, lambda code=code, cap=cap: tune.step_contains_nat(x, w, w, 1, code, -cap), None)
+    for cap in (4, 8):
+        cases[f"filter+final dpp rule3 prefetch grid={cap}/CU"] = (
+            1028, lambda cap=cap: tune.step_contains_nat(x, w, w, 1, 136, -cap, final=fin),
+            lambda: torch.equal(fin, ref_next))
     for code in (8, 40, 72, 104):
         cases[f"filter+final {names[code]}"] = (
             1028, lambda code=code: tune.step_contains_nat(x, w, w, 1, code, 0, final=fin),

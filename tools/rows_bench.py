@@ -66,7 +66,14 @@ def main():
     n = int(sys.argv[sys.argv.index('--n') + 1]) if '--n' in sys.argv else 1 << 20
     x = hip.fill_random(n, seed=7)
     y = torch.empty_like(x)
-    report("k_step (1 gen)", n, 1024, timed(lambda: hip.step(x, out=y, generations=1)))
+    pp = [x, y]
+
+    def step_pingpong():  # a Step() loop over the batch, as bench.py's timed region
+        hip.step(pp[0], out=pp[1], generations=1)
+        pp.reverse()
+
+    report("k_step (1 gen)", n, 1024, timed(step_pingpong))
+    x = hip.fill_random(n, seed=7)  # (the loop overwrote it)
     report("k_pop", n, 516, timed(lambda: hip.pop(x)))
     report("k_hash", n, 520, timed(lambda: hip.hashes(x)))
     w = x[:1].clone()

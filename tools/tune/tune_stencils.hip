@@ -16,12 +16,15 @@ extern "C" {
 int lifeapi_tune_stable_pass(uint64_t *d_planes, uint8_t *d_flags, size_t n, int pass, uint32_t max_iters,
                              int blocks_per_cu, void *stream, int reverse) {
   if (n == 0) return LIFEAPI_OK;
-  if (!d_planes || !d_flags || !aligned8(d_planes) || pass < 0 || pass > 5)
+  // pass 8 + k: pass k with the prefetching loop (k_stable<k, true>)
+  if (!d_planes || !d_flags || !aligned8(d_planes) || pass < 0 || pass > 13 || (pass > 5 && pass < 8))
     return fail(LIFEAPI_E_INVALID, "bad argument to lifeapi_tune_stable_pass%s");
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
   using Fn = void (*)(uint64_t *, uint8_t *, uint64_t, uint32_t, uint32_t);
-  const Fn fns[6] = {k_stable<0>, k_stable<1>, k_stable<2>, k_stable<3>, k_stable<4>, k_stable<5>};
+  const Fn fns[14] = {k_stable<0>, k_stable<1>, k_stable<2>, k_stable<3>, k_stable<4>, k_stable<5>, nullptr, nullptr,
+                      k_stable<0, true>, k_stable<1, true>, k_stable<2, true>, k_stable<3, true>, k_stable<4, true>,
+                      k_stable<5, true>};
   // blocks_per_cu < 0: uncapped grid, at most -blocks_per_cu blocks resident
   // per CU (unused dynamic LDS out of the CU's 160 KiB)
   unsigned lds = 0;

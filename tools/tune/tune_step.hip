@@ -502,6 +502,9 @@ int lifeapi_tune_step_contains_nat(const uint64_t *d_in, uint64_t *d_final, cons
         : upw == 36 ? (Fn)k_step_contains<4, false, XLDS, 3> : upw == 40 ? (Fn)k_step_contains<8, false, XLDS, 3>
         : upw == 68 ? (Fn)k_step_contains<4, false, XDPP, 14> : upw == 72 ? (Fn)k_step_contains<8, false, XDPP, 14>
         : upw == 100 ? (Fn)k_step_contains<4, false, XLDS, 14> : upw == 104 ? (Fn)k_step_contains<8, false, XLDS, 14>
+        // 128 + U: the prefetching loop (give a capped grid, resident < 0); 192 + U: with RULE 14
+        : upw == 132 ? (Fn)k_step_contains<4, false, XDPP, 3, true> : upw == 136 ? (Fn)k_step_contains<8, false, XDPP, 3, true>
+        : upw == 200 ? (Fn)k_step_contains<8, false, XDPP, 14, true>
         : nullptr;
   if (!fn) return fail(LIFEAPI_E_INVALID, "universes per wave: 1, 2, 4 or 8 (16 + 2, 4, 8: 16-byte form)%s");
   if (upw > 16 && (((uintptr_t)d_in | (uintptr_t)d_final) & 15u))
