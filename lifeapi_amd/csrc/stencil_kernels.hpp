@@ -35,14 +35,14 @@ __device__ __forceinline__ void ncount3(W a, W &b2, W &b1, W &b0) {
 // MODE 1: InteractionCounts (LifeAPI.hpp:956-993): out1, out2, outMore.
 // MODE 2: InteractionCountsAndNext (LifeAPI.hpp:997-1040): out1, out2,
 //         outMore, next.
-template <int MODE>
+template <int MODE, bool CHUNK = false>
 __global__ __launch_bounds__(kBlock) void k_counts(const uint64_t *__restrict__ in,
                                                    uint64_t *__restrict__ out, uint64_t n) {
   constexpr int P = MODE == 1 ? 3 : 4;
   const int lane = threadIdx.x & (kWave - 1);
   const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock;
-  for (uint64_t u = (uint64_t)blockIdx.x * kWavesPerBlock + wib; u < n; u += stride) {
+  for (uint64_t u = block_index<CHUNK>() * kWavesPerBlock + wib; u < n; u += stride) {
     const W a = ld<true>(in + u * kWave + lane);
     const W up = rot_up(a), dn = rot_dn(a);
     const W c0 = lut3<kXor3>(up, dn, a), c1 = lut3<kMaj>(up, dn, a);
@@ -96,6 +96,7 @@ __device__ __forceinline__ W weld_gen(W s, W f2, W f1, W f0) {
 // the last one stepped starts on the welds that launch touched last, part of
 // which the memory-side Infinity Cache still holds (as k_step).
 constexpr uint32_t kWeldReverse = 1u << 31;
+template <bool CHUNK = false>
 __global__ __launch_bounds__(kBlock) void k_weld(uint64_t *__restrict__ welds, uint64_t n,
                                                  uint32_t gens, uint64_t plain_from) {
   const int lane = threadIdx.x & (kWave - 1);
@@ -103,7 +104,7 @@ __global__ __launch_bounds__(kBlock) void k_weld(uint64_t *__restrict__ welds, u
   const bool rev = (gens & kWeldReverse) != 0;
   gens &= ~kWeldReverse;
   const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock;
-  for (uint64_t k = (uint64_t)blockIdx.x * kWavesPerBlock + wib; k < n; k += stride) {
+  for (uint64_t k = block_index<CHUNK>() * kWavesPerBlock + wib; k < n; k += stride) {
     const uint64_t u = rev ? n - 1 - k : k;
     uint64_t *p = welds + u * 4 * kWave + lane;
     if (k < plain_from) {
@@ -262,13 +263,13 @@ __device__ __forceinline__ void refined_one(const W (&pl)[11], uint64_t *out, ui
 // before this one's ~1000-instruction network runs (register double buffer),
 // so HBM traffic overlaps the VALU work of the same wave.  OCC = minimum
 // waves per SIMD requested from the register allocator (0 = no bound).
-template <int PF, int OCC>
+template <int PF, int OCC, bool CHUNK = false>
 __global__ __launch_bounds__(kBlock, OCC > 0 ? OCC : 1) void k_refined(
     const uint64_t *__restrict__ in, uint64_t *__restrict__ out, uint64_t n) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock;
-  uint64_t u = (uint64_t)blockIdx.x * kWavesPerBlock + wib;
+  uint64_t u = block_index<CHUNK>() * kWavesPerBlock + wib;
   if (u >= n) return;
   if constexpr (PF == 0) {
     for (; u < n; u += stride) {

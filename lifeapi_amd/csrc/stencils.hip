@@ -78,8 +78,14 @@ int lifeapi_stable_pass_batch_dev(uint64_t *d_planes, uint8_t *d_flags, size_t n
   }
   // One order: alternating it, as k_weld does, was 1-2 % slower on repeated
   // passes in place (tools/stable_order_ab.py, profiles/r02/stable_order_ab.jsonl).
+  // Each XCD takes a contiguous eighth of the batch (the last argument's bit
+  // 1, device.hpp xcd_chunk_block): on 1M LifeStables, same process, fresh
+  // copies (tools/stable_xcd_ab.py, profiles/r03/stable_xcd_ab.jsonl)
+  // Propagate 1.96 -> 1.77 ms, sync 1.77 -> 1.63, options 1.62 -> 1.54,
+  // signal 1.83 -> 1.72, PropagateStep 1.95 -> 1.86, StabiliseOptions
+  // 1.79 -> 1.66.
   hipLaunchKernelGGL(fns[pass], dim3(grid_for(n, cus, 0)), dim3(kBlock), lds, (hipStream_t)stream,
-                     d_planes, d_flags, (uint64_t)n, max_iters ? max_iters : 1u << 20, 0u);
+                     d_planes, d_flags, (uint64_t)n, max_iters ? max_iters : 1u << 20, 2u);
   return launched("k_stable launch");
 }
 
@@ -95,9 +101,9 @@ int lifeapi_stable_vulnerable_batch_dev(const uint64_t *d_planes, uint64_t *d_ou
   // CU (0.96-0.97 ms at 1M against 0.97-1.00 unlimited and 1.02-1.04 on a
   // looping grid; profiles/r02/stable_occupancy_*.jsonl)
   unsigned lds = 0;
-  rc = occupancy_lds(reinterpret_cast<const void *>(k_stable_vulnerable), kStableResidentBlocks, lds);
+  rc = occupancy_lds(reinterpret_cast<const void *>(k_stable_vulnerable<false>), kStableResidentBlocks, lds);
   if (rc != LIFEAPI_OK) return rc;
-  hipLaunchKernelGGL(k_stable_vulnerable, dim3(grid_for(n, cus, 0)), dim3(kBlock), lds, (hipStream_t)stream,
+  hipLaunchKernelGGL(k_stable_vulnerable<false>, dim3(grid_for(n, cus, 0)), dim3(kBlock), lds, (hipStream_t)stream,
                      d_planes, d_out, (uint64_t)n);
   return launched("k_stable_vulnerable launch");
 }
@@ -122,10 +128,10 @@ int lifeapi_weld_step_batch_dev(uint64_t *d_welds, size_t n, uint32_t generation
     // with every slot (6: 0.458; 5: 0.472), same process, exact caps
     // (tools/stencil_occupancy_ab.py, profiles/r03/stencil_caps.jsonl).
     unsigned lds = 0;
-    rc = occupancy_lds(reinterpret_cast<const void *>(k_weld), kWeldResidentBlocks, lds);
+    rc = occupancy_lds(reinterpret_cast<const void *>(k_weld<false>), kWeldResidentBlocks, lds);
     if (rc != LIFEAPI_OK) return rc;
     const uint32_t rev = launch_reverse(d_welds, d_welds, (uint64_t)n * 2048) ? kWeldReverse : 0u;
-    hipLaunchKernelGGL(k_weld, dim3(grid_for(n, cus, 0)), dim3(kBlock), lds, (hipStream_t)stream, d_welds,
+    hipLaunchKernelGGL(k_weld<false>, dim3(grid_for(n, cus, 0)), dim3(kBlock), lds, (hipStream_t)stream, d_welds,
                        (uint64_t)n, generations | rev, (uint64_t)n);
   }
   return launched("k_weld launch");

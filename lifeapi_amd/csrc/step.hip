@@ -61,6 +61,16 @@ constexpr uint64_t kFilterOrderUniverses = 1ull << 21;  // the same for the 1-2 
 constexpr const char *kStreamName =
     "k_step<dpp, 4 universes/wave, nt loads, 7-LUT network; alternating order, the last min(256 MiB, half) of "
     "each launch stored plain, the rest nt>";
+// Above kCachedUniverses there is no Infinity Cache reuse to arrange: one
+// order, every store nontemporal, and each XCD streams a contiguous eighth
+// of the batch (kXcdChunk, device.hpp xcd_chunk_block).  Same process,
+// ping-pong, 7 blocks per CU (tools/step_xcd_ab.py,
+// profiles/r03/step_xcd_ab.jsonl): 16M universes 2.736 ms against 2.836 for
+// the order/plain-tail launch and 2.845 with the plain block mapping; 8M
+// 1.396 against 1.410 / 1.427; at 4M the chunked mapping was 1 % slower, at
+// 1M equal.
+constexpr const char *kStreamBigName =
+    "k_step<dpp, 4 universes/wave, nt, 7-LUT network; each XCD a contiguous eighth, one order>";
 struct StepLaunch {
   StepFn fn;
   uint64_t universes_per_wave;
@@ -68,16 +78,19 @@ struct StepLaunch {
   bool alternate;        // alternate the group order between launches
   uint64_t plain_bytes;  // the last bytes of a launch stored plain
   const char *name;
+  uint32_t flags;        // kXcdChunk or 0
 };
 StepLaunch shipped_step(uint32_t gens, uint64_t n) {
+  if (gens <= 2 && n > kCachedUniverses)
+    return {k_step<XDPP, 4, true, 3, true>, 4, kStreamResidentBlocks, false, 0, kStreamBigName, kXcdChunk};
   if (gens <= 2)
-    return {k_step<XDPP, 4, true, 3, true>, 4, n <= kCachedUniverses ? 0 : kStreamResidentBlocks, true,
-            std::min<uint64_t>(kPlainBytes, n * 512 / 2), kStreamName};
+    return {k_step<XDPP, 4, true, 3, true>, 4, 0, true, std::min<uint64_t>(kPlainBytes, n * 512 / 2), kStreamName,
+            0u};
   if (gens < 32)
     return {k_step_split<8, 1, true, 6, kAsmLoop>, 4, 0, false, 0,
-            "k_step_split<8-way split, 4 universes/wave, nt, 6-LUT tail, assembly loop>"};
+            "k_step_split<8-way split, 4 universes/wave, nt, 6-LUT tail, assembly loop>", 0u};
   return {k_step_split<8, 1, false, 6, kAsmLoop>, 4, 0, false, 0,
-          "k_step_split<8-way split, 4 universes/wave, 6-LUT tail, assembly loop>"};
+          "k_step_split<8-way split, 4 universes/wave, 6-LUT tail, assembly loop>", 0u};
 }
 
 }  // namespace
@@ -105,7 +118,7 @@ int lifeapi_step_batch_dev(const uint64_t *d_in, uint64_t *d_out, size_t n, uint
   if (l.alternate && n >= kOrderMinUniverses) order = launch_reverse(d_in, d_out, (uint64_t)n * 512) ? kReverse : 0u;
   else note_forward_write(d_out, (uint64_t)n * 512);
   hipLaunchKernelGGL(l.fn, dim3(grid_for(waves, cus, 0)), dim3(kBlock), lds, (hipStream_t)stream, d_in,
-                     d_out, (uint64_t)n, generations | order, plain < waves ? waves - plain : (uint64_t)0);
+                     d_out, (uint64_t)n, generations | order | l.flags, plain < waves ? waves - plain : (uint64_t)0);
   return launched("k_step launch");
 }
 

@@ -124,6 +124,9 @@ __device__ __forceinline__ W life_gen(W a, uint64_t *slot, int lane) {
 // launch to read first, and the nontemporal rest does not evict it
 // (DESIGN.md 3.1).  The launcher sets both only for gens <= 2.
 constexpr uint32_t kReverse = 1u << 31;
+// Bit 30 of `gens` (kXcdChunk): each XCD takes a contiguous eighth of the
+// groups (xcd_chunk_block); the launcher sets it for large batches.
+constexpr uint32_t kXcdChunk = 1u << 30;
 // NTS: nontemporal stores (default: as the loads) before `plain_from`.
 template <int X, int U, bool NT, int RULE, bool NTS>
 __device__ __forceinline__ void step_body(const uint64_t *in, uint64_t *out, uint64_t n, uint32_t gens,
@@ -134,9 +137,10 @@ __device__ __forceinline__ void step_body(const uint64_t *in, uint64_t *out, uin
   // tests below are scalar branches
   const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const bool rev = (gens & kReverse) != 0;
-  gens &= ~kReverse;
+  const uint64_t blk = (gens & kXcdChunk) ? xcd_chunk_block() : (uint64_t)blockIdx.x;
+  gens &= ~(kReverse | kXcdChunk);
   const uint64_t groups = (n + U - 1) / U, wstride = (uint64_t)gridDim.x * kWavesPerBlock;
-  for (uint64_t grp = (uint64_t)blockIdx.x * kWavesPerBlock + wib; grp < groups; grp += wstride) {
+  for (uint64_t grp = blk * kWavesPerBlock + wib; grp < groups; grp += wstride) {
     const uint64_t u0 = (rev ? groups - 1 - grp : grp) * U;
     W a[U];
 #pragma unroll

@@ -430,6 +430,46 @@ def test_config4_all_shards_vs_reference_digests(hip):
     assert f"{combine(got):016x}" == d["output_digest"]
 
 
+def test_config4_one_launch_vs_reference_digest(hip):
+    """Config 4's 16M universes in ONE launch: the large-batch launch (above
+    4M universes: one order, nontemporal, each XCD a contiguous eighth of the
+    batch, step.hip shipped_step) against the reference's digest."""
+    import json
+    import os
+
+    from lifeapi_amd.digest import batch_digest, combine
+    with open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")) as f:
+        d = json.load(f)["digests"]["config4"]
+    n, per = d["universes"], d["universes"] // d["shards"]
+    a = hip.fill_random(n, seed=d["seed"])
+    b = hip.step(a, generations=1)
+    h = hip.hashes(b).cpu().numpy()
+    got = [batch_digest(h[k * per:(k + 1) * per], k * per) for k in range(d["shards"])]
+    assert f"{combine(got):016x}" == d["output_digest"]
+    del a, b
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("n", [(1 << 22) + 4099, (5 << 20) + 3])
+def test_large_batch_launch_equals_small_batch_launches(hip, n):
+    """Batches above 4M universes take the XCD-chunked launch, whose grid
+    need not be a multiple of 8 blocks (ragged n here): ping-pong and in
+    place, every universe equals the small-batch launches (checked against
+    the reference above) stepping the same universes in pieces of <= 4M."""
+    x = hip.fill_random(n, seed=31)
+    want = torch.empty_like(x)
+    half = n // 2
+    hip.step(x[:half], out=want[:half], generations=1)
+    hip.step(x[half:], out=want[half:], generations=1)
+    got = hip.step(x, generations=1)
+    assert torch.equal(got, want)
+    y = x.clone()
+    hip.step(y, out=y, generations=1)
+    assert torch.equal(y, want)
+    del x, want, got, y
+    torch.cuda.empty_cache()
+
+
 def test_config3_full_size_vs_reference_digest(hip):
     """Config 3 (64K x 1024 generations, one launch) vs the reference's digest."""
     import json
@@ -508,11 +548,11 @@ def test_stable_passes_golden_gpu(hip):
         assert (fl.cpu().numpy() == g[name + "_flags"]).all(), name
 
 
-def test_stable_passes_vs_oracle(hip, port):
+def _stable_cases(port, n, seed=5):
     """Seeded still-life neighbourhoods with an unknown window (mostly
-    consistent) and random planes (mostly inconsistent), every pass."""
-    rng = np.random.default_rng(5)
-    n = 300
+    consistent) and, every fourth, random option planes (mostly
+    inconsistent), as (n, 640) uint64 planes."""
+    rng = np.random.default_rng(seed)
     x = np.zeros((n, 10, 64), np.uint64)
     blocks = port.parse("2o$2o!")
     for u in range(n):
@@ -528,7 +568,13 @@ def test_stable_passes_vs_oracle(hip, port):
         if u % 4 == 3:
             f = port.fill(10, seed=u)
             x[u, 2:] = f[2:] & port.fill(8, seed=u + 1000)
-    x = x.reshape(n, 640)
+    return x.reshape(n, 640)
+
+
+def test_stable_passes_vs_oracle(hip, port):
+    """_stable_cases, every pass, then Vulnerable."""
+    n = 300
+    x = _stable_cases(port, n)
     results = {}
     for w, name in enumerate(hip.STABLE_PASSES):
         d = to_dev(x).reshape(n, 640)
@@ -545,6 +591,24 @@ def test_stable_passes_vs_oracle(hip, port):
         exp = port.stable_vulnerable(planes)
         assert (to_host(got) == exp).all()
     assert exp.any()
+
+
+def test_stable_passes_chunked_grid_ragged(hip, port):
+    """The passes deal each XCD a contiguous eighth of the batch
+    (device.hpp xcd_chunk_block) on any grid: 20003 LifeStables (5001
+    blocks, not a multiple of 8), every pass against the oracle."""
+    n = 20003
+    x = _stable_cases(port, n, seed=9)
+    for w, name in enumerate(hip.STABLE_PASSES):
+        d = to_dev(x).reshape(n, 640)
+        fl = hip.stable_pass(d, name).cpu().numpy()
+        want, wfl = port.stable_pass(x, w)
+        assert (d.cpu().numpy().view(np.uint64) == want).all(), name
+        assert (fl == wfl).all(), name
+        if name == "propagate":
+            assert (wfl & 1).sum() > n // 3
+    got = hip.stable_vulnerable(to_dev(x).reshape(n, 640))
+    assert (to_host(got) == port.stable_vulnerable(x)).all()
 
 
 @pytest.mark.parametrize("density", [0.2, 0.5, 0.8])

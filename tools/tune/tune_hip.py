@@ -85,14 +85,15 @@ lib.lifeapi_tune_step_order.restype = _int
 
 def step_order(states: torch.Tensor, out: torch.Tensor, generations: int = 1, reverse: bool = False,
                nts: bool = True, resident: int = 6, upw: int = 4, plain_bytes: int = 0,
-               stream=None) -> torch.Tensor:
+               stream=None, xcd_chunk: bool = False) -> torch.Tensor:
     """The shipped gens <= 2 kernel with nontemporal or plain stores, at most
     `resident` blocks per CU, `upw` universes per wave, universes taken in
     reverse order if asked; plain stores for the groups that store the last
     `plain_bytes` of the launch's order whatever `nts` says."""
     n = hip._universes(states)
     hip._check(lib.lifeapi_tune_step_order(states.data_ptr(), out.data_ptr(), n,
-                                           generations | ((1 << 31) if reverse else 0), hip._stream(stream),
+                                           generations | ((1 << 31) if reverse else 0) |
+                                           ((1 << 30) if xcd_chunk else 0), hip._stream(stream),
                                            1 if nts else 0, resident, upw, plain_bytes))
     return out
 
@@ -117,11 +118,12 @@ lib.lifeapi_tune_stable_vulnerable.restype = _int
 
 
 def stable_pass(planes: torch.Tensor, which: int, blocks_per_cu: int, max_iters: int = 0, stream=None,
-                reverse: bool = False):
+                reverse: bool = False, xcd_chunk: bool = False):
     n = planes.numel() // (10 * 64)
     flags = torch.empty(n, dtype=torch.uint8, device=planes.device)
     hip._check(lib.lifeapi_tune_stable_pass(planes.data_ptr(), flags.data_ptr(), n, which, max_iters,
-                                            blocks_per_cu, hip._stream(stream), 1 if reverse else 0))
+                                            blocks_per_cu, hip._stream(stream),
+                                            (1 if reverse else 0) | (2 if xcd_chunk else 0)))
     return flags
 
 

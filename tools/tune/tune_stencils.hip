@@ -31,23 +31,30 @@ int lifeapi_tune_stable_pass(uint64_t *d_planes, uint8_t *d_flags, size_t n, int
   if (blocks_per_cu < 0 && (rc = occupancy_lds((const void *)fns[pass], -blocks_per_cu, lds)) != LIFEAPI_OK) return rc;
   hipLaunchKernelGGL(fns[pass], dim3(grid_for(n, cus, blocks_per_cu > 0 ? blocks_per_cu : 0)), dim3(kBlock), lds,
                      (hipStream_t)stream, d_planes, d_flags, (uint64_t)n, max_iters ? max_iters : 1u << 20,
-                     reverse ? 1u : 0u);
+                     (uint32_t)reverse);
   return launched("k_stable (tuning) launch");
 }
 
 int lifeapi_tune_stable_vulnerable(const uint64_t *d_planes, uint64_t *d_out, size_t n, int blocks_per_cu,
                                    void *stream) {
+  // blocks_per_cu + 1000: the XCD-chunked block mapping (k_stable_vulnerable<true>)
+  const bool chunk = blocks_per_cu >= 500;
+  if (chunk) blocks_per_cu -= 1000;
   if (n == 0) return LIFEAPI_OK;
   if (!d_planes || !d_out || !aligned8(d_planes) || !aligned8(d_out))
     return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_tune_stable_vulnerable%s");
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
+  const void *fn = chunk ? (const void *)k_stable_vulnerable<true> : (const void *)k_stable_vulnerable<false>;
   unsigned lds = 0;
-  if (blocks_per_cu < 0 &&
-      (rc = occupancy_lds((const void *)k_stable_vulnerable, -blocks_per_cu, lds)) != LIFEAPI_OK)
-    return rc;
-  hipLaunchKernelGGL(k_stable_vulnerable, dim3(grid_for(n, cus, blocks_per_cu > 0 ? blocks_per_cu : 0)),
-                     dim3(kBlock), lds, (hipStream_t)stream, d_planes, d_out, (uint64_t)n);
+  if (blocks_per_cu < 0 && (rc = occupancy_lds(fn, -blocks_per_cu, lds)) != LIFEAPI_OK) return rc;
+  const dim3 grid(grid_for(n, cus, blocks_per_cu > 0 ? blocks_per_cu : 0));
+  if (chunk)
+    hipLaunchKernelGGL(k_stable_vulnerable<true>, grid, dim3(kBlock), lds, (hipStream_t)stream, d_planes, d_out,
+                       (uint64_t)n);
+  else
+    hipLaunchKernelGGL(k_stable_vulnerable<false>, grid, dim3(kBlock), lds, (hipStream_t)stream, d_planes, d_out,
+                       (uint64_t)n);
   return launched("k_stable_vulnerable (tuning) launch");
 }
 
@@ -55,34 +62,43 @@ int lifeapi_tune_stable_vulnerable(const uint64_t *d_planes, uint64_t *d_out, si
  * (0 = as many as fit): kind 0..2 = k_counts<kind> (NeighbourCount,
  * InteractionCounts, ...AndNext; in = n universes, out = their planes),
  * 3 = k_weld one generation (in place on in = n LifeWelds), 4 = k_refined
- * (in = n x 11 planes, out = n x 3 planes)                                */
-int lifeapi_tune_stencil(int kind, const uint64_t *d_in, uint64_t *d_out, size_t n, int resident, void *stream) {
-  if (n == 0) return LIFEAPI_OK;
-  if (!d_in || kind < 0 || kind > 4 || resident < 0 || (kind != 3 && !d_out))
-    return fail(LIFEAPI_E_INVALID, "bad argument to lifeapi_tune_stencil%s");
+ * (in = n x 11 planes, out = n x 3 planes); kind + 8: the same with the
+ * XCD-chunked block mapping (CHUNK = true)                                  */
+}  // extern "C"
+template <bool C>
+static int tune_stencil(int kind, const uint64_t *d_in, uint64_t *d_out, size_t n, int resident, void *stream) {
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
   unsigned lds = 0;
   if (resident) {
-    const void *fns[5] = {(const void *)k_counts<0>, (const void *)k_counts<1>, (const void *)k_counts<2>,
-                          (const void *)k_weld, (const void *)k_refined<1, 0>};
+    const void *fns[5] = {(const void *)k_counts<0, C>, (const void *)k_counts<1, C>, (const void *)k_counts<2, C>,
+                          (const void *)k_weld<C>, (const void *)k_refined<1, 0, C>};
     rc = occupancy_lds(fns[kind], resident, lds);
     if (rc != LIFEAPI_OK) return rc;
   }
   const dim3 grid(grid_for(n, cus, 0));
   switch (kind) {
-    case 0: hipLaunchKernelGGL(k_counts<0>, grid, dim3(kBlock), lds, (hipStream_t)stream, d_in, d_out, (uint64_t)n); break;
-    case 1: hipLaunchKernelGGL(k_counts<1>, grid, dim3(kBlock), lds, (hipStream_t)stream, d_in, d_out, (uint64_t)n); break;
-    case 2: hipLaunchKernelGGL(k_counts<2>, grid, dim3(kBlock), lds, (hipStream_t)stream, d_in, d_out, (uint64_t)n); break;
+    case 0: hipLaunchKernelGGL((k_counts<0, C>), grid, dim3(kBlock), lds, (hipStream_t)stream, d_in, d_out, (uint64_t)n); break;
+    case 1: hipLaunchKernelGGL((k_counts<1, C>), grid, dim3(kBlock), lds, (hipStream_t)stream, d_in, d_out, (uint64_t)n); break;
+    case 2: hipLaunchKernelGGL((k_counts<2, C>), grid, dim3(kBlock), lds, (hipStream_t)stream, d_in, d_out, (uint64_t)n); break;
     case 3:
       // one order, nontemporal throughout (the launch before the product's order policy)
-      hipLaunchKernelGGL(k_weld, grid, dim3(kBlock), lds, (hipStream_t)stream, (uint64_t *)d_in, (uint64_t)n, 1u,
+      hipLaunchKernelGGL(k_weld<C>, grid, dim3(kBlock), lds, (hipStream_t)stream, (uint64_t *)d_in, (uint64_t)n, 1u,
                          ~(uint64_t)0);
       break;
     default:
-      hipLaunchKernelGGL((k_refined<1, 0>), grid, dim3(kBlock), lds, (hipStream_t)stream, d_in, d_out, (uint64_t)n);
+      hipLaunchKernelGGL((k_refined<1, 0, C>), grid, dim3(kBlock), lds, (hipStream_t)stream, d_in, d_out, (uint64_t)n);
   }
   return launched("stencil (tuning) launch");
+}
+extern "C" {
+int lifeapi_tune_stencil(int kind, const uint64_t *d_in, uint64_t *d_out, size_t n, int resident, void *stream) {
+  if (n == 0) return LIFEAPI_OK;
+  const int k = kind & 7;
+  if (!d_in || kind < 0 || kind > 12 || k > 4 || resident < 0 || (k != 3 && !d_out))
+    return fail(LIFEAPI_E_INVALID, "bad argument to lifeapi_tune_stencil%s");
+  return kind >= 8 ? tune_stencil<true>(k, d_in, d_out, n, resident, stream)
+                   : tune_stencil<false>(k, d_in, d_out, n, resident, stream);
 }
 
 /* resident blocks per CU of a shipped kernel under the occupancy cap
@@ -93,7 +109,7 @@ int lifeapi_tune_capped_occupancy(int which, int want, int *got) {
   const void *fns[8] = {(const void *)k_step<XDPP, 4, true, 3, true>,
                         (const void *)k_stable<0>, (const void *)k_stable<1>, (const void *)k_stable<2>,
                         (const void *)k_stable<3>, (const void *)k_stable<4>, (const void *)k_stable<5>,
-                        (const void *)k_stable_vulnerable};
+                        (const void *)k_stable_vulnerable<false>};
   unsigned lds = 0;
   int rc = occupancy_lds(fns[which], want, lds);
   if (rc != LIFEAPI_OK) return rc;
@@ -118,7 +134,7 @@ int lifeapi_tune_weld_order(uint64_t *d_welds, size_t n, int reverse, uint64_t p
   if (!d_welds) return fail(LIFEAPI_E_INVALID, "bad argument to lifeapi_tune_weld_order%s");
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
-  hipLaunchKernelGGL(k_weld, dim3(grid_for(n, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream, d_welds, (uint64_t)n,
+  hipLaunchKernelGGL(k_weld<false>, dim3(grid_for(n, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream, d_welds, (uint64_t)n,
                      1u | (reverse ? kWeldReverse : 0u), plain_welds < n ? (uint64_t)n - plain_welds : (uint64_t)0);
   return launched("k_weld (order) launch");
 }

@@ -579,7 +579,7 @@ int lifeapi_tune_step_order(const uint64_t *d_in, uint64_t *d_out, size_t n, uin
                             int nts, int resident, int upw, uint64_t plain_bytes) {
   int rc = check_batch(d_in, d_out, n);
   if (rc != LIFEAPI_OK || n == 0) return rc;
-  if ((generations & ~kReverse) > 2) return fail(LIFEAPI_E_INVALID, "streaming step: generations <= 2%s");
+  if ((generations & ~(kReverse | kXcdChunk)) > 2) return fail(LIFEAPI_E_INVALID, "streaming step: generations <= 2%s");
   const StepFn fn = upw == 2 ? order_fn<2>(nts) : upw == 4 ? order_fn<4>(nts) : upw == 8 ? order_fn<8>(nts) : nullptr;
   if (!fn) return fail(LIFEAPI_E_INVALID, "universes per wave: 2, 4 or 8%s");
   int cus = 0;
