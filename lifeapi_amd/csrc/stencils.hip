@@ -99,11 +99,15 @@ int lifeapi_stable_vulnerable_batch_dev(const uint64_t *d_planes, uint64_t *d_ou
   if (rc != LIFEAPI_OK) return rc;
   // as the passes: one wave per LifeStable, at most 4 blocks resident per
   // CU (0.96-0.97 ms at 1M against 0.97-1.00 unlimited and 1.02-1.04 on a
-  // looping grid; profiles/r02/stable_occupancy_*.jsonl)
+  // looping grid; profiles/r02/stable_occupancy_*.jsonl), each XCD a
+  // contiguous eighth of the batch (0.998 -> 0.905 ms at 1M, same process;
+  // tools/stencil_xcd_ab.py, profiles/r03/stencil_xcd_ab.jsonl; the counts,
+  // k_weld and k_refined at config 5's 256K measured within noise or slower
+  // with it and keep the plain mapping)
   unsigned lds = 0;
-  rc = occupancy_lds(reinterpret_cast<const void *>(k_stable_vulnerable<false>), kStableResidentBlocks, lds);
+  rc = occupancy_lds(reinterpret_cast<const void *>(k_stable_vulnerable<true>), kStableResidentBlocks, lds);
   if (rc != LIFEAPI_OK) return rc;
-  hipLaunchKernelGGL(k_stable_vulnerable<false>, dim3(grid_for(n, cus, 0)), dim3(kBlock), lds, (hipStream_t)stream,
+  hipLaunchKernelGGL(k_stable_vulnerable<true>, dim3(grid_for(n, cus, 0)), dim3(kBlock), lds, (hipStream_t)stream,
                      d_planes, d_out, (uint64_t)n);
   return launched("k_stable_vulnerable launch");
 }
