@@ -40,7 +40,7 @@ class Runtime:
 
     @staticmethod
     def neutral(states, out, generations=1, reverse=False, nts=True, resident=0, upw=4, plain_bytes=0,
-                stream=None):
+                stream=None, xcd_chunk=False):
         """stand-in for the tuning build's fixed-order launcher (same result)"""
         return step(states, out=out, generations=generations)
 
