@@ -11,20 +11,82 @@
 
 using namespace lifeapi_impl;
 
+namespace {
+
+// The prefetching loop (round 3, measured slower): each wave
+// loops over the batch (a grid of at most the resident waves) and loads the
+// next LifeStable's planes before it works on the current one.
+template <int PASS>
+__device__ __forceinline__ int stable_run(W (&p)[10], uint32_t max_iters) {
+  if constexpr (PASS == 0) return stable_sync(p);
+  else if constexpr (PASS == 1) return stable_options(p);
+  else if constexpr (PASS == 2) return stable_signal(p);
+  else if constexpr (PASS == 3) return stable_step(p);
+  int ever = 0;
+  for (uint32_t it = 0; it < max_iters; ++it) {
+    if constexpr (PASS == 5) {  // StabiliseOptions (LifeStable.hpp:677-693)
+      const int k = stable_sync(p);
+      if (!(k & 1)) return 0;
+      const int o = stable_options(p);
+      if (!(o & 1)) return 0;
+      if (!((k | o) & 2)) return 1 | ever;
+    } else {  // Propagate (LifeStable.hpp:718-729)
+      const int s = stable_step(p);
+      if (!(s & 1)) return 0;
+      if (!(s & 2)) return 1 | ever;
+    }
+    ever = 2;
+  }
+  return 1 | ever | 4;
+}
+
+template <int PASS>
+__global__ __launch_bounds__(kBlock) void k_stable_pf(uint64_t *__restrict__ planes, uint8_t *__restrict__ flags,
+                                                      uint64_t n, uint32_t max_iters, uint32_t mode) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock;
+  uint64_t k0 = (uint64_t)blockIdx.x * kWavesPerBlock + wib;
+  if (k0 >= n) return;
+  const bool rev = (mode & 1u) != 0;
+  W p[10], pn[10];
+  {
+    const uint64_t *q = planes + (rev ? n - 1 - k0 : k0) * 10 * kWave + lane;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) p[k] = ld<true>(q + k * kWave);
+  }
+  for (; k0 < n; k0 += stride) {
+    const uint64_t u = rev ? n - 1 - k0 : k0, k1 = k0 + stride;
+    if (k1 < n) {
+      const uint64_t *qn = planes + (rev ? n - 1 - k1 : k1) * 10 * kWave + lane;
+#pragma unroll
+      for (int k = 0; k < 10; ++k) pn[k] = ld<true>(qn + k * kWave);
+    }
+    const int r = stable_run<PASS>(p, max_iters);
+    uint64_t *q = planes + u * 10 * kWave + lane;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) st<true>(q + k * kWave, p[k]);
+    if (lane == 0) flags[u] = (uint8_t)r;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) p[k] = pn[k];
+  }
+}
+
+}  // namespace
+
 extern "C" {
 
 int lifeapi_tune_stable_pass(uint64_t *d_planes, uint8_t *d_flags, size_t n, int pass, uint32_t max_iters,
                              int blocks_per_cu, void *stream, int reverse) {
   if (n == 0) return LIFEAPI_OK;
-  // pass 8 + k: pass k with the prefetching loop (k_stable<k, true>)
+  // pass 8 + k: pass k with the prefetching loop (k_stable_pf<k>)
   if (!d_planes || !d_flags || !aligned8(d_planes) || pass < 0 || pass > 13 || (pass > 5 && pass < 8))
     return fail(LIFEAPI_E_INVALID, "bad argument to lifeapi_tune_stable_pass%s");
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
   using Fn = void (*)(uint64_t *, uint8_t *, uint64_t, uint32_t, uint32_t);
   const Fn fns[14] = {k_stable<0>, k_stable<1>, k_stable<2>, k_stable<3>, k_stable<4>, k_stable<5>, nullptr, nullptr,
-                      k_stable<0, true>, k_stable<1, true>, k_stable<2, true>, k_stable<3, true>, k_stable<4, true>,
-                      k_stable<5, true>};
+                      k_stable_pf<0>, k_stable_pf<1>, k_stable_pf<2>, k_stable_pf<3>, k_stable_pf<4>, k_stable_pf<5>};
   // blocks_per_cu < 0: uncapped grid, at most -blocks_per_cu blocks resident
   // per CU (unused dynamic LDS out of the CU's 160 KiB)
   unsigned lds = 0;
