@@ -192,16 +192,18 @@ __global__ __launch_bounds__(kBlock) void k_step_ab(const uint64_t *in, uint64_t
 // (gens_split_pipe).
 constexpr int kPipe = -1;
 constexpr int kAsmLoop = -3;  // the hand-allocated rule-11 loop (split_asm.inc)
-template <int S, int G, bool NT, int NET, int D = 0, int V = 0>
-__global__ __launch_bounds__(kBlock) void k_step_split(const uint64_t *in, uint64_t *out, uint64_t n,
-                                                       uint32_t gens, uint64_t /* plain_from: k_step's */) {
+// WPB: waves per block (the tuning build's A/B of finer blocks; the product
+// launches kWavesPerBlock).
+template <int S, int G, bool NT, int NET, int D = 0, int V = 0, int WPB = kWavesPerBlock>
+__global__ __launch_bounds__(WPB * kWave) void k_step_split(const uint64_t *in, uint64_t *out, uint64_t n,
+                                                            uint32_t gens, uint64_t /* plain_from: k_step's */) {
   constexpr int P = S / 2;
-  __shared__ uint32_t lds[kWavesPerBlock * G * S * kWave];
+  __shared__ uint32_t lds[WPB * G * S * kWave];
   const int lane = threadIdx.x & (kWave - 1);
   const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint64_t per_wave = (uint64_t)G * P;
-  const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock * per_wave;
-  for (uint64_t u0 = ((uint64_t)blockIdx.x * kWavesPerBlock + wib) * per_wave; u0 < n; u0 += stride) {
+  const uint64_t stride = (uint64_t)gridDim.x * WPB * per_wave;
+  for (uint64_t u0 = ((uint64_t)blockIdx.x * WPB + wib) * per_wave; u0 < n; u0 += stride) {
     uint32_t r[G][S];
 #pragma unroll
     for (int g = 0; g < G; ++g) {

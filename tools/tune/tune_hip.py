@@ -265,3 +265,15 @@ def fill16(out: torch.Tensor, seed: int, first_universe: int = 0, mode: int = 0,
     hip._check(lib.lifeapi_tune_fill16(out.data_ptr(), hip._universes(out), seed, first_universe, mode,
                                        blocks_per_cu, hip._stream(stream)))
     return out
+
+
+lib.lifeapi_tune_step_split_wpb.argtypes = [_vp, _vp, _sz, _u32, _int, _vp]
+lib.lifeapi_tune_step_split_wpb.restype = _int
+
+
+def step_split_wpb(states: torch.Tensor, out: torch.Tensor, generations: int, wpb: int, stream=None):
+    """the shipped gens > 2 kernel with wpb waves per block (1, 2, 4 = shipped)"""
+    n = hip._universes(states)
+    hip._check(lib.lifeapi_tune_step_split_wpb(states.data_ptr(), out.data_ptr(), n, generations, wpb,
+                                               hip._stream(stream)))
+    return out

@@ -596,6 +596,25 @@ int lifeapi_tune_step_order(const uint64_t *d_in, uint64_t *d_out, size_t n, uin
   return launched("k_step (order) launch");
 }
 
+/* the shipped gens > 2 kernel (k_step_split<8, 1, NT, 6, asm loop>) with
+ * `wpb` waves per block (1, 2 or 4 = shipped): finer blocks let the
+ * dispatcher balance the last round of waves over the SIMDs              */
+int lifeapi_tune_step_split_wpb(const uint64_t *d_in, uint64_t *d_out, size_t n, uint32_t generations, int wpb,
+                                void *stream) {
+  int rc = check_batch(d_in, d_out, n);
+  if (rc != LIFEAPI_OK || n == 0) return rc;
+  const bool nt = generations < 32;
+  const uint64_t waves = (n + 3) / 4;
+  const dim3 grid((unsigned)((waves + wpb - 1) / wpb)), block(64 * wpb);
+  StepFn fn = nullptr;
+  if (wpb == 1) fn = nt ? k_step_split<8, 1, true, 6, kAsmLoop, 0, 1> : k_step_split<8, 1, false, 6, kAsmLoop, 0, 1>;
+  if (wpb == 2) fn = nt ? k_step_split<8, 1, true, 6, kAsmLoop, 0, 2> : k_step_split<8, 1, false, 6, kAsmLoop, 0, 2>;
+  if (wpb == 4) fn = nt ? k_step_split<8, 1, true, 6, kAsmLoop, 0, 4> : k_step_split<8, 1, false, 6, kAsmLoop, 0, 4>;
+  if (!fn) return fail(LIFEAPI_E_INVALID, "waves per block: 1, 2 or 4%s");
+  hipLaunchKernelGGL(fn, grid, block, 0, (hipStream_t)stream, d_in, d_out, (uint64_t)n, generations, (uint64_t)0);
+  return launched("k_step_split (wpb) launch");
+}
+
 /* the shipped gens > 2 kernel with clock stamps (see k_step_split_clock);
  * d_stamps: 4 words per wave, one wave per 4 universes, one-shot grid      */
 int lifeapi_tune_step_clock(const uint64_t *d_in, uint64_t *d_out, size_t n, uint32_t generations,
