@@ -276,7 +276,8 @@ __global__ __launch_bounds__(kBlock) void k_step_contains(const uint64_t *in, ui
   const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const W w = split(wanted[lane]), uw = split(unwanted[lane]);
   const bool rev = (gens & kReverse) != 0;
-  gens &= ~kReverse;
+  const uint64_t blk = (gens & kXcdChunk) ? xcd_chunk_block() : (uint64_t)blockIdx.x;
+  gens &= ~(kReverse | kXcdChunk);
   const uint64_t groups = (n + U - 1) / U, wstride = (uint64_t)gridDim.x * kWavesPerBlock;
   uint64_t *st_w = stage + (WIDE || uses_lds(X) ? wib * U * kWave : 0);
   const int half = lane >> 5, col = (lane & 31) * 2;
@@ -288,10 +289,10 @@ __global__ __launch_bounds__(kBlock) void k_step_contains(const uint64_t *in, ui
     for (int k = 0; k < U; ++k) dst[k] = (v0 + k < n) ? ld<true>(in + (v0 + k) * kWave + lane) : W{0u, 0u};
   };
   if constexpr (PF) {
-    const uint64_t g0 = (uint64_t)blockIdx.x * kWavesPerBlock + wib;
+    const uint64_t g0 = blk * kWavesPerBlock + wib;
     if (g0 < groups) load_group(g0, an);
   }
-  for (uint64_t grp = (uint64_t)blockIdx.x * kWavesPerBlock + wib; grp < groups; grp += wstride) {
+  for (uint64_t grp = blk * kWavesPerBlock + wib; grp < groups; grp += wstride) {
     const uint64_t u0 = (rev ? groups - 1 - grp : grp) * U;
     W a[U];
     if constexpr (PF) {

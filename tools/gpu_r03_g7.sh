@@ -1,3 +1,3 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-timeout -k 10 300 python -u tools/c3_overhead.py > gpurun_out/c3_overhead.jsonl 2> gpurun_out/c3_overhead.err
+timeout -k 10 300 python -u tools/filter_more_ab.py > gpurun_out/filter_more_ab.jsonl 2> gpurun_out/filter_more_ab.err

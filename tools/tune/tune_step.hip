@@ -487,6 +487,9 @@ int lifeapi_tune_step_contains_nat(const uint64_t *d_in, uint64_t *d_final, cons
                                    const uint64_t *d_unwanted, uint32_t *d_first_gen, size_t n,
                                    uint32_t generations, int upw, int resident, void *stream) {
   if (n == 0) return LIFEAPI_OK;
+  // upw + 1024: each XCD a contiguous eighth of the batch (kXcdChunk)
+  const uint32_t chunk = upw >= 1024 ? kXcdChunk : 0u;
+  upw &= 1023;
   if (!d_in || !d_wanted || !d_unwanted || !d_first_gen) return fail(LIFEAPI_E_INVALID, "bad argument%s");
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
@@ -505,18 +508,20 @@ int lifeapi_tune_step_contains_nat(const uint64_t *d_in, uint64_t *d_final, cons
         // 128 + U: the prefetching loop (give a capped grid, resident < 0); 192 + U: with RULE 14
         : upw == 132 ? (Fn)k_step_contains<4, false, XDPP, 3, true> : upw == 136 ? (Fn)k_step_contains<8, false, XDPP, 3, true>
         : upw == 200 ? (Fn)k_step_contains<8, false, XDPP, 14, true>
+        : upw == 16 ? (Fn)k_step_contains<16> : upw == 12 ? (Fn)k_step_contains<12>
         : nullptr;
   if (!fn) return fail(LIFEAPI_E_INVALID, "universes per wave: 1, 2, 4 or 8 (16 + 2, 4, 8: 16-byte form)%s");
   if (upw > 16 && (((uintptr_t)d_in | (uintptr_t)d_final) & 15u))
     return fail(LIFEAPI_E_INVALID, "the 16-byte form needs 16-byte aligned batches%s");
-  upw &= 15;
+  const int universes_per_wave = upw == 16 ? 16 : upw == 12 ? 12 : upw & 15;
   if (resident > 0) {
     rc = occupancy_lds((const void *)fn, resident, lds);
     if (rc != LIFEAPI_OK) return rc;
   }
   // one order, nontemporal stores (the launch before the product's order policy)
-  hipLaunchKernelGGL(fn, dim3(grid_for((n + upw - 1) / upw, cus, cap)), dim3(kBlock), lds, (hipStream_t)stream, d_in,
-                     d_final, d_wanted, d_unwanted, d_first_gen, (uint64_t)n, generations, ~(uint64_t)0);
+  hipLaunchKernelGGL(fn, dim3(grid_for((n + universes_per_wave - 1) / universes_per_wave, cus, cap)), dim3(kBlock), lds,
+                     (hipStream_t)stream, d_in, d_final, d_wanted, d_unwanted, d_first_gen, (uint64_t)n,
+                     generations | chunk, ~(uint64_t)0);
   return launched("k_step_contains (tuning) launch");
 }
 
