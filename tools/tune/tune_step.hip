@@ -146,6 +146,75 @@ __device__ __forceinline__ void st2(uint64_t *p, u64x2 v) {
   else *reinterpret_cast<u64x2 *>(p) = v;
 }
 
+// ---- the streaming step with two adjacent columns per lane (round 3 A/B) --
+// Lane l of a wave holds columns 2i, 2i+1 (i = l & 31) of universe 2k + (l >> 5):
+// one 16-byte access per lane moves two universes per wave-instruction.  Only
+// a lane's outer columns cross lanes: column 2i's left neighbour is lane
+// i-1's column 2i+1 and column 2i+1's right one lane i+1's column 2i (within
+// the 32-lane half, wrapping), fetched by ds_bpermute on the LDS pipe (4 per
+// two universes) instead of DPP moves on the VALU (8 per two universes).
+__device__ __forceinline__ void pair_neighbours(W c0, W c1, W &l1, W &r0, int lane) {
+  const int h = lane & 32, i = lane & 31;
+  const int pa = (h | ((i + 31) & 31)) << 2, na = (h | ((i + 1) & 31)) << 2;
+  l1 = W{(uint32_t)__builtin_amdgcn_ds_bpermute(pa, (int)c1.lo), (uint32_t)__builtin_amdgcn_ds_bpermute(pa, (int)c1.hi)};
+  r0 = W{(uint32_t)__builtin_amdgcn_ds_bpermute(na, (int)c0.lo), (uint32_t)__builtin_amdgcn_ds_bpermute(na, (int)c0.hi)};
+}
+
+template <int U, bool NTS>
+__global__ __launch_bounds__(kBlock) void k_step_pairnat(const uint64_t *in, uint64_t *out, uint64_t n,
+                                                         uint32_t gens, uint64_t plain_from) {
+  static_assert(U % 2 == 0, "universes come in pairs");
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int h = lane >> 5, col = (lane & 31) * 2;
+  const bool rev = (gens & kReverse) != 0;
+  const uint64_t blk = (gens & kXcdChunk) ? xcd_chunk_block() : (uint64_t)blockIdx.x;
+  gens &= ~(kReverse | kXcdChunk);
+  const uint64_t groups = (n + U - 1) / U, wstride = (uint64_t)gridDim.x * kWavesPerBlock;
+  for (uint64_t grp = blk * kWavesPerBlock + wib; grp < groups; grp += wstride) {
+    const uint64_t u0 = (rev ? groups - 1 - grp : grp) * U;
+    W c0[U / 2], c1[U / 2];
+#pragma unroll
+    for (int k = 0; k < U / 2; ++k) {
+      const uint64_t u = u0 + 2 * k + h;
+      const u64x2 v = u < n ? ld2<true>(in + u * kWave + col) : u64x2{0, 0};
+      c0[k] = split(v[0]);
+      c1[k] = split(v[1]);
+    }
+    for (uint32_t g = 0; g < gens; ++g) {
+#pragma unroll
+      for (int k = 0; k < U / 2; ++k) {
+        W l1, r0;
+        pair_neighbours(c0[k], c1[k], l1, r0, lane);
+        const W a0 = c0[k], a1 = c1[k];
+        // column 2i: (L, a, R) = (l1, a0, a1); column 2i+1: (a0, a1, r0)
+        const W h00 = lut3<kXor3>(l1, a0, a1), h10 = lut3<kMaj>(l1, a0, a1);
+        const W h01 = lut3<kXor3>(a0, a1, r0), h11 = lut3<kMaj>(a0, a1, r0);
+        auto tail = [](W a, W h0, W h1) __attribute__((always_inline)) {
+          const W h0u = rot_up(h0), h0d = rot_dn(h0), h1u = rot_up(h1), h1d = rot_dn(h1);
+          const W s0 = lut3<kLe1>(h0u, h0, h0d), s1 = lut3<kNae>(h0u, h0, h0d);
+          const W s2 = lut3<kLe1>(h1u, h1, h1d), s3 = lut3<kEven>(h1u, h1, h1d);
+          const W t1 = lut3<kT1>(s0, s1, a);
+          const W t2 = lut3<kT2>(s2, a, t1);
+          return lut3<kT3>(s1, s3, t2);
+        };
+        c0[k] = tail(a0, h00, h10);
+        c1[k] = tail(a1, h01, h11);
+      }
+    }
+    const bool nt = grp < plain_from;
+#pragma unroll
+    for (int k = 0; k < U / 2; ++k) {
+      const uint64_t u = u0 + 2 * k + h;
+      if (u < n) {
+        const u64x2 v = {join(c0[k]), join(c1[k])};
+        if (nt && NTS) st2<true>(out + u * kWave + col, v);
+        else st2<false>(out + u * kWave + col, v);
+      }
+    }
+  }
+}
+
 template <int S, int C, int X, bool NT, int NET>
 __global__ __launch_bounds__(kBlock) void k_step_tile(const uint64_t *__restrict__ in,
                                                       uint64_t *__restrict__ out, uint64_t n,
@@ -585,8 +654,13 @@ int lifeapi_tune_step_order(const uint64_t *d_in, uint64_t *d_out, size_t n, uin
   int rc = check_batch(d_in, d_out, n);
   if (rc != LIFEAPI_OK || n == 0) return rc;
   if ((generations & ~(kReverse | kXcdChunk)) > 2) return fail(LIFEAPI_E_INVALID, "streaming step: generations <= 2%s");
-  const StepFn fn = upw == 2 ? order_fn<2>(nts) : upw == 4 ? order_fn<4>(nts) : upw == 8 ? order_fn<8>(nts) : nullptr;
+  // upw 32 + U: the column-pair form (k_step_pairnat<U>, 16-byte accesses; 16-byte-aligned batches)
+  const StepFn fn = upw == 2 ? order_fn<2>(nts) : upw == 4 ? order_fn<4>(nts) : upw == 8 ? order_fn<8>(nts)
+                  : upw == 36 ? (nts ? (StepFn)k_step_pairnat<4, true> : (StepFn)k_step_pairnat<4, false>)
+                  : upw == 40 ? (nts ? (StepFn)k_step_pairnat<8, true> : (StepFn)k_step_pairnat<8, false>)
+                  : nullptr;
   if (!fn) return fail(LIFEAPI_E_INVALID, "universes per wave: 2, 4 or 8%s");
+  upw &= 31;
   int cus = 0;
   rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
