@@ -591,11 +591,14 @@ def secondary_config4_1gpu(hip, rt, steps=20, warm=20):
     torch.cuda.empty_cache()
     gb = lambda t: n * BYTES_PER_UNIVERSE_GEN / (t / 1e3) / 1e9 if t else None  # noqa: E731
     spread = (max(ms) - min(ms)) / med
+    q = np.percentile(ms, [10, 90])
+    spread_p = float((q[1] - q[0]) / med)  # robust to a single hiccup (a host interrupt between launches)
     return {"workload": "config4 on 1 GPU: 16777216 universes x 1 generation per launch",
             "value": n / (b2b / 1e3), "value_best": n / (mn / 1e3), "unit": "universe-gen/s",
             "kernel_ms": b2b,
             "kernel_ms_median": med, "kernel_ms_min": mn, "kernel_ms_all": ms,
             "kernel_ms_spread": spread, "flat_within_3pct": spread <= 0.03,
+            "kernel_ms_spread_p10_p90": spread_p, "flat_within_3pct_p10_p90": spread_p <= 0.03,
             "timing": f"{warm} warm launches, then {steps} ping-pong launches each between events on the stream "
                       f"(kernel_ms_all: the series, flatness), then 3 runs of {steps} launches back to back between "
                       "one pair of events, median (kernel_ms, value, roofline: the timed region's method)",
