@@ -63,10 +63,12 @@ const char *lifeapi_step_kernel_name(uint32_t generations);
 /* ---- device-resident, stream-ordered (the hot path) -------------------- */
 
 /* out[u] = in[u] stepped `generations` times (0 = copy), for u < n.  For
- * 1-2 generations and n <= 2M the library alternates, per device, the order
- * in which it walks the batch from one call to the next (a cache-locality
- * choice for back-to-back calls on the batch just written);
- * results never depend on it, and calls from several threads are safe.    */
+ * 1-2 generations and 192K <= n <= 4M a call whose input is a batch an
+ * earlier call wrote walks it in the opposite order to that call (a per-device
+ * book of the last batches written; a cache-locality choice for back-to-back
+ * calls on the batch just written); above 4M each XCD takes a contiguous
+ * eighth of the batch.  Results never depend on either, and
+ * calls from several threads are safe.                                    */
 int lifeapi_step_batch_dev(const uint64_t *d_in, uint64_t *d_out, size_t n,
                            uint32_t generations, void *stream);
 /* d_pop[u] = population of universe u                                     */
