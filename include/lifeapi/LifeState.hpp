@@ -93,7 +93,49 @@ struct alignas(64) LifeState {
     for (int i = 0; i < N; ++i) d |= (state[i] & pat[i]) ^ pat[i];
     return d == 0;
   }
+  bool AreDisjoint(const LifeState &pat) const {  // LifeAPI.hpp:377-386
+    uint64_t d = 0;
+    for (int i = 0; i < N; ++i) d |= state[i] & pat[i];
+    return d == 0;
+  }
+  // the offset forms (LifeAPI.hpp:399-421): target column i against state
+  // column i + dx rotated right by dy
+  bool Contains(const LifeState &pat, int dx, int dy) const {
+    const int y = int(torus_wrap(dy));
+    for (int i = 0; i < N; ++i)
+      if ((std::rotr(state[torus_wrap(i + dx)], y) & pat[i]) != pat[i]) return false;
+    return true;
+  }
+  bool AreDisjoint(const LifeState &pat, int dx, int dy) const {
+    const int y = int(torus_wrap(dy));
+    for (int i = 0; i < N; ++i)
+      if ((std::rotr(state[torus_wrap(i + dx)], y) & pat[i]) != 0) return false;
+    return true;
+  }
   inline bool Contains(const struct LifeTarget &t) const;
+  inline bool Contains(const struct LifeTarget &t, int dx, int dy) const;
+
+  // ---- ZOI (LifeAPI.hpp:521-538): the 3x3 dilation on the torus, and the
+  // cells next to the pattern but not in it
+  LifeState ZOI() const {
+    LifeState v(InitializedTag::UNINITIALIZED), r(InitializedTag::UNINITIALIZED);
+    for (int i = 0; i < N; ++i) v.state[i] = state[i] | std::rotl(state[i], 1) | std::rotr(state[i], 1);
+    for (int i = 0; i < N; ++i)
+      r.state[i] = v.state[(i + N - 1) & (N - 1)] | v.state[i] | v.state[(i + 1) & (N - 1)];
+    return r;
+  }
+  LifeState GetBoundary() const { return ZOI() & ~*this; }
+
+  // ---- Move / Moved (LifeAPI.hpp:682-735): cell (x, y) -> (x + dx, y + dy) on the torus
+  void Move(int dx, int dy) { *this = Moved(dx, dy); }
+  void Move(std::pair<int, int> v) { Move(v.first, v.second); }
+  LifeState Moved(int dx, int dy) const {
+    LifeState r(InitializedTag::UNINITIALIZED);
+    const int y = int(torus_wrap(dy));
+    for (int i = 0; i < N; ++i) r.state[torus_wrap(i + dx)] = std::rotl(state[i], y);
+    return r;
+  }
+  LifeState Moved(std::pair<int, int> v) const { return Moved(v.first, v.second); }
 
   // ---- bitsliced adders (LifeAPI.hpp:822-833)
   static void HalfAdd(uint64_t &out0, uint64_t &out1, uint64_t a, uint64_t b) {
@@ -258,12 +300,17 @@ struct alignas(64) LifeState {
 
 static_assert(sizeof(LifeState) == 512 && alignof(LifeState) == 64, "LifeAPI.hpp:39-40 layout");
 
-// LifeTarget.hpp:5-36 (hot-path subset)
+// LifeTarget.hpp:5-36 (the search-loop subset; no Transform)
 struct LifeTarget {
   LifeState wanted;
   LifeState unwanted;
   LifeTarget() = default;
+  // the pattern and its boundary: the cells around it must be dead (:10-13)
+  explicit LifeTarget(const LifeState &state) : wanted(state), unwanted(state.GetBoundary()) {}
   LifeTarget(const LifeState &w, const LifeState &u) : wanted(w), unwanted(u) {}
+  LifeTarget Moved(std::pair<int, int> v) const {  // :33-35
+    return LifeTarget(wanted.Moved(v), unwanted.Moved(v));
+  }
 };
 
 // LifeTarget.hpp:44-51
@@ -271,6 +318,10 @@ inline bool LifeState::Contains(const LifeTarget &t) const {
   uint64_t d = 0;
   for (int i = 0; i < N; ++i) d |= (state[i] ^ t.wanted[i]) & (t.wanted[i] | t.unwanted[i]);
   return d == 0;
+}
+// LifeTarget.hpp:38-42
+inline bool LifeState::Contains(const LifeTarget &t, int dx, int dy) const {
+  return Contains(t.wanted, dx, dy) && AreDisjoint(t.unwanted, dx, dy);
 }
 
 // NeighbourCount.hpp:7-102 (hot-path subset): inclusive 3x3 count 0..9 as

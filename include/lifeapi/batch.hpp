@@ -173,6 +173,46 @@ std::vector<uint8_t> ContainsBatch(std::span<const S> in, const T &target, int d
   return r;
 }
 
+// The pattern tests (LifeAPI.hpp:377-421) are targets with one plane empty:
+//     s.Contains(pat)          == s.Contains(LifeTarget{pat, {}})
+//     s.AreDisjoint(pat)       == s.Contains(LifeTarget{{}, pat})
+// and their (dx, dy) forms the same against pat Moved(dx, dy).  All run the
+// batched Contains, which reads only the columns the pattern occupies.
+namespace detail {
+template <LifeStateLayout S>
+std::vector<uint8_t> pattern_batch(std::span<const S> in, const uint64_t *pat, bool disjoint, int dx, int dy,
+                                   int device) {
+  uint64_t t[128] = {};
+  const unsigned x = (unsigned)dx & 63u, y = (unsigned)dy & 63u;
+  uint64_t *plane = t + (disjoint ? 64 : 0);
+  for (unsigned i = 0; i < 64; ++i) plane[(i + x) & 63u] = std::rotl(pat[i], (int)y);
+  std::vector<uint8_t> r(in.size());
+  check(lifeapi_contains_batch(words(in.data()), t, t + 64, r.data(), in.size(), device));
+  return r;
+}
+}  // namespace detail
+
+// r[i] = in[i].Contains(pat)  (LifeAPI.hpp:388-397)
+template <LifeStateLayout S, LifeStateLayout P>
+std::vector<uint8_t> ContainsBatch(std::span<const S> in, const P &pat, int device = 0) {
+  return detail::pattern_batch(in, words(&pat), false, 0, 0, device);
+}
+// r[i] = in[i].Contains(pat, dx, dy)  (LifeAPI.hpp:399-409)
+template <LifeStateLayout S, LifeStateLayout P>
+std::vector<uint8_t> ContainsBatch(std::span<const S> in, const P &pat, int dx, int dy, int device = 0) {
+  return detail::pattern_batch(in, words(&pat), false, dx, dy, device);
+}
+// r[i] = in[i].AreDisjoint(pat)  (LifeAPI.hpp:377-386)
+template <LifeStateLayout S, LifeStateLayout P>
+std::vector<uint8_t> AreDisjointBatch(std::span<const S> in, const P &pat, int device = 0) {
+  return detail::pattern_batch(in, words(&pat), true, 0, 0, device);
+}
+// r[i] = in[i].AreDisjoint(pat, dx, dy)  (LifeAPI.hpp:411-421)
+template <LifeStateLayout S, LifeStateLayout P>
+std::vector<uint8_t> AreDisjointBatch(std::span<const S> in, const P &pat, int dx, int dy, int device = 0) {
+  return detail::pattern_batch(in, words(&pat), true, dx, dy, device);
+}
+
 // The search-loop idiom over a batch, in place (LifeAPI.hpp:1196-1216,
 // LifeTarget.hpp:44-51):
 //     for (unsigned g = 1; g <= gens; ++g) { s.Step(); if (!first && s.Contains(target)) first = g; }

@@ -1,0 +1,140 @@
+// cone_kernels.hpp -- Contains(LifeTarget) (LifeTarget.hpp:44-51) and the
+// 1-2 generation search filter (Step(), LifeAPI.hpp:1196-1216, then
+// Contains) reading only the target's light cone.
+//
+// Whether generation g of a universe contains a target depends only on the
+// input columns within distance g of the target's care columns (wanted |
+// unwanted): a cell's next state reads its 3x3 neighbourhood.  Every wave
+// finds the smallest cyclic window [x0, x0 + w) of columns holding the care
+// cells (care_window, the same search as the row window of the iterated
+// kernel) and loads only columns [x0 - g, x0 + w + g) mod 64 -- K = w + 2g
+// columns, K * 8 bytes of each 512-byte universe, so that the 128-byte lines
+// outside never leave HBM.
+//
+// Lane layout: P = the next power of two >= K lanes per universe, 64 / P
+// universes per wave register ("set"); lane j of group q holds column
+// (x0 - g + j) mod 64 of its universe.  The generation is the streaming
+// step's network (life_gen<XDPP, 3>) unchanged: its 64-lane DPP rotate hands
+// a group's edge lanes their neighbour group's columns, which is wrong data
+// -- but only for the g margin columns on either side, which the test never
+// reads (after g generations the error has moved g columns in).  The care
+// columns are exact.  A window with K >= 64 loads the whole board from
+// column 0, where the rotate is the true torus.
+#pragma once
+
+#include "step_kernels.hpp"
+
+namespace lifeapi_impl {
+namespace {
+
+// One wave's UPW universes u0 .. u0 + UPW - 1 under the window (xs = first
+// loaded column, K <= P loaded columns).  FIRST: out[u] = the first
+// generation in 1..gens whose state contains the target (0 = never), else
+// out[u] = Contains(target) of the state as loaded (gens unused).  Register
+// sets go RMAX at a time: all their loads are issued before the first test.
+template <int P, int UPW, int RMAX, bool FIRST, typename OutT>
+__device__ __forceinline__ void cone_wave(const uint64_t *in, const uint64_t *__restrict__ wanted,
+                                          const uint64_t *__restrict__ unwanted, OutT *__restrict__ out,
+                                          uint64_t n, uint64_t u0, uint32_t gens, uint32_t xs, uint32_t K,
+                                          int lane) {
+  constexpr int GPS = kWave / P;  // universes per register set
+  static_assert(UPW % GPS == 0, "a wave takes whole register sets");
+  constexpr int R = UPW / GPS;
+  constexpr int RB = R < RMAX ? R : RMAX;
+  static_assert(R % RB == 0, "passes of RB sets");
+  const uint32_t j = (uint32_t)lane & (P - 1), q = (uint32_t)lane / P;
+  const uint32_t col = (xs + j) & (kWave - 1);
+  const bool live = j < K;
+  // the target's column under this lane (zero outside the window: the care
+  // columns all lie in [x0, x0 + w), and no lane j >= K or margin lane maps
+  // onto one while K <= 64)
+  const uint64_t w64 = live ? wanted[col] : 0ull, m64 = live ? (w64 | unwanted[col]) : 0ull;
+  const W tw = split(w64), tm = split(m64);
+  const uint32_t sh = q * P;
+  auto clean = [&](W s) __attribute__((always_inline)) {
+    const uint32_t d = ((s.lo ^ tw.lo) & tm.lo) | ((s.hi ^ tw.hi) & tm.hi);
+    const uint64_t bad = __ballot(d != 0u);  // wave-uniform
+    if constexpr (P == kWave) return bad == 0ull;
+    else return ((bad >> sh) & ((1ull << P) - 1)) == 0ull;
+  };
+#pragma unroll 1
+  for (int pass = 0; pass < R / RB; ++pass) {
+    const uint64_t ub = u0 + (uint64_t)pass * RB * GPS + q;
+    W a[RB];
+#pragma unroll
+    for (int k = 0; k < RB; ++k) {
+      const uint64_t u = ub + (uint64_t)k * GPS;
+      a[k] = (live && u < n) ? ld<true>(in + u * kWave + col) : W{0u, 0u};
+    }
+    uint32_t res[RB];
+    if constexpr (FIRST) {
+#pragma unroll
+      for (int k = 0; k < RB; ++k) res[k] = 0;
+      for (uint32_t g = 1; g <= gens; ++g) {
+#pragma unroll
+        for (int k = 0; k < RB; ++k) {
+          a[k] = life_gen<XDPP, 3>(a[k], nullptr, lane);
+          if (res[k] == 0 && clean(a[k])) res[k] = g;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < RB; ++k) res[k] = clean(a[k]) ? 1u : 0u;
+    }
+    if (j == 0) {
+#pragma unroll
+      for (int k = 0; k < RB; ++k) {
+        const uint64_t u = ub + (uint64_t)k * GPS;
+        if (u < n) out[u] = (OutT)res[k];
+      }
+    }
+  }
+}
+
+// The column window of the care cells, widened by the light cone of `gens`
+// generations: xs = first column, K = columns (64: the whole board from 0).
+__device__ __forceinline__ void cone_window(const uint64_t *__restrict__ wanted,
+                                            const uint64_t *__restrict__ unwanted, uint32_t gens, int lane,
+                                            uint32_t &xs, uint32_t &K) {
+  const uint64_t cols = __ballot((wanted[lane] | unwanted[lane]) != 0ull);  // bit x: column x has care cells
+  uint32_t x0, w;
+  care_window(cols, x0, w);
+  K = w + 2 * gens;
+  xs = (x0 - gens) & (kWave - 1);
+  if (K >= (uint32_t)kWave) K = kWave, xs = 0;
+}
+
+// UPW universes per wave (one-shot grid of ceil(n / UPW) waves), every wave
+// choosing its lane layout from the window (wave-uniform: the target is the
+// same for all).  Each choice runs its own copy of the pass.
+template <int UPW, int RMAX, bool FIRST, typename OutT>
+__global__ __launch_bounds__(kBlock) void k_cone(const uint64_t *in, const uint64_t *__restrict__ wanted,
+                                                 const uint64_t *__restrict__ unwanted, OutT *__restrict__ out,
+                                                 uint64_t n, uint32_t gens) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint64_t u0 = wave * UPW;
+  if (u0 >= n) return;
+  uint32_t xs, K;
+  cone_window(wanted, unwanted, FIRST ? gens : 0u, lane, xs, K);
+  if (K <= 4) cone_wave<4, UPW, RMAX, FIRST>(in, wanted, unwanted, out, n, u0, gens, xs, K, lane);
+  else if (K <= 8) cone_wave<8, UPW, RMAX, FIRST>(in, wanted, unwanted, out, n, u0, gens, xs, K, lane);
+  else if (K <= 16) cone_wave<16, UPW, RMAX, FIRST>(in, wanted, unwanted, out, n, u0, gens, xs, K, lane);
+  else if (K <= 32) cone_wave<32, UPW, RMAX, FIRST>(in, wanted, unwanted, out, n, u0, gens, xs, K, lane);
+  else cone_wave<64, UPW, RMAX, FIRST>(in, wanted, unwanted, out, n, u0, gens, xs, K, lane);
+}
+
+// the shipped shape (tools/cone_ab.py)
+constexpr int kConeUniverses = 32, kConeSets = 8;
+
+// Launches k_cone on a one-shot grid.
+template <int UPW, int RMAX, bool FIRST, typename OutT>
+int launch_cone(const uint64_t *d_in, const uint64_t *d_wanted, const uint64_t *d_unwanted, OutT *d_out, size_t n,
+                uint32_t gens, int cus, hipStream_t stream) {
+  hipLaunchKernelGGL((k_cone<UPW, RMAX, FIRST, OutT>), dim3(grid_for((n + UPW - 1) / UPW, cus, 0)), dim3(kBlock), 0,
+                     stream, d_in, d_wanted, d_unwanted, d_out, (uint64_t)n, gens);
+  return launched("k_cone launch");
+}
+
+}  // namespace
+}  // namespace lifeapi_impl

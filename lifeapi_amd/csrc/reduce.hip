@@ -4,6 +4,7 @@
 #include "device.hpp"
 #include "host.hpp"
 #include "reduce_kernels.hpp"
+#include "cone_kernels.hpp"
 
 using namespace lifeapi_impl;
 
@@ -115,18 +116,9 @@ int lifeapi_contains_batch_dev(const uint64_t *d_states, const uint64_t *d_wante
     return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_contains_batch_dev%s");
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
-  // 8 universes per wave, one-shot grid (0.0867 ms on 1M against 0.0892 for
-  // 4 per wave on the capped grid, profiles/r02/reduce_ab.jsonl), with
-  // 16-byte loads: 0.0827 against 0.0884 for 8-byte ones, same process
-  // (tools/rows_ab.py, profiles/r03/rows_ab.jsonl); 8-byte-aligned batches
-  // keep the 8-byte kernel
-  if (aligned16(d_states))
-    hipLaunchKernelGGL(k_contains16<8>, dim3(grid_for((n + 7) / 8, cus, 0)), dim3(kBlock), 0,
-                       (hipStream_t)stream, d_states, d_wanted, d_unwanted, d_out, (uint64_t)n);
-  else
-    hipLaunchKernelGGL(k_contains<8>, dim3(grid_for((n + 7) / 8, cus, 0)), dim3(kBlock), 0,
-                       (hipStream_t)stream, d_states, d_wanted, d_unwanted, d_out, (uint64_t)n);
-  return launched("k_contains launch");
+  // only the columns holding the target's care cells (cone_kernels.hpp)
+  return launch_cone<kConeUniverses, kConeSets, false>(d_states, d_wanted, d_unwanted, d_out, n, 0u, cus,
+                                                        (hipStream_t)stream);
 }
 
 int lifeapi_fill_random_dev(uint64_t *d_out, size_t n, uint64_t seed, uint64_t first_universe,

@@ -6,7 +6,7 @@
 // tools/tune/tune_step.hip, and are not part of this library.
 #include <algorithm>
 
-#include "step_kernels.hpp"
+#include "cone_kernels.hpp"
 
 using namespace lifeapi_impl;
 
@@ -154,6 +154,11 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
       if (rc != LIFEAPI_OK) return rc;
     }
     return LIFEAPI_OK;
+  } else if (!d_final) {
+    // the search filter proper (first hits only): the target's light cone
+    // (cone_kernels.hpp)
+    return launch_cone<kConeUniverses, kConeSets, true>(d_in, d_wanted, d_unwanted, d_first_gen, n, generations, cus,
+                                                         (hipStream_t)stream);
   } else {
     // 8 universes per wave, every block slot (tools/filter_ab.py,
     // profiles/r02/filter_ab.jsonl, 1M universes x 1 generation, same

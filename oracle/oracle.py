@@ -222,6 +222,12 @@ class Ref:
         L.ref_weld_step.argtypes = [_u64p, ctypes.c_uint]
         L.ref_unknown_step_refined.argtypes = [_u64p, _u64p]
         L.ref_refined_step_batch.argtypes = [_u64p, _u64p, ctypes.c_size_t]
+        L.ref_stable_pass.argtypes = [_u64p, ctypes.c_int]
+        L.ref_stable_vulnerable.argtypes = [_u64p, _u64p]
+        L.ref_contains_batch.argtypes = [_u64p, ctypes.c_size_t, _u64p, _u64p, ctypes.c_char_p]
+        L.ref_pattern_batch.argtypes = [_u64p, ctypes.c_size_t, _u64p, _u64p, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_int, ctypes.c_char_p]
+        L.ref_target_from_state.argtypes = [_u64p, ctypes.c_int, ctypes.c_int, _u64p, _u64p]
         L.ref_step_contains_batch.argtypes = [_u64p, _u64p, ctypes.c_size_t, ctypes.c_uint, _u64p, _u64p,
                                               ctypes.POINTER(ctypes.c_uint32), ctypes.c_int]
 
@@ -284,6 +290,35 @@ class Ref:
         a, w, u = (np.ascontiguousarray(x, dtype=np.uint64).reshape(64) for x in (state, wanted, unwanted))
         return bool(self.lib.ref_contains_target(_p64(a), _p64(w), _p64(u)))
 
+    def contains_batch(self, states, wanted, unwanted) -> np.ndarray:
+        """uint8 per universe: the reference's Contains(LifeTarget) (LifeTarget.hpp:44-51)"""
+        src = np.ascontiguousarray(states, dtype=np.uint64).reshape(-1, 64)
+        w, u = (np.ascontiguousarray(x, dtype=np.uint64).reshape(64) for x in (wanted, unwanted))
+        out = ctypes.create_string_buffer(max(1, src.shape[0]))
+        self.lib.ref_contains_batch(_p64(src), src.shape[0], _p64(w), _p64(u), out)
+        return np.frombuffer(out.raw[:src.shape[0]], dtype=np.uint8).copy()
+
+    PATTERN_KINDS = ("contains", "disjoint", "contains_at", "disjoint_at", "target_at")
+
+    def pattern_batch(self, states, kind: str, pat, pat2=None, dx: int = 0, dy: int = 0) -> np.ndarray:
+        """uint8 per universe: Contains(pat) / AreDisjoint(pat) / their (dx, dy)
+        forms / Contains(LifeTarget{pat, pat2}, dx, dy) (LifeAPI.hpp:378-422,
+        LifeTarget.hpp:38-42)"""
+        src = np.ascontiguousarray(states, dtype=np.uint64).reshape(-1, 64)
+        p = np.ascontiguousarray(pat, dtype=np.uint64).reshape(64)
+        p2 = np.zeros(64, np.uint64) if pat2 is None else np.ascontiguousarray(pat2, dtype=np.uint64).reshape(64)
+        out = ctypes.create_string_buffer(max(1, src.shape[0]))
+        self.lib.ref_pattern_batch(_p64(src), src.shape[0], _p64(p), _p64(p2), self.PATTERN_KINDS.index(kind),
+                                   dx, dy, out)
+        return np.frombuffer(out.raw[:src.shape[0]], dtype=np.uint8).copy()
+
+    def target_from_state(self, state, dx: int = 0, dy: int = 0):
+        """(wanted, unwanted) of LifeTarget(state).Moved({dx, dy}) (LifeTarget.hpp:10-13,33-35)"""
+        s = np.ascontiguousarray(state, dtype=np.uint64).reshape(64)
+        w, u = np.zeros(64, np.uint64), np.zeros(64, np.uint64)
+        self.lib.ref_target_from_state(_p64(s), dx, dy, _p64(w), _p64(u))
+        return w, u
+
     def neighbour_count(self, state) -> np.ndarray:
         s = np.ascontiguousarray(state, dtype=np.uint64).reshape(64)
         b = np.zeros((4, 64), dtype=np.uint64)
@@ -300,6 +335,18 @@ class Ref:
         out = np.ascontiguousarray(welds, dtype=np.uint64).reshape(-1, 256).copy()
         for u in range(out.shape[0]):
             self.lib.ref_weld_step(_p64(out[u]), gens)
+        return out
+
+    def stable_pass(self, planes: np.ndarray, which: int) -> int:
+        """one LifeStable pass in place on one object's 10 x 64 planes
+        (ref_shim.cpp ref_stable_pass): returns consistent | changed << 1"""
+        assert planes.dtype == np.uint64 and planes.flags.c_contiguous and planes.size == 640
+        return int(self.lib.ref_stable_pass(_p64(planes), which))
+
+    def stable_vulnerable(self, planes: np.ndarray) -> np.ndarray:
+        s = np.ascontiguousarray(planes, dtype=np.uint64).reshape(640)
+        out = np.zeros(64, np.uint64)
+        self.lib.ref_stable_vulnerable(_p64(s), _p64(out))
         return out
 
     def refined_step(self, planes: np.ndarray) -> np.ndarray:

@@ -6,6 +6,10 @@
 // restatement in lifeapi_oracle.c, (2) generate tests/golden/ fixtures, and
 // (3) time the reference's CPU Step() as bench.py's cpu_baseline
 // ("kind": "reference").  Nothing here is shipped in the product.
+#include <cstring>
+#include <thread>
+#include <vector>
+
 #include "LifeAPI.hpp"
 #include "NeighbourCount.hpp"
 #include "LifeTarget.hpp"
@@ -167,6 +171,39 @@ unsigned ref_pop(const uint64_t *s) { return load(s).GetPop(); }
 int ref_contains_target(const uint64_t *s, const uint64_t *wanted, const uint64_t *unwanted) {
   LifeTarget t(load(wanted), load(unwanted));
   return load(s).Contains(t) ? 1 : 0;
+}
+// LifeState::Contains(const LifeTarget&) over a batch: out[u] = 0/1
+void ref_contains_batch(const uint64_t *s, size_t n, const uint64_t *wanted, const uint64_t *unwanted,
+                        uint8_t *out) {
+  const LifeTarget t(load(wanted), load(unwanted));
+  for (size_t u = 0; u < n; ++u) out[u] = load(s + u * 64).Contains(t) ? 1 : 0;
+}
+// The pattern tests over a batch (LifeAPI.hpp:378-422, LifeTarget.hpp:38-42):
+// kind 0 Contains(pat), 1 AreDisjoint(pat), 2 Contains(pat, dx, dy),
+// 3 AreDisjoint(pat, dx, dy), 4 Contains(LifeTarget{pat, pat2}, dx, dy)
+void ref_pattern_batch(const uint64_t *s, size_t n, const uint64_t *pat, const uint64_t *pat2, int kind, int dx,
+                       int dy, uint8_t *out) {
+  const LifeState p = load(pat), p2 = load(pat2);
+  const LifeTarget t(p, p2);
+  for (size_t u = 0; u < n; ++u) {
+    const LifeState a = load(s + u * 64);
+    bool r = false;
+    switch (kind) {
+      case 0: r = a.Contains(p); break;
+      case 1: r = a.AreDisjoint(p); break;
+      case 2: r = a.Contains(p, dx, dy); break;
+      case 3: r = a.AreDisjoint(p, dx, dy); break;
+      default: r = a.Contains(t, dx, dy); break;
+    }
+    out[u] = r ? 1 : 0;
+  }
+}
+// LifeTarget(const LifeState&) (LifeTarget.hpp:10-13) and Moved (:33-35):
+// the unwanted plane GetBoundary() (LifeAPI.hpp:521-538) of the moved target
+void ref_target_from_state(const uint64_t *state, int dx, int dy, uint64_t *wanted, uint64_t *unwanted) {
+  const LifeTarget t = LifeTarget(load(state)).Moved({dx, dy});
+  store(t.wanted, wanted);
+  store(t.unwanted, unwanted);
 }
 // LifeState::Parse  Parsing.hpp:192-198
 void ref_parse(const char *rle, uint64_t *out) { store(LifeState::Parse(std::string(rle)), out); }

@@ -10,7 +10,8 @@
 // for the two image gaps it bridges).  The binary travels to the GPU box with
 // oracle/_ref/; nothing reads /root/reference at run time.  Run by
 // tests/test_cpp_facade.py.  Exit status = number of failed checks.
-#include <lifeapi/batch.hpp>  // first: ref_prelude.hpp defines `constexpr` away
+#include <lifeapi/LifeState.hpp>  // first: ref_prelude.hpp defines `constexpr` away
+#include <lifeapi/batch.hpp>
 
 #include "ref_prelude.hpp"
 
@@ -22,6 +23,7 @@
 #include "Parsing.hpp"
 
 #include <cstdio>
+#include <cstring>
 #include <span>
 #include <vector>
 
@@ -181,6 +183,105 @@ static void StepContains_SearchLoop() {
   EXPECT_TRUE(hits > 0);
 }
 
+// the standalone facade (lifeapi/LifeState.hpp) against the reference
+static lifeapi::LifeState facade(const LifeState &s) {
+  lifeapi::LifeState r;
+  std::memcpy(r.state, s.state, sizeof r.state);
+  return r;
+}
+static bool same(const lifeapi::LifeState &a, const LifeState &b) {
+  return std::memcmp(a.state, b.state, sizeof a.state) == 0;
+}
+
+// LifeTarget(const LifeState&) (LifeTarget.hpp:10-13: unwanted =
+// GetBoundary(), LifeAPI.hpp:521-538), Moved (:33-35, LifeAPI.hpp:699-735),
+// and the single-state pattern tests (LifeAPI.hpp:377-421, LifeTarget.hpp:38-42)
+static void Facade_TargetAndPatternTests() {
+  const int offs[][2] = {{0, 0}, {1, 0}, {0, -1}, {5, -3}, {-7, 60}, {63, 63}, {-64, 1}, {130, -200}};
+  for (int k = 0; k < 200; ++k) {
+    const LifeState pat = LifeState::RandomState() & LifeState::RandomState() & LifeState::RandomState() &
+                          LifeState::Parse("8o$8o$8o$8o$8o$8o!").Moved(k % 64, (7 * k) % 64);
+    const LifeTarget want(pat);
+    const lifeapi::LifeTarget got(facade(pat));
+    EXPECT_TRUE(same(got.wanted, want.wanted) && same(got.unwanted, want.unwanted));
+    EXPECT_TRUE(same(facade(pat).ZOI(), pat.ZOI()) && same(facade(pat).GetBoundary(), pat.GetBoundary()));
+    for (const auto &o : offs) {
+      const LifeTarget wm = want.Moved({o[0], o[1]});
+      const lifeapi::LifeTarget gm = got.Moved({o[0], o[1]});
+      EXPECT_TRUE(same(gm.wanted, wm.wanted) && same(gm.unwanted, wm.unwanted));
+      EXPECT_TRUE(same(facade(pat).Moved(o[0], o[1]), pat.Moved(o[0], o[1])));
+      LifeState s = LifeState::RandomState() & LifeState::RandomState();
+      if (k % 2) s = (s & ~pat.ZOI().Moved(o[0], o[1])) | pat.Moved(o[0], o[1]);
+      const lifeapi::LifeState fs = facade(s);
+      EXPECT_TRUE(fs.Contains(facade(pat), o[0], o[1]) == s.Contains(pat, o[0], o[1]));
+      EXPECT_TRUE(fs.AreDisjoint(facade(pat), o[0], o[1]) == s.AreDisjoint(pat, o[0], o[1]));
+      EXPECT_TRUE(fs.AreDisjoint(facade(pat)) == s.AreDisjoint(pat));
+      EXPECT_TRUE(fs.Contains(got, o[0], o[1]) == s.Contains(want, o[0], o[1]));
+      EXPECT_TRUE(fs.Contains(gm) == s.Contains(wm));
+    }
+  }
+}
+
+// the batched pattern tests on the reference's own ::LifeState:
+// Contains(pat), Contains(pat, dx, dy), AreDisjoint(pat), AreDisjoint(pat, dx, dy)
+static void PatternBatches() {
+  const LifeState glider = LifeState::Parse("bo$2bo$3o!");
+  const int offs[][2] = {{0, 0}, {30, 30}, {62, 5}, {-3, -3}, {100, -70}};
+  for (const auto &o : offs) {
+    std::vector<LifeState> s(3000);
+    for (size_t i = 0; i < s.size(); ++i) {
+      s[i] = LifeState::RandomState() & LifeState::RandomState();
+      if (i % 3 == 0) s[i] |= glider.Moved(o[0], o[1]);
+      if (i % 3 == 1) s[i] &= ~glider.Moved(o[0], o[1]);
+    }
+    const std::span<const LifeState> in(s);
+    const auto c = lifeapi::ContainsBatch(in, glider), co = lifeapi::ContainsBatch(in, glider, o[0], o[1]);
+    const auto d = lifeapi::AreDisjointBatch(in, glider), dd = lifeapi::AreDisjointBatch(in, glider, o[0], o[1]);
+    int hits = 0, apart = 0;
+    for (size_t i = 0; i < s.size(); ++i) {
+      EXPECT_TRUE((c[i] != 0) == s[i].Contains(glider));
+      EXPECT_TRUE((co[i] != 0) == s[i].Contains(glider, o[0], o[1]));
+      EXPECT_TRUE((d[i] != 0) == s[i].AreDisjoint(glider));
+      EXPECT_TRUE((dd[i] != 0) == s[i].AreDisjoint(glider, o[0], o[1]));
+      hits += co[i] != 0;
+      apart += dd[i] != 0;
+    }
+    EXPECT_TRUE(hits >= 1000 && apart >= 1000);
+  }
+}
+
+// A search loop written against the standalone facade with LifeTarget(pattern)
+// (it did not compile before the constructor existed), against the
+// reference's own loop on the same states
+static void Facade_SearchLoopWithPatternTarget() {
+  const LifeState block = LifeState::Parse("2o$2o!").Moved(40, 9);
+  std::vector<LifeState> ref(2000);
+  for (size_t i = 0; i < ref.size(); ++i) {
+    ref[i] = LifeState::RandomState() & LifeState::RandomState();
+    if (i % 4 == 0) ref[i] = (ref[i] & ~block.ZOI()) | block;
+  }
+  std::vector<lifeapi::LifeState> fs(ref.size());
+  for (size_t i = 0; i < ref.size(); ++i) fs[i] = facade(ref[i]);
+  const lifeapi::LifeTarget target(facade(block));
+  const std::vector<uint32_t> got = lifeapi::StepContainsBatch(std::span(fs), target, 1);
+  const std::vector<uint32_t> got6 = lifeapi::StepContainsBatch(std::span(fs), target, 6);
+  const LifeTarget want_t(block);
+  int hits = 0;
+  for (size_t i = 0; i < ref.size(); ++i) {
+    LifeState t = ref[i];
+    uint32_t w1 = 0, w6 = 0;
+    t.Step();
+    if (t.Contains(want_t)) w1 = 1;
+    for (unsigned g = 2; g <= 7; ++g) {
+      t.Step();
+      if (!w6 && t.Contains(want_t)) w6 = g - 1;
+    }
+    EXPECT_TRUE(got[i] == w1 && got6[i] == w6 && same(fs[i], t));
+    hits += w1 != 0;
+  }
+  EXPECT_TRUE(hits >= 300);
+}
+
 // NeighbourCount(state) (NeighbourCount.hpp:40-70)
 static void NeighbourCount_Planes() {
   std::vector<LifeState> s(1000);
@@ -281,6 +382,9 @@ int main() {
   Contains_TargetOffset();
   StepContains_Offset();
   StepContains_SearchLoop();
+  Facade_TargetAndPatternTests();
+  PatternBatches();
+  Facade_SearchLoopWithPatternTarget();
   NeighbourCount_Planes();
   LifeWeld_Step();
   LifeStable_Propagate();

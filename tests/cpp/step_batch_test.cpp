@@ -163,6 +163,34 @@ static void Counts_And_Contains() {
   EXPECT_TRUE(hit[3] != 0);
 }
 
+// the pattern tests and LifeTarget(pattern) on the standalone facade: the
+// batch forms against the facade's own single-state members
+static void Pattern_Batches() {
+  uint64_t seed = 4242;
+  const LifeState loaf = LifeState::Parse("b2o$o2bo$bobo$2bo!");
+  const lifeapi::LifeTarget t(loaf);  // unwanted = loaf.GetBoundary()
+  EXPECT_TRUE(t.unwanted == (loaf.ZOI() & ~loaf) && t.unwanted.GetPop() == 23u);  // 30 cells in the ZOI, 7 live
+  std::vector<LifeState> s(1500);
+  for (size_t i = 0; i < s.size(); ++i) {
+    s[i] = LifeState::RandomState(seed) & LifeState::RandomState(seed);
+    if (i % 3 == 0) s[i] = (s[i] & ~loaf.ZOI().Moved(9, -4)) | loaf.Moved(9, -4);
+  }
+  const std::span<const LifeState> in(s);
+  const auto c = lifeapi::ContainsBatch(in, loaf, 9, -4), d = lifeapi::AreDisjointBatch(in, loaf, 9, -4);
+  const auto c0 = lifeapi::ContainsBatch(in, loaf), d0 = lifeapi::AreDisjointBatch(in, loaf);
+  const auto tm = lifeapi::ContainsBatch(in, t.Moved({9, -4}));
+  int hits = 0;
+  for (size_t i = 0; i < s.size(); ++i) {
+    EXPECT_EQ(c[i] != 0, s[i].Contains(loaf, 9, -4));
+    EXPECT_EQ(d[i] != 0, s[i].AreDisjoint(loaf, 9, -4));
+    EXPECT_EQ(c0[i] != 0, s[i].Contains(loaf));
+    EXPECT_EQ(d0[i] != 0, s[i].AreDisjoint(loaf));
+    EXPECT_EQ(tm[i] != 0, s[i].Contains(t, 9, -4));
+    hits += tm[i] != 0;
+  }
+  EXPECT_TRUE(hits >= 500);
+}
+
 // LifeStable propagation: a block field with an unknown window stays
 // consistent and fills in; an inconsistent (unstable) known region is flagged
 static void Stable_Propagate() {
@@ -226,6 +254,7 @@ int main() {
   HostPin_ManyChunks();
   LifeWeld_StableAndRandom();
   Counts_And_Contains();
+  Pattern_Batches();
   Stable_Propagate();
   Rle_Batch();
   Errors_Throw();

@@ -69,6 +69,27 @@ def test_bench_gpus2_strong_config4_spawns_two_ranks():
     assert c["final_digest"] == _expected_collect(1 << 14, 4, 1 + 1 + 3)
 
 
+def test_bench_gpus8_strong_config4_rehearsal():
+    """The N the scaling target names (8 GPUs, config 4: one 16M problem
+    strong-split), rehearsed at 16K universes: 8 ranks spawned by bench.py
+    itself, each shard on the golden chunk grid (2K universes per rank = one
+    config4_small chunk), every shard verified against the reference-generated
+    digest, all 16K hashes gathered."""
+    line, err = _bench("--gpus", "8", "--config", "4", "--universes", str(1 << 14),
+                       "--steps", "2", "--warmup", "1", "--no-cpu-baseline", timeout=600)
+    assert "torch.distributed.run" in err
+    assert line["n_gpus"] == 8 and line["collective_world_size"] == 8 and line["scaling"] == "strong"
+    assert [p["universes"] for p in line["per_rank"]] == [1 << 11] * 8
+    v = line["verified"]
+    assert v["ok"] is True and v["per_rank_ok"] == [True] * 8 and v["global_ok"] is True
+    assert "config4_small" in v["against"]
+    assert line["value"] > 0 and line["value_cache_neutral"] > 0
+    assert all(p["GBps_cache_neutral"] > 0 for p in line["per_rank"])
+    c = line["collect"]
+    assert c["universes_gathered"] == 1 << 14
+    assert c["final_digest"] == _expected_collect(1 << 14, 4, 1 + 0 + 2)
+
+
 def test_bench_gpus2_weak_config2():
     line, _ = _bench("--gpus", "2", "--config", "2", "--universes", str(1 << 11),
                      "--steps", "2", "--warmup", "1", "--no-cpu-baseline")

@@ -1,0 +1,157 @@
+"""CPU: the light-cone kernels' data flow (lifeapi_amd/csrc/cone_kernels.hpp),
+modelled lane for lane and checked against the oracle's direct answer.
+
+k_cone packs 64 / P universes into one 64-lane register set, lane j of group
+q holding column (xs + j) mod 64 of its universe (zero for j >= K), and steps
+the set with the streaming network, whose neighbour exchange is a 64-lane
+rotate.  A register set is therefore stepped exactly as Step()
+(LifeAPI.hpp:1196-1216) steps a LifeState whose column l is lane l -- so the
+model assembles those "lane states", steps them with the oracle, and applies
+the kernel's per-group test.  Agreement with Contains of the true state
+(LifeTarget.hpp:44-51) on every window shape is the light-cone argument,
+checked without a GPU: the neighbouring groups' columns that the rotate
+brings into a group's margins never reach its care columns within g
+generations.  The window search restates care_window (step_kernels.hpp).
+"""
+import numpy as np
+import pytest
+
+M64 = (1 << 64) - 1
+
+
+def care_window(mask: int):
+    """(x0, w): step_kernels.hpp care_window -- the complement of the longest
+    cyclic run of empty positions, the lowest-starting run on ties; (0, 1)
+    for an empty mask"""
+    if mask == 0:
+        return 0, 1
+    best_len, best_start = 0, 0
+    for p in range(64):
+        run = 0
+        while run < 64 and not (mask >> ((p + run) % 64)) & 1:
+            run += 1
+        if run > best_len:
+            best_len, best_start = run, p
+    if best_len == 0:
+        return 0, 64
+    return (best_start + best_len) % 64, 64 - best_len
+
+
+def cone_layout(wanted, unwanted, gens):
+    cols = 0
+    for x in range(64):
+        if int(wanted[x]) | int(unwanted[x]):
+            cols |= 1 << x
+    x0, w = care_window(cols)
+    K, xs = w + 2 * gens, (x0 - gens) % 64
+    if K >= 64:
+        K, xs = 64, 0
+    P = 4
+    while P < K:
+        P *= 2
+    return xs, K, P
+
+
+def cone_model(port, states, wanted, unwanted, gens, upw=32):
+    """first generation 1..gens containing the target (gens >= 1), or
+    Contains of the state as loaded (gens == 0), as k_cone computes them"""
+    n = len(states)
+    xs, K, P = cone_layout(wanted, unwanted, gens)
+    gps = 64 // P
+    lanes = np.arange(64)
+    j, q = lanes % P, lanes // P
+    col = (xs + j) % 64
+    live = j < K
+    tw = np.where(live, wanted[col], np.uint64(0))
+    tm = np.where(live, wanted[col] | unwanted[col], np.uint64(0))
+    n_sets = -(-n // gps)
+    u = np.arange(n_sets)[:, None] * gps + q[None, :]            # universe of each (set, lane)
+    ok = live[None, :] & (u < n)
+    sets = np.where(ok, states[np.minimum(u, n - 1), col[None, :]], np.uint64(0))
+    res = np.zeros((n_sets, gps), np.uint32)
+
+    def clean(s):
+        bad = ((s ^ tw) & tm) != 0                               # per lane
+        return ~bad.reshape(n_sets, gps, P).any(axis=2)          # per group
+
+    if gens == 0:
+        res = clean(sets).astype(np.uint32)
+    for g in range(1, gens + 1):
+        sets = port.step_batch(sets, 1)                         # the 64-lane rotate = the torus of a lane state
+        c = clean(sets)
+        res[(res == 0) & c] = g
+    return res.reshape(-1)[:n]
+
+
+def direct(port, states, wanted, unwanted, gens):
+    if gens == 0:
+        return (((states ^ wanted) & (wanted | unwanted)) == 0).all(axis=1).astype(np.uint32)
+    first, s = np.zeros(len(states), np.uint32), states
+    for g in range(1, gens + 1):
+        s = port.step_batch(s, 1)
+        hit = (((s ^ wanted) & (wanted | unwanted)) == 0).all(axis=1)
+        first[(first == 0) & hit] = g
+    return first
+
+
+def test_care_window_is_the_smallest_cyclic_window():
+    rng = np.random.default_rng(3)
+    for _ in range(400):
+        k = int(rng.integers(1, 10))
+        mask = 0
+        for c in rng.integers(0, 64, size=k):
+            mask |= 1 << int(c)
+        if rng.random() < 0.3:                                   # a dense block across the seam
+            a = int(rng.integers(64))
+            for i in range(int(rng.integers(1, 64))):
+                mask |= 1 << ((a + i) % 64)
+        x0, w = care_window(mask)
+        cover = sum(1 << ((x0 + i) % 64) for i in range(w))
+        assert mask & ~cover == 0
+        assert w == 64 or (mask >> x0) & 1 and (mask >> ((x0 + w - 1) % 64)) & 1
+        # nothing shorter covers it
+        assert not any(mask & ~sum(1 << ((s + i) % 64) for i in range(w - 1)) == 0 for s in range(64)) or w == 1
+    assert care_window(0) == (0, 1) and care_window(M64) == (0, 64)
+    assert care_window((1 << 63) | 1) == (63, 2)
+
+
+@pytest.mark.parametrize("w", [1, 2, 3, 4, 5, 6, 7, 8, 9, 13, 15, 16, 17, 28, 30, 31, 32, 33, 47, 60, 61, 62, 63, 64])
+def test_cone_model_equals_contains(port, w):
+    rng = np.random.default_rng(w)
+    n = 97                                                       # ragged: partial sets and groups
+    x = port.fill(n, seed=w) & port.fill(n, seed=w + 100)
+    x[::4] = x[0]
+    for x0 in (int(rng.integers(64)), (64 - w // 2) % 64, 63):
+        box = np.zeros(64, np.uint64)
+        for i in range(w):
+            if i in (0, w - 1) or rng.random() < 0.5:
+                box[(x0 + i) % 64] = np.uint64(int(rng.integers(1, 1 << 63)))
+        for g in (0, 1, 2):
+            ahead = port.step_batch(x[:1], g)[0] if g else x[0]
+            tw, tu = ahead & box, box & ~ahead
+            for gens in (0, 1, 2):
+                want = direct(port, x, tw, tu, gens)
+                got = cone_model(port, x, tw, tu, gens)
+                assert (got == want).all(), (w, x0, g, gens, np.nonzero(got != want)[0][:8])
+                if gens == g:
+                    assert want[0] != 0
+
+
+def test_cone_model_without_margins_is_wrong(port):
+    """The margins are necessary: the same model with K = w (no light cone)
+    gets the 1-generation filter wrong on random states -- the check above
+    would notice a kernel that dropped them."""
+    x = port.fill(400, seed=5)
+    tw = np.zeros(64, np.uint64)
+    tu = np.zeros(64, np.uint64)
+    tw[20] = np.uint64(1 << 30)                                   # one live and one dead cell
+    tu[21] = np.uint64(1 << 30)
+    global cone_layout
+    keep = cone_layout
+    try:
+        cone_layout = lambda w_, u_, gens: (20, 2, 4)            # noqa: E731  (no margins)
+        got = cone_model(port, x, tw, tu, 1)
+    finally:
+        cone_layout = keep
+    want = direct(port, x, tw, tu, 1)
+    assert 0 < want.sum() < len(x) and (got != want).any()

@@ -395,3 +395,56 @@ def test_rle_equals_reference(port, ref):
     x[16:, 5] = np.uint64(1) << np.arange(8, dtype=np.uint64) * np.uint64(7)
     for s in x:
         assert port.rle(s) == ref.rle(s)
+
+
+def test_prelude_build_matches_minimal_recipe(ref, port):
+    """The reference shim built with ref_prelude.hpp (`#define constexpr`
+    forced into every translation unit) against the same shim built by
+    SURVEY.md 8(c)'s minimal recipe (oracle/build_ref_sed.sh: only the two
+    corona lines, LifeAPI.hpp:1185,1190, made const in a temporary copy; no
+    prelude): identical on every fixture input and on fresh seeded batches,
+    for every entry point the tests and the bench use."""
+    from oracle.oracle import HERE, Ref
+    sed = os.path.join(HERE, "_ref", "libref_sed.so")
+    if not os.path.exists(sed):
+        pytest.skip("oracle/_ref/libref_sed.so not built (make -C oracle ref)")
+    a, b = ref, Ref(sed)
+    states = [load("random_step.npz")["input"], load("edge_cases.npz")["input"],
+              load("randomstate_kat.npz")["input"], load("contains.npz")["states"],
+              load("counts.npz")["input"], load("rle.npz")["states"], port.fill(512, seed=808)]
+    x = np.concatenate(states)
+    for gens in (1, 2, 7, 64):
+        assert (a.step_batch(x, gens, nthreads=4) == b.step_batch(x, gens, nthreads=4)).all(), gens
+    assert (a.step_alt(x) == b.step_alt(x)).all()
+    assert (a.step_nc(x) == b.step_nc(x)).all()
+    c = load("contains.npz")
+    for w, u in ((c["wanted"], c["unwanted"]), (x[3], x[7] & ~x[3])):
+        fa, sa = a.step_contains_batch(x, w, u, 5, nthreads=4)
+        fb, sb = b.step_contains_batch(x, w, u, 5, nthreads=4)
+        assert (fa == fb).all() and (sa == sb).all()
+        assert (a.contains_batch(x, w, u) == b.contains_batch(x, w, u)).all()
+        for kind in Ref.PATTERN_KINDS:
+            assert (a.pattern_batch(x, kind, w, u, 5, -3) == b.pattern_batch(x, kind, w, u, 5, -3)).all(), kind
+    for s in x[:64]:
+        assert (a.neighbour_count(s) == b.neighbour_count(s)).all()
+        assert (a.interaction_counts(s) == b.interaction_counts(s)).all()
+        assert a.rle(s) == b.rle(s) and a.pop(s) == b.pop(s)
+        assert all((p == q).all() for p, q in zip(a.target_from_state(s, 3, -9), b.target_from_state(s, 3, -9)))
+    r = load("rle.npz")
+    for u in range(len(r["parse_offsets"]) - 1):
+        t = bytes(r["parse_text"][int(r["parse_offsets"][u]):int(r["parse_offsets"][u + 1])]).decode()
+        assert (a.parse(t) == b.parse(t)).all()
+    wl = load("weld.npz")["input"]
+    assert (a.weld_step(wl, 7) == b.weld_step(wl, 7)).all()
+    rf = load("refined_step.npz")["input"]
+    assert (a.refined_step(rf) == b.refined_step(rf)).all()
+    st = load("stable.npz")["input"]
+    for which in range(6):
+        pa, pb = st.copy(), st.copy()
+        for u in range(len(st)):
+            fa_ = a.stable_pass(pa[u], which)
+            fb_ = b.stable_pass(pb[u], which)
+            assert fa_ == fb_
+        assert (pa == pb).all(), which
+    for u in range(len(st)):
+        assert (a.stable_vulnerable(st[u]) == b.stable_vulnerable(st[u])).all()

@@ -249,3 +249,70 @@ def test_search_loop_beyond_2_32_words(hip, R, port, gens):
     assert len(seen) >= 2, seen
     del d, first
     torch.cuda.empty_cache()
+
+
+def _column_box_target(rng, state, x0, w):
+    """a target whose care cells (wanted | unwanted) span exactly the cyclic
+    columns [x0, x0 + w): the box of those columns x random rows, wanted =
+    the state's live cells in it, unwanted = its dead cells"""
+    cols = [(x0 + i) % 64 for i in range(w)]
+    keep = [cols[0], cols[-1]] + [c for c in cols[1:-1] if rng.random() < 0.6]
+    box = np.zeros(64, np.uint64)
+    for c in keep:
+        box[c] = np.uint64(int(rng.integers(1, 1 << 63)) | 1 << int(rng.integers(64)))
+    return state & box, box & ~state
+
+
+CONE_WIDTHS = [1, 2, 3, 4, 5, 6, 7, 8, 9, 12, 14, 15, 16, 17, 28, 30, 31, 32, 33, 40, 60, 61, 62, 63, 64]
+
+
+@pytest.mark.parametrize("w", CONE_WIDTHS)
+def test_cone_contains_and_filter_vs_reference(hip, R, port, w):
+    """The light-cone kernels (cone_kernels.hpp): batched Contains(LifeTarget)
+    and the 1-2 generation search filter with first hits only, against the
+    reference's own Contains (LifeTarget.hpp:44-51) and Step() + Contains loop,
+    on targets whose care columns span exactly w columns -- every lane layout
+    (P = 4 .. 64 lanes per universe, margins included), windows straddling
+    the column seam 63|0, and w + 2g >= 64 (the whole board).  Universe 0's
+    own future is the target, and every 5th universe is a copy of it, so hits
+    and misses both occur."""
+    rng = np.random.default_rng(1000 + w)
+    n = 4099                                     # ragged against 32 universes per wave
+    x = port.fill(n, seed=200 + w) & port.fill(n, seed=300 + w)
+    x[::5] = x[0]
+    for x0 in (int(rng.integers(64)), 64 - w // 2 if w > 1 else 63, 0):
+        for g in (0, 1, 2):
+            ahead = R.step_batch(x[:1], g)[0] if g else x[0]
+            tw, tu = _column_box_target(rng, ahead, x0, w)
+            dw, du = to_dev(tw[None]), to_dev(tu[None])
+            if g == 0:
+                got = hip.contains(to_dev(x), dw, du).cpu().numpy()
+                want = R.contains_batch(x, tw, tu)
+                assert (got == want).all(), (w, x0, np.nonzero(got != want)[0][:8])
+                assert want[0] == 1 and 0 < want.sum() < n
+            for gens in (0, 1, 2):
+                first, _ = hip.step_contains(to_dev(x), dw, du, gens)
+                exp, _ = R.step_contains_batch(x, tw, tu, gens, nthreads=THREADS)
+                got = first.cpu().numpy().astype(np.uint32)
+                assert (got == exp).all(), (w, x0, g, gens, np.nonzero(got != exp)[0][:8])
+                if gens >= g >= 1:
+                    assert 1 <= exp[0] <= g
+
+
+@pytest.mark.parametrize("n", [1, 2, 15, 16, 17, 31, 33, 65, 127])
+def test_cone_ragged_and_empty_target_vs_reference(hip, R, port, n):
+    """ragged batches (partial register sets and waves) for a narrow and a
+    wide window, and the empty target (contained by every state)"""
+    rng = np.random.default_rng(n)
+    x = port.fill(n, seed=900 + n) & port.fill(n, seed=901 + n)
+    zero = np.zeros(64, np.uint64)
+    targets = [_column_box_target(rng, x[0], 62, 3), _column_box_target(rng, x[-1], 5, 40), (zero, zero)]
+    for tw, tu in targets:
+        dw, du = to_dev(tw[None]), to_dev(tu[None])
+        assert (hip.contains(to_dev(x), dw, du).cpu().numpy() == R.contains_batch(x, tw, tu)).all()
+        for gens in (1, 2):
+            first, _ = hip.step_contains(to_dev(x), dw, du, gens)
+            exp, _ = R.step_contains_batch(x, tw, tu, gens)
+            assert (first.cpu().numpy().astype(np.uint32) == exp).all(), (n, gens)
+    first, _ = hip.step_contains(to_dev(x), to_dev(zero[None]), to_dev(zero[None]), 2)
+    assert (first.cpu().numpy() == 1).all()

@@ -210,3 +210,39 @@ def test_step_contains_pair_capped_grid(tune, hip, port, caps, kind):
     ship, shipfin = hip.step_contains(to_dev(x), to_dev(w[None]), to_dev(u[None]), gens, final=torch.empty_like(fin))
     assert torch.equal(got, ship) and torch.equal(fin, shipfin)
     assert (to_host(fin) == port.step_batch(x, gens)).all()
+
+
+CONE_SHAPES = [(16, 4), (16, 8), (16, 16), (32, 4), (32, 8), (32, 16), (32, 32), (64, 8), (64, 16), (64, 32)]
+
+
+@pytest.mark.parametrize("upw,rmax", CONE_SHAPES)
+def test_cone_shapes(tune, port, upw, rmax):
+    """every measured shape of the light-cone kernel (tune_cone.hip) against
+    the oracle: Contains and the 1-2 generation filter, windows of 1..64
+    columns anywhere on the board, a ragged batch"""
+    rng = np.random.default_rng(upw * 100 + rmax)
+    n = 1031
+    x = port.fill(n, seed=upw + rmax) & port.fill(n, seed=7 * upw + rmax)
+    x[::3] = x[0]
+    d = to_dev(x)
+    for w in (1, 3, 6, 13, 29, 31, 60, 64):
+        x0 = int(rng.integers(64))
+        box = np.zeros(64, np.uint64)
+        for c in {x0 % 64, (x0 + w - 1) % 64}:
+            box[c] = np.uint64(int(rng.integers(1, 1 << 63)))
+        for gens in (0, 1, 2):
+            ahead = port.step_batch(x[:1], gens)[0] if gens else x[0]
+            tw, tu = ahead & box, box & ~ahead
+            want = np.zeros(n, np.uint32)
+            s = x.copy()
+            if gens == 0:
+                want = (((x ^ tw) & (tw | tu)) == 0).all(axis=1).astype(np.uint8)
+                got = tune.cone(d, to_dev(tw[None]), to_dev(tu[None]), 0, upw, rmax, first=False).cpu().numpy()
+            else:
+                for g in range(1, gens + 1):
+                    s = port.step_batch(s, 1)
+                    hit = (((s ^ tw) & (tw | tu)) == 0).all(axis=1)
+                    want[(want == 0) & hit] = g
+                got = tune.cone(d, to_dev(tw[None]), to_dev(tu[None]), gens, upw, rmax).cpu().numpy()
+            assert (got.astype(np.uint32) == want).all(), (w, x0, gens, np.nonzero(got != want)[0][:8])
+            assert want[0] != 0

@@ -1,0 +1,51 @@
+// tune_cone.hip -- TUNING build: shapes of the light-cone Contains / search
+// filter (k_cone, lifeapi_amd/csrc/cone_kernels.hpp) for A/Bs.  Every shape
+// computes the same answers as the shipped one.
+#include "lifeapi_tune.h"
+#include "cone_kernels.hpp"
+
+using namespace lifeapi_impl;
+
+namespace {
+
+template <bool FIRST, typename OutT>
+int cone_by_shape(const uint64_t *in, const uint64_t *w, const uint64_t *u, OutT *out, size_t n, uint32_t gens,
+                  int upw, int rmax, int cus, hipStream_t st) {
+#define LIFEAPI_CONE(U, R) \
+  if (upw == U && rmax == R) return launch_cone<U, R, FIRST>(in, w, u, out, n, gens, cus, st);
+  LIFEAPI_CONE(16, 4)
+  LIFEAPI_CONE(16, 8)
+  LIFEAPI_CONE(16, 16)
+  LIFEAPI_CONE(32, 4)
+  LIFEAPI_CONE(32, 8)
+  LIFEAPI_CONE(32, 16)
+  LIFEAPI_CONE(32, 32)
+  LIFEAPI_CONE(64, 8)
+  LIFEAPI_CONE(64, 16)
+  LIFEAPI_CONE(64, 32)
+#undef LIFEAPI_CONE
+  return fail(LIFEAPI_E_INVALID, "cone shapes: upw 16/32/64 x rmax 4/8/16/32%s");
+}
+
+}  // namespace
+
+extern "C" {
+
+/* first != 0: the search filter (d_out uint32 first generations, gens <= 2);
+ * first == 0: Contains (d_out uint8).  upw universes per wave, rmax register
+ * sets per pass. */
+int lifeapi_tune_cone(int first, const uint64_t *d_in, const uint64_t *d_wanted, const uint64_t *d_unwanted,
+                      void *d_out, size_t n, uint32_t gens, int upw, int rmax, void *stream) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!d_in || !d_wanted || !d_unwanted || !d_out || gens > 2)
+    return fail(LIFEAPI_E_INVALID, "bad argument to lifeapi_tune_cone%s");
+  int cus = 0, rc = device_cus(cus);
+  if (rc != LIFEAPI_OK) return rc;
+  if (first)
+    return cone_by_shape<true>(d_in, d_wanted, d_unwanted, (uint32_t *)d_out, n, gens, upw, rmax, cus,
+                               (hipStream_t)stream);
+  return cone_by_shape<false>(d_in, d_wanted, d_unwanted, (uint8_t *)d_out, n, 0u, upw, rmax, cus,
+                              (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -277,3 +277,19 @@ def step_split_wpb(states: torch.Tensor, out: torch.Tensor, generations: int, wp
     hip._check(lib.lifeapi_tune_step_split_wpb(states.data_ptr(), out.data_ptr(), n, generations, wpb,
                                                hip._stream(stream)))
     return out
+
+
+lib.lifeapi_tune_cone.argtypes = [_int, _vp, _vp, _vp, _vp, _sz, _u32, _int, _int, _vp]
+lib.lifeapi_tune_cone.restype = _int
+
+
+def cone(states, wanted, unwanted, generations, upw, rmax, first=True, out=None, stream=None):
+    """the light-cone kernel (k_cone) with `upw` universes per wave and `rmax`
+    register sets per pass: first generations (int32, first=True, gens <= 2)
+    or Contains (uint8)"""
+    n = hip._universes(states)
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32 if first else torch.uint8, device=states.device)
+    hip._check(lib.lifeapi_tune_cone(1 if first else 0, states.data_ptr(), wanted.data_ptr(), unwanted.data_ptr(),
+                                     out.data_ptr(), n, generations, upw, rmax, hip._stream(stream)))
+    return out
