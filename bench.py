@@ -216,6 +216,45 @@ def back_to_back_ms(rt, fn, a, b, reps=20, warm=5, repeats=3):
     return float(np.median(runs))
 
 
+SCRUB_MIB = 768  # > 2 x the 256 MiB Infinity Cache (MI355X_MICROARCH.md, memory hierarchy)
+
+
+class Scrub:
+    """SCRUB_MIB of unrelated plain reads and writes (one torch add_ on the
+    rank's stream): run before a timed launch, it leaves nothing that launch
+    reads in the 256 MiB memory-side Infinity Cache or the L2s, so the launch
+    is timed from HBM alone."""
+
+    def __init__(self, rt, mib=SCRUB_MIB):
+        self.rt, self.mib = rt, mib
+        self.buf = torch.zeros(mib << 17, dtype=torch.int64, device=rt.device)
+
+    def __call__(self):
+        with torch.cuda.stream(self.rt.stream):
+            self.buf.add_(1)
+
+
+def scrubbed_ms(rt, fn, a, b, scrub, reps=10, warm=3):
+    """per-launch ms of fn(src, dst) ping-ponged between a and b with a scrub
+    before every launch: `warm` untimed launches, then `reps` launches each
+    between a pair of events on the rank's stream that bracket the launch
+    only (not the scrub).  Returns (median, all)."""
+    bufs = [a, b]
+    for k in range(warm):
+        scrub()
+        fn(bufs[k % 2], bufs[1 - k % 2])
+    ms = []
+    for k in range(reps):
+        scrub()
+        e0, e1 = rt.event(), rt.event()
+        e0.record(rt.stream)
+        fn(bufs[(warm + k) % 2], bufs[1 - (warm + k) % 2])
+        e1.record(rt.stream)
+        e1.synchronize()
+        ms.append(e0.elapsed_time(e1))
+    return float(np.median(ms)), ms
+
+
 def side_fn(rt, gens, neutral):
     """A side launch of the shipped streaming kernel's code through the
     tuning build (tools/tune step_order, kernel k_step_ab: the same code as
@@ -264,6 +303,11 @@ def stream_figures(hip, rt, a, b, gens, reps=20):
     for key, g, neu in (("neutral_ms", gens, True), ("copy_ms", 0, False), ("copy_neutral_ms", 0, True)):
         fn = side_fn(rt, g, neu)
         out[key] = back_to_back_ms(rt, fn, a, b, reps) if fn is not None else None
+    # the shipped launch itself with a scrub before each launch: HBM only
+    scrub = Scrub(rt) if rt.kind == "hip" else (lambda: None)
+    out["scrubbed_ms"], _ = scrubbed_ms(rt, lambda x, y: hip.step(x, out=y, generations=gens, stream=rt.stream),
+                                        a, b, scrub)
+    del scrub
     out["bytes"] = n * BYTES_PER_UNIVERSE_GEN
     return out
 
@@ -606,12 +650,100 @@ def secondary_config4_1gpu(hip, rt, steps=20, warm=20):
             "verified": digest == golden_digest("config4"),
             "roofline": {"bound": "hbm", "achieved": gb(b2b), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": gb(b2b) / HBM_PEAK_GBS,
-                         "cache_neutral": {"achieved": gb(figs["neutral_ms"]),
-                                           "frac": gb(figs["neutral_ms"]) / HBM_PEAK_GBS
-                                           if figs["neutral_ms"] else None,
-                                           "kernel_ms": figs["neutral_ms"]},
-                         "copy_ceiling_GBps": gb(figs["copy_ms"]),
-                         "copy_ceiling_cache_neutral_GBps": gb(figs["copy_neutral_ms"])}}
+                         "cache_neutral": {"achieved": gb(figs["scrubbed_ms"]),
+                                           "frac": gb(figs["scrubbed_ms"]) / HBM_PEAK_GBS,
+                                           "kernel_ms": figs["scrubbed_ms"],
+                                           "method": "the shipped launch after a 768 MiB scrub, events "
+                                                     "around the launch only, median of 10"},
+                         "fixed_order_nt_back_to_back": {"achieved": gb(figs["neutral_ms"]),
+                                                         "kernel_ms": figs["neutral_ms"]},
+                         "copy_same_shape_GBps": gb(figs["copy_ms"]),
+                         "copy_note": "the step kernel's code with 0 generations in the same launch shape; at "
+                                      "16M universes it runs below the step, so it is no ceiling here"},
+            "kernel": hip.step_kernel_name(1, n)}
+
+
+def _cone_columns(wanted: np.ndarray, unwanted: np.ndarray, gens: int):
+    """(first column, columns) the light-cone kernels load for this target
+    (cone_kernels.hpp cone_window: the smallest cyclic window of the care
+    columns, widened by `gens` on each side; the whole board from column 0
+    once that reaches 64)"""
+    care = [bool(int(wanted[x]) | int(unwanted[x])) for x in range(64)]
+    if not any(care):
+        x0, w = 0, 1
+    else:
+        run, start = 0, 0
+        for p in range(64):
+            r = 0
+            while r < 64 and not care[(p + r) % 64]:
+                r += 1
+            if r > run:
+                run, start = r, p
+        x0, w = (start + run) % 64, 64 - run
+    k = w + 2 * gens
+    return (0, 64) if k >= 64 else ((x0 - gens) % 64, k)
+
+
+def _lines_touched(xs: int, k: int, line: int = 128) -> int:
+    """128-byte lines of one 512-byte universe holding columns [xs, xs + k) mod 64"""
+    return len({((xs + i) % 64) * 8 // line for i in range(k)})
+
+
+def secondary_filter(hip, rt):
+    """The search filter as loops consume Step (SURVEY 8(f) row 1,
+    LifeTarget.hpp:44-51): 1M config-2 universes, Step() then
+    Contains(target), first hits only -- and batched Contains alone -- on the
+    light-cone kernels (cone_kernels.hpp), which read only the columns within
+    one generation of the target's care columns.  Each launch is timed alone
+    after a 768 MiB scrub (the cone of a small target fits in the Infinity
+    Cache, so back-to-back launches on one input would read it from there);
+    results checked against the reference's own loop
+    (tests/golden/golden.json digests.config2_filter, ref_shim.cpp)."""
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "golden.json")) as f:
+            gold = json.load(f)["digests"]["config2_filter"]
+    except (OSError, ValueError, KeyError):
+        return None
+    n = gold["universes"]
+    x = hip.fill_random(n, seed=gold["seed"], device=rt.device, stream=rt.stream)
+    scrub = Scrub(rt)
+    out = {"workload": f"config2 input: {n} universes, Step() then Contains(target) (first hits only), "
+                       "and Contains(target) alone",
+           "timing": "3 warm, 10 timed launches, each after a 768 MiB scrub, events around the launch only, "
+                     "median; b2b: 20 launches back to back on the same input (Infinity Cache warm)",
+           "targets": {}}
+    for name, t in gold["targets"].items():
+        w, u = (np.array([int(v, 16) for v in t[k]], dtype=np.uint64) for k in ("wanted", "unwanted"))
+        tw, tu = (torch.from_numpy(v.view(np.int64)[None].copy()).to(rt.device) for v in (w, u))
+        first, _ = hip.step_contains(x, tw, tu, 1, stream=rt.stream)
+        cont = hip.contains(x, tw, tu, stream=rt.stream)
+        rt.sync()
+        fd = f"{batch_digest(first.cpu().numpy().astype(np.uint64)):016x}"
+        cd = f"{batch_digest(cont.cpu().numpy().astype(np.uint64)):016x}"
+        hits = int((first > 0).sum().item())
+        row = {"verified": fd == t["first_digest"] and hits == t["hits"] and cd == t["contains_digest"],
+               "hits": hits}
+        for op, gens, outb, fn in (
+                ("filter_1gen", 1, 4, lambda a, b: hip.step_contains(a, tw, tu, 1, stream=rt.stream)),
+                ("contains", 0, 1, lambda a, b: hip.contains(a, tw, tu, stream=rt.stream))):
+            xs, k = _cone_columns(w, u, gens)
+            lines = _lines_touched(xs, k)
+            ms, allms = scrubbed_ms(rt, fn, x, x, scrub)
+            b2b = back_to_back_ms(rt, fn, x, x)
+            row[op] = {"objects_per_s": n / (ms / 1e3), "kernel_ms": ms, "kernel_ms_all": allms,
+                       "kernel_ms_b2b": b2b, "objects_per_s_b2b": n / (b2b / 1e3),
+                       "cone_columns": k, "cone_first_column": xs, "lines_128B_per_universe": lines,
+                       "roofline": {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+                                    "algorithmic_bytes_per_universe": lines * 128 + outb,
+                                    "achieved": n * (lines * 128 + outb) / (ms / 1e3) / 1e9,
+                                    "frac": n * (lines * 128 + outb) / (ms / 1e3) / 1e9 / HBM_PEAK_GBS,
+                                    "definition": "the 128-byte lines of each universe that hold its light "
+                                                  "cone (the fetch granularity) + the output, per launch"},
+                       "full_read_equivalent_GBps": n * (512 + outb) / (ms / 1e3) / 1e9}
+        out["targets"][name] = row
+    del scrub, x
+    torch.cuda.empty_cache()
+    return out
 
 
 def secondary_config5(hip, rt):
@@ -721,7 +853,7 @@ def main(argv=None):
     # side figures on the rank's own buffers (after the hashes: they overwrite
     # both): cache-neutral step and live copy ceilings, gathered per rank
     figs = stream_figures(hip, rt, final, bufs[1 - cur], gens) if gens <= 2 else None
-    fig_keys = ("neutral_ms", "copy_ms", "copy_neutral_ms")
+    fig_keys = ("scrubbed_ms", "copy_ms", "copy_neutral_ms", "neutral_ms")
     fv = [(-1.0 if figs is None or figs[k] is None else figs[k]) for k in fig_keys]
     if world > 1:
         ft = torch.tensor(fv, dtype=torch.float64, device=COLL_DEV)
@@ -747,7 +879,8 @@ def main(argv=None):
     if rank == 0 and world == 1 and not args.no_secondary and rt.kind == "hip":
         csec = 0.0 if args.no_cpu_baseline else args.cpu_seconds / 3
         secondary = {"config3": secondary_config3(hip, rt, csec),
-                     "config5": secondary_config5(hip, rt)}
+                     "config5": secondary_config5(hip, rt),
+                     "filter": secondary_filter(hip, rt)}
         if cfg == 2:
             del a, b, bufs, final
             torch.cuda.empty_cache()
@@ -779,6 +912,7 @@ def main(argv=None):
         neu = [gbps(f[0], c) for f, (_, c) in zip(rank_figs, per_rank)]
         cpy = [copy_gbps(f[1], c) for f, (_, c) in zip(rank_figs, per_rank)]
         cpy_neu = [copy_gbps(f[2], c) for f, (_, c) in zip(rank_figs, per_rank)]
+        fixed = [gbps(f[3], c) for f, (_, c) in zip(rank_figs, per_rank)]
         agg_neu = sum(neu) if all(v is not None for v in neu) else None
         val_neu = (sum(c * gens / (f[0] / 1e3) for f, (_, c) in zip(rank_figs, per_rank))
                    if all(f[0] for f in rank_figs) else None)
@@ -793,35 +927,48 @@ def main(argv=None):
                                     f"per step, split into {world} contiguous shards"),
                        "universes_per_gpu": n_rank, "global_universes": n_total, "gens_per_step": gens,
                        "parallelism": f"dp{world} (contiguous universe shards, no data-path collective)",
-                       "kernel": hip.step_kernel_name(gens)},
+                       "kernel": hip.step_kernel_name(gens, n)},
             "cell_updates_per_s": value * 4096,
             "kernel_ms_avg": avg_launch,
             "kernel_timing": "HIP events on the launch stream around the K timed launches / K",
             "per_rank": [{"rank": r, "universes": c, "kernel_ms_avg": ms,
                           "GBps": c * gens * BYTES_PER_UNIVERSE_GEN / (ms / 1e3) / 1e9 if gens == 1 else None,
                           "kernel_ms_cache_neutral": rank_figs[r][0], "GBps_cache_neutral": neu[r],
+                          "GBps_fixed_order_nt_back_to_back": fixed[r],
                           "copy_GBps": cpy[r], "copy_GBps_cache_neutral": cpy_neu[r]}
                          for r, (ms, c) in enumerate(per_rank)],
             "value_cache_neutral": val_neu,
             "value_cache_neutral_note": ("universe-gen/s if every rank ran its shard at its cache-neutral rate "
-                                         "(the same kernel in one fixed order with all stores nontemporal, "
-                                         "timed per rank after the timed region): the 8-vs-1 ratio without "
-                                         "Infinity Cache reuse on either side"),
+                                         "(the shipped launch timed alone after a 768 MiB scrub of the "
+                                         "Infinity Cache, per rank after the timed region): the 8-vs-1 ratio "
+                                         "without Infinity Cache reuse on either side"),
             "collective_world_size": coll_world,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-                         "frac_kind": "effective: algorithmic bytes / launch time; with the batch-keyed "
-                                      "launch order and the plain-stored tail part of each launch's reads are "
-                                      "served by the 256 MB memory-side Infinity Cache (DESIGN.md 3.1, 5.2); "
-                                      "cache_neutral is the HBM-only figure",
+                         "frac_kind": ("effective: algorithmic bytes / launch time; with the batch-keyed "
+                                       "launch order and the plain-stored tail part of each launch's reads are "
+                                       "served by the 256 MB memory-side Infinity Cache (DESIGN.md 3.1, 5.2); "
+                                       "cache_neutral is the HBM-only figure"
+                                       if n <= (1 << 22) else
+                                       "effective: algorithmic bytes / launch time; above 4M universes per "
+                                       "GPU the launch takes one order with every store nontemporal "
+                                       "(nothing is arranged for Infinity Cache reuse); cache_neutral is the "
+                                       "HBM-only figure"),
                          "cache_neutral": ({"achieved": neu[0], "frac": neu[0] / HBM_PEAK_GBS,
                                             "kernel_ms": rank_figs[0][0],
-                                            "method": "the step kernel's code (k_step_ab), same size, same "
-                                                      "process, rank 0: one fixed group order, every store "
-                                                      "nontemporal, no plain-stored tail (tools/tune "
-                                                      "step_order), 5 warm ping-pong launches, then 3 runs of "
-                                                      "20 back to back between one pair of events, median"}
+                                            "method": "the shipped launch (lifeapi_step_batch_dev), same size, "
+                                                      "same process, rank 0, with a 768 MiB scrub (plain "
+                                                      "read + write of an unrelated buffer) on the stream "
+                                                      "before each launch and events around the launch only: "
+                                                      "3 warm, 10 timed ping-pong launches, median"}
                                            if neu[0] else None),
+                         "fixed_order_nt_back_to_back": ({"achieved": fixed[0], "frac": fixed[0] / HBM_PEAK_GBS,
+                                                          "kernel_ms": rank_figs[0][3],
+                                                          "method": "round 3's cache-neutral form: the step "
+                                                                    "kernel's code (k_step_ab) in one fixed order, "
+                                                                    "every store nontemporal, 20 launches back to "
+                                                                    "back, median of 3 runs"}
+                                                         if fixed[0] else None),
                          "cache_gain": (achieved / neu[0] - 1) if (achieved and neu[0]) else None,
                          "traffic": traffic, "traffic_source": tsrc,
                          "traffic_note": "FETCH_SIZE/WRITE_SIZE count L2-to-fabric bytes, so reads the "

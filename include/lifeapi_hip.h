@@ -57,7 +57,10 @@ int lifeapi_abi_version(void);
 const char *lifeapi_last_error(void);
 int lifeapi_device_count(void);
 /* which shipped kernel configuration lifeapi_step_batch[_dev] runs for this
- * many generations (a static string, for logs and benchmark records)       */
+ * many generations on a batch of n universes (the launch shape changes with
+ * the batch size above 4M universes; a static string, for logs and benchmark
+ * records); lifeapi_step_kernel_name(g) is the name for batches of at most 4M */
+const char *lifeapi_step_kernel_name_n(uint32_t generations, size_t n);
 const char *lifeapi_step_kernel_name(uint32_t generations);
 
 /* ---- device-resident, stream-ordered (the hot path) -------------------- */

@@ -91,6 +91,41 @@ __device__ __forceinline__ void cone_wave(const uint64_t *in, const uint64_t *__
   }
 }
 
+// Contains over the whole board (K = 64) on a 16-byte aligned batch: lane l
+// reads words 2(l mod 32), 2(l mod 32) + 1 of universe 2k + l / 32 (one
+// dwordx4 moves two universes per wave-instruction, as k_contains16), RMAX
+// loads in flight per pass.
+template <int UPW, int RMAX>
+__device__ __forceinline__ void cone_wave_full16(const uint64_t *in, const uint64_t *__restrict__ wanted,
+                                                 const uint64_t *__restrict__ unwanted, uint8_t *__restrict__ out,
+                                                 uint64_t n, uint64_t u0, int lane) {
+  constexpr int RB = UPW / 2 < RMAX ? UPW / 2 : RMAX;
+  static_assert(UPW % (2 * RB) == 0, "passes of 2 RB universes");
+  const int half = lane >> 5, col = (lane & 31) * 2;
+  const uint64_t w0 = wanted[col], w1 = wanted[col + 1];
+  const uint64_t m0 = w0 | unwanted[col], m1 = w1 | unwanted[col + 1];
+#pragma unroll 1
+  for (int pass = 0; pass < UPW / (2 * RB); ++pass) {
+    const uint64_t ub = u0 + (uint64_t)pass * 2 * RB;
+    u64x2 v[RB];
+#pragma unroll
+    for (int k = 0; k < RB; ++k) {
+      const uint64_t u = ub + 2 * k + half;
+      v[k] = u < n ? __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(in + u * kWave + col))
+                   : u64x2{w0, w1};
+    }
+#pragma unroll
+    for (int k = 0; k < RB; ++k) {
+      const uint64_t d = ((v[k][0] ^ w0) & m0) | ((v[k][1] ^ w1) & m1);
+      const uint64_t bad = __ballot(d != 0ull);  // lanes 0-31: universe 2k, 32-63: 2k+1
+      if (lane == 0) {
+        if (ub + 2 * k < n) out[ub + 2 * k] = (uint32_t)bad == 0u ? 1 : 0;
+        if (ub + 2 * k + 1 < n) out[ub + 2 * k + 1] = (uint32_t)(bad >> 32) == 0u ? 1 : 0;
+      }
+    }
+  }
+}
+
 // The column window of the care cells, widened by the light cone of `gens`
 // generations: xs = first column, K = columns (64: the whole board from 0).
 __device__ __forceinline__ void cone_window(const uint64_t *__restrict__ wanted,
@@ -106,8 +141,9 @@ __device__ __forceinline__ void cone_window(const uint64_t *__restrict__ wanted,
 
 // UPW universes per wave (one-shot grid of ceil(n / UPW) waves), every wave
 // choosing its lane layout from the window (wave-uniform: the target is the
-// same for all).  Each choice runs its own copy of the pass.
-template <int UPW, int RMAX, bool FIRST, typename OutT>
+// same for all).  Each choice runs its own copy of the pass.  A16: the batch
+// is 16-byte aligned (Contains over the whole board then takes 16-byte loads).
+template <int UPW, int RMAX, bool FIRST, typename OutT, bool A16 = false>
 __global__ __launch_bounds__(kBlock) void k_cone(const uint64_t *in, const uint64_t *__restrict__ wanted,
                                                  const uint64_t *__restrict__ unwanted, OutT *__restrict__ out,
                                                  uint64_t n, uint32_t gens) {
@@ -117,6 +153,9 @@ __global__ __launch_bounds__(kBlock) void k_cone(const uint64_t *in, const uint6
   if (u0 >= n) return;
   uint32_t xs, K;
   cone_window(wanted, unwanted, FIRST ? gens : 0u, lane, xs, K);
+  if constexpr (!FIRST && A16) {
+    if (K == (uint32_t)kWave) return cone_wave_full16<UPW, RMAX>(in, wanted, unwanted, out, n, u0, lane);
+  }
   if (K <= 4) cone_wave<4, UPW, RMAX, FIRST>(in, wanted, unwanted, out, n, u0, gens, xs, K, lane);
   else if (K <= 8) cone_wave<8, UPW, RMAX, FIRST>(in, wanted, unwanted, out, n, u0, gens, xs, K, lane);
   else if (K <= 16) cone_wave<16, UPW, RMAX, FIRST>(in, wanted, unwanted, out, n, u0, gens, xs, K, lane);
@@ -131,8 +170,13 @@ constexpr int kConeUniverses = 32, kConeSets = 8;
 template <int UPW, int RMAX, bool FIRST, typename OutT>
 int launch_cone(const uint64_t *d_in, const uint64_t *d_wanted, const uint64_t *d_unwanted, OutT *d_out, size_t n,
                 uint32_t gens, int cus, hipStream_t stream) {
-  hipLaunchKernelGGL((k_cone<UPW, RMAX, FIRST, OutT>), dim3(grid_for((n + UPW - 1) / UPW, cus, 0)), dim3(kBlock), 0,
-                     stream, d_in, d_wanted, d_unwanted, d_out, (uint64_t)n, gens);
+  const dim3 grid(grid_for((n + UPW - 1) / UPW, cus, 0));
+  if (!FIRST && aligned16(d_in))
+    hipLaunchKernelGGL((k_cone<UPW, RMAX, FIRST, OutT, true>), grid, dim3(kBlock), 0, stream, d_in, d_wanted,
+                       d_unwanted, d_out, (uint64_t)n, gens);
+  else
+    hipLaunchKernelGGL((k_cone<UPW, RMAX, FIRST, OutT, false>), grid, dim3(kBlock), 0, stream, d_in, d_wanted,
+                       d_unwanted, d_out, (uint64_t)n, gens);
   return launched("k_cone launch");
 }
 

@@ -5,9 +5,11 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 #include <thread>
+#include <tuple>
 #include <vector>
 
 #include "host.hpp"
@@ -71,7 +73,43 @@ int device_cus(int &cus) {
   return rc;
 }
 
+// occupancy_lds results per (device, kernel, blocks per CU): the answer
+// depends on nothing else, and computing it takes several occupancy queries
+struct OccKey {
+  int dev;
+  const void *kernel;
+  int blocks;
+  bool operator<(const OccKey &o) const {
+    return std::tie(dev, kernel, blocks) < std::tie(o.dev, o.kernel, o.blocks);
+  }
+};
+std::mutex g_occ_mu;
+std::map<OccKey, unsigned> g_occ;
+
+static int occupancy_lds_uncached(const void *kernel, int blocks_per_cu, unsigned &bytes);
+
 int occupancy_lds(const void *kernel, int blocks_per_cu, unsigned &bytes) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return fail_hip(e, "hipGetDevice");
+  const OccKey key{dev, kernel, blocks_per_cu};
+  {
+    std::lock_guard<std::mutex> lk(g_occ_mu);
+    auto it = g_occ.find(key);
+    if (it != g_occ.end()) {
+      bytes = it->second;
+      return LIFEAPI_OK;
+    }
+  }
+  const int rc = occupancy_lds_uncached(kernel, blocks_per_cu, bytes);
+  if (rc == LIFEAPI_OK) {
+    std::lock_guard<std::mutex> lk(g_occ_mu);
+    g_occ[key] = bytes;
+  }
+  return rc;
+}
+
+static int occupancy_lds_uncached(const void *kernel, int blocks_per_cu, unsigned &bytes) {
   DevInfo d;
   int rc = device_info(d);
   if (rc != LIFEAPI_OK) return rc;
@@ -369,7 +407,7 @@ int host_device(int device) {
 // device >= 0: fn(0, n, device) on that device.  device -1: one contiguous
 // shard per visible device, fn(lo, hi, dev) on one host thread each, with the
 // given host ranges page-locked once for all shards (shard boundaries share
-// pages).  LIFEAPI_HOST_SHARDS=k (1 <= k <= 64, else LIFEAPI_E_INVALID)
+// pages).  LIFEAPI_HOST_SHARDS=k (1 <= k <= 64, else LIFEAPI_E_INVALID; empty = unset)
 // overrides the shard count (at most n shards), shard s
 // running on device s mod ndev: a rehearsal knob that runs the threaded path
 // on a machine with fewer GPUs (tests/test_host_multidev.py).  The first
@@ -382,7 +420,8 @@ int over_devices(size_t n, int device, const std::pair<const void *, size_t> *ra
   if (device >= ndev || device < -1) return fail(LIFEAPI_E_NODEVICE, "bad device index%s");
   int shards = ndev;
   if (device < 0) {
-    if (const char *e = std::getenv("LIFEAPI_HOST_SHARDS")) {
+    const char *e = std::getenv("LIFEAPI_HOST_SHARDS");
+    if (e && *e) {  // (set but empty = unset, as `export LIFEAPI_HOST_SHARDS=` leaves it)
       char *end = nullptr;
       const long k = std::strtol(e, &end, 10);
       if (end == e || *end != '\0' || k < 1 || k > kMaxHostShards)

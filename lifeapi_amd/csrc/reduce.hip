@@ -129,6 +129,7 @@ int lifeapi_fill_random_dev(uint64_t *d_out, size_t n, uint64_t seed, uint64_t f
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
   const uint64_t words = (uint64_t)n * kWave;
+  note_forward_write(d_out, words * 8);
   // 16-byte stores (two words per lane): 0.0836 ms on 1M against 0.0862 for
   // 8-byte ones (tools/rows_ab.py, profiles/r03/rows_ab.jsonl)
   if (aligned16(d_out))

@@ -256,6 +256,7 @@ int lifeapi_parse_rle_batch_dev(const char *d_text, const uint64_t *d_offsets, s
     return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_parse_rle_batch_dev%s");
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
+  note_forward_write(d_out, (uint64_t)n * 512);
   hipLaunchKernelGGL(k_parse_rle, dim3(grid_for(n, cus, 8)), dim3(kBlock), 0, (hipStream_t)stream,
                      d_text, d_offsets, d_out, d_status, (uint64_t)n);
   return launched("k_parse_rle launch");

@@ -38,6 +38,7 @@ static int counts_launch(const uint64_t *d_in, uint64_t *d_out, size_t n, int mo
   if (rc != LIFEAPI_OK) return rc;
   using Fn = void (*)(const uint64_t *, uint64_t *, uint64_t);
   Fn fn = mode == 0 ? (Fn)k_counts<0> : mode == 1 ? (Fn)k_counts<1> : (Fn)k_counts<2>;
+  note_forward_write(d_out, (uint64_t)n * planes * 512);
   hipLaunchKernelGGL(fn, dim3(grid_for(n, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream, d_in,
                      d_out, (uint64_t)n);
   return launched("k_counts launch");
@@ -84,6 +85,7 @@ int lifeapi_stable_pass_batch_dev(uint64_t *d_planes, uint8_t *d_flags, size_t n
   // Propagate 1.96 -> 1.77 ms, sync 1.77 -> 1.63, options 1.62 -> 1.54,
   // signal 1.83 -> 1.72, PropagateStep 1.95 -> 1.86, StabiliseOptions
   // 1.79 -> 1.66.
+  note_forward_write(d_planes, (uint64_t)n * 10 * 512);
   hipLaunchKernelGGL(fns[pass], dim3(grid_for(n, cus, 0)), dim3(kBlock), lds, (hipStream_t)stream,
                      d_planes, d_flags, (uint64_t)n, max_iters ? max_iters : 1u << 20, 2u);
   return launched("k_stable launch");
@@ -107,6 +109,7 @@ int lifeapi_stable_vulnerable_batch_dev(const uint64_t *d_planes, uint64_t *d_ou
   unsigned lds = 0;
   rc = occupancy_lds(reinterpret_cast<const void *>(k_stable_vulnerable<true>), kStableResidentBlocks, lds);
   if (rc != LIFEAPI_OK) return rc;
+  note_forward_write(d_out, (uint64_t)n * 512);
   hipLaunchKernelGGL(k_stable_vulnerable<true>, dim3(grid_for(n, cus, 0)), dim3(kBlock), lds, (hipStream_t)stream,
                      d_planes, d_out, (uint64_t)n);
   return launched("k_stable_vulnerable launch");
@@ -118,11 +121,12 @@ int lifeapi_weld_step_batch_dev(uint64_t *d_welds, size_t n, uint32_t generation
     return fail(LIFEAPI_E_INVALID, "bad pointer to lifeapi_weld_step_batch_dev%s");
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
-  if (generations >= 12)  // state resident in VGPRs on the split layout (k_weld_split)
+  if (generations >= 12) {  // state resident in VGPRs on the split layout (k_weld_split)
+    note_forward_write(d_welds, (uint64_t)n * 2048);
     hipLaunchKernelGGL(generations < 32 ? k_weld_split<true> : k_weld_split<false>,
                        dim3(grid_for((n + 3) / 4, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream,
                        d_welds, (uint64_t)n, generations);
-  else {
+  } else {
     // the order keyed on the batch (host.hpp launch_reverse: in place, so
     // it alternates between calls on the same welds), nontemporal
     // throughout: in a loop stepping the batch in place, +15 % at 256K
@@ -161,6 +165,7 @@ int lifeapi_refined_step_batch_dev(const uint64_t *d_in, uint64_t *d_out, size_t
   // prefetch the next universe, one-shot grid, no occupancy bound -> 6.3 TB/s
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
+  note_forward_write(d_out, (uint64_t)n * 3 * 512);
   hipLaunchKernelGGL((k_refined<1, 0>), dim3(grid_for(n, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream, d_in,
                      d_out, (uint64_t)n);
   return launched("k_refined launch");

@@ -97,6 +97,9 @@ StepLaunch shipped_step(uint32_t gens, uint64_t n) {
 
 extern "C" {
 
+const char *lifeapi_step_kernel_name_n(uint32_t generations, size_t n) {
+  return shipped_step(generations, n).name;
+}
 const char *lifeapi_step_kernel_name(uint32_t generations) { return shipped_step(generations, 1).name; }
 
 int lifeapi_step_batch_dev(const uint64_t *d_in, uint64_t *d_out, size_t n, uint32_t generations,

@@ -39,6 +39,7 @@ _SIGS = {
     "lifeapi_last_error": ([], ctypes.c_char_p),
     "lifeapi_device_count": ([], _int),
     "lifeapi_step_kernel_name": ([_u32], ctypes.c_char_p),
+    "lifeapi_step_kernel_name_n": ([_u32, _sz], ctypes.c_char_p),
     "lifeapi_step_batch_dev": ([_vp, _vp, _sz, _u32, _vp], _int),
     "lifeapi_pop_batch_dev": ([_vp, _vp, _sz, _vp], _int),
     "lifeapi_hash_batch_dev": ([_vp, _vp, _sz, _vp], _int),
@@ -90,9 +91,12 @@ def device_count() -> int:
     return lib.lifeapi_device_count()
 
 
-def step_kernel_name(generations: int = 1) -> str:
-    """The shipped kernel configuration a step of `generations` runs."""
-    return lib.lifeapi_step_kernel_name(generations).decode()
+def step_kernel_name(generations: int = 1, n: int | None = None) -> str:
+    """The shipped kernel configuration a step of `generations` runs on a
+    batch of `n` universes (None: the name for batches of at most 4M)."""
+    if n is None:
+        return lib.lifeapi_step_kernel_name(generations).decode()
+    return lib.lifeapi_step_kernel_name_n(generations, n).decode()
 
 
 def _stream(stream) -> int:

@@ -52,7 +52,7 @@ class Runtime:
         return _Event()
 
 
-def step_kernel_name(generations: int = 1) -> str:
+def step_kernel_name(generations: int = 1, n: int | None = None) -> str:
     return "stub: oracle C port on the CPU"
 
 

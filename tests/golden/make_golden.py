@@ -234,7 +234,46 @@ def batch_digests() -> dict:
     return dig
 
 
+def filter_targets():
+    """The search-filter targets of bench.py's secondary.filter: the config-3
+    block + ring (care columns 9-12) and a whole-board one (row 10 of every
+    third column must be dead: a care window of 62 columns, K = 64 at g = 1)"""
+    bw, bu = np.zeros(64, np.uint64), np.zeros(64, np.uint64)
+    bw[10] = bw[11] = np.uint64(3 << 40)
+    for c in (9, 10, 11, 12):
+        bu[c] = np.uint64(15 << 39)
+    bu &= ~bw
+    ww, wu = np.zeros(64, np.uint64), np.zeros(64, np.uint64)
+    wu[0::3] = np.uint64(1 << 10)
+    return {"block": (bw, bu), "whole_board": (ww, wu)}
+
+
+def filter_digests() -> dict:
+    """The 1-generation search filter and batched Contains on the config-2
+    input (1M universes, seed 2): the reference's own Step() + Contains and
+    Contains (ref_shim.cpp), as digests of the per-universe answers"""
+    x = P.fill(1 << 20, seed=2)
+    out = {"universes": 1 << 20, "seed": 2, "generations": 1, "targets": {}}
+    for name, (w, u) in filter_targets().items():
+        first, _ = R.step_contains_batch(x, w, u, 1, nthreads=8)
+        cont = R.contains_batch(x, w, u)
+        out["targets"][name] = {
+            "wanted": [f"{int(v):016x}" for v in w], "unwanted": [f"{int(v):016x}" for v in u],
+            "first_digest": f"{P.digest(first.astype(np.uint64)):016x}", "hits": int((first > 0).sum()),
+            "contains_digest": f"{P.digest(cont.astype(np.uint64)):016x}", "contained": int(cont.sum())}
+    return out
+
+
 def main():
+    if "--only-filter" in sys.argv:  # add / refresh digests.config2_filter alone
+        path = os.path.join(HERE, "golden.json")
+        with open(path) as f:
+            meta = json.load(f)
+        meta["digests"]["config2_filter"] = filter_digests()
+        with open(path, "w") as f:
+            json.dump(meta, f, indent=1)
+        print(json.dumps(meta["digests"]["config2_filter"]["targets"], indent=1))
+        return
     meta = {"generator": "tests/golden/make_golden.py", "reference_lib": os.path.basename(R.path),
             "reference": "scorbiclife/LifeAPI snapshot 2025-02-22 (/root/reference)"}
 
@@ -347,6 +386,7 @@ def main():
                                                   "dead4", "dead5", "dead6"]}
 
     meta["digests"] = batch_digests()
+    meta["digests"]["config2_filter"] = filter_digests()
     with open(os.path.join(HERE, "golden.json"), "w") as f:
         json.dump(meta, f, indent=1)
     print(json.dumps(meta["digests"], indent=1))

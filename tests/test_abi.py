@@ -60,6 +60,10 @@ def test_abi_version_and_shipped_kernels():
     assert hip.step_kernel_name(1).startswith("k_step<dpp")
     assert hip.step_kernel_name(3).startswith("k_step_split<8-way")
     assert "nt" in hip.step_kernel_name(31) and "nt" not in hip.step_kernel_name(32).split(",")[2]
+    # the launch above 4M universes is a different shape, and named so
+    assert hip.step_kernel_name(1, 1 << 22) == hip.step_kernel_name(1)
+    assert "XCD" in hip.step_kernel_name(1, (1 << 22) + 1) and "alternating" not in hip.step_kernel_name(1, 1 << 24)
+    assert hip.step_kernel_name(3, 1 << 24) == hip.step_kernel_name(3)
 
 
 def test_no_tuning_knobs_in_product_library():
