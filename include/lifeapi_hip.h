@@ -79,13 +79,18 @@ int lifeapi_pop_batch_dev(const uint64_t *d_states, uint32_t *d_pop, size_t n, v
 /* d_hash[u] = build-defined 64-bit hash of universe u     */
 int lifeapi_hash_batch_dev(const uint64_t *d_states, uint64_t *d_hash, size_t n, void *stream);
 /* d_out[u] = Contains(target) for target = (wanted, unwanted), both device
- * pointers to 64 words                                                    */
+ * pointers to 64 words (LifeTarget.hpp:44-51).  Only the columns holding the
+ * target's care cells (wanted | unwanted) are read from each universe.  With
+ * unwanted = 0 this is Contains(pat), with wanted = 0 AreDisjoint(pat)
+ * (LifeAPI.hpp:377-397); the (dx, dy) forms are these on the pattern moved by
+ * (dx, dy) (LifeAPI.hpp:399-421).                                           */
 int lifeapi_contains_batch_dev(const uint64_t *d_states, const uint64_t *d_wanted,
                                const uint64_t *d_unwanted, uint8_t *d_out, size_t n,
                                void *stream);
 /* fused Step^gens + Contains: d_out[u] = first generation g in 1..gens at
  * which Stepped(g) contains the target, or 0 if none; d_final (may be NULL)
- * receives Stepped(gens)                                                  */
+ * receives Stepped(gens).  With d_final NULL and gens <= 2 (the search
+ * filter) only the columns within gens of the target's care columns are read. */
 int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
                                     const uint64_t *d_wanted, const uint64_t *d_unwanted,
                                     uint32_t *d_first_gen, size_t n, uint32_t generations,

@@ -45,8 +45,12 @@ using StepFn = void (*)(const uint64_t *, uint64_t *, uint64_t, uint32_t, uint64
 // the batch) of a launch use plain stores, which leave that part in the 256 MB
 // memory-side Infinity Cache, and the rest nontemporal ones, which do not
 // evict it.  Batches of up to kCachedUniverses use every block slot, larger
-// ones the cap.  Against round 2's launch (nontemporal, one order, capped):
-// +12 % at 1M universes, +10 % at 2M, +3-5 % at 512K and 4M, equal at 8M-16M.
+// ones the cap.  Against round 2's launch (nontemporal, one order, capped at
+// what turned out to be 5 blocks per CU): +12 % at 1M universes, +10 % at 2M,
+// +3-5 % at 512K and 4M, equal at 8M-16M -- most of it from dropping the cap:
+// against one fixed order with every store nontemporal and no cap the order
+// policy gains +1-4 % at 1M (round 3's same-process A/B +4 %, round 4's
+// footprint sweep +1.8 %, profiles/r04/footprint.jsonl).
 constexpr uint64_t kCachedUniverses = 1ull << 22;
 constexpr int kStreamResidentBlocks = 7;
 // Below this batch size the order stays fixed: at 64K universes (64 MiB per

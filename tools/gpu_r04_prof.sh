@@ -5,7 +5,7 @@
 # and the light-cone kernels' fetched bytes and request sizes.
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
-O="$R/gpurun_out/r04/prof"
+O="$R/gpurun_out/${PROF_TAG:-r04/prof}"
 mkdir -p "$O"
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
 cd /tmp

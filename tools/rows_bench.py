@@ -1,7 +1,9 @@
 """Throughput and HBM roofline fraction of every SURVEY 8(f) kernel on
 1M objects (--n) (one JSON line each).  Algorithmic bytes = what the entry point
 must read and write per object; peak = 8 TB/s (MI355X_MICROARCH.md).  A timing is K launches back to back
-between two events (per launch: / K), median over 7 timings."""
+between two events (per launch: / K), median over 7 timings; `scrubbed`: the
+launch alone after a 768 MiB scrub of the Infinity Cache (bench.py Scrub),
+events around the launch only, median of 10 -- the HBM-only figure."""
 import json
 import os
 import sys
@@ -10,7 +12,41 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
 import lifeapi_amd.hip as hip  # noqa: E402
+
+
+class _RT:
+    kind = "hip"
+
+    def __init__(self):
+        self.device = torch.device("cuda", 0)
+        self.stream = torch.cuda.current_stream()
+
+    @staticmethod
+    def event():
+        return torch.cuda.Event(enable_timing=True)
+
+
+RT = None
+SCRUB = None
+
+
+def scrubbed(fn, prep=None):
+    """median ms of fn() alone after a scrub (prep() before each, untimed)"""
+    ms = []
+    for k in range(13):
+        if prep:
+            prep()
+        SCRUB()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        b.synchronize()
+        if k >= 3:
+            ms.append(a.elapsed_time(b))
+    return sorted(ms)[len(ms) // 2]
 
 PEAK = 8000.0  # GB/s
 
@@ -33,12 +69,20 @@ def timed(fn, reps=7):
     return sorted(ms)[len(ms) // 2]
 
 
-def report(name, n, nbytes, ms, extra=None):
+def report(name, n, nbytes, ms, extra=None, scrub_ms=None):
     gbs = n * nbytes / (ms / 1e3) / 1e9
     d = {"kernel": name, "objects": n, "algorithmic_bytes_per_object": nbytes, "ms": ms,
          "objects_per_s": n / ms * 1e3, "GBps": gbs, "hbm_frac": gbs / PEAK}
+    if scrub_ms:
+        d.update({"scrubbed_ms": scrub_ms, "scrubbed_objects_per_s": n / scrub_ms * 1e3,
+                  "scrubbed_GBps": n * nbytes / (scrub_ms / 1e3) / 1e9,
+                  "scrubbed_hbm_frac": n * nbytes / (scrub_ms / 1e3) / 1e9 / PEAK})
     d.update(extra or {})
     print(json.dumps(d), flush=True)
+
+
+def both(name, n, nbytes, fn, extra=None):
+    report(name, n, nbytes, timed(fn), extra, scrubbed(fn))
 
 
 def stable_inputs(n):
@@ -63,6 +107,9 @@ def stable_inputs(n):
 
 
 def main():
+    global RT, SCRUB
+    RT = _RT()
+    SCRUB = bench.Scrub(RT)
     n = int(sys.argv[sys.argv.index('--n') + 1]) if '--n' in sys.argv else 1 << 20
     x = hip.fill_random(n, seed=7)
     y = torch.empty_like(x)
@@ -72,23 +119,29 @@ def main():
         hip.step(pp[0], out=pp[1], generations=1)
         pp.reverse()
 
-    report("k_step (1 gen)", n, 1024, timed(step_pingpong))
+    both("k_step (1 gen)", n, 1024, step_pingpong)
     x = hip.fill_random(n, seed=7)  # (the loop overwrote it)
-    report("k_pop", n, 516, timed(lambda: hip.pop(x)))
-    report("k_hash", n, 520, timed(lambda: hip.hashes(x)))
+    both("k_pop", n, 516, lambda: hip.pop(x))
+    both("k_hash", n, 520, lambda: hip.hashes(x))
     w = x[:1].clone()
-    report("k_contains", n, 513, timed(lambda: hip.contains(x, w, w)))
-    report("k_step_contains 1 gen (first hit only)", n, 516, timed(lambda: hip.step_contains(x, w, w, 1)))
-    report("k_step_contains 1 gen + final states", n, 1028,
-           timed(lambda: hip.step_contains(x, w, w, 1, final=y)))
-    report("k_fill", n, 512, timed(lambda: hip.fill_random(n, seed=9)))
-    report("k_counts NeighbourCount", n, 512 + 2048, timed(lambda: hip.neighbour_count(x)))
-    report("k_counts InteractionCounts", n, 512 + 1536, timed(lambda: hip.interaction_counts(x)))
-    report("k_counts InteractionCountsAndNext", n, 512 + 2048,
-           timed(lambda: hip.interaction_counts(x, with_next=True)))
+    both("k_cone Contains, whole-board target", n, 513, lambda: hip.contains(x, w, w))
+    both("k_cone 1 gen (first hit only), whole-board target", n, 516, lambda: hip.step_contains(x, w, w, 1))
+    bw, bu = torch.zeros_like(w), torch.zeros_like(w)
+    bw[0, 10] = bw[0, 11] = 3 << 40
+    bu[0, 9:13] = 15 << 39
+    bu &= ~bw
+    both("k_cone Contains, 2x2 block + ring (4 columns)", n, 513, lambda: hip.contains(x, bw, bu),
+         {"lines_128B_per_object": 1})
+    both("k_cone 1 gen (first hit only), 2x2 block + ring", n, 516, lambda: hip.step_contains(x, bw, bu, 1),
+         {"lines_128B_per_object": 1})
+    both("k_step_contains 1 gen + final states", n, 1028, lambda: hip.step_contains(x, w, w, 1, final=y))
+    both("k_fill", n, 512, lambda: hip.fill_random(n, seed=9))
+    both("k_counts NeighbourCount", n, 512 + 2048, lambda: hip.neighbour_count(x))
+    both("k_counts InteractionCounts", n, 512 + 1536, lambda: hip.interaction_counts(x))
+    both("k_counts InteractionCountsAndNext", n, 512 + 2048, lambda: hip.interaction_counts(x, with_next=True))
     welds = torch.cat([hip.fill_random(n, seed=s).view(n, 1, 64) for s in (11, 12, 13, 14)], 1).reshape(n, 256)
     welds[:, 64:] &= hip.fill_random(3 * n, seed=15).view(n, 192)
-    report("k_weld (1 gen)", n, 2048 + 512, timed(lambda: hip.weld_step(welds, 1)))
+    both("k_weld (1 gen)", n, 2048 + 512, lambda: hip.weld_step(welds, 1))
     # iterated welds (k_weld_split, VALU-bound): weld-generations per second
     nw, gw = 1 << 18, 256
     ms = timed(lambda: hip.weld_step(welds[:nw], gw))
@@ -111,11 +164,15 @@ def main():
             b.record()
             b.synchronize()
             ms.append(a.elapsed_time(b) / ks)
-        report(f"k_stable {name}", n, 2 * 5120 + 1, sorted(ms)[len(ms) // 2])
+        sm = scrubbed(lambda: hip.stable_pass(works[0], name), prep=lambda: works[0].copy_(st))
+        report(f"k_stable {name}", n, 2 * 5120 + 1, sorted(ms)[len(ms) // 2], scrub_ms=sm)
     del works
-    report("k_stable_vulnerable", n, 5120 + 512, timed(lambda: hip.stable_vulnerable(st)))
+    both("k_stable_vulnerable", n, 5120 + 512, lambda: hip.stable_vulnerable(st))
     planes = hip.fill_random(11 * n, seed=21).view(n, 11 * 64)
-    report("k_refined (config 5)", n, 7168, timed(lambda: hip.refined_step(planes)))
+    both("k_refined (config 5)", n, 7168, lambda: hip.refined_step(planes))
+    n5 = 1 << 18
+    p5 = planes[:n5].contiguous()
+    both("k_refined (config 5, 256K)", n5, 7168, lambda: hip.refined_step(p5))
 
 
 if __name__ == "__main__":
