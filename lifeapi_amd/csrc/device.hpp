@@ -312,8 +312,8 @@ __device__ __forceinline__ int last_set(uint64_t m) { return m ? 63 - __builtin_
 // XCD touches every 8th stretch of the whole batch.  Numbering XCD x's i-th
 // block x*q + min(x, r) + i (grid = 8q + r) is a bijection onto [0, grid)
 // that gives XCD x one contiguous eighth: +5-11 % on the in-place LifeStable
-// passes and +2-4 % on 8M-16M-universe steps (tools/stable_xcd_ab.py,
-// tools/step_xcd_ab.py).
+// passes and +2-4 % on 8M-16M-universe steps (tools/ab/stable_xcd_ab.py,
+// tools/ab/step_xcd_ab.py).
 __device__ __forceinline__ uint64_t xcd_chunk_block() {
   const uint32_t b = blockIdx.x, nb = gridDim.x, q = nb >> 3, r = nb & 7u, x = b & 7u;
   return (uint64_t)x * q + (x < r ? x : r) + (b >> 3);

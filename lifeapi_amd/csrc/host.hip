@@ -264,7 +264,7 @@ void pin_acquire(const void *p, size_t bytes, std::vector<uintptr_t> &keys) {
   if (overlap || bytes < kPinMinBytes) return;
   // Leave ranges the caller pinned alone: the runtime accepts a second
   // registration without counting it, so our unregister would undo theirs
-  // (tools/pin_probe.cpp; hipHostGetFlags fails on registered memory, the
+  // (tools/ab/pin_probe.cpp; hipHostGetFlags fails on registered memory, the
   // pointer attributes report it as host memory).
   for (uintptr_t q : {lo, hi - 1}) {
     hipPointerAttribute_t a{};

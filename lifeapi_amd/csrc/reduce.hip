@@ -84,7 +84,7 @@ int lifeapi_pop_batch_dev(const uint64_t *d_states, uint32_t *d_pop, size_t n, v
   if (rc != LIFEAPI_OK) return rc;
   // 16-byte loads (two universes per wave-instruction), 8 universes per
   // wave, one-shot grid: 0.0820 ms on 1M against 0.0918 for the 8-byte
-  // k_pop<4> on the 32-blocks-per-CU grid, same process (tools/rows_ab.py,
+  // k_pop<4> on the 32-blocks-per-CU grid, same process (tools/ab/rows_ab.py,
   // profiles/r03/rows_ab.jsonl); batches that are only 8-byte aligned keep
   // the 8-byte kernel
   if (aligned16(d_states))
@@ -131,7 +131,7 @@ int lifeapi_fill_random_dev(uint64_t *d_out, size_t n, uint64_t seed, uint64_t f
   const uint64_t words = (uint64_t)n * kWave;
   note_forward_write(d_out, words * 8);
   // 16-byte stores (two words per lane): 0.0836 ms on 1M against 0.0862 for
-  // 8-byte ones (tools/rows_ab.py, profiles/r03/rows_ab.jsonl)
+  // 8-byte ones (tools/ab/rows_ab.py, profiles/r03/rows_ab.jsonl)
   if (aligned16(d_out))
     hipLaunchKernelGGL(k_fill16, dim3(grid_for(words / (2 * kWave), cus, 0)), dim3(kBlock), 0,
                        (hipStream_t)stream, d_out, words, seed, first_universe * kWave, mode);

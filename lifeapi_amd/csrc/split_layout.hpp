@@ -12,7 +12,7 @@ namespace lifeapi_impl {
 // vertical neighbours of row 2k are O bits k-1 and k; those of row 2k+1 are
 // E bits k and k+1.  So a vertical triple costs one 32-bit rotate per plane
 // and parity instead of two 64-bit rotates (four v_alignbit) per plane, and a
-// v_alignbit issues at half rate on gfx950 (tools/bank_probe.hip).
+// v_alignbit issues at half rate on gfx950 (tools/ab/bank_probe.hip).
 __device__ __forceinline__ uint32_t delta_swap(uint32_t x, uint32_t m, int s) {
   const uint32_t t = ((x >> s) ^ x) & m;
   return x ^ t ^ (t << s);

@@ -18,7 +18,7 @@ constexpr int kStableResidentBlocks = 4;
 constexpr int kWeldResidentBlocks = 7;  // k_weld (below 12 generations)
 // per pass (sync, options, signal, step, propagate, stabilise): 0 = every
 // slot.  Round 3, exact caps, 1M LifeStables of three families, same process
-// (tools/stable_grid_ab.py, profiles/r03/stable_caps_1m.jsonl): the single
+// (tools/ab/stable_grid_ab.py, profiles/r03/stable_caps_1m.jsonl): the single
 // passes 2-5 % faster with 3 resident blocks than with 4 (sync 1.79-1.81
 // against 1.86 ms, signal 1.80-1.82 against 1.83-1.87); Propagate keeps
 // every slot (3 blocks: +25 % on still lifes; 4-6 within 3 % of it) and
@@ -55,7 +55,7 @@ int lifeapi_stable_pass_batch_dev(uint64_t *d_planes, uint8_t *d_flags, size_t n
   if (rc != LIFEAPI_OK) return rc;
   using Fn = void (*)(uint64_t *, uint8_t *, uint64_t, uint32_t, uint32_t);
   const Fn fns[6] = {k_stable<0>, k_stable<1>, k_stable<2>, k_stable<3>, k_stable<4>, k_stable<5>};
-  // Launch shape (same-process A/Bs, tools/stable_grid_ab.py, on still lifes
+  // Launch shape (same-process A/Bs, tools/ab/stable_grid_ab.py, on still lifes
   // around an unknown window with fresh options -- the state a search
   // propagates from --, sparse soups and random planes, 64K and 1M
   // LifeStables; profiles/r02/stable_occupancy_*.jsonl): one wave per
@@ -78,10 +78,10 @@ int lifeapi_stable_pass_batch_dev(uint64_t *d_planes, uint8_t *d_flags, size_t n
     if (rc != LIFEAPI_OK) return rc;
   }
   // One order: alternating it, as k_weld does, was 1-2 % slower on repeated
-  // passes in place (tools/stable_order_ab.py, profiles/r02/stable_order_ab.jsonl).
+  // passes in place (tools/ab/stable_order_ab.py, profiles/r02/stable_order_ab.jsonl).
   // Each XCD takes a contiguous eighth of the batch (the last argument's bit
   // 1, device.hpp xcd_chunk_block): on 1M LifeStables, same process, fresh
-  // copies (tools/stable_xcd_ab.py, profiles/r03/stable_xcd_ab.jsonl)
+  // copies (tools/ab/stable_xcd_ab.py, profiles/r03/stable_xcd_ab.jsonl)
   // Propagate 1.96 -> 1.77 ms, sync 1.77 -> 1.63, options 1.62 -> 1.54,
   // signal 1.83 -> 1.72, PropagateStep 1.95 -> 1.86, StabiliseOptions
   // 1.79 -> 1.66.
@@ -103,7 +103,7 @@ int lifeapi_stable_vulnerable_batch_dev(const uint64_t *d_planes, uint64_t *d_ou
   // CU (0.96-0.97 ms at 1M against 0.97-1.00 unlimited and 1.02-1.04 on a
   // looping grid; profiles/r02/stable_occupancy_*.jsonl), each XCD a
   // contiguous eighth of the batch (0.998 -> 0.905 ms at 1M, same process;
-  // tools/stencil_xcd_ab.py, profiles/r03/stencil_xcd_ab.jsonl; the counts,
+  // tools/ab/stencil_xcd_ab.py, profiles/r03/stencil_xcd_ab.jsonl; the counts,
   // k_weld and k_refined at config 5's 256K measured within noise or slower
   // with it and keep the plain mapping)
   unsigned lds = 0;
@@ -131,10 +131,10 @@ int lifeapi_weld_step_batch_dev(uint64_t *d_welds, size_t n, uint32_t generation
     // it alternates between calls on the same welds), nontemporal
     // throughout: in a loop stepping the batch in place, +15 % at 256K
     // welds, +7 % at 512K, +3.5 % at 1M, +1.5 % at 2M; a plain-stored tail
-    // adds nothing here (tools/weld_order_ab.py, profiles/r02/weld_order_ab.jsonl)
+    // adds nothing here (tools/ab/weld_order_ab.py, profiles/r02/weld_order_ab.jsonl)
     // At most 7 blocks resident per CU: 0.459 against 0.484 ms for 1M welds
     // with every slot (6: 0.458; 5: 0.472), same process, exact caps
-    // (tools/stencil_occupancy_ab.py, profiles/r03/stencil_caps.jsonl).
+    // (tools/ab/stencil_occupancy_ab.py, profiles/r03/stencil_caps.jsonl).
     unsigned lds = 0;
     rc = occupancy_lds(reinterpret_cast<const void *>(k_weld<false>), kWeldResidentBlocks, lds);
     if (rc != LIFEAPI_OK) return rc;

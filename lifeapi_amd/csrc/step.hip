@@ -27,17 +27,17 @@ using StepFn = void (*)(const uint64_t *, uint64_t *, uint64_t, uint32_t, uint64
 // resident per CU instead of the 8 its registers allow, set by unused dynamic
 // LDS: fewer concurrent streams per CU, better served by HBM.  Round 3,
 // exact caps (host.hip occupancy_lds), same process, ping-pong with the
-// batch-keyed order (tools/order_interleave_ab.py --caps,
+// batch-keyed order (tools/ab/order_interleave_ab.py --caps,
 // profiles/r03/order_caps.jsonl): 8M universes 6.25 TB/s with 7 and 6.22
 // with 6 against 6.09 uncapped and 5.76 with 5; 16M 6.13 with 6 or 7 against
 // 5.95 uncapped and 5.71 with 5; at 4M 7 and uncapped equal (6.44 / 6.39),
 // at 1M-3M uncapped best (7 is 3-4 % slower, 6 up to 7 %).  The fixed-order
-// sweep agrees (tools/step_occupancy_ab.py, profiles/r03/step_occupancy.jsonl:
+// sweep agrees (tools/ab/step_occupancy_ab.py, profiles/r03/step_occupancy.jsonl:
 // 16M 6.09 / 6.07 TB/s with 6 / 7 against 5.78 uncapped and 5.67 with 5).
 // Round 2 shipped "6", but its LDS arithmetic rounded the share up and gave
 // one block fewer whenever the cap did not divide 160 KiB (6 -> 5, 7 -> 6):
 // it ran 5; occupancy_lds now checks the count on the occupancy API.
-// Launch order and store policy (tools/order_ab.py, profiles/r02/order_*.jsonl,
+// Launch order and store policy (tools/ab/order_ab.py, profiles/r02/order_*.jsonl,
 // same process, ping-pong as the bench): a launch whose input batch an
 // earlier launch wrote takes the groups in the reverse of that launch's order
 // (host.hpp launch_reverse, keyed on the batch), so it starts on what was
@@ -57,7 +57,7 @@ constexpr int kStreamResidentBlocks = 7;
 // launch) the fixed order was 4 % faster, single batch and two interleaved,
 // and at 128K the two boxes disagreed (-4 / +1 %); from 192K on the
 // batch-keyed order is as fast or faster (+1-3 % at 192K-384K, +7-8 % for two
-// interleaved 512K batches, +16 % for one 1M batch; tools/order_interleave_ab.py,
+// interleaved 512K batches, +16 % for one 1M batch; tools/ab/order_interleave_ab.py,
 // profiles/r03/order_interleave*.jsonl)
 constexpr uint64_t kOrderMinUniverses = 3ull << 16;
 constexpr uint64_t kPlainBytes = 256ull << 20;
@@ -68,7 +68,7 @@ constexpr const char *kStreamName =
 // Above kCachedUniverses there is no Infinity Cache reuse to arrange: one
 // order, every store nontemporal, and each XCD streams a contiguous eighth
 // of the batch (kXcdChunk, device.hpp xcd_chunk_block).  Same process,
-// ping-pong, 7 blocks per CU (tools/step_xcd_ab.py,
+// ping-pong, 7 blocks per CU (tools/ab/step_xcd_ab.py,
 // profiles/r03/step_xcd_ab.jsonl): 16M universes 2.736 ms against 2.836 for
 // the order/plain-tail launch and 2.845 with the plain block mapping; 8M
 // 1.396 against 1.410 / 1.427; at 4M the chunked mapping was 1 % slower, at
@@ -167,14 +167,14 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
     return launch_cone<kConeUniverses, kConeSets, true>(d_in, d_wanted, d_unwanted, d_first_gen, n, generations, cus,
                                                          (hipStream_t)stream);
   } else {
-    // 8 universes per wave, every block slot (tools/filter_ab.py,
+    // 8 universes per wave, every block slot (tools/ab/filter_ab.py,
     // profiles/r02/filter_ab.jsonl, 1M universes x 1 generation, same
     // process): 0.087 ms = 6.25 TB/s on the 516 B per universe of the bare
     // filter, 0.181 ms with final states (5.96 TB/s on 1028 B); 4 per wave
     // 0.107 / 0.179, with fewer blocks resident slower; one per wave 0.229.
     // With final states, the launch order and plain-stored tail of the step
     // (above): a loop that filters the states the last call left gets them
-    // partly from the Infinity Cache (tools/filter_order_ab.py).
+    // partly from the Infinity Cache (tools/ab/filter_order_ab.py).
     const uint64_t groups = (n + 7) / 8;
     // Up to 2M universes: +3.4 % at 512K and 1M, +2 % at 2M, none at 4M
     // (profiles/r02/filter_order_ab.jsonl).

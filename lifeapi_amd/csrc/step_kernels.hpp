@@ -58,7 +58,7 @@ __device__ __forceinline__ W life_gen(W a, uint64_t *slot, int lane) {
   }
   if constexpr (RULE == 2) {
     // Row-first form of the same adder network.  A DPP move issues at half
-    // the VALU rate on gfx950 (tools/valu_probe.hip: 8 DPP of 32 instructions
+    // the VALU rate on gfx950 (tools/ab/valu_probe.hip: 8 DPP of 32 instructions
     // cost 25 % of the loop), so exchange the raw column (4 DPP) instead of
     // its two vertical-sum planes (8 DPP):
     //   horizontal 3-sums  H0 = xor3(L,a,R), H1 = maj(L,a,R)   (2-bit, 0..3)

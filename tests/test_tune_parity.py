@@ -69,7 +69,7 @@ def test_step_all_cfgs(tune, port, xchg, upw, nt, rule):
 @pytest.mark.parametrize("reverse", [False, True])
 def test_step_order(tune, port, nts, reverse):
     """The streaming step in either group order, plain or nontemporal
-    stores (tools/order_ab.py), 2, 4 or 8 universes per wave, ragged against
+    stores (tools/ab/order_ab.py), 2, 4 or 8 universes per wave, ragged against
     each, 1 and 2 generations."""
     import torch
     n = 4096 + 3

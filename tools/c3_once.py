@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Config 3 (64K universes x 1024 generations, default launch cfg) run a few
-times: the target program of the PMC passes in tools/gpu_pmc_c3.sh."""
+times: the target program of the PMC passes in tools/ab/gpu_pmc_c3.sh."""
 import os
 import sys
 

@@ -6,7 +6,7 @@ lifeapi_amd/csrc/split_asm.inc, used by k_step_split with LIFEAPI_XCHG_ASM.
 
 Why: the compiler's allocation of the rule-11 loop puts 30 of its 68 VALU on
 two sources in one VGPR bank (bank = vN mod 4, tools/vbank.py), and such a
-v_bitop3 issues at about half rate (tools/bank_probe.hip).  16 of them are the
+v_bitop3 issues at about half rate (tools/ab/bank_probe.hip).  16 of them are the
 h-layer xor3 / maj(L, r, R), which cannot avoid it: r, L and R all live in
 even-aligned b128 tuples (ds_write_b128 / ds_read_b128), so word j sits at the
 same position parity in each and only two banks are left for three operands.

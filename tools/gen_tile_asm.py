@@ -4,7 +4,7 @@ LIFEAPI_XCHG_ASM: 8-way row split, 4 columns per lane, LDS edge exchange) as
 inline gfx950 assembly: tools/tune/tile_asm.inc (tuning build only).
 
 Why: a v_bitop3_b32 whose sources sit in two or three VGPRs of one bank (bank =
-vN mod 4) issues at about half rate on gfx950 (tools/bank_probe.hip:
+vN mod 4) issues at about half rate on gfx950 (tools/ab/bank_probe.hip:
 1.8 vs 1.0 ns per instruction per SIMD), and the compiler's allocation of the
 tile loop puts 60 % of its VALU in that case (tools/vbank.py).  Here every
 instruction reads distinct banks by construction:

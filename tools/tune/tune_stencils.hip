@@ -1,8 +1,8 @@
 // tune_stencils.hip -- TUNING build: the LifeStable kernels of the product
 // (stable_kernels.hpp) launched on an explicit grid, for the grid-cap A/Bs
-// behind stencils.hip's launch choices (tools/stable_grid_ab.py); and the
+// behind stencils.hip's launch choices (tools/ab/stable_grid_ab.py); and the
 // other streaming stencils (stencil_kernels.hpp) with an occupancy cap
-// (tools/stencil_occupancy_ab.py).
+// (tools/ab/stencil_occupancy_ab.py).
 #include "lifeapi_tune.h"
 #include "host.hpp"
 #include "stable_kernels.hpp"

@@ -3,7 +3,7 @@
 // layouts, tiles and assembly-loop schedules), selectable per launch by
 // lifeapi_launch_cfg (lifeapi_tune.h).  Built into tools/tune/
 // liblifeapi_tune.so by __graft_entry__.build_tools(); used by
-// tools/tune.py and the ablation parity tests (tests/test_tune_parity.py).
+// tools/ab/tune.py and the ablation parity tests (tests/test_tune_parity.py).
 // Not part of the product library or its header: the shipped
 // configurations are fixed in lifeapi_amd/csrc/step.hip.
 #include <algorithm>
@@ -26,7 +26,7 @@ namespace {
 // `gens` generations of one universe in the (E, O) layout (RULE 4), as one
 // hand-allocated loop.  The compiler's allocation puts two or three sources
 // of about half of the v_bitop3 in one VGPR bank (tools/vbank.py), and such an
-// instruction issues at half rate (tools/bank_probe.hip).  Here every VALU
+// instruction issues at half rate (tools/ab/bank_probe.hip).  Here every VALU
 // instruction reads its sources from distinct banks (bank = vN mod 4):
 //   A = (E, O) v0:v1 (banks 0,1)   R = right column v2:v3 (2,3)
 //   L = left column v5 (E, bank 1), v4 (O, bank 0)
