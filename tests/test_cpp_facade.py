@@ -14,6 +14,20 @@ def test_facade_compiles_without_gpu():
                     "-I" + os.path.join(ROOT, "include"), src], check=True)
 
 
+def test_facade_members_equal_reference_cpu():
+    """The standalone facade's single-state members (Step, StepAlt, ZOI,
+    GetBoundary, Move(d), Contains / AreDisjoint with and without offsets,
+    LifeTarget(state), LifeTarget::Moved) against the reference's own, on the
+    CPU (tests/cpp/facade_cpu_test.cpp, built against the reference headers by
+    oracle/Makefile, target ref)."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "facade_cpu_test")
+    if not os.path.exists(exe):
+        pytest.skip("oracle/_ref/facade_cpu_test needs the reference headers at build time")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    print(r.stdout, r.stderr[-4000:])
+    assert r.returncode == 0, r.stderr[-4000:]
+
+
 @pytest.mark.gpu
 def test_step_batch_cpp():
     exe = os.path.join(ROOT, "build", "step_batch_test")
