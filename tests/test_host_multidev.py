@@ -154,7 +154,7 @@ def test_bad_device_index(hip):
         hip.step_host(x, 1, device=-2)
 
 
-@pytest.mark.parametrize("bad", ["0", "65", "100000", "-3", "4x", ""])
+@pytest.mark.parametrize("bad", ["0", "65", "100000", "-3", "4x", " "])
 def test_shard_override_rejects_bad_values(hip, shards, bad):
     """LIFEAPI_HOST_SHARDS outside 1..64 (or not an integer) is a caller
     error, not a request for that many threads (host.hip over_devices)"""
@@ -164,6 +164,15 @@ def test_shard_override_rejects_bad_values(hip, shards, bad):
     with pytest.raises(hip.LifeApiError) as e:
         hip.step_host(x, 1, device=-1)
     assert e.value.code == -1 and "LIFEAPI_HOST_SHARDS" in str(e.value)  # LIFEAPI_E_INVALID
+
+
+def test_shard_override_empty_means_unset(hip, stepper, shards):
+    """`export LIFEAPI_HOST_SHARDS=` leaves the variable set but empty: that
+    is no override (one shard per visible device), not an error"""
+    shards("")
+    from oracle.oracle import Port
+    x = Port().fill(7, seed=77)
+    assert (hip.step_host(x, 3, device=-1) == stepper.step_batch(x, 3)).all()
 
 
 def test_shard_override_capped_at_n(hip, stepper, shards):

@@ -81,6 +81,39 @@ def test_order_book_in_place_and_foreign_writes(tune):
     assert tune.order_probe(x.data_ptr(), p, nb) is False
 
 
+def test_every_device_writer_records_its_output(tune, hip):
+    """A batch the book holds as written in reverse is read forward next;
+    once another kernel rewrites it (the fill, the counts, a LifeStable
+    pass, the split weld, the refined step), the book must hold it as written
+    forward, so the next reader of that extent reverses (only the
+    step, the filter and k_weld below 12 generations used to record)"""
+    n = 4096
+    big = torch.empty(n * 16 * 64, dtype=torch.int64, device="cuda")
+    src = big.data_ptr()                       # a stand-in input address (the book never reads memory)
+    zp = src + 8 * n * 512
+
+    def check(ptr, nbytes, write):
+        tune.order_note(src, nbytes)
+        assert tune.order_probe(src, ptr, nbytes) is True     # ptr recorded as written in reverse
+        write()
+        torch.cuda.synchronize()
+        assert tune.order_probe(ptr, zp, nbytes) is True      # rewritten forward: the next reader reverses
+
+    y = torch.zeros((n, 64), dtype=torch.int64, device="cuda")
+    check(y.data_ptr(), n * 512, lambda: hip.fill_random(n, seed=1, out=y))
+    counts = torch.empty((n, 4, 64), dtype=torch.int64, device="cuda")
+    check(counts.data_ptr(), n * 2048,
+          lambda: hip._check(hip.lib.lifeapi_neighbour_count_batch_dev(y.data_ptr(), counts.data_ptr(), n,
+                                                                       hip._stream(None))))
+    st = torch.zeros((n // 8, 640), dtype=torch.int64, device="cuda")
+    check(st.data_ptr(), (n // 8) * 5120, lambda: hip.stable_pass(st, "sync"))
+    welds = torch.zeros((n // 4, 256), dtype=torch.int64, device="cuda")
+    check(welds.data_ptr(), (n // 4) * 2048, lambda: hip.weld_step(welds, 12))
+    planes = torch.zeros((n // 8, 11 * 64), dtype=torch.int64, device="cuda")
+    out = torch.empty((n // 8, 3 * 64), dtype=torch.int64, device="cuda")
+    check(out.data_ptr(), (n // 8) * 1536, lambda: hip.refined_step(planes, out=out))
+
+
 @pytest.mark.parametrize("n", [1, 4099, 300000])
 def test_interleaved_batches_equal_reference(hip, stepper, n):
     """the streaming step over two batches in turn (A, B, A, B, ...), ping-pong
