@@ -6,6 +6,8 @@
 // occupancy settings for A/Bs.
 #pragma once
 
+#include <type_traits>
+
 #include "device.hpp"
 #include "split_layout.hpp"
 
@@ -96,28 +98,41 @@ __device__ __forceinline__ W weld_gen(W s, W f2, W f1, W f0) {
 // the last one stepped starts on the welds that launch touched last, part of
 // which the memory-side Infinity Cache still holds (as k_step).
 constexpr uint32_t kWeldReverse = 1u << 31;
-template <bool CHUNK = false>
+// U welds per wave (their 4 U loads issued before the first generation); the
+// tuning build measures U = 2, 4 (tools/ab/weld_u_ab.py)
+template <bool CHUNK = false, int U = 1>
 __global__ __launch_bounds__(kBlock) void k_weld(uint64_t *__restrict__ welds, uint64_t n,
                                                  uint32_t gens, uint64_t plain_from) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const bool rev = (gens & kWeldReverse) != 0;
   gens &= ~kWeldReverse;
+  const uint64_t groups = (n + U - 1) / U;
   const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock;
-  for (uint64_t k = block_index<CHUNK>() * kWavesPerBlock + wib; k < n; k += stride) {
-    const uint64_t u = rev ? n - 1 - k : k;
-    uint64_t *p = welds + u * 4 * kWave + lane;
-    if (k < plain_from) {
-      W s = ld<true>(p);
-      const W f2 = ld<true>(p + kWave), f1 = ld<true>(p + 2 * kWave), f0 = ld<true>(p + 3 * kWave);
-      for (uint32_t g = 0; g < gens; ++g) s = weld_gen(s, f2, f1, f0);
-      st<true>(p, s);
-    } else {
-      W s = ld<false>(p);
-      const W f2 = ld<false>(p + kWave), f1 = ld<false>(p + 2 * kWave), f0 = ld<false>(p + 3 * kWave);
-      for (uint32_t g = 0; g < gens; ++g) s = weld_gen(s, f2, f1, f0);
-      st<false>(p, s);
-    }
+  for (uint64_t k = block_index<CHUNK>() * kWavesPerBlock + wib; k < groups; k += stride) {
+    const uint64_t g0 = (rev ? groups - 1 - k : k) * U;
+    auto run = [&](auto nt) __attribute__((always_inline)) {
+      constexpr bool NT = decltype(nt)::value;
+      W s[U], f2[U], f1[U], f0[U];
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        const uint64_t *p = welds + (g0 + j) * 4 * kWave + lane;
+        const bool ok = U == 1 || g0 + j < n;
+        s[j] = ok ? ld<NT>(p) : W{0u, 0u};
+        f2[j] = ok ? ld<NT>(p + kWave) : W{0u, 0u};
+        f1[j] = ok ? ld<NT>(p + 2 * kWave) : W{0u, 0u};
+        f0[j] = ok ? ld<NT>(p + 3 * kWave) : W{0u, 0u};
+      }
+      for (uint32_t g = 0; g < gens; ++g) {
+#pragma unroll
+        for (int j = 0; j < U; ++j) s[j] = weld_gen(s[j], f2[j], f1[j], f0[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < U; ++j)
+        if (U == 1 || g0 + j < n) st<NT>(welds + (g0 + j) * 4 * kWave + lane, s[j]);
+    };
+    if (k < plain_from) run(std::true_type{});
+    else run(std::false_type{});
   }
 }
 

@@ -258,7 +258,8 @@ static void Facade_SearchLoopWithPatternTarget() {
   std::vector<LifeState> ref(2000);
   for (size_t i = 0; i < ref.size(); ++i) {
     ref[i] = LifeState::RandomState() & LifeState::RandomState();
-    if (i % 4 == 0) ref[i] = (ref[i] & ~block.ZOI()) | block;
+    // clear two cells around the block: then nothing can be born in its ring
+    if (i % 4 == 0) ref[i] = (ref[i] & ~block.ZOI().ZOI()) | block;
   }
   std::vector<lifeapi::LifeState> fs(ref.size());
   for (size_t i = 0; i < ref.size(); ++i) fs[i] = facade(ref[i]);

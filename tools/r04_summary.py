@@ -27,7 +27,7 @@ def counters(path):
     out = {}
     with open(path) as f:
         for row in csv.DictReader(f):
-            k = row["Kernel_Name"].split("(")[0].replace("void ", "")
+            k = row["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
             k = k.split("::")[-1]
             out.setdefault(k, {}).setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
     return out
@@ -53,13 +53,13 @@ def main(tag):
         shutil.copy(stats, os.path.join(dst, rel))
     pmc = {}
     for cc in glob.glob(os.path.join(src, "**", "*counter_collection.csv"), recursive=True):
-        run = os.path.relpath(cc, src).split(os.sep)
-        run = run[-3] if len(run) >= 3 else run[0]
+        run = os.path.basename(os.path.dirname(cc))
         rel = os.path.relpath(cc, src).replace(os.sep, "_")
         shutil.copy(cc, os.path.join(dst, rel))
         per = {}
         for k, cs in counters(cc).items():
             d = {c: statistics.mean(v) for c, v in cs.items()}
+            d["per_dispatch"] = {c: v for c, v in cs.items()}
             d["dispatches"] = max(len(v) for v in cs.values())
             if "FETCH_SIZE" in d:
                 d["fetch_bytes_x2"] = d["FETCH_SIZE"] * 1024 * 2

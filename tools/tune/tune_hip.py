@@ -293,3 +293,14 @@ def cone(states, wanted, unwanted, generations, upw, rmax, first=True, out=None,
     hip._check(lib.lifeapi_tune_cone(1 if first else 0, states.data_ptr(), wanted.data_ptr(), unwanted.data_ptr(),
                                      out.data_ptr(), n, generations, upw, rmax, hip._stream(stream)))
     return out
+
+
+lib.lifeapi_tune_weld_u.argtypes = [_vp, _sz, _int, _int, _int, _vp]
+lib.lifeapi_tune_weld_u.restype = _int
+
+
+def weld_u(welds, u: int, resident: int = 0, chunk: bool = False, stream=None):
+    """k_weld one generation in place with u welds per wave (tune_stencils.hip)"""
+    hip._check(lib.lifeapi_tune_weld_u(welds.data_ptr(), welds.shape[0], u, resident, 1 if chunk else 0,
+                                       hip._stream(stream)))
+    return welds

@@ -189,6 +189,25 @@ int lifeapi_tune_order_probe(const void *d_in, const void *d_out, uint64_t bytes
 /* the book's note_forward_write: d_out (bytes) recorded as written forward */
 void lifeapi_tune_order_note(const void *d_out, uint64_t bytes) { note_forward_write(d_out, bytes); }
 
+/* k_weld one generation in place with u welds per wave (1, 2, 4), at most
+ * `resident` blocks per CU (0 = all), each XCD a contiguous eighth if
+ * `chunk`, nontemporal throughout, one order                                */
+int lifeapi_tune_weld_u(uint64_t *d_welds, size_t n, int u, int resident, int chunk, void *stream) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!d_welds || (u != 1 && u != 2 && u != 4) || resident < 0) return fail(LIFEAPI_E_INVALID, "bad argument%s");
+  int cus = 0, rc = device_cus(cus);
+  if (rc != LIFEAPI_OK) return rc;
+  using Fn = void (*)(uint64_t *, uint64_t, uint32_t, uint64_t);
+  const Fn fns[2][3] = {{k_weld<false, 1>, k_weld<false, 2>, k_weld<false, 4>},
+                        {k_weld<true, 1>, k_weld<true, 2>, k_weld<true, 4>}};
+  const Fn fn = fns[chunk ? 1 : 0][u == 1 ? 0 : u == 2 ? 1 : 2];
+  unsigned lds = 0;
+  if (resident && (rc = occupancy_lds((const void *)fn, resident, lds)) != LIFEAPI_OK) return rc;
+  hipLaunchKernelGGL(fn, dim3(grid_for((n + u - 1) / u, cus, 0)), dim3(kBlock), lds, (hipStream_t)stream, d_welds,
+                     (uint64_t)n, 1u, ~(uint64_t)0);
+  return launched("k_weld (u) launch");
+}
+
 /* k_weld one generation in place, the order reversed if `reverse`, the
  * welds taken from position n - plain_welds on loaded and stored plain     */
 int lifeapi_tune_weld_order(uint64_t *d_welds, size_t n, int reverse, uint64_t plain_welds, void *stream) {
