@@ -220,18 +220,26 @@ SCRUB_MIB = 768  # > 2 x the 256 MiB Infinity Cache (MI355X_MICROARCH.md, memory
 
 
 class Scrub:
-    """SCRUB_MIB of unrelated plain reads and writes (one torch add_ on the
-    rank's stream): run before a timed launch, it leaves nothing that launch
-    reads in the 256 MiB memory-side Infinity Cache or the L2s, so the launch
-    is timed from HBM alone."""
+    """SCRUB_MIB of unrelated plain reads (one torch sum on the rank's stream):
+    run before a timed launch, it leaves nothing that launch reads in the
+    256 MiB memory-side Infinity Cache or the L2s, so the launch is timed
+    from HBM alone.  Reads only (mode "read", the default): the lines it
+    leaves cached are clean, so the timed launch pays no write-back of the
+    scrub's own data; mode "rw" (one add_, plain reads and writes) leaves up
+    to 256 MiB of dirty lines behind, kept for the comparison in
+    tools/footprint_sweep.py."""
 
-    def __init__(self, rt, mib=SCRUB_MIB):
-        self.rt, self.mib = rt, mib
-        self.buf = torch.zeros(mib << 17, dtype=torch.int64, device=rt.device)
+    def __init__(self, rt, mib=SCRUB_MIB, mode="read"):
+        self.rt, self.mib, self.mode = rt, mib, mode
+        self.buf = torch.ones(mib << 17, dtype=torch.int64, device=rt.device)
+        self.sink = torch.empty((), dtype=torch.int64, device=rt.device)
 
     def __call__(self):
         with torch.cuda.stream(self.rt.stream):
-            self.buf.add_(1)
+            if self.mode == "rw":
+                self.buf.add_(1)
+            else:
+                torch.sum(self.buf, dtype=torch.int64, out=self.sink)
 
 
 def scrubbed_ms(rt, fn, a, b, scrub, reps=10, warm=3):
@@ -970,10 +978,10 @@ def main(argv=None):
                          "cache_neutral": ({"achieved": neu[0], "frac": neu[0] / HBM_PEAK_GBS,
                                             "kernel_ms": rank_figs[0][0],
                                             "method": "the shipped launch (lifeapi_step_batch_dev), same size, "
-                                                      "same process, rank 0, with a 768 MiB scrub (plain "
-                                                      "read + write of an unrelated buffer) on the stream "
-                                                      "before each launch and events around the launch only: "
-                                                      "3 warm, 10 timed ping-pong launches, median"}
+                                                      "same process, rank 0, with a 768 MiB scrub (a read "
+                                                      "of an unrelated buffer) on the stream before each "
+                                                      "launch and events around the launch only: 3 warm, 10 "
+                                                      "timed ping-pong launches, median"}
                                            if neu[0] else None),
                          "fixed_order_nt_back_to_back": ({"achieved": fixed[0], "frac": fixed[0] / HBM_PEAK_GBS,
                                                           "kernel_ms": rank_figs[0][3],

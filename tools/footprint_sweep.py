@@ -3,8 +3,10 @@
 shipped launch (lifeapi_step_batch_dev)
   b2b       ping-pong, 20 launches back to back, median of 3 runs (the timed
             region's method);
-  scrubbed  the same launch alone after a 768 MiB scrub (bench.py Scrub),
-            events around the launch only, median of 10 -- HBM only;
+  scrubbed  the same launch alone after a 768 MiB read-only scrub (bench.py
+            Scrub), events around the launch only, median of 10 -- HBM only;
+  scrub_rw  the same after a read + write scrub (round 4's first form), which
+            leaves dirty lines in the cache for the launch to write back;
   fixed     round 3's cache-neutral form: the kernel's code in one fixed
             order with every store nontemporal (tools/tune step_order), b2b;
   fixed_scr the fixed form after a scrub.
@@ -38,6 +40,7 @@ class RT:
 def main():
     rt = RT()
     scrub = bench.Scrub(rt)
+    scrub_rw = bench.Scrub(rt, mode="rw")
     sizes = [1 << k for k in range(18, 25)]
     if "--sizes" in sys.argv:
         sizes = [int(v) for v in sys.argv[sys.argv.index("--sizes") + 1].split(",")]
@@ -57,9 +60,10 @@ def main():
         row = {"universes": n, "MiB_per_buffer": n * 512 >> 20, "kernel": hip.step_kernel_name(1, n)}
         row["b2b_ms"] = bench.back_to_back_ms(rt, shipped, a, b)
         row["scrubbed_ms"], row["scrubbed_all"] = bench.scrubbed_ms(rt, shipped, a, b, scrub)
+        row["scrub_rw_ms"], _ = bench.scrubbed_ms(rt, shipped, a, b, scrub_rw)
         row["fixed_b2b_ms"] = bench.back_to_back_ms(rt, fixed, a, b)
         row["fixed_scrubbed_ms"], _ = bench.scrubbed_ms(rt, fixed, a, b, scrub)
-        for k in ("b2b", "scrubbed", "fixed_b2b", "fixed_scrubbed"):
+        for k in ("b2b", "scrubbed", "scrub_rw", "fixed_b2b", "fixed_scrubbed"):
             row[k + "_GBps"] = gb(row[k + "_ms"])
         print(json.dumps(row), flush=True)
         del a, b
