@@ -239,7 +239,7 @@ class Scrub:
             if self.mode == "rw":
                 self.buf.add_(1)
             else:
-                torch.sum(self.buf, dtype=torch.int64, out=self.sink)
+                torch.sum(self.buf, 0, out=self.sink)
 
 
 def scrubbed_ms(rt, fn, a, b, scrub, reps=10, warm=3):
