@@ -135,12 +135,20 @@ int lifeapi_weld_step_batch_dev(uint64_t *d_welds, size_t n, uint32_t generation
     // At most 7 blocks resident per CU: 0.459 against 0.484 ms for 1M welds
     // with every slot (6: 0.458; 5: 0.472), same process, exact caps
     // (tools/ab/stencil_occupancy_ab.py, profiles/r03/stencil_caps.jsonl).
+    // Round 4: two welds per wave (their 8 loads issued together) and each XCD
+    // a contiguous eighth of the batch: 1M welds in one order 0.4218 ms
+    // against 0.4680 with one weld per wave and 0.4505 for round 3's shipped
+    // launch with its alternating order (0.796 / 0.717 / 0.745 of 8 TB/s;
+    // after a read-only scrub 0.794 / 0.731 / 0.740); either change alone
+    // gains less (tools/ab/weld_u_ab.py, profiles/r04/r04b/weld_u_ab.jsonl).
+    constexpr int kWeldU = 2;
     unsigned lds = 0;
-    rc = occupancy_lds(reinterpret_cast<const void *>(k_weld<false>), kWeldResidentBlocks, lds);
+    rc = occupancy_lds(reinterpret_cast<const void *>(k_weld<true, kWeldU>), kWeldResidentBlocks, lds);
     if (rc != LIFEAPI_OK) return rc;
     const uint32_t rev = launch_reverse(d_welds, d_welds, (uint64_t)n * 2048) ? kWeldReverse : 0u;
-    hipLaunchKernelGGL(k_weld<false>, dim3(grid_for(n, cus, 0)), dim3(kBlock), lds, (hipStream_t)stream, d_welds,
-                       (uint64_t)n, generations | rev, (uint64_t)n);
+    const uint64_t groups = (n + kWeldU - 1) / kWeldU;
+    hipLaunchKernelGGL((k_weld<true, kWeldU>), dim3(grid_for(groups, cus, 0)), dim3(kBlock), lds,
+                       (hipStream_t)stream, d_welds, (uint64_t)n, generations | rev, groups);
   }
   return launched("k_weld launch");
 }
