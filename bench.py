@@ -276,9 +276,10 @@ def side_fn(rt, gens, neutral):
                launch of a ping-pong from 192K universes on (what the
                batch-keyed order does there), the last min(256 MiB, half)
                of each launch stored plain; above 4M universes one order,
-               every store nontemporal, at most 7 blocks per CU and each XCD
-               a contiguous eighth of the batch (both forms then use that
-               block mapping, which reuses nothing from the cache).
+               every store nontemporal, 8 universes per wave, at most 7
+               blocks per CU and each XCD a contiguous eighth of the batch
+               (both forms then use that launch, which reuses nothing from
+               the cache).
     With gens = 0 the kernel is a copy of exactly that access shape."""
     if rt.neutral is None:
         return None
@@ -289,7 +290,7 @@ def side_fn(rt, gens, neutral):
         big = n > (1 << 22)
         resident = 7 if big else 0
         if neutral or big:
-            rt.neutral(src, dst, generations=gens, reverse=False, nts=True, resident=resident, upw=4,
+            rt.neutral(src, dst, generations=gens, reverse=False, nts=True, resident=resident, upw=8 if big else 4,
                        plain_bytes=0, stream=rt.stream, xcd_chunk=big)
         else:
             rev = flip[0] and n >= 3 * (1 << 16)

@@ -73,8 +73,13 @@ constexpr const char *kStreamName =
 // the order/plain-tail launch and 2.845 with the plain block mapping; 8M
 // 1.396 against 1.410 / 1.427; at 4M the chunked mapping was 1 % slower, at
 // 1M equal.
+// Round 4: 8 universes per wave for these batches (4 KiB in flight per
+// wave): same process, interleaved, 7 rounds (tools/ab/big_upw_ab.py,
+// profiles/r04/r04d/big_upw_ab.jsonl): 8M 6.12 against 5.83 TB/s back to
+// back (6.40 / 6.17 after a read-only scrub), 16M and 4M equal (6.38 / 6.38,
+// 6.40 / 6.36).
 constexpr const char *kStreamBigName =
-    "k_step<dpp, 4 universes/wave, nt, 7-LUT network; each XCD a contiguous eighth, one order>";
+    "k_step<dpp, 8 universes/wave, nt, 7-LUT network; each XCD a contiguous eighth, one order>";
 struct StepLaunch {
   StepFn fn;
   uint64_t universes_per_wave;
@@ -86,7 +91,7 @@ struct StepLaunch {
 };
 StepLaunch shipped_step(uint32_t gens, uint64_t n) {
   if (gens <= 2 && n > kCachedUniverses)
-    return {k_step<XDPP, 4, true, 3, true>, 4, kStreamResidentBlocks, false, 0, kStreamBigName, kXcdChunk};
+    return {k_step<XDPP, 8, true, 3, true>, 8, kStreamResidentBlocks, false, 0, kStreamBigName, kXcdChunk};
   if (gens <= 2)
     return {k_step<XDPP, 4, true, 3, true>, 4, 0, true, std::min<uint64_t>(kPlainBytes, n * 512 / 2), kStreamName,
             0u};

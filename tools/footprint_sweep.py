@@ -53,7 +53,8 @@ def main():
             hip.step(x, out=y, generations=1)
 
         def fixed(x, y):
-            tune.step_order(x, y, generations=1, reverse=False, nts=True, resident=7 if big else 0, upw=4,
+            tune.step_order(x, y, generations=1, reverse=False, nts=True, resident=7 if big else 0,
+                            upw=8 if big else 4,
                             plain_bytes=0, xcd_chunk=big)
 
         gb = lambda ms: n * 1024 / (ms / 1e3) / 1e9  # noqa: E731

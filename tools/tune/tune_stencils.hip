@@ -168,7 +168,7 @@ int lifeapi_tune_stencil(int kind, const uint64_t *d_in, uint64_t *d_out, size_t
  * k_stable<which-1>, 7 = k_stable_vulnerable): *got from the occupancy API */
 int lifeapi_tune_capped_occupancy(int which, int want, int *got) {
   if (!got || which < 0 || which > 7 || want < 1) return fail(LIFEAPI_E_INVALID, "bad argument%s");
-  const void *fns[8] = {(const void *)k_step<XDPP, 4, true, 3, true>,
+  const void *fns[8] = {(const void *)k_step<XDPP, 8, true, 3, true>,
                         (const void *)k_stable<0>, (const void *)k_stable<1>, (const void *)k_stable<2>,
                         (const void *)k_stable<3>, (const void *)k_stable<4>, (const void *)k_stable<5>,
                         (const void *)k_stable_vulnerable<false>};
