@@ -50,7 +50,7 @@ using StepFn = void (*)(const uint64_t *, uint64_t *, uint64_t, uint32_t, uint64
 // +3-5 % at 512K and 4M, equal at 8M-16M -- most of it from dropping the cap:
 // against one fixed order with every store nontemporal and no cap the order
 // policy gains +1-4 % at 1M (round 3's same-process A/B +4 %, round 4's
-// footprint sweep +1.8 %, profiles/r04/footprint.jsonl).
+// footprint sweeps +1-2 %, profiles/r04/r04e/footprint.jsonl).
 constexpr uint64_t kCachedUniverses = 1ull << 22;
 constexpr int kStreamResidentBlocks = 7;
 // Below this batch size the order stays fixed: at 64K universes (64 MiB per
