@@ -27,16 +27,17 @@
 namespace lifeapi_impl {
 namespace {
 
-// One wave's UPW universes u0 .. u0 + UPW - 1 under the window (xs = first
-// loaded column, K <= P loaded columns).  FIRST: out[u] = the first
+// One wave's chunks of UPW universes u0 .. u0 + UPW - 1, u0 = u_first,
+// u_first + u_step, ... (< n), under the window (xs = first loaded column,
+// K <= P loaded columns).  FIRST: out[u] = the first
 // generation in 1..gens whose state contains the target (0 = never), else
 // out[u] = Contains(target) of the state as loaded (gens unused).  Register
 // sets go RMAX at a time: all their loads are issued before the first test.
 template <int P, int UPW, int RMAX, bool FIRST, typename OutT>
 __device__ __forceinline__ void cone_wave(const uint64_t *in, const uint64_t *__restrict__ wanted,
                                           const uint64_t *__restrict__ unwanted, OutT *__restrict__ out,
-                                          uint64_t n, uint64_t u0, uint32_t gens, uint32_t xs, uint32_t K,
-                                          int lane) {
+                                          uint64_t n, uint64_t u_first, uint64_t u_step, uint32_t gens,
+                                          uint32_t xs, uint32_t K, int lane) {
   constexpr int GPS = kWave / P;  // universes per register set
   static_assert(UPW % GPS == 0, "a wave takes whole register sets");
   constexpr int R = UPW / GPS;
@@ -57,6 +58,7 @@ __device__ __forceinline__ void cone_wave(const uint64_t *in, const uint64_t *__
     if constexpr (P == kWave) return bad == 0ull;
     else return ((bad >> sh) & ((1ull << P) - 1)) == 0ull;
   };
+  for (uint64_t u0 = u_first; u0 < n; u0 += u_step) {
 #pragma unroll 1
   for (int pass = 0; pass < R / RB; ++pass) {
     const uint64_t ub = u0 + (uint64_t)pass * RB * GPS + q;
@@ -89,6 +91,7 @@ __device__ __forceinline__ void cone_wave(const uint64_t *in, const uint64_t *__
       }
     }
   }
+  }
 }
 
 // Contains over the whole board (K = 64) on a 16-byte aligned batch: lane l
@@ -98,12 +101,13 @@ __device__ __forceinline__ void cone_wave(const uint64_t *in, const uint64_t *__
 template <int UPW, int RMAX>
 __device__ __forceinline__ void cone_wave_full16(const uint64_t *in, const uint64_t *__restrict__ wanted,
                                                  const uint64_t *__restrict__ unwanted, uint8_t *__restrict__ out,
-                                                 uint64_t n, uint64_t u0, int lane) {
+                                                 uint64_t n, uint64_t u_first, uint64_t u_step, int lane) {
   constexpr int RB = UPW / 2 < RMAX ? UPW / 2 : RMAX;
   static_assert(UPW % (2 * RB) == 0, "passes of 2 RB universes");
   const int half = lane >> 5, col = (lane & 31) * 2;
   const uint64_t w0 = wanted[col], w1 = wanted[col + 1];
   const uint64_t m0 = w0 | unwanted[col], m1 = w1 | unwanted[col + 1];
+  for (uint64_t u0 = u_first; u0 < n; u0 += u_step) {
 #pragma unroll 1
   for (int pass = 0; pass < UPW / (2 * RB); ++pass) {
     const uint64_t ub = u0 + (uint64_t)pass * 2 * RB;
@@ -123,6 +127,7 @@ __device__ __forceinline__ void cone_wave_full16(const uint64_t *in, const uint6
         if (ub + 2 * k + 1 < n) out[ub + 2 * k + 1] = (uint32_t)(bad >> 32) == 0u ? 1 : 0;
       }
     }
+  }
   }
 }
 
@@ -149,18 +154,18 @@ __global__ __launch_bounds__(kBlock) void k_cone(const uint64_t *in, const uint6
                                                  uint64_t n, uint32_t gens) {
   const int lane = threadIdx.x & (kWave - 1);
   const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  const uint64_t u0 = wave * UPW;
+  const uint64_t u0 = wave * UPW, step = (uint64_t)gridDim.x * kWavesPerBlock * UPW;  // grid-stride (capped grids)
   if (u0 >= n) return;
   uint32_t xs, K;
   cone_window(wanted, unwanted, FIRST ? gens : 0u, lane, xs, K);
   if constexpr (!FIRST && A16) {
-    if (K == (uint32_t)kWave) return cone_wave_full16<UPW, RMAX>(in, wanted, unwanted, out, n, u0, lane);
+    if (K == (uint32_t)kWave) return cone_wave_full16<UPW, RMAX>(in, wanted, unwanted, out, n, u0, step, lane);
   }
-  if (K <= 4) cone_wave<4, UPW, RMAX, FIRST>(in, wanted, unwanted, out, n, u0, gens, xs, K, lane);
-  else if (K <= 8) cone_wave<8, UPW, RMAX, FIRST>(in, wanted, unwanted, out, n, u0, gens, xs, K, lane);
-  else if (K <= 16) cone_wave<16, UPW, RMAX, FIRST>(in, wanted, unwanted, out, n, u0, gens, xs, K, lane);
-  else if (K <= 32) cone_wave<32, UPW, RMAX, FIRST>(in, wanted, unwanted, out, n, u0, gens, xs, K, lane);
-  else cone_wave<64, UPW, RMAX, FIRST>(in, wanted, unwanted, out, n, u0, gens, xs, K, lane);
+  if (K <= 4) cone_wave<4, UPW, RMAX, FIRST>(in, wanted, unwanted, out, n, u0, step, gens, xs, K, lane);
+  else if (K <= 8) cone_wave<8, UPW, RMAX, FIRST>(in, wanted, unwanted, out, n, u0, step, gens, xs, K, lane);
+  else if (K <= 16) cone_wave<16, UPW, RMAX, FIRST>(in, wanted, unwanted, out, n, u0, step, gens, xs, K, lane);
+  else if (K <= 32) cone_wave<32, UPW, RMAX, FIRST>(in, wanted, unwanted, out, n, u0, step, gens, xs, K, lane);
+  else cone_wave<64, UPW, RMAX, FIRST>(in, wanted, unwanted, out, n, u0, step, gens, xs, K, lane);
 }
 
 // the shipped shape (tools/cone_ab.py)
@@ -169,8 +174,8 @@ constexpr int kConeUniverses = 32, kConeSets = 8;
 // Launches k_cone on a one-shot grid.
 template <int UPW, int RMAX, bool FIRST, typename OutT>
 int launch_cone(const uint64_t *d_in, const uint64_t *d_wanted, const uint64_t *d_unwanted, OutT *d_out, size_t n,
-                uint32_t gens, int cus, hipStream_t stream) {
-  const dim3 grid(grid_for((n + UPW - 1) / UPW, cus, 0));
+                uint32_t gens, int cus, hipStream_t stream, int blocks_per_cu = 0) {
+  const dim3 grid(grid_for((n + UPW - 1) / UPW, cus, blocks_per_cu));
   if (!FIRST && aligned16(d_in))
     hipLaunchKernelGGL((k_cone<UPW, RMAX, FIRST, OutT, true>), grid, dim3(kBlock), 0, stream, d_in, d_wanted,
                        d_unwanted, d_out, (uint64_t)n, gens);

@@ -212,7 +212,8 @@ def test_step_contains_pair_capped_grid(tune, hip, port, caps, kind):
     assert (to_host(fin) == port.step_batch(x, gens)).all()
 
 
-CONE_SHAPES = [(16, 4), (16, 8), (16, 16), (32, 4), (32, 8), (32, 16), (32, 32), (64, 8), (64, 16), (64, 32)]
+CONE_SHAPES = [(16, 4), (16, 8), (16, 16), (32, 4), (32, 8), (32, 16), (32, 32), (64, 8), (64, 16), (64, 32),
+               (1000 + 32, 8), (2000 + 64, 16), (8000 + 32, 8)]  # + 1000 c: at most c blocks per CU, grid-stride
 
 
 @pytest.mark.parametrize("upw,rmax", CONE_SHAPES)

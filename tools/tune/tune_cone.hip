@@ -10,9 +10,9 @@ namespace {
 
 template <bool FIRST, typename OutT>
 int cone_by_shape(const uint64_t *in, const uint64_t *w, const uint64_t *u, OutT *out, size_t n, uint32_t gens,
-                  int upw, int rmax, int cus, hipStream_t st) {
+                  int upw, int rmax, int cus, hipStream_t st, int cap) {
 #define LIFEAPI_CONE(U, R) \
-  if (upw == U && rmax == R) return launch_cone<U, R, FIRST>(in, w, u, out, n, gens, cus, st);
+  if (upw == U && rmax == R) return launch_cone<U, R, FIRST>(in, w, u, out, n, gens, cus, st, cap);
   LIFEAPI_CONE(16, 4)
   LIFEAPI_CONE(16, 8)
   LIFEAPI_CONE(16, 16)
@@ -33,7 +33,8 @@ extern "C" {
 
 /* first != 0: the search filter (d_out uint32 first generations, gens <= 2);
  * first == 0: Contains (d_out uint8).  upw universes per wave, rmax register
- * sets per pass. */
+ * sets per pass; upw + 1000 * c: a grid of at most c blocks per CU looping
+ * over the batch (each wave finds the window once). */
 int lifeapi_tune_cone(int first, const uint64_t *d_in, const uint64_t *d_wanted, const uint64_t *d_unwanted,
                       void *d_out, size_t n, uint32_t gens, int upw, int rmax, void *stream) {
   if (n == 0) return LIFEAPI_OK;
@@ -41,11 +42,13 @@ int lifeapi_tune_cone(int first, const uint64_t *d_in, const uint64_t *d_wanted,
     return fail(LIFEAPI_E_INVALID, "bad argument to lifeapi_tune_cone%s");
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
+  const int cap = upw / 1000;
+  upw %= 1000;
   if (first)
     return cone_by_shape<true>(d_in, d_wanted, d_unwanted, (uint32_t *)d_out, n, gens, upw, rmax, cus,
-                               (hipStream_t)stream);
+                               (hipStream_t)stream, cap);
   return cone_by_shape<false>(d_in, d_wanted, d_unwanted, (uint8_t *)d_out, n, 0u, upw, rmax, cus,
-                              (hipStream_t)stream);
+                              (hipStream_t)stream, cap);
 }
 
 }  // extern "C"
