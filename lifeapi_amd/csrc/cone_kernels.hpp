@@ -60,37 +60,37 @@ __device__ __forceinline__ void cone_wave(const uint64_t *in, const uint64_t *__
   };
   for (uint64_t u0 = u_first; u0 < n; u0 += u_step) {
 #pragma unroll 1
-  for (int pass = 0; pass < R / RB; ++pass) {
-    const uint64_t ub = u0 + (uint64_t)pass * RB * GPS + q;
-    W a[RB];
-#pragma unroll
-    for (int k = 0; k < RB; ++k) {
-      const uint64_t u = ub + (uint64_t)k * GPS;
-      a[k] = (live && u < n) ? ld<true>(in + u * kWave + col) : W{0u, 0u};
-    }
-    uint32_t res[RB];
-    if constexpr (FIRST) {
-#pragma unroll
-      for (int k = 0; k < RB; ++k) res[k] = 0;
-      for (uint32_t g = 1; g <= gens; ++g) {
-#pragma unroll
-        for (int k = 0; k < RB; ++k) {
-          a[k] = life_gen<XDPP, 3>(a[k], nullptr, lane);
-          if (res[k] == 0 && clean(a[k])) res[k] = g;
-        }
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < RB; ++k) res[k] = clean(a[k]) ? 1u : 0u;
-    }
-    if (j == 0) {
+    for (int pass = 0; pass < R / RB; ++pass) {
+      const uint64_t ub = u0 + (uint64_t)pass * RB * GPS + q;
+      W a[RB];
 #pragma unroll
       for (int k = 0; k < RB; ++k) {
         const uint64_t u = ub + (uint64_t)k * GPS;
-        if (u < n) out[u] = (OutT)res[k];
+        a[k] = (live && u < n) ? ld<true>(in + u * kWave + col) : W{0u, 0u};
+      }
+      uint32_t res[RB];
+      if constexpr (FIRST) {
+#pragma unroll
+        for (int k = 0; k < RB; ++k) res[k] = 0;
+        for (uint32_t g = 1; g <= gens; ++g) {
+#pragma unroll
+          for (int k = 0; k < RB; ++k) {
+            a[k] = life_gen<XDPP, 3>(a[k], nullptr, lane);
+            if (res[k] == 0 && clean(a[k])) res[k] = g;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < RB; ++k) res[k] = clean(a[k]) ? 1u : 0u;
+      }
+      if (j == 0) {
+#pragma unroll
+        for (int k = 0; k < RB; ++k) {
+          const uint64_t u = ub + (uint64_t)k * GPS;
+          if (u < n) out[u] = (OutT)res[k];
+        }
       }
     }
-  }
   }
 }
 
@@ -109,25 +109,25 @@ __device__ __forceinline__ void cone_wave_full16(const uint64_t *in, const uint6
   const uint64_t m0 = w0 | unwanted[col], m1 = w1 | unwanted[col + 1];
   for (uint64_t u0 = u_first; u0 < n; u0 += u_step) {
 #pragma unroll 1
-  for (int pass = 0; pass < UPW / (2 * RB); ++pass) {
-    const uint64_t ub = u0 + (uint64_t)pass * 2 * RB;
-    u64x2 v[RB];
+    for (int pass = 0; pass < UPW / (2 * RB); ++pass) {
+      const uint64_t ub = u0 + (uint64_t)pass * 2 * RB;
+      u64x2 v[RB];
 #pragma unroll
-    for (int k = 0; k < RB; ++k) {
-      const uint64_t u = ub + 2 * k + half;
-      v[k] = u < n ? __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(in + u * kWave + col))
-                   : u64x2{w0, w1};
-    }
+      for (int k = 0; k < RB; ++k) {
+        const uint64_t u = ub + 2 * k + half;
+        v[k] = u < n ? __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(in + u * kWave + col))
+                     : u64x2{w0, w1};
+      }
 #pragma unroll
-    for (int k = 0; k < RB; ++k) {
-      const uint64_t d = ((v[k][0] ^ w0) & m0) | ((v[k][1] ^ w1) & m1);
-      const uint64_t bad = __ballot(d != 0ull);  // lanes 0-31: universe 2k, 32-63: 2k+1
-      if (lane == 0) {
-        if (ub + 2 * k < n) out[ub + 2 * k] = (uint32_t)bad == 0u ? 1 : 0;
-        if (ub + 2 * k + 1 < n) out[ub + 2 * k + 1] = (uint32_t)(bad >> 32) == 0u ? 1 : 0;
+      for (int k = 0; k < RB; ++k) {
+        const uint64_t d = ((v[k][0] ^ w0) & m0) | ((v[k][1] ^ w1) & m1);
+        const uint64_t bad = __ballot(d != 0ull);  // lanes 0-31: universe 2k, 32-63: 2k+1
+        if (lane == 0) {
+          if (ub + 2 * k < n) out[ub + 2 * k] = (uint32_t)bad == 0u ? 1 : 0;
+          if (ub + 2 * k + 1 < n) out[ub + 2 * k + 1] = (uint32_t)(bad >> 32) == 0u ? 1 : 0;
+        }
       }
     }
-  }
   }
 }
 
