@@ -168,8 +168,15 @@ __global__ __launch_bounds__(kBlock) void k_cone(const uint64_t *in, const uint6
   else cone_wave<64, UPW, RMAX, FIRST>(in, wanted, unwanted, out, n, u0, step, gens, xs, K, lane);
 }
 
-// the shipped shape (tools/cone_ab.py)
-constexpr int kConeUniverses = 32, kConeSets = 8;
+// The shipped shape: 64 universes per wave, register sets 8 at a time, one-
+// shot grid.  Same process, 1M universes, each launch after a read-only scrub
+// (tools/ab/cone_grid_ab.py, profiles/r04/r04g/cone_grid_ab.jsonl): the
+// 4-column target's filter 0.0270 against 0.0288 ms with 32 per wave (back to
+// back 0.0221 / 0.0240), Contains 0.0246 / 0.0256, a loaf box alike; the
+// whole-board filter 0.0933 / 0.0892 (back to back 0.0928 / 0.0940).  Capped
+// grids whose waves find the window once and loop over the batch: within
+// +-3 % of the one-shot grid for small targets, slower for the whole board.
+constexpr int kConeUniverses = 64, kConeSets = 8;
 
 // Launches k_cone on a one-shot grid.
 template <int UPW, int RMAX, bool FIRST, typename OutT>
