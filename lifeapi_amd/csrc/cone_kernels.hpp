@@ -183,12 +183,17 @@ template <int UPW, int RMAX, bool FIRST, typename OutT>
 int launch_cone(const uint64_t *d_in, const uint64_t *d_wanted, const uint64_t *d_unwanted, OutT *d_out, size_t n,
                 uint32_t gens, int cus, hipStream_t stream, int blocks_per_cu = 0) {
   const dim3 grid(grid_for((n + UPW - 1) / UPW, cus, blocks_per_cu));
-  if (!FIRST && aligned16(d_in))
-    hipLaunchKernelGGL((k_cone<UPW, RMAX, FIRST, OutT, true>), grid, dim3(kBlock), 0, stream, d_in, d_wanted,
-                       d_unwanted, d_out, (uint64_t)n, gens);
-  else
-    hipLaunchKernelGGL((k_cone<UPW, RMAX, FIRST, OutT, false>), grid, dim3(kBlock), 0, stream, d_in, d_wanted,
-                       d_unwanted, d_out, (uint64_t)n, gens);
+  bool a16 = false;
+  if constexpr (!FIRST) a16 = aligned16(d_in);
+  if constexpr (!FIRST) {
+    if (a16) {
+      hipLaunchKernelGGL((k_cone<UPW, RMAX, FIRST, OutT, true>), grid, dim3(kBlock), 0, stream, d_in, d_wanted,
+                         d_unwanted, d_out, (uint64_t)n, gens);
+      return launched("k_cone launch");
+    }
+  }
+  hipLaunchKernelGGL((k_cone<UPW, RMAX, FIRST, OutT, false>), grid, dim3(kBlock), 0, stream, d_in, d_wanted,
+                     d_unwanted, d_out, (uint64_t)n, gens);
   return launched("k_cone launch");
 }
 
