@@ -134,7 +134,13 @@ def main():
          {"lines_128B_per_object": 1})
     both("k_cone 1 gen (first hit only), 2x2 block + ring", n, 516, lambda: hip.step_contains(x, bw, bu, 1),
          {"lines_128B_per_object": 1})
-    both("k_step_contains 1 gen + final states", n, 1028, lambda: hip.step_contains(x, w, w, 1, final=y))
+    fp = [x.clone(), y]
+
+    def filter_pingpong():  # a loop stepping its batch with the filter: final states ping-ponged
+        hip.step_contains(fp[0], w, w, 1, final=fp[1])
+        fp.reverse()
+
+    both("k_step_contains 1 gen + final states (ping-pong)", n, 1028, filter_pingpong)
     both("k_fill", n, 512, lambda: hip.fill_random(n, seed=9))
     both("k_counts NeighbourCount", n, 512 + 2048, lambda: hip.neighbour_count(x))
     both("k_counts InteractionCounts", n, 512 + 1536, lambda: hip.interaction_counts(x))
