@@ -131,33 +131,23 @@ __device__ __forceinline__ void cone_wave_full16(const uint64_t *in, const uint6
   }
 }
 
-// The column window of the care cells, widened by the light cone of `gens`
-// generations: xs = first column, K = columns (64: the whole board from 0).
-__device__ __forceinline__ void cone_window(const uint64_t *__restrict__ wanted,
-                                            const uint64_t *__restrict__ unwanted, uint32_t gens, int lane,
-                                            uint32_t &xs, uint32_t &K) {
-  const uint64_t cols = __ballot((wanted[lane] | unwanted[lane]) != 0ull);  // bit x: column x has care cells
-  uint32_t x0, w;
-  care_window(cols, x0, w);
-  K = w + 2 * gens;
-  xs = (x0 - gens) & (kWave - 1);
-  if (K >= (uint32_t)kWave) K = kWave, xs = 0;
-}
-
 // UPW universes per wave (one-shot grid of ceil(n / UPW) waves), every wave
 // choosing its lane layout from the window (wave-uniform: the target is the
 // same for all).  Each choice runs its own copy of the pass.  A16: the batch
 // is 16-byte aligned (Contains over the whole board then takes 16-byte loads).
+// kmax: a wave whose window K exceeds it returns at once (the iterated
+// search loop's split-layout kernels answer those, step.hip).
 template <int UPW, int RMAX, bool FIRST, typename OutT, bool A16 = false>
 __global__ __launch_bounds__(kBlock) void k_cone(const uint64_t *in, const uint64_t *__restrict__ wanted,
                                                  const uint64_t *__restrict__ unwanted, OutT *__restrict__ out,
-                                                 uint64_t n, uint32_t gens) {
+                                                 uint64_t n, uint32_t gens, uint32_t kmax) {
   const int lane = threadIdx.x & (kWave - 1);
   const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint64_t u0 = wave * UPW, step = (uint64_t)gridDim.x * kWavesPerBlock * UPW;  // grid-stride (capped grids)
   if (u0 >= n) return;
   uint32_t xs, K;
   cone_window(wanted, unwanted, FIRST ? gens : 0u, lane, xs, K);
+  if (K > kmax) return;
   if constexpr (!FIRST && A16) {
     if (K == (uint32_t)kWave) return cone_wave_full16<UPW, RMAX>(in, wanted, unwanted, out, n, u0, step, lane);
   }
@@ -177,23 +167,28 @@ __global__ __launch_bounds__(kBlock) void k_cone(const uint64_t *in, const uint6
 // grids whose waves find the window once and loop over the batch: within
 // +-3 % of the one-shot grid for small targets, slower for the whole board.
 constexpr int kConeUniverses = 64, kConeSets = 8;
+// The iterated search loop (gens > 2, no final states) takes the light-cone
+// kernel while the cone spans at most this many columns (P <= 32 lanes per
+// universe: at most half the natural layout's work per universe-generation,
+// against the split layout's 18 issue slots plus its layout change).
+constexpr uint32_t kConeIterColumns = 32;
 
 // Launches k_cone on a one-shot grid.
 template <int UPW, int RMAX, bool FIRST, typename OutT>
 int launch_cone(const uint64_t *d_in, const uint64_t *d_wanted, const uint64_t *d_unwanted, OutT *d_out, size_t n,
-                uint32_t gens, int cus, hipStream_t stream, int blocks_per_cu = 0) {
+                uint32_t gens, int cus, hipStream_t stream, int blocks_per_cu = 0, uint32_t kmax = kWave) {
   const dim3 grid(grid_for((n + UPW - 1) / UPW, cus, blocks_per_cu));
   bool a16 = false;
   if constexpr (!FIRST) a16 = aligned16(d_in);
   if constexpr (!FIRST) {
     if (a16) {
       hipLaunchKernelGGL((k_cone<UPW, RMAX, FIRST, OutT, true>), grid, dim3(kBlock), 0, stream, d_in, d_wanted,
-                         d_unwanted, d_out, (uint64_t)n, gens);
+                         d_unwanted, d_out, (uint64_t)n, gens, kmax);
       return launched("k_cone launch");
     }
   }
   hipLaunchKernelGGL((k_cone<UPW, RMAX, FIRST, OutT, false>), grid, dim3(kBlock), 0, stream, d_in, d_wanted,
-                     d_unwanted, d_out, (uint64_t)n, gens);
+                     d_unwanted, d_out, (uint64_t)n, gens, kmax);
   return launched("k_cone launch");
 }
 

@@ -149,19 +149,30 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
   if (generations > 2) {  // the layout of the shipped step for gens > 2
+    // Without final states, a target whose light cone over `generations`
+    // spans at most kConeIterColumns columns is answered by the light-cone
+    // kernel (natural layout, only those columns loaded and stepped; its
+    // waves leave wider cones alone), and the split kernels' waves skip it.
+    uint32_t cone_max = 0;
+    if (!d_final) {
+      rc = launch_cone<kConeUniverses, kConeSets, true>(d_in, d_wanted, d_unwanted, d_first_gen, n, generations, cus,
+                                                         (hipStream_t)stream, 0, kConeIterColumns);
+      if (rc != LIFEAPI_OK) return rc;
+      cone_max = kConeIterColumns;
+    }
     // two kernels, one per register layout (a target window of <= 4 rows in
     // 62 VGPRs, 8 waves per SIMD; the rest in 70, 7 waves): each wave finds
     // the window and only the matching kernel works (step_kernels.hpp
     // kContainsLo / kContainsHi)
     using Fn = void (*)(const uint64_t *, uint64_t *, const uint64_t *, const uint64_t *, uint32_t *, uint64_t,
-                        uint32_t);
+                        uint32_t, uint32_t);
     const Fn fns[2] = {k_step_contains_split<8, kContainsNet, kContainsLo>,
                        k_step_contains_split<8, kContainsNet, kContainsHi>};
     const dim3 grid(grid_for((n + 3) / 4, cus, 0));
     if (d_final) note_forward_write(d_final, (uint64_t)n * 512);
     for (const Fn fn : fns) {
       hipLaunchKernelGGL(fn, grid, dim3(kBlock), 0, (hipStream_t)stream, d_in, d_final, d_wanted, d_unwanted,
-                         d_first_gen, (uint64_t)n, generations);
+                         d_first_gen, (uint64_t)n, generations, cone_max);
       rc = launched("k_step_contains_split launch");
       if (rc != LIFEAPI_OK) return rc;
     }

@@ -433,17 +433,40 @@ __device__ __forceinline__ void care_window(uint64_t rm, uint32_t &y0, uint32_t 
   h = 64 - len;
   y0 = len ? ((uint32_t)__builtin_ctzll(cur) + len) & 63 : 0;
 }
+// The column window of a target's care cells, widened by the light cone of
+// `gens` generations: xs = first column, K = columns (64: the whole board
+// from column 0; also for gens >= 32, whatever the window).  The light-cone
+// kernels (cone_kernels.hpp) load exactly these columns.
+__device__ __forceinline__ void cone_window(const uint64_t *__restrict__ wanted,
+                                            const uint64_t *__restrict__ unwanted, uint32_t gens, int lane,
+                                            uint32_t &xs, uint32_t &K) {
+  const uint64_t cols = __ballot((wanted[lane] | unwanted[lane]) != 0ull);  // bit x: column x has care cells
+  uint32_t x0, w;
+  care_window(cols, x0, w);
+  K = gens >= (uint32_t)kWave / 2 ? (uint32_t)kWave : w + 2 * gens;
+  xs = (x0 - gens) & (kWave - 1);
+  if (K >= (uint32_t)kWave) K = kWave, xs = 0;
+}
+
+// cone_max: with no final states, a wave whose target's light cone spans at
+// most cone_max columns returns at once -- the light-cone kernel launched
+// beside it answers those (step.hip); 0 = never.
 template <int S, int NET, int ASM = 0>
 __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *in, uint64_t *fin,
                                                                 const uint64_t *__restrict__ wanted,
                                                                 const uint64_t *__restrict__ unwanted,
                                                                 uint32_t *__restrict__ first, uint64_t n,
-                                                                uint32_t gens) {
+                                                                uint32_t gens, uint32_t cone_max) {
   constexpr int P = S / 2;
   constexpr uint32_t every = P == 1 ? ~0u : P == 2 ? 0x55555555u : P == 4 ? 0x11111111u : 0x01010101u;
   __shared__ uint32_t lds[kWavesPerBlock * S * kWave];
   const int lane = threadIdx.x & (kWave - 1);
   const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  if (cone_max && !fin) {
+    uint32_t cxs, cK;
+    cone_window(wanted, unwanted, gens, lane, cxs, cK);
+    if (cK <= cone_max) return;
+  }
   uint32_t y0 = 0, h = S;  // the row window of ASM 3 (else: no rotation, all registers)
   if constexpr (ASM >= 3) {
     const uint64_t col = wanted[lane] | unwanted[lane];  // this lane's column of care cells

@@ -155,3 +155,25 @@ def test_cone_model_without_margins_is_wrong(port):
         cone_layout = keep
     want = direct(port, x, tw, tu, 1)
     assert 0 < want.sum() < len(x) and (got != want).any()
+
+
+@pytest.mark.parametrize("w,gens", [(1, 3), (2, 8), (4, 5), (4, 13), (6, 7), (6, 13), (10, 11), (16, 8), (20, 6),
+                                    (3, 15), (1, 31), (30, 17)])
+def test_cone_model_iterated(port, w, gens):
+    """The iterated search loop on the light cone (gens > 2, no final
+    states): the margins grow with g (K = w + 2g), and a cone that reaches 64
+    columns (or g >= 32) is the whole board; equal to the direct loop"""
+    rng = np.random.default_rng(100 * w + gens)
+    n = 65
+    x = port.fill(n, seed=w + gens) & port.fill(n, seed=3 * w + gens)
+    x[::3] = x[0]
+    x0 = int(rng.integers(64))
+    box = np.zeros(64, np.uint64)
+    for i in range(w):
+        if i in (0, w - 1) or rng.random() < 0.5:
+            box[(x0 + i) % 64] = np.uint64(int(rng.integers(1, 1 << 63)))
+    ahead = port.step_batch(x[:1], gens // 2)[0]
+    tw, tu = ahead & box, box & ~ahead
+    want = direct(port, x, tw, tu, gens)
+    assert (cone_model(port, x, tw, tu, gens) == want).all()
+    assert want[0] != 0

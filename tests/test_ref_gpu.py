@@ -316,3 +316,29 @@ def test_cone_ragged_and_empty_target_vs_reference(hip, R, port, n):
             assert (first.cpu().numpy().astype(np.uint32) == exp).all(), (n, gens)
     first, _ = hip.step_contains(to_dev(x), to_dev(zero[None]), to_dev(zero[None]), 2)
     assert (first.cpu().numpy() == 1).all()
+
+
+@pytest.mark.parametrize("w,gens", [(1, 3), (4, 3), (4, 8), (4, 14), (6, 9), (6, 13), (6, 14), (10, 11), (16, 8),
+                                    (20, 6), (26, 3), (30, 1), (3, 15), (2, 16), (1, 40)])
+def test_iterated_search_loop_cone_and_split_vs_reference(hip, R, port, w, gens):
+    """gens > 2 with no final states: targets whose light cone spans at most
+    32 columns are answered by the cone kernel, the rest by the split-layout
+    pair (each wave of each launch checks), with final states always by the
+    pair; both against the reference's own Step() + Contains loop, windows
+    straddling the seam, ragged n"""
+    rng = np.random.default_rng(7 * w + gens)
+    n = 1031
+    x = port.fill(n, seed=500 + w) & port.fill(n, seed=600 + gens)
+    x[::4] = x[0]
+    for x0 in (int(rng.integers(64)), 62):
+        tw, tu = _column_box_target(rng, R.step_batch(x[:1], max(1, gens // 2))[0], x0, w)
+        dw, du = to_dev(tw[None]), to_dev(tu[None])
+        exp_first, exp_fin = R.step_contains_batch(x, tw, tu, gens, nthreads=THREADS)
+        first, _ = hip.step_contains(to_dev(x), dw, du, gens)
+        got = first.cpu().numpy().astype(np.uint32)
+        assert (got == exp_first).all(), (w, gens, x0, np.nonzero(got != exp_first)[0][:8])
+        fin = torch.empty((n, 64), dtype=torch.int64, device="cuda")
+        first, _ = hip.step_contains(to_dev(x), dw, du, gens, final=fin)
+        assert (first.cpu().numpy().astype(np.uint32) == exp_first).all()
+        _check(to_host(fin), exp_fin, f"final states, w={w} gens={gens}")
+        assert 1 <= exp_first[0] <= gens

@@ -31,14 +31,15 @@ int cone_by_shape(const uint64_t *in, const uint64_t *w, const uint64_t *u, OutT
 
 extern "C" {
 
-/* first != 0: the search filter (d_out uint32 first generations, gens <= 2);
+/* first != 0: the search filter (d_out uint32 first generations, any gens;
+ * every window, the whole board included);
  * first == 0: Contains (d_out uint8).  upw universes per wave, rmax register
  * sets per pass; upw + 1000 * c: a grid of at most c blocks per CU looping
  * over the batch (each wave finds the window once). */
 int lifeapi_tune_cone(int first, const uint64_t *d_in, const uint64_t *d_wanted, const uint64_t *d_unwanted,
                       void *d_out, size_t n, uint32_t gens, int upw, int rmax, void *stream) {
   if (n == 0) return LIFEAPI_OK;
-  if (!d_in || !d_wanted || !d_unwanted || !d_out || gens > 2)
+  if (!d_in || !d_wanted || !d_unwanted || !d_out)
     return fail(LIFEAPI_E_INVALID, "bad argument to lifeapi_tune_cone%s");
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;

@@ -538,7 +538,8 @@ int lifeapi_tune_step_contains(const uint64_t *d_in, uint64_t *d_final, const ui
   }
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
-  using Fn = void (*)(const uint64_t *, uint64_t *, const uint64_t *, const uint64_t *, uint32_t *, uint64_t, uint32_t);
+  using Fn = void (*)(const uint64_t *, uint64_t *, const uint64_t *, const uint64_t *, uint32_t *, uint64_t, uint32_t,
+                      uint32_t);
   const Fn fns[9] = {k_step_contains_split<8, kContainsNet, 0>, k_step_contains_split<8, kContainsNet, 1>,
                      k_step_contains_split<8, kContainsNet, 2>, k_step_contains_split<8, kContainsNet, 3>,
                      k_step_contains_split<8, kContainsNet, 4>, k_step_contains_split<8, kContainsNet, 5>,
@@ -546,7 +547,7 @@ int lifeapi_tune_step_contains(const uint64_t *d_in, uint64_t *d_final, const ui
                      k_step_contains_split<8, kContainsNet, 8>};
   if (variant < 0 || variant > 8) return fail(LIFEAPI_E_INVALID, "unknown contains variant%s");
   hipLaunchKernelGGL(fns[variant], dim3(grid_for((n + 3) / 4, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream, d_in,
-                     d_final, d_wanted, d_unwanted, d_first_gen, (uint64_t)n, generations);
+                     d_final, d_wanted, d_unwanted, d_first_gen, (uint64_t)n, generations, 0u);
   return launched("k_step_contains_split (tuning) launch");
 }
 
@@ -610,12 +611,12 @@ int lifeapi_tune_step_contains_pair(const uint64_t *d_in, uint64_t *d_final, con
   if (rc != LIFEAPI_OK) return rc;
   hipLaunchKernelGGL((k_step_contains_split<8, kContainsNet, 7>), dim3(grid_for((n + 3) / 4, cus, cap_lo)),
                      dim3(kBlock), 0, (hipStream_t)stream, d_in, d_final, d_wanted, d_unwanted, d_first_gen,
-                     (uint64_t)n, generations);
+                     (uint64_t)n, generations, 0u);
   rc = launched("k_step_contains_split (tuning) launch");
   if (rc != LIFEAPI_OK) return rc;
   hipLaunchKernelGGL((k_step_contains_split<8, kContainsNet, 8>), dim3(grid_for((n + 3) / 4, cus, cap_hi)),
                      dim3(kBlock), 0, (hipStream_t)stream, d_in, d_final, d_wanted, d_unwanted, d_first_gen,
-                     (uint64_t)n, generations);
+                     (uint64_t)n, generations, 0u);
   return launched("k_step_contains_split (tuning) launch");
 }
 
