@@ -151,7 +151,9 @@ __global__ __launch_bounds__(kBlock) void k_cone(const uint64_t *in, const uint6
   if constexpr (!FIRST && A16) {
     if (K == (uint32_t)kWave) return cone_wave_full16<UPW, RMAX>(in, wanted, unwanted, out, n, u0, step, lane);
   }
-  if (K <= 4) cone_wave<4, UPW, RMAX, FIRST>(in, wanted, unwanted, out, n, u0, step, gens, xs, K, lane);
+  // (a wave of UPW universes takes whole register sets: P >= 64 / UPW)
+  if (K <= 4 && UPW >= 16) cone_wave<UPW >= 16 ? 4 : 8, UPW, RMAX, FIRST>(in, wanted, unwanted, out, n, u0, step, gens,
+                                                                         xs, K, lane);
   else if (K <= 8) cone_wave<8, UPW, RMAX, FIRST>(in, wanted, unwanted, out, n, u0, step, gens, xs, K, lane);
   else if (K <= 16) cone_wave<16, UPW, RMAX, FIRST>(in, wanted, unwanted, out, n, u0, step, gens, xs, K, lane);
   else if (K <= 32) cone_wave<32, UPW, RMAX, FIRST>(in, wanted, unwanted, out, n, u0, step, gens, xs, K, lane);
@@ -172,6 +174,9 @@ constexpr int kConeUniverses = 64, kConeSets = 8;
 // universe: at most half the natural layout's work per universe-generation,
 // against the split layout's 18 issue slots plus its layout change).
 constexpr uint32_t kConeIterColumns = 32;
+// ... with 8 universes per wave (1-4 register sets): that work is VALU-bound,
+// and 64 universes per wave would leave 64K universes one wave per SIMD.
+constexpr int kConeIterUniverses = 8;
 
 // Launches k_cone on a one-shot grid.
 template <int UPW, int RMAX, bool FIRST, typename OutT>

@@ -13,6 +13,7 @@ int cone_by_shape(const uint64_t *in, const uint64_t *w, const uint64_t *u, OutT
                   int upw, int rmax, int cus, hipStream_t st, int cap) {
 #define LIFEAPI_CONE(U, R) \
   if (upw == U && rmax == R) return launch_cone<U, R, FIRST>(in, w, u, out, n, gens, cus, st, cap);
+  LIFEAPI_CONE(8, 8)
   LIFEAPI_CONE(16, 4)
   LIFEAPI_CONE(16, 8)
   LIFEAPI_CONE(16, 16)
