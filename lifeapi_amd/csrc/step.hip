@@ -156,7 +156,8 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
     uint32_t cone_max = 0;
     if (!d_final) {
       rc = launch_cone<kConeIterUniverses, kConeSets, true>(d_in, d_wanted, d_unwanted, d_first_gen, n, generations,
-                                                             cus, (hipStream_t)stream, 0, kConeIterColumns);
+                                                             cus, (hipStream_t)stream, kConeIterBlocksPerCU,
+                                                             kConeIterColumns);
       if (rc != LIFEAPI_OK) return rc;
       cone_max = kConeIterColumns;
     }
