@@ -1,0 +1,59 @@
+"""The iterated search loop without final states as the product launches it
+(the cone kernel, then the split pair skipping the cone's waves), with the
+cone grid and the split grids capped at c blocks per CU (0 = one-shot): a
+4-column block target (the cone answers up to 13 generations) and a
+whole-board target (the split pair answers), 64K and 1M universes, gens 3,
+8, 13, 64; back to back, median of 3 x 20; results equal across caps."""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools", "tune"))
+import bench  # noqa: E402
+import lifeapi_amd.hip as hip  # noqa: E402
+import tune_hip as tune  # noqa: E402
+
+
+class RT:
+    kind = "hip"
+
+    def __init__(self):
+        self.device = torch.device("cuda", 0)
+        self.stream = torch.cuda.current_stream()
+
+    @staticmethod
+    def event():
+        return torch.cuda.Event(enable_timing=True)
+
+
+def main():
+    rt = RT()
+    bw, bu = np.zeros(64, np.uint64), np.zeros(64, np.uint64)
+    bw[10] = bw[11] = np.uint64(3 << 40)
+    for c in (9, 10, 11, 12):
+        bu[c] = np.uint64(15 << 39)
+    bu &= ~bw
+    ww, wu = np.zeros(64, np.uint64), np.zeros(64, np.uint64)
+    wu[0::3] = np.uint64(1 << 10)
+    caps = [(0, 0), (8, 0), (8, 16), (8, 32), (8, 64), (4, 32), (16, 32)]
+    for tname, (w, u) in (("block", (bw, bu)), ("whole", (ww, wu))):
+        dw, du = (torch.from_numpy(v.view(np.int64)[None].copy()).cuda() for v in (w, u))
+        for n in (1 << 16, 1 << 20):
+            x = hip.fill_random(n, seed=3)
+            for gens in (3, 8, 13, 64):
+                ref = tune.step_contains(x, dw, du, gens, 8 if tname == "whole" else 7)
+                r = {"target": tname, "universes": n, "gens": gens}
+                for cc, sc in caps:
+                    fn = lambda a, b, g=gens, cc=cc, sc=sc: tune.search_iter(x, dw, du, g, cc, sc)  # noqa: E731
+                    r[f"c{cc}_s{sc}_equal"] = bool((fn(0, 0) == ref).all().item())
+                    r[f"c{cc}_s{sc}_ms"] = bench.back_to_back_ms(rt, fn, x, x)
+                print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -53,4 +53,29 @@ int lifeapi_tune_cone(int first, const uint64_t *d_in, const uint64_t *d_wanted,
                               (hipStream_t)stream, cap);
 }
 
+/* the product's launch sequence for the iterated search loop without final
+ * states (step.hip, gens > 2): the cone kernel (8 universes per wave, cones
+ * of <= 32 columns, grid capped at cone_cap blocks per CU, 0 = one-shot), then
+ * the split pair (kContainsLo, kContainsHi) skipping those waves, each grid
+ * capped at split_cap blocks per CU (0 = one-shot)                           */
+int lifeapi_tune_search_iter(const uint64_t *d_in, const uint64_t *d_wanted, const uint64_t *d_unwanted,
+                             uint32_t *d_first, size_t n, uint32_t gens, int cone_cap, int split_cap, void *stream) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!d_in || !d_wanted || !d_unwanted || !d_first || gens <= 2 || cone_cap < 0 || split_cap < 0)
+    return fail(LIFEAPI_E_INVALID, "bad argument to lifeapi_tune_search_iter%s");
+  int cus = 0, rc = device_cus(cus);
+  if (rc != LIFEAPI_OK) return rc;
+  rc = launch_cone<kConeIterUniverses, kConeSets, true>(d_in, d_wanted, d_unwanted, d_first, n, gens, cus,
+                                                         (hipStream_t)stream, cone_cap, kConeIterColumns);
+  if (rc != LIFEAPI_OK) return rc;
+  const dim3 grid(grid_for((n + 3) / 4, cus, split_cap));
+  hipLaunchKernelGGL((k_step_contains_split<8, kContainsNet, kContainsLo>), grid, dim3(kBlock), 0, (hipStream_t)stream,
+                     d_in, (uint64_t *)nullptr, d_wanted, d_unwanted, d_first, (uint64_t)n, gens, kConeIterColumns);
+  rc = launched("k_step_contains_split (tuning) launch");
+  if (rc != LIFEAPI_OK) return rc;
+  hipLaunchKernelGGL((k_step_contains_split<8, kContainsNet, kContainsHi>), grid, dim3(kBlock), 0, (hipStream_t)stream,
+                     d_in, (uint64_t *)nullptr, d_wanted, d_unwanted, d_first, (uint64_t)n, gens, kConeIterColumns);
+  return launched("k_step_contains_split (tuning) launch");
+}
+
 }  // extern "C"

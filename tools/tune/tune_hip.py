@@ -304,3 +304,16 @@ def weld_u(welds, u: int, resident: int = 0, chunk: bool = False, stream=None):
     hip._check(lib.lifeapi_tune_weld_u(welds.data_ptr(), welds.shape[0], u, resident, 1 if chunk else 0,
                                        hip._stream(stream)))
     return welds
+
+
+lib.lifeapi_tune_search_iter.argtypes = [_vp, _vp, _vp, _vp, _sz, _u32, _int, _int, _vp]
+lib.lifeapi_tune_search_iter.restype = _int
+
+
+def search_iter(states, wanted, unwanted, generations, cone_cap, split_cap, stream=None):
+    """step.hip's gens > 2 launch sequence without final states, caps given"""
+    n = hip._universes(states)
+    first = torch.empty(n, dtype=torch.int32, device=states.device)
+    hip._check(lib.lifeapi_tune_search_iter(states.data_ptr(), wanted.data_ptr(), unwanted.data_ptr(), first.data_ptr(),
+                                            n, generations, cone_cap, split_cap, hip._stream(stream)))
+    return first
