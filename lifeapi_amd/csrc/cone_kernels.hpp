@@ -177,11 +177,14 @@ constexpr uint32_t kConeIterColumns = 32;
 // ... with 8 universes per wave (1-4 register sets): that work is VALU-bound,
 // and 64 universes per wave would leave 64K universes one wave per SIMD.
 constexpr int kConeIterUniverses = 8;
-// ... on a grid of at most 8 blocks (32 waves) per CU looping over the
+// ... on a grid of at most 16 blocks (64 waves) per CU looping over the
 // batch: when the split kernels answer (wider cones), the cone launch's waves
 // all return after the window search, and a one-shot grid of n / 8 waves
 // would cost that many wave launches.
-constexpr int kConeIterBlocksPerCU = 8;
+constexpr int kConeIterBlocksPerCU = 16;
+// ... and the split pair after it on grids of at most 32 blocks per CU
+// (step.hip): one of the two always idles.
+constexpr int kSplitIterBlocksPerCU = 32;
 
 // Launches k_cone on a one-shot grid.
 template <int UPW, int RMAX, bool FIRST, typename OutT>
