@@ -58,7 +58,9 @@ __device__ __forceinline__ void cone_wave(const uint64_t *in, const uint64_t *__
     if constexpr (P == kWave) return bad == 0ull;
     else return ((bad >> sh) & ((1ull << P) - 1)) == 0ull;
   };
+  static_assert(UPW <= kWave, "one result per lane");
   for (uint64_t u0 = u_first; u0 < n; u0 += u_step) {
+    uint32_t mine = 0;  // lane L: the result of universe u0 + L (one coalesced store per chunk)
 #pragma unroll 1
     for (int pass = 0; pass < R / RB; ++pass) {
       const uint64_t ub = u0 + (uint64_t)pass * RB * GPS + q;
@@ -83,14 +85,17 @@ __device__ __forceinline__ void cone_wave(const uint64_t *in, const uint64_t *__
 #pragma unroll
         for (int k = 0; k < RB; ++k) res[k] = clean(a[k]) ? 1u : 0u;
       }
-      if (j == 0) {
+      // set k's group q is universe u0 + pass * RB * GPS + k * GPS + q: its
+      // result (uniform over the group) moves to that lane
 #pragma unroll
-        for (int k = 0; k < RB; ++k) {
-          const uint64_t u = ub + (uint64_t)k * GPS;
-          if (u < n) out[u] = (OutT)res[k];
-        }
+      for (int k = 0; k < RB; ++k) {
+        const uint32_t first = (uint32_t)(pass * RB + k) * GPS, rel = (uint32_t)lane - first;
+        uint32_t v = res[k];
+        if constexpr (GPS > 1) v = (uint32_t)__shfl((int)v, (int)((rel & (GPS - 1)) * P));
+        if (rel < (uint32_t)GPS) mine = v;
       }
     }
+    if (lane < UPW && u0 + lane < n) out[u0 + lane] = (OutT)mine;
   }
 }
 
@@ -108,6 +113,7 @@ __device__ __forceinline__ void cone_wave_full16(const uint64_t *in, const uint6
   const uint64_t w0 = wanted[col], w1 = wanted[col + 1];
   const uint64_t m0 = w0 | unwanted[col], m1 = w1 | unwanted[col + 1];
   for (uint64_t u0 = u_first; u0 < n; u0 += u_step) {
+    uint32_t mine = 0;  // lane L: the answer for universe u0 + L
 #pragma unroll 1
     for (int pass = 0; pass < UPW / (2 * RB); ++pass) {
       const uint64_t ub = u0 + (uint64_t)pass * 2 * RB;
@@ -122,12 +128,11 @@ __device__ __forceinline__ void cone_wave_full16(const uint64_t *in, const uint6
       for (int k = 0; k < RB; ++k) {
         const uint64_t d = ((v[k][0] ^ w0) & m0) | ((v[k][1] ^ w1) & m1);
         const uint64_t bad = __ballot(d != 0ull);  // lanes 0-31: universe 2k, 32-63: 2k+1
-        if (lane == 0) {
-          if (ub + 2 * k < n) out[ub + 2 * k] = (uint32_t)bad == 0u ? 1 : 0;
-          if (ub + 2 * k + 1 < n) out[ub + 2 * k + 1] = (uint32_t)(bad >> 32) == 0u ? 1 : 0;
-        }
+        const uint32_t rel = (uint32_t)lane - (uint32_t)(pass * 2 * RB + 2 * k);
+        if (rel < 2u) mine = (uint32_t)(bad >> (32 * rel)) == 0u ? 1u : 0u;
       }
     }
+    if (lane < UPW && u0 + lane < n) out[u0 + lane] = (uint8_t)mine;
   }
 }
 
