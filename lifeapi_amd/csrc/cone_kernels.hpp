@@ -27,78 +27,6 @@
 namespace lifeapi_impl {
 namespace {
 
-// One wave's chunks of UPW universes u0 .. u0 + UPW - 1, u0 = u_first,
-// u_first + u_step, ... (< n), under the window (xs = first loaded column,
-// K <= P loaded columns).  FIRST: out[u] = the first
-// generation in 1..gens whose state contains the target (0 = never), else
-// out[u] = Contains(target) of the state as loaded (gens unused).  Register
-// sets go RMAX at a time: all their loads are issued before the first test.
-template <int P, int UPW, int RMAX, bool FIRST, typename OutT>
-__device__ __forceinline__ void cone_wave(const uint64_t *in, const uint64_t *__restrict__ wanted,
-                                          const uint64_t *__restrict__ unwanted, OutT *__restrict__ out,
-                                          uint64_t n, uint64_t u_first, uint64_t u_step, uint32_t gens,
-                                          uint32_t xs, uint32_t K, int lane) {
-  constexpr int GPS = kWave / P;  // universes per register set
-  static_assert(UPW % GPS == 0, "a wave takes whole register sets");
-  constexpr int R = UPW / GPS;
-  constexpr int RB = R < RMAX ? R : RMAX;
-  static_assert(R % RB == 0, "passes of RB sets");
-  const uint32_t j = (uint32_t)lane & (P - 1), q = (uint32_t)lane / P;
-  const uint32_t col = (xs + j) & (kWave - 1);
-  const bool live = j < K;
-  // the target's column under this lane (zero outside the window: the care
-  // columns all lie in [x0, x0 + w), and no lane j >= K or margin lane maps
-  // onto one while K <= 64)
-  const uint64_t w64 = live ? wanted[col] : 0ull, m64 = live ? (w64 | unwanted[col]) : 0ull;
-  const W tw = split(w64), tm = split(m64);
-  const uint32_t sh = q * P;
-  auto clean = [&](W s) __attribute__((always_inline)) {
-    const uint32_t d = ((s.lo ^ tw.lo) & tm.lo) | ((s.hi ^ tw.hi) & tm.hi);
-    const uint64_t bad = __ballot(d != 0u);  // wave-uniform
-    if constexpr (P == kWave) return bad == 0ull;
-    else return ((bad >> sh) & ((1ull << P) - 1)) == 0ull;
-  };
-  static_assert(UPW <= kWave, "one result per lane");
-  for (uint64_t u0 = u_first; u0 < n; u0 += u_step) {
-    uint32_t mine = 0;  // lane L: the result of universe u0 + L (one coalesced store per chunk)
-#pragma unroll 1
-    for (int pass = 0; pass < R / RB; ++pass) {
-      const uint64_t ub = u0 + (uint64_t)pass * RB * GPS + q;
-      W a[RB];
-#pragma unroll
-      for (int k = 0; k < RB; ++k) {
-        const uint64_t u = ub + (uint64_t)k * GPS;
-        a[k] = (live && u < n) ? ld<true>(in + u * kWave + col) : W{0u, 0u};
-      }
-      uint32_t res[RB];
-      if constexpr (FIRST) {
-#pragma unroll
-        for (int k = 0; k < RB; ++k) res[k] = 0;
-        for (uint32_t g = 1; g <= gens; ++g) {
-#pragma unroll
-          for (int k = 0; k < RB; ++k) {
-            a[k] = life_gen<XDPP, 3>(a[k], nullptr, lane);
-            if (res[k] == 0 && clean(a[k])) res[k] = g;
-          }
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < RB; ++k) res[k] = clean(a[k]) ? 1u : 0u;
-      }
-      // set k's group q is universe u0 + pass * RB * GPS + k * GPS + q: its
-      // result (uniform over the group) moves to that lane
-#pragma unroll
-      for (int k = 0; k < RB; ++k) {
-        const uint32_t first = (uint32_t)(pass * RB + k) * GPS, rel = (uint32_t)lane - first;
-        uint32_t v = res[k];
-        if constexpr (GPS > 1) v = (uint32_t)__shfl((int)v, (int)((rel & (GPS - 1)) * P));
-        if (rel < (uint32_t)GPS) mine = v;
-      }
-    }
-    if (lane < UPW && u0 + lane < n) out[u0 + lane] = (OutT)mine;
-  }
-}
-
 // Contains over the whole board (K = 64) on a 16-byte aligned batch: lane l
 // reads words 2(l mod 32), 2(l mod 32) + 1 of universe 2k + l / 32 (one
 // dwordx4 moves two universes per wave-instruction, as k_contains16), RMAX
@@ -174,22 +102,20 @@ __global__ __launch_bounds__(kBlock) void k_cone(const uint64_t *in, const uint6
 // grids whose waves find the window once and loop over the batch: within
 // +-3 % of the one-shot grid for small targets, slower for the whole board.
 constexpr int kConeUniverses = 64, kConeSets = 8;
-// The iterated search loop (gens > 2, no final states) takes the light-cone
-// kernel while the cone spans at most this many columns (P <= 32 lanes per
-// universe: at most half the natural layout's work per universe-generation,
-// against the split layout's 18 issue slots plus its layout change).
+// The iterated search loop (gens > 2, no final states) steps the light cone
+// while it spans at most this many columns (P <= 32 lanes per universe: at
+// most half the natural layout's work per universe-generation, against the
+// split layout's 18 issue slots plus its layout change) -- inside
+// kContainsLo (step_kernels.hpp, kConeLoUniverses = 8 universes per wave
+// chunk: that work is VALU-bound, and 64 per wave would leave 64K universes
+// one wave per SIMD).
 constexpr uint32_t kConeIterColumns = 32;
-// ... with 8 universes per wave (1-4 register sets): that work is VALU-bound,
-// and 64 universes per wave would leave 64K universes one wave per SIMD.
-constexpr int kConeIterUniverses = 8;
-// ... on a grid of at most 16 blocks (64 waves) per CU looping over the
-// batch: when the split kernels answer (wider cones), the cone launch's waves
-// all return after the window search, and a one-shot grid of n / 8 waves
-// would cost that many wave launches.
-constexpr int kConeIterBlocksPerCU = 16;
-// ... and the split pair after it on grids of at most 32 blocks per CU
-// (step.hip): one of the two always idles.
+// ... with both split kernels on grids of at most 32 blocks per CU looping
+// over the batch (step.hip): one of the two always idles.
 constexpr int kSplitIterBlocksPerCU = 32;
+// The tuning build's separate-launch form of the same (k_cone before the
+// pair): 8 universes per wave, at most 16 blocks per CU.
+constexpr int kConeIterUniverses = 8, kConeIterBlocksPerCU = 16;
 
 // Launches k_cone on a one-shot grid.
 template <int UPW, int RMAX, bool FIRST, typename OutT>

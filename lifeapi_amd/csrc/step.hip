@@ -150,25 +150,15 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
   if (rc != LIFEAPI_OK) return rc;
   if (generations > 2) {  // the layout of the shipped step for gens > 2
     // Without final states, a target whose light cone over `generations`
-    // spans at most kConeIterColumns columns is answered by the light-cone
-    // kernel (natural layout, only those columns loaded and stepped; its
-    // waves leave wider cones alone), and the split kernels' waves skip it.
-    // Both grids are capped here (blocks per CU, looping over the batch):
-    // the idle kernel's waves then cost a few microseconds instead of a full
-    // wave launch per 4 universes (tools/ab/search_iter_caps_ab.py,
-    // profiles/r04/r04k: 1M universes, a 4-column block target, 3 generations
-    // 0.166 -> 0.071 ms, 64 generations 1.70 -> 1.56 ms; a whole-board target
-    // 0.34 -> 0.20 and 1.71 -> 1.56 ms; 64K unchanged or faster).
+    // spans at most kConeIterColumns columns is answered on that cone:
+    // kContainsLo's waves step only those columns in the natural layout
+    // (cone_wave) and kContainsHi's return.  Both grids are then capped
+    // (blocks per CU, looping over the batch), so that the idle kernel's
+    // waves cost a few microseconds instead of a wave launch per 4 universes
+    // (tools/ab/search_iter_caps_ab.py).
     uint32_t cone_max = 0;
     int split_cap = 0;
-    if (!d_final) {
-      rc = launch_cone<kConeIterUniverses, kConeSets, true>(d_in, d_wanted, d_unwanted, d_first_gen, n, generations,
-                                                             cus, (hipStream_t)stream, kConeIterBlocksPerCU,
-                                                             kConeIterColumns);
-      if (rc != LIFEAPI_OK) return rc;
-      cone_max = kConeIterColumns;
-      split_cap = kSplitIterBlocksPerCU;
-    }
+    if (!d_final) cone_max = kConeIterColumns, split_cap = kSplitIterBlocksPerCU;
     // two kernels, one per register layout (a target window of <= 4 rows in
     // 62 VGPRs, 8 waves per SIMD; the rest in 70, 7 waves): each wave finds
     // the window and only the matching kernel works (step_kernels.hpp

@@ -406,6 +406,8 @@ constexpr int kContainsNet = 6;  // tail network of the fused kernel (as k_step'
 // sees one assembly loop's pins at a time: 8 takes 70 VGPRs (7 waves per
 // SIMD), where one shared pass took 84 (5), and 7 takes 62 (8 waves).
 constexpr int kContainsLo = 7, kContainsHi = 8;
+// the light-cone path of kContainsLo (cone_max below): universes per wave chunk
+constexpr int kConeLoUniverses = 8;
 constexpr uint32_t kLowRows = 4;  // tools/gen_split_asm.py LOW_H
 
 __device__ __forceinline__ uint64_t rotr64(uint64_t v, uint32_t k) {
@@ -448,9 +450,83 @@ __device__ __forceinline__ void cone_window(const uint64_t *__restrict__ wanted,
   if (K >= (uint32_t)kWave) K = kWave, xs = 0;
 }
 
-// cone_max: with no final states, a wave whose target's light cone spans at
-// most cone_max columns returns at once -- the light-cone kernel launched
-// beside it answers those (step.hip); 0 = never.
+// The light-cone pass (cone_kernels.hpp; here for the iterated search
+// loop's low-layout kernel, below).  One wave's chunks of UPW universes u0 .. u0 + UPW - 1, u0 = u_first,
+// u_first + u_step, ... (< n), under the window (xs = first loaded column,
+// K <= P loaded columns).  FIRST: out[u] = the first
+// generation in 1..gens whose state contains the target (0 = never), else
+// out[u] = Contains(target) of the state as loaded (gens unused).  Register
+// sets go RMAX at a time: all their loads are issued before the first test.
+template <int P, int UPW, int RMAX, bool FIRST, typename OutT>
+__device__ __forceinline__ void cone_wave(const uint64_t *in, const uint64_t *__restrict__ wanted,
+                                          const uint64_t *__restrict__ unwanted, OutT *__restrict__ out,
+                                          uint64_t n, uint64_t u_first, uint64_t u_step, uint32_t gens,
+                                          uint32_t xs, uint32_t K, int lane) {
+  constexpr int GPS = kWave / P;  // universes per register set
+  static_assert(UPW % GPS == 0, "a wave takes whole register sets");
+  constexpr int R = UPW / GPS;
+  constexpr int RB = R < RMAX ? R : RMAX;
+  static_assert(R % RB == 0, "passes of RB sets");
+  const uint32_t j = (uint32_t)lane & (P - 1), q = (uint32_t)lane / P;
+  const uint32_t col = (xs + j) & (kWave - 1);
+  const bool live = j < K;
+  // the target's column under this lane (zero outside the window: the care
+  // columns all lie in [x0, x0 + w), and no lane j >= K or margin lane maps
+  // onto one while K <= 64)
+  const uint64_t w64 = live ? wanted[col] : 0ull, m64 = live ? (w64 | unwanted[col]) : 0ull;
+  const W tw = split(w64), tm = split(m64);
+  const uint32_t sh = q * P;
+  auto clean = [&](W s) __attribute__((always_inline)) {
+    const uint32_t d = ((s.lo ^ tw.lo) & tm.lo) | ((s.hi ^ tw.hi) & tm.hi);
+    const uint64_t bad = __ballot(d != 0u);  // wave-uniform
+    if constexpr (P == kWave) return bad == 0ull;
+    else return ((bad >> sh) & ((1ull << P) - 1)) == 0ull;
+  };
+  static_assert(UPW <= kWave, "one result per lane");
+  for (uint64_t u0 = u_first; u0 < n; u0 += u_step) {
+    uint32_t mine = 0;  // lane L: the result of universe u0 + L (one coalesced store per chunk)
+#pragma unroll 1
+    for (int pass = 0; pass < R / RB; ++pass) {
+      const uint64_t ub = u0 + (uint64_t)pass * RB * GPS + q;
+      W a[RB];
+#pragma unroll
+      for (int k = 0; k < RB; ++k) {
+        const uint64_t u = ub + (uint64_t)k * GPS;
+        a[k] = (live && u < n) ? ld<true>(in + u * kWave + col) : W{0u, 0u};
+      }
+      uint32_t res[RB];
+      if constexpr (FIRST) {
+#pragma unroll
+        for (int k = 0; k < RB; ++k) res[k] = 0;
+        for (uint32_t g = 1; g <= gens; ++g) {
+#pragma unroll
+          for (int k = 0; k < RB; ++k) {
+            a[k] = life_gen<XDPP, 3>(a[k], nullptr, lane);
+            if (res[k] == 0 && clean(a[k])) res[k] = g;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < RB; ++k) res[k] = clean(a[k]) ? 1u : 0u;
+      }
+      // set k's group q is universe u0 + pass * RB * GPS + k * GPS + q: its
+      // result (uniform over the group) moves to that lane
+#pragma unroll
+      for (int k = 0; k < RB; ++k) {
+        const uint32_t first = (uint32_t)(pass * RB + k) * GPS, rel = (uint32_t)lane - first;
+        uint32_t v = res[k];
+        if constexpr (GPS > 1) v = (uint32_t)__shfl((int)v, (int)((rel & (GPS - 1)) * P));
+        if (rel < (uint32_t)GPS) mine = v;
+      }
+    }
+    if (lane < UPW && u0 + lane < n) out[u0 + lane] = (OutT)mine;
+  }
+}
+
+// cone_max: with no final states, a target whose light cone spans at most
+// cone_max columns (0 = never) is answered on that cone: kContainsLo's waves
+// step only those columns in the natural layout (cone_wave, 8 universes per
+// wave chunk, looping over the batch), every other ASM's waves return at once.
 template <int S, int NET, int ASM = 0>
 __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *in, uint64_t *fin,
                                                                 const uint64_t *__restrict__ wanted,
@@ -465,7 +541,17 @@ __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *
   if (cone_max && !fin) {
     uint32_t cxs, cK;
     cone_window(wanted, unwanted, gens, lane, cxs, cK);
-    if (cK <= cone_max) return;
+    if (cK <= cone_max) {
+      if constexpr (ASM == kContainsLo) {
+        constexpr int U = kConeLoUniverses;
+        const uint64_t u0 = ((uint64_t)blockIdx.x * kWavesPerBlock + wib) * U,
+                       step = (uint64_t)gridDim.x * kWavesPerBlock * U;
+        if (cK <= 8) cone_wave<8, U, 8, true>(in, wanted, unwanted, first, n, u0, step, gens, cxs, cK, lane);
+        else if (cK <= 16) cone_wave<16, U, 8, true>(in, wanted, unwanted, first, n, u0, step, gens, cxs, cK, lane);
+        else if (cK <= 32) cone_wave<32, U, 8, true>(in, wanted, unwanted, first, n, u0, step, gens, cxs, cK, lane);
+      }
+      return;
+    }
   }
   uint32_t y0 = 0, h = S;  // the row window of ASM 3 (else: no rotation, all registers)
   if constexpr (ASM >= 3) {

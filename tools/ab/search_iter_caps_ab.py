@@ -1,6 +1,9 @@
-"""The iterated search loop without final states as the product launches it
-(the cone kernel, then the split pair skipping the cone's waves), with the
-cone grid and the split grids capped at c blocks per CU (0 = one-shot): a
+"""The iterated search loop without final states: round 4's first form (the
+cone kernel launched alone, then the split pair, whose low-layout kernel
+now steps the cone as well), with the cone grid and the split grids capped
+at c blocks per CU (0 = one-shot); round 3's launch (the uncapped pair, no
+cone); the product (kContainsLo stepping the cone, capped pair); and the
+cone kernel alone (8 universes per wave, a lower bound for narrow cones): a
 4-column block target (the cone answers up to 13 generations) and a
 whole-board target (the split pair answers); cone cap + 1000 * u: u universes
 per cone wave, 64K and 1M universes, gens 3,
@@ -41,7 +44,7 @@ def main():
     bu &= ~bw
     ww, wu = np.zeros(64, np.uint64), np.zeros(64, np.uint64)
     wu[0::3] = np.uint64(1 << 10)
-    caps = [(0, 0), (16, 32)]
+    caps = [(16, 32)]
     for tname, (w, u) in (("block", (bw, bu)), ("whole", (ww, wu))):
         dw, du = (torch.from_numpy(v.view(np.int64)[None].copy()).cuda() for v in (w, u))
         for n in (1 << 16, 1 << 20):
@@ -55,7 +58,8 @@ def main():
                     r[f"c{cc}_s{sc}_ms"] = bench.back_to_back_ms(rt, fn, x, x)
                 # round 3's launch (the uncapped split pair, no cone) and the product
                 forms = {"round3": lambda a, b, g=gens: tune.step_contains_pair(x, dw, du, g, 0, 0),
-                         "product": lambda a, b, g=gens: hip.step_contains(x, dw, du, generations=g)[0]}
+                         "product": lambda a, b, g=gens: hip.step_contains(x, dw, du, generations=g)[0],
+                         "cone8_alone": lambda a, b, g=gens: tune.cone(x, dw, du, g, 8, 8)}
                 for k, fn in forms.items():
                     r[k + "_equal"] = bool((fn(0, 0) == ref).all().item())
                     r[k + "_ms"] = bench.back_to_back_ms(rt, fn, x, x)

@@ -10,7 +10,3 @@ timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 tail -1 $O/tests.log
 timeout -k 10 300 python -u tools/ab/search_iter_caps_ab.py > $O/caps.jsonl 2> $O/caps.err || { tail -20 $O/caps.err; exit 2; }
 echo caps ok
-timeout -k 10 300 python -u tools/cone_ab.py > $O/cone_ab.jsonl 2> $O/cone_ab.err || { tail -20 $O/cone_ab.err; exit 3; }
-echo cone_ab ok
-timeout -k 10 400 python -u bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 5; }
-echo bench ok

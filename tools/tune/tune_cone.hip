@@ -53,27 +53,30 @@ int lifeapi_tune_cone(int first, const uint64_t *d_in, const uint64_t *d_wanted,
                               (hipStream_t)stream, cap);
 }
 
-/* the product's launch sequence for the iterated search loop without final
- * states (step.hip, gens > 2): the cone kernel (8 universes per wave, cones
- * of <= 32 columns, grid capped at cone_cap blocks per CU, 0 = one-shot), then
- * the split pair (kContainsLo, kContainsHi) skipping those waves, each grid
- * capped at split_cap blocks per CU (0 = one-shot)                           */
+/* the iterated search loop without final states (gens > 2), round 4's first
+ * form: the cone kernel launched alone (8 universes per wave, cones of <= 32
+ * columns, grid capped at cone_cap blocks per CU, 0 = one-shot), then the
+ * split pair (kContainsLo, kContainsHi) with each grid capped at split_cap
+ * blocks per CU (0 = one-shot) -- whose kContainsLo now also steps the cone
+ * (step_kernels.hpp), so the cone launch's waves have answered first and
+ * Lo's rewrite the same values.  cone_cap < 0: no cone launch (the shipped
+ * form, step.hip).                                                          */
 int lifeapi_tune_search_iter(const uint64_t *d_in, const uint64_t *d_wanted, const uint64_t *d_unwanted,
                              uint32_t *d_first, size_t n, uint32_t gens, int cone_cap, int split_cap, void *stream) {
   if (n == 0) return LIFEAPI_OK;
-  if (!d_in || !d_wanted || !d_unwanted || !d_first || gens <= 2 || cone_cap < 0 || split_cap < 0)
+  if (!d_in || !d_wanted || !d_unwanted || !d_first || gens <= 2 || split_cap < 0)
     return fail(LIFEAPI_E_INVALID, "bad argument to lifeapi_tune_search_iter%s");
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
-  // cone_cap + 1000 * u: u universes per cone wave (8, 16, 32; 0 = shipped)
-  const int upw = cone_cap / 1000;
+  // cone_cap + 1000 * u: u universes per cone wave (8, 16, 32; 0 = 8)
+  const int upw = cone_cap < 0 ? -1 : cone_cap / 1000;
   cone_cap %= 1000;
   const hipStream_t st = (hipStream_t)stream;
   if (upw == 16) rc = launch_cone<16, 8, true>(d_in, d_wanted, d_unwanted, d_first, n, gens, cus, st, cone_cap, kConeIterColumns);
   else if (upw == 32) rc = launch_cone<32, 8, true>(d_in, d_wanted, d_unwanted, d_first, n, gens, cus, st, cone_cap, kConeIterColumns);
   else if (upw == 8) rc = launch_cone<8, 8, true>(d_in, d_wanted, d_unwanted, d_first, n, gens, cus, st, cone_cap, kConeIterColumns);
-  else rc = launch_cone<kConeIterUniverses, kConeSets, true>(d_in, d_wanted, d_unwanted, d_first, n, gens, cus, st,
-                                                             cone_cap, kConeIterColumns);
+  else if (upw == 0) rc = launch_cone<kConeIterUniverses, kConeSets, true>(d_in, d_wanted, d_unwanted, d_first, n, gens,
+                                                                          cus, st, cone_cap, kConeIterColumns);
   if (rc != LIFEAPI_OK) return rc;
   const dim3 grid(grid_for((n + 3) / 4, cus, split_cap));
   hipLaunchKernelGGL((k_step_contains_split<8, kContainsNet, kContainsLo>), grid, dim3(kBlock), 0, (hipStream_t)stream,
