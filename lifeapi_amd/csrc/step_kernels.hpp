@@ -439,15 +439,19 @@ __device__ __forceinline__ void care_window(uint64_t rm, uint32_t &y0, uint32_t 
 // `gens` generations: xs = first column, K = columns (64: the whole board
 // from column 0; also for gens >= 32, whatever the window).  The light-cone
 // kernels (cone_kernels.hpp) load exactly these columns.
-__device__ __forceinline__ void cone_window(const uint64_t *__restrict__ wanted,
-                                            const uint64_t *__restrict__ unwanted, uint32_t gens, int lane,
-                                            uint32_t &xs, uint32_t &K) {
-  const uint64_t cols = __ballot((wanted[lane] | unwanted[lane]) != 0ull);  // bit x: column x has care cells
+// care_col: this lane's column of care cells (wanted | unwanted).
+__device__ __forceinline__ void cone_window(uint64_t care_col, uint32_t gens, uint32_t &xs, uint32_t &K) {
+  const uint64_t cols = __ballot(care_col != 0ull);  // bit x: column x has care cells
   uint32_t x0, w;
   care_window(cols, x0, w);
   K = gens >= (uint32_t)kWave / 2 ? (uint32_t)kWave : w + 2 * gens;
   xs = (x0 - gens) & (kWave - 1);
   if (K >= (uint32_t)kWave) K = kWave, xs = 0;
+}
+__device__ __forceinline__ void cone_window(const uint64_t *__restrict__ wanted,
+                                            const uint64_t *__restrict__ unwanted, uint32_t gens, int lane,
+                                            uint32_t &xs, uint32_t &K) {
+  cone_window(wanted[lane] | unwanted[lane], gens, xs, K);
 }
 
 // The light-cone pass (cone_kernels.hpp; here for the iterated search
@@ -538,9 +542,19 @@ __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *
   __shared__ uint32_t lds[kWavesPerBlock * S * kWave];
   const int lane = threadIdx.x & (kWave - 1);
   const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  if (cone_max && !fin) {
+  // the target's care cells in this lane's column, loaded once for both
+  // windows (the row window's and the light cone's)
+  const uint64_t care_col = wanted[lane] | unwanted[lane];
+  uint32_t y0 = 0, h = S;  // the row window of ASM 3 (else: no rotation, all registers)
+  if constexpr (ASM >= 3) {
+    const uint32_t lo = wave_or_u32_dpp((uint32_t)care_col), hi = wave_or_u32_dpp((uint32_t)(care_col >> 32));
+    care_window((uint64_t)lo | (uint64_t)hi << 32, y0, h);
+    if (h > S) y0 = 0, h = S;
+    if (ASM == 8 && h <= kLowRows) return;  // the low layout's (or the light cone's) target
+  }
+  if (cone_max && !fin && 2 * gens < cone_max) {
     uint32_t cxs, cK;
-    cone_window(wanted, unwanted, gens, lane, cxs, cK);
+    cone_window(care_col, gens, cxs, cK);
     if (cK <= cone_max) {
       if constexpr (ASM == kContainsLo) {
         constexpr int U = kConeLoUniverses;
@@ -553,14 +567,8 @@ __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *
       return;
     }
   }
-  uint32_t y0 = 0, h = S;  // the row window of ASM 3 (else: no rotation, all registers)
-  if constexpr (ASM >= 3) {
-    const uint64_t col = wanted[lane] | unwanted[lane];  // this lane's column of care cells
-    const uint32_t lo = wave_or_u32_dpp((uint32_t)col), hi = wave_or_u32_dpp((uint32_t)(col >> 32));
-    care_window((uint64_t)lo | (uint64_t)hi << 32, y0, h);
-    if (h > S) y0 = 0, h = S;
-    if ((ASM == 6 || ASM == 7) && h > kLowRows) return;  // the low layout: windows of <= 4 rows only
-    if (ASM == 8 && h <= kLowRows) return;                // ... and 8 the rest
+  if constexpr (ASM == 6 || ASM == 7) {
+    if (h > kLowRows) return;  // the low layout: windows of <= 4 rows only (8 the rest)
   }
   uint32_t tw[S], tu[S];
   {
