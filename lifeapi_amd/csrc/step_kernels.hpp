@@ -542,16 +542,10 @@ __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *
   __shared__ uint32_t lds[kWavesPerBlock * S * kWave];
   const int lane = threadIdx.x & (kWave - 1);
   const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  // the target's care cells in this lane's column, loaded once for both
-  // windows (the row window's and the light cone's)
+  // the target's care cells in this lane's column (both windows read it;
+  // the cone test first: after the row window's, it costs kContainsHi 6
+  // VGPRs, 70 -> 76)
   const uint64_t care_col = wanted[lane] | unwanted[lane];
-  uint32_t y0 = 0, h = S;  // the row window of ASM 3 (else: no rotation, all registers)
-  if constexpr (ASM >= 3) {
-    const uint32_t lo = wave_or_u32_dpp((uint32_t)care_col), hi = wave_or_u32_dpp((uint32_t)(care_col >> 32));
-    care_window((uint64_t)lo | (uint64_t)hi << 32, y0, h);
-    if (h > S) y0 = 0, h = S;
-    if (ASM == 8 && h <= kLowRows) return;  // the low layout's (or the light cone's) target
-  }
   if (cone_max && !fin && 2 * gens < cone_max) {
     uint32_t cxs, cK;
     cone_window(care_col, gens, cxs, cK);
@@ -566,6 +560,13 @@ __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *
       }
       return;
     }
+  }
+  uint32_t y0 = 0, h = S;  // the row window of ASM 3 (else: no rotation, all registers)
+  if constexpr (ASM >= 3) {
+    const uint32_t lo = wave_or_u32_dpp((uint32_t)care_col), hi = wave_or_u32_dpp((uint32_t)(care_col >> 32));
+    care_window((uint64_t)lo | (uint64_t)hi << 32, y0, h);
+    if (h > S) y0 = 0, h = S;
+    if (ASM == 8 && h <= kLowRows) return;  // the low layout's target
   }
   if constexpr (ASM == 6 || ASM == 7) {
     if (h > kLowRows) return;  // the low layout: windows of <= 4 rows only (8 the rest)
