@@ -110,6 +110,7 @@ constexpr int kConeUniverses = 64, kConeSets = 8;
 // chunk: that work is VALU-bound, and 64 per wave would leave 64K universes
 // one wave per SIMD).
 constexpr uint32_t kConeIterColumns = 32;
+static_assert(kConeIterColumns <= 32, "kContainsLo's cone passes take P <= 32");
 // ... with both split kernels on grids of at most 32 blocks per CU looping
 // over the batch (step.hip): one of the two always idles.
 constexpr int kSplitIterBlocksPerCU = 32;

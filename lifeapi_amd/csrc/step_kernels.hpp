@@ -448,6 +448,17 @@ __device__ __forceinline__ void cone_window(uint64_t care_col, uint32_t gens, ui
   xs = (x0 - gens) & (kWave - 1);
   if (K >= (uint32_t)kWave) K = kWave, xs = 0;
 }
+// Whether cone_window's K is at most kmax, for 2 gens < kmax <= 64: the care
+// columns then leave a cyclic run of at least L = 64 - kmax + 2 gens > 32
+// empty columns -- tested directly (runs of 32 by doubling, then one shifted
+// AND for the rest, about 25 scalar instructions against care_window's ~100;
+// the split kernels' waves ask this on every launch of the iterated loop).
+__device__ __forceinline__ bool cone_fits(uint64_t care_col, uint32_t gens, uint32_t kmax) {
+  uint64_t run = ~__ballot(care_col != 0ull);  // bit p: column p empty
+#pragma unroll
+  for (int k = 0; k < 5; ++k) run &= rotr64(run, 1u << k);  // bit p: columns p .. p + 2^(k+1) - 1 empty
+  return (run & rotr64(run, 64u - kmax + 2u * gens - 32u)) != 0ull;
+}
 __device__ __forceinline__ void cone_window(const uint64_t *__restrict__ wanted,
                                             const uint64_t *__restrict__ unwanted, uint32_t gens, int lane,
                                             uint32_t &xs, uint32_t &K) {
@@ -546,20 +557,20 @@ __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *
   // the cone test first: after the row window's, it costs kContainsHi 6
   // VGPRs, 70 -> 76)
   const uint64_t care_col = wanted[lane] | unwanted[lane];
-  if (cone_max && !fin && 2 * gens < cone_max) {
-    uint32_t cxs, cK;
-    cone_window(care_col, gens, cxs, cK);
-    if (cK <= cone_max) {
-      if constexpr (ASM == kContainsLo) {
+  if (cone_max && cone_max <= 32u && !fin && 2 * gens < cone_max && cone_fits(care_col, gens, cone_max)) {
+    if constexpr (ASM == kContainsLo) {
+      uint32_t cxs, cK;
+      cone_window(care_col, gens, cxs, cK);  // cK <= cone_max (cone_fits)
+      {
         constexpr int U = kConeLoUniverses;
         const uint64_t u0 = ((uint64_t)blockIdx.x * kWavesPerBlock + wib) * U,
                        step = (uint64_t)gridDim.x * kWavesPerBlock * U;
         if (cK <= 8) cone_wave<8, U, 8, true>(in, wanted, unwanted, first, n, u0, step, gens, cxs, cK, lane);
         else if (cK <= 16) cone_wave<16, U, 8, true>(in, wanted, unwanted, first, n, u0, step, gens, cxs, cK, lane);
-        else if (cK <= 32) cone_wave<32, U, 8, true>(in, wanted, unwanted, first, n, u0, step, gens, cxs, cK, lane);
+        else cone_wave<32, U, 8, true>(in, wanted, unwanted, first, n, u0, step, gens, cxs, cK, lane);
       }
-      return;
     }
+    return;
   }
   uint32_t y0 = 0, h = S;  // the row window of ASM 3 (else: no rotation, all registers)
   if constexpr (ASM >= 3) {

@@ -115,6 +115,41 @@ def test_care_window_is_the_smallest_cyclic_window():
     assert care_window((1 << 63) | 1) == (63, 2)
 
 
+def rotr64(v: int, k: int) -> int:
+    return ((v >> k) | (v << ((64 - k) % 64))) & M64
+
+
+def cone_fits(mask: int, gens: int, kmax: int) -> bool:
+    """step_kernels.hpp cone_fits: a cyclic run of >= 64 - kmax + 2 gens empty
+    columns, by doubling to runs of 32 and one shifted AND"""
+    run = ~mask & M64
+    for k in range(5):
+        run &= rotr64(run, 1 << k)
+    return run & rotr64(run, 64 - kmax + 2 * gens - 32) != 0
+
+
+def test_cone_fits_is_cone_window_k_at_most_kmax():
+    """the split kernels' quick test agrees with cone_window's K <= kmax
+    (K = w + 2 gens) on every mask family, 2 gens < kmax <= 32"""
+    rng = np.random.default_rng(11)
+    masks = [0, M64, 1, (1 << 63) | 1]
+    for _ in range(600):
+        w = int(rng.integers(1, 65))
+        a = int(rng.integers(64))
+        m = (1 << a) | (1 << ((a + w - 1) % 64))                 # a window of exactly w columns
+        for c in rng.integers(0, w, size=int(rng.integers(0, 6))):
+            m |= 1 << ((a + int(c)) % 64)
+        masks.append(m)
+        masks.append(int(rng.integers(0, 1 << 63)) & int(rng.integers(0, 1 << 63)))
+    for m in masks:
+        _, w = care_window(m)
+        for kmax in (4, 8, 17, 24, 32):
+            for g in range(0, (kmax + 1) // 2):
+                if 2 * g >= kmax:
+                    continue
+                assert cone_fits(m, g, kmax) == (w + 2 * g <= kmax), (hex(m), g, kmax)
+
+
 @pytest.mark.parametrize("w", [1, 2, 3, 4, 5, 6, 7, 8, 9, 13, 15, 16, 17, 28, 30, 31, 32, 33, 47, 60, 61, 62, 63, 64])
 def test_cone_model_equals_contains(port, w):
     rng = np.random.default_rng(w)
