@@ -18,20 +18,21 @@ namespace {
 // next LifeStable's planes before it works on the current one.
 template <int PASS>
 __device__ __forceinline__ int stable_run(W (&p)[10], uint32_t max_iters) {
-  if constexpr (PASS == 0) return stable_sync(p);
-  else if constexpr (PASS == 1) return stable_options(p);
-  else if constexpr (PASS == 2) return stable_signal(p);
-  else if constexpr (PASS == 3) return stable_step(p);
+  W chg = W{0u, 0u};  // (this form stores every line)
+  if constexpr (PASS == 0) return stable_sync(p, chg);
+  else if constexpr (PASS == 1) return stable_options(p, chg);
+  else if constexpr (PASS == 2) return stable_signal(p, chg);
+  else if constexpr (PASS == 3) return stable_step(p, chg);
   int ever = 0;
   for (uint32_t it = 0; it < max_iters; ++it) {
     if constexpr (PASS == 5) {  // StabiliseOptions (LifeStable.hpp:677-693)
-      const int k = stable_sync(p);
+      const int k = stable_sync(p, chg);
       if (!(k & 1)) return 0;
-      const int o = stable_options(p);
+      const int o = stable_options(p, chg);
       if (!(o & 1)) return 0;
       if (!((k | o) & 2)) return 1 | ever;
     } else {  // Propagate (LifeStable.hpp:718-729)
-      const int s = stable_step(p);
+      const int s = stable_step(p, chg);
       if (!(s & 1)) return 0;
       if (!(s & 2)) return 1 | ever;
     }
