@@ -89,8 +89,9 @@ int lifeapi_contains_batch_dev(const uint64_t *d_states, const uint64_t *d_wante
                                void *stream);
 /* fused Step^gens + Contains: d_out[u] = first generation g in 1..gens at
  * which Stepped(g) contains the target, or 0 if none; d_final (may be NULL)
- * receives Stepped(gens).  With d_final NULL and gens <= 2 (the search
- * filter) only the columns within gens of the target's care columns are read. */
+ * receives Stepped(gens).  With d_final NULL (the search filter) only the
+ * columns within gens of the target's care columns are read and stepped
+ * when gens <= 2, or gens > 2 and those columns number at most 32.        */
 int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
                                     const uint64_t *d_wanted, const uint64_t *d_unwanted,
                                     uint32_t *d_first_gen, size_t n, uint32_t generations,
@@ -114,7 +115,8 @@ int lifeapi_interaction_counts_batch_dev(const uint64_t *d_in, uint64_t *d_out, 
  * 5 StabiliseOptions (:677-693, the same bound).
  * d_flags[u] = consistent | changed << 1 (| 4 if max_iters stopped 4 / 5),
  * i.e. the PropagateResult; planes are left exactly as the reference leaves
- * them, including on an inconsistent early return.                        */
+ * them, including on an inconsistent early return.  Only the 128-byte lines
+ * holding a changed column are written back (the rest is already there).  */
 int lifeapi_stable_pass_batch_dev(uint64_t *d_planes, uint8_t *d_flags, size_t n, int pass,
                                   uint32_t max_iters, void *stream);
 /* LifeStable::Vulnerable() (LifeStable.hpp:366-412) of every LifeStable[n]
