@@ -14,7 +14,7 @@ echo trace ok
 P="python3 $R/tools/pmc_r04.py"
 run() {  # name counters args...
   local name=$1 ctr=$2; shift 2
-  timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-include-regex "k_step|k_cone|k_fill" -d "$O/$name" -o pmc --output-format csv -- $P "$@" > "$O/$name.out" 2> "$O/$name.err" || { tail -20 "$O/$name.err"; exit 3; }
+  timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-include-regex "k_step|k_cone|k_fill|k_stable" -d "$O/$name" -o pmc --output-format csv -- $P "$@" > "$O/$name.out" 2> "$O/$name.err" || { tail -20 "$O/$name.err"; exit 3; }
   echo "$name ok"
 }
 run tlb_1m "TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_REQUEST_sum" step 1048576
@@ -23,3 +23,5 @@ run fetch_cone FETCH_SIZE cone
 run rdreq_cone "TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum" cone
 run write_cone WRITE_SIZE cone
 run fetch_step_1m FETCH_SIZE step 1048576
+run write_stable WRITE_SIZE stable
+run fetch_stable FETCH_SIZE stable

@@ -7,6 +7,9 @@ of one cold launch.
   cone        the search filter (1 gen) and Contains on 1M config-2
               universes, for bench.py's two targets (golden.json
               digests.config2_filter): block first, then whole_board
+  stable      Propagate on 1M LifeStables (tools/rows_bench.py's still
+              lifes around an unknown window), each launch on a fresh copy:
+              the bytes the changed-line stores write
 """
 import json
 import os
@@ -40,6 +43,15 @@ def main():
         for k in range(reps):
             scrub()
             hip.step(a if k % 2 == 0 else b, out=b if k % 2 == 0 else a, generations=1)
+    elif sys.argv[1] == "stable":
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        from rows_bench import stable_inputs
+        st = stable_inputs(1 << 20)
+        w = st.clone()
+        for _ in range(reps):
+            w.copy_(st)
+            scrub()
+            hip.stable_pass(w, "propagate")
     else:
         with open(os.path.join(ROOT, "tests", "golden", "golden.json")) as f:
             gold = json.load(f)["digests"]["config2_filter"]
