@@ -342,3 +342,36 @@ def test_iterated_search_loop_cone_and_split_vs_reference(hip, R, port, w, gens)
         assert (first.cpu().numpy().astype(np.uint32) == exp_first).all()
         _check(to_host(fin), exp_fin, f"final states, w={w} gens={gens}")
         assert 1 <= exp_first[0] <= gens
+
+
+@pytest.mark.parametrize("w,h,gens", [(2, 1, 3), (2, 2, 8), (4, 4, 13), (4, 5, 13), (6, 7, 9), (6, 8, 3),
+                                      (20, 3, 5), (20, 6, 5), (27, 2, 3), (28, 4, 3), (4, 3, 15), (4, 6, 16),
+                                      (12, 4, 24), (12, 6, 24)])
+def test_iterated_search_loop_short_targets_vs_reference(hip, R, port, w, h, gens):
+    """gens > 2, no final states, targets of w columns x h rows (cyclic, at
+    the seams): the cone test comes first in both split kernels, so a cone
+    target of <= 4 rows (the low layout's) and one of more rows (the high
+    layout's) both go to kContainsLo's cone pass and kContainsHi returns;
+    wider cones (w + 2 gens > 32) go to the layout their height picks.
+    Against the reference's Step() + Contains loop."""
+    rng = np.random.default_rng(100 * w + 10 * h + gens)
+    n = 777
+    x = port.fill(n, seed=700 + w) & port.fill(n, seed=800 + h)
+    x[::3] = x[0]
+    for x0, y0 in ((int(rng.integers(64)), int(rng.integers(64))), (62, 63)):
+        rows = 0
+        for i in range(h):
+            rows |= 1 << ((y0 + i) % 64)
+        rows_mask = np.uint64(rows)
+        ref_state = R.step_batch(x[:1], max(1, gens // 2))[0]
+        cols = [(x0 + i) % 64 for i in range(w)]
+        box = np.zeros(64, np.uint64)
+        for c in cols:
+            box[c] = rows_mask
+        tw, tu = ref_state & box, box & ~ref_state
+        dw, du = to_dev(tw[None]), to_dev(tu[None])
+        exp_first, _ = R.step_contains_batch(x, tw, tu, gens, nthreads=THREADS)
+        first, _ = hip.step_contains(to_dev(x), dw, du, gens)
+        got = first.cpu().numpy().astype(np.uint32)
+        assert (got == exp_first).all(), (w, h, gens, x0, y0, np.nonzero(got != exp_first)[0][:8])
+        assert 1 <= exp_first[0] <= gens
