@@ -78,8 +78,10 @@ __global__ __launch_bounds__(kBlock) void k_cone(const uint64_t *in, const uint6
   const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint64_t u0 = wave * UPW, step = (uint64_t)gridDim.x * kWavesPerBlock * UPW;  // grid-stride (capped grids)
   if (u0 >= n) return;
-  uint32_t xs, K;
-  cone_window(wanted, unwanted, FIRST ? gens : 0u, lane, xs, K);
+  const uint32_t g = FIRST ? gens : 0u;
+  const uint64_t care_col = wanted[lane] | unwanted[lane];
+  uint32_t xs = 0, K = kWave;
+  if (!cone_whole(care_col, g)) cone_window(care_col, g, xs, K);  // (a whole-board target skips the search)
   if (K > kmax) return;
   if constexpr (!FIRST && A16) {
     if (K == (uint32_t)kWave) return cone_wave_full16<UPW, RMAX>(in, wanted, unwanted, out, n, u0, step, lane);

@@ -448,6 +448,29 @@ __device__ __forceinline__ void cone_window(uint64_t care_col, uint32_t gens, ui
   xs = (x0 - gens) & (kWave - 1);
   if (K >= (uint32_t)kWave) K = kWave, xs = 0;
 }
+// Whether the cyclic mask e holds a run of at least L (1 .. 64) set bits:
+// runs of 2^k by doubling, then the binary digits of L (about 40 scalar
+// instructions, no data-dependent selects).
+__device__ __forceinline__ bool has_run(uint64_t e, uint32_t L) {
+  if (L >= 64u) return e == ~0ull;
+  uint64_t run[6];
+  run[0] = e;
+#pragma unroll
+  for (int k = 1; k < 6; ++k) run[k] = run[k - 1] & rotr64(run[k - 1], 1u << (k - 1));
+  uint64_t cur = ~0ull;
+  uint32_t len = 0;
+#pragma unroll
+  for (int k = 5; k >= 0; --k)
+    if ((L >> k) & 1u) cur &= rotr64(run[k], len), len += 1u << k;
+  return cur != 0ull;
+}
+// Whether cone_window's K is 64 (the whole board from column 0): the care
+// columns leave no cyclic run of 2 gens + 1 empty columns, or gens >= 32.
+// The light-cone kernels ask this before the full window search, which a
+// whole-board target then skips.
+__device__ __forceinline__ bool cone_whole(uint64_t care_col, uint32_t gens) {
+  return gens >= (uint32_t)kWave / 2 || !has_run(~__ballot(care_col != 0ull), 2u * gens + 1u);
+}
 // Whether cone_window's K is at most kmax, for 2 gens < kmax <= 64: the care
 // columns then leave a cyclic run of at least L = 64 - kmax + 2 gens > 32
 // empty columns -- tested directly (runs of 32 by doubling, then one shifted

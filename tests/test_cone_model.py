@@ -128,6 +128,41 @@ def cone_fits(mask: int, gens: int, kmax: int) -> bool:
     return run & rotr64(run, 64 - kmax + 2 * gens - 32) != 0
 
 
+def has_run(e: int, L: int) -> bool:
+    """step_kernels.hpp has_run: a cyclic run of >= L set bits in e"""
+    if L >= 64:
+        return e == M64
+    run = [e]
+    for k in range(1, 6):
+        run.append(run[-1] & rotr64(run[-1], 1 << (k - 1)))
+    cur, ln = M64, 0
+    for k in range(5, -1, -1):
+        if (L >> k) & 1:
+            cur &= rotr64(run[k], ln)
+            ln += 1 << k
+    return cur != 0
+
+
+def test_cone_whole_is_cone_window_k_64():
+    """k_cone's quick whole-board test (cone_whole) agrees with cone_window's
+    K = 64 for every gens 0..40 on every mask family"""
+    rng = np.random.default_rng(12)
+    masks = [0, M64, 1, (1 << 63) | 1, M64 ^ 1, M64 ^ (3 << 20)]
+    for _ in range(500):
+        m = M64
+        for _ in range(int(rng.integers(0, 4))):             # a few empty runs
+            a, ln = int(rng.integers(64)), int(rng.integers(1, 40))
+            for i in range(ln):
+                m &= ~(1 << ((a + i) % 64))
+        masks.append(m)
+        masks.append(int(rng.integers(0, 1 << 63)))
+    for m in masks:
+        _, w = care_window(m)
+        for g in range(0, 41):
+            whole = g >= 32 or not has_run(~m & M64, 2 * g + 1)
+            assert whole == (g >= 32 or w + 2 * g >= 64), (hex(m), g)
+
+
 def test_cone_fits_is_cone_window_k_at_most_kmax():
     """the split kernels' quick test agrees with cone_window's K <= kmax
     (K = w + 2 gens) on every mask family, 2 gens < kmax <= 32"""
