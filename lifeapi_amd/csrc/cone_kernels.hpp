@@ -104,6 +104,12 @@ __global__ __launch_bounds__(kBlock) void k_cone(const uint64_t *in, const uint6
 // grids whose waves find the window once and loop over the batch: within
 // +-3 % of the one-shot grid for small targets, slower for the whole board.
 constexpr int kConeUniverses = 64, kConeSets = 8;
+// Contains (no generations) takes register sets 16 at a time: same process,
+// 1M universes, back to back (tools/cone_ab.py, profiles/r04/first and r04n):
+// the whole board 0.0804 against 0.0833 ms (16-byte loads, 32 in flight per
+// wave), a 14-column target 0.0407 / 0.0428, the small targets within 1 %.
+// (The filter keeps 8: 16 was 5 % slower on the whole board.)
+constexpr int kConeContainsSets = 16;
 // The iterated search loop (gens > 2, no final states) steps the light cone
 // while it spans at most this many columns (P <= 32 lanes per universe: at
 // most half the natural layout's work per universe-generation, against the

@@ -117,7 +117,7 @@ int lifeapi_contains_batch_dev(const uint64_t *d_states, const uint64_t *d_wante
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
   // only the columns holding the target's care cells (cone_kernels.hpp)
-  return launch_cone<kConeUniverses, kConeSets, false>(d_states, d_wanted, d_unwanted, d_out, n, 0u, cus,
+  return launch_cone<kConeUniverses, kConeContainsSets, false>(d_states, d_wanted, d_unwanted, d_out, n, 0u, cus,
                                                         (hipStream_t)stream);
 }
 

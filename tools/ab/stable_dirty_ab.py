@@ -4,7 +4,8 @@ that hold a changed column (shipped) against storing every line (round 3's
 k_stable: the tuning build with mode bit 2), each pass's shipped launch shape
 (stencils.hip kStablePassResident, XCD-chunked).  Inputs: the rows_bench
 still lifes around an unknown window with fresh options (the state a search
-propagates from) and random planes.  Each timing runs KS passes back to back
+propagates from), the next node of such a search (those propagated to their
+fixpoint, then one unknown cell decided ON) and random planes.  Each timing runs KS passes back to back
 on fresh copies; planes and flags are checked equal between the forms and
 to the shipped pass.  One JSON line per (input, pass, form), median over rounds.
 
@@ -34,7 +35,19 @@ def arg(name, default):
 
 def main():
     n, rounds, ks = arg("--n", 1 << 20), arg("--rounds", 5), 4
-    families = {"still_lifes": stable_inputs(n),
+    still = stable_inputs(n)
+    # a search's next node: the still lifes propagated to their fixpoint, then
+    # one unknown cell (the lowest of the first unknown column) decided ON
+    nxt = still.clone()
+    hip.stable_pass(nxt, "propagate")
+    unk = nxt[:, 64:128]
+    c = (unk != 0).to(torch.int8).argmax(1)
+    u = unk.gather(1, c[:, None])
+    low = u & -u
+    nxt[:, 64:128].scatter_(1, c[:, None], u & ~low)
+    st0 = nxt[:, 0:64].gather(1, c[:, None])
+    nxt[:, 0:64].scatter_(1, c[:, None], st0 | low)
+    families = {"still_lifes": still, "next_node": nxt,
                 "random": hip.fill_random(10 * n, seed=31).view(n, 640)}
     for fam, st in families.items():
         works = [st.clone() for _ in range(ks)]
