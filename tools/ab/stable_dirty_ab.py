@@ -23,7 +23,7 @@ sys.path.insert(0, os.path.join(ROOT, "tools", "tune"))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 import lifeapi_amd.hip as hip  # noqa: E402
 import tune_hip as tune  # noqa: E402
-from rows_bench import stable_inputs  # noqa: E402
+from rows_bench import stable_inputs, stable_next_node  # noqa: E402
 
 PEAK = 8000.0
 CAPS = {0: -3, 1: -3, 2: -3, 3: -3, 4: 0, 5: -4}   # stencils.hip kStablePassResident
@@ -36,17 +36,7 @@ def arg(name, default):
 def main():
     n, rounds, ks = arg("--n", 1 << 20), arg("--rounds", 5), 4
     still = stable_inputs(n)
-    # a search's next node: the still lifes propagated to their fixpoint, then
-    # one unknown cell (the lowest of the first unknown column) decided ON
-    nxt = still.clone()
-    hip.stable_pass(nxt, "propagate")
-    unk = nxt[:, 64:128]
-    c = (unk != 0).to(torch.int8).argmax(1)
-    u = unk.gather(1, c[:, None])
-    low = u & -u
-    nxt[:, 64:128].scatter_(1, c[:, None], u & ~low)
-    st0 = nxt[:, 0:64].gather(1, c[:, None])
-    nxt[:, 0:64].scatter_(1, c[:, None], st0 | low)
+    nxt = stable_next_node(still)
     families = {"still_lifes": still, "next_node": nxt,
                 "random": hip.fill_random(10 * n, seed=31).view(n, 640)}
     for fam, st in families.items():

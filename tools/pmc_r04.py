@@ -7,8 +7,10 @@ of one cold launch.
   cone        the search filter (1 gen) and Contains on 1M config-2
               universes, for bench.py's two targets (golden.json
               digests.config2_filter): block first, then whole_board
-  stable      Propagate on 1M LifeStables (tools/rows_bench.py's still
-              lifes around an unknown window), each launch on a fresh copy:
+  stable      Propagate on 1M LifeStables, each launch on a fresh copy: 3
+              launches on tools/rows_bench.py's still lifes around an
+              unknown window (every column changes), then 3 on a search's
+              next node (rows_bench.stable_next_node: a few columns change):
               the bytes the changed-line stores write
 """
 import json
@@ -45,13 +47,15 @@ def main():
             hip.step(a if k % 2 == 0 else b, out=b if k % 2 == 0 else a, generations=1)
     elif sys.argv[1] == "stable":
         sys.path.insert(0, os.path.join(ROOT, "tools"))
-        from rows_bench import stable_inputs
+        from rows_bench import stable_inputs, stable_next_node
         st = stable_inputs(1 << 20)
+        nxt = stable_next_node(st)
         w = st.clone()
-        for _ in range(reps):
-            w.copy_(st)
-            scrub()
-            hip.stable_pass(w, "propagate")
+        for src in (st, nxt):
+            for _ in range(reps):
+                w.copy_(src)
+                scrub()
+                hip.stable_pass(w, "propagate")
     else:
         with open(os.path.join(ROOT, "tests", "golden", "golden.json")) as f:
             gold = json.load(f)["digests"]["config2_filter"]
