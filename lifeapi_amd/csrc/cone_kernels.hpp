@@ -70,7 +70,7 @@ __device__ __forceinline__ void cone_wave_full16(const uint64_t *in, const uint6
 // is 16-byte aligned (Contains over the whole board then takes 16-byte loads).
 // kmax: a wave whose window K exceeds it returns at once (the iterated
 // search loop's split-layout kernels answer those, step.hip).
-template <int UPW, int RMAX, bool FIRST, typename OutT, bool A16 = false>
+template <int UPW, int RMAX, bool FIRST, typename OutT, bool A16 = false, bool PIPE = false>
 __global__ __launch_bounds__(kBlock) void k_cone(const uint64_t *in, const uint64_t *__restrict__ wanted,
                                                  const uint64_t *__restrict__ unwanted, OutT *__restrict__ out,
                                                  uint64_t n, uint32_t gens, uint32_t kmax) {
@@ -87,12 +87,12 @@ __global__ __launch_bounds__(kBlock) void k_cone(const uint64_t *in, const uint6
     if (K == (uint32_t)kWave) return cone_wave_full16<UPW, RMAX>(in, wanted, unwanted, out, n, u0, step, lane);
   }
   // (a wave of UPW universes takes whole register sets: P >= 64 / UPW)
-  if (K <= 4 && UPW >= 16) cone_wave<UPW >= 16 ? 4 : 8, UPW, RMAX, FIRST>(in, wanted, unwanted, out, n, u0, step, gens,
+  if (K <= 4 && UPW >= 16) cone_wave<UPW >= 16 ? 4 : 8, UPW, RMAX, FIRST, OutT, PIPE>(in, wanted, unwanted, out, n, u0, step, gens,
                                                                          xs, K, lane);
-  else if (K <= 8) cone_wave<8, UPW, RMAX, FIRST>(in, wanted, unwanted, out, n, u0, step, gens, xs, K, lane);
-  else if (K <= 16) cone_wave<16, UPW, RMAX, FIRST>(in, wanted, unwanted, out, n, u0, step, gens, xs, K, lane);
-  else if (K <= 32) cone_wave<32, UPW, RMAX, FIRST>(in, wanted, unwanted, out, n, u0, step, gens, xs, K, lane);
-  else cone_wave<64, UPW, RMAX, FIRST>(in, wanted, unwanted, out, n, u0, step, gens, xs, K, lane);
+  else if (K <= 8) cone_wave<8, UPW, RMAX, FIRST, OutT, PIPE>(in, wanted, unwanted, out, n, u0, step, gens, xs, K, lane);
+  else if (K <= 16) cone_wave<16, UPW, RMAX, FIRST, OutT, PIPE>(in, wanted, unwanted, out, n, u0, step, gens, xs, K, lane);
+  else if (K <= 32) cone_wave<32, UPW, RMAX, FIRST, OutT, PIPE>(in, wanted, unwanted, out, n, u0, step, gens, xs, K, lane);
+  else cone_wave<64, UPW, RMAX, FIRST, OutT, PIPE>(in, wanted, unwanted, out, n, u0, step, gens, xs, K, lane);
 }
 
 // The shipped shape: 64 universes per wave, register sets 8 at a time, one-
@@ -127,7 +127,7 @@ constexpr int kSplitIterBlocksPerCU = 32;
 constexpr int kConeIterUniverses = 8, kConeIterBlocksPerCU = 16;
 
 // Launches k_cone on a one-shot grid.
-template <int UPW, int RMAX, bool FIRST, typename OutT>
+template <int UPW, int RMAX, bool FIRST, typename OutT, bool PIPE = false>
 int launch_cone(const uint64_t *d_in, const uint64_t *d_wanted, const uint64_t *d_unwanted, OutT *d_out, size_t n,
                 uint32_t gens, int cus, hipStream_t stream, int blocks_per_cu = 0, uint32_t kmax = kWave) {
   const dim3 grid(grid_for((n + UPW - 1) / UPW, cus, blocks_per_cu));
@@ -135,12 +135,12 @@ int launch_cone(const uint64_t *d_in, const uint64_t *d_wanted, const uint64_t *
   if constexpr (!FIRST) a16 = aligned16(d_in);
   if constexpr (!FIRST) {
     if (a16) {
-      hipLaunchKernelGGL((k_cone<UPW, RMAX, FIRST, OutT, true>), grid, dim3(kBlock), 0, stream, d_in, d_wanted,
+      hipLaunchKernelGGL((k_cone<UPW, RMAX, FIRST, OutT, true, PIPE>), grid, dim3(kBlock), 0, stream, d_in, d_wanted,
                          d_unwanted, d_out, (uint64_t)n, gens, kmax);
       return launched("k_cone launch");
     }
   }
-  hipLaunchKernelGGL((k_cone<UPW, RMAX, FIRST, OutT, false>), grid, dim3(kBlock), 0, stream, d_in, d_wanted,
+  hipLaunchKernelGGL((k_cone<UPW, RMAX, FIRST, OutT, false, PIPE>), grid, dim3(kBlock), 0, stream, d_in, d_wanted,
                      d_unwanted, d_out, (uint64_t)n, gens, kmax);
   return launched("k_cone launch");
 }

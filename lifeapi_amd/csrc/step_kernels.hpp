@@ -495,7 +495,9 @@ __device__ __forceinline__ void cone_window(const uint64_t *__restrict__ wanted,
 // generation in 1..gens whose state contains the target (0 = never), else
 // out[u] = Contains(target) of the state as loaded (gens unused).  Register
 // sets go RMAX at a time: all their loads are issued before the first test.
-template <int P, int UPW, int RMAX, bool FIRST, typename OutT>
+// PIPE: a pass issues the next pass's loads before it steps its own sets
+// (twice the registers for the data; an A/B, tools/cone_ab.py).
+template <int P, int UPW, int RMAX, bool FIRST, typename OutT, bool PIPE = false>
 __device__ __forceinline__ void cone_wave(const uint64_t *in, const uint64_t *__restrict__ wanted,
                                           const uint64_t *__restrict__ unwanted, OutT *__restrict__ out,
                                           uint64_t n, uint64_t u_first, uint64_t u_step, uint32_t gens,
@@ -523,14 +525,25 @@ __device__ __forceinline__ void cone_wave(const uint64_t *in, const uint64_t *__
   static_assert(UPW <= kWave, "one result per lane");
   for (uint64_t u0 = u_first; u0 < n; u0 += u_step) {
     uint32_t mine = 0;  // lane L: the result of universe u0 + L (one coalesced store per chunk)
-#pragma unroll 1
-    for (int pass = 0; pass < R / RB; ++pass) {
+    auto load = [&](int pass, W (&a)[RB]) __attribute__((always_inline)) {
       const uint64_t ub = u0 + (uint64_t)pass * RB * GPS + q;
-      W a[RB];
 #pragma unroll
       for (int k = 0; k < RB; ++k) {
         const uint64_t u = ub + (uint64_t)k * GPS;
         a[k] = (live && u < n) ? ld<true>(in + u * kWave + col) : W{0u, 0u};
+      }
+    };
+    W nx[RB];
+    if constexpr (PIPE) load(0, nx);
+#pragma unroll 1
+    for (int pass = 0; pass < R / RB; ++pass) {
+      W a[RB];
+      if constexpr (PIPE) {
+#pragma unroll
+        for (int k = 0; k < RB; ++k) a[k] = nx[k];
+        if (pass + 1 < R / RB) load(pass + 1, nx);
+      } else {
+        load(pass, a);
       }
       uint32_t res[RB];
       if constexpr (FIRST) {

@@ -12,7 +12,8 @@ template <bool FIRST, typename OutT>
 int cone_by_shape(const uint64_t *in, const uint64_t *w, const uint64_t *u, OutT *out, size_t n, uint32_t gens,
                   int upw, int rmax, int cus, hipStream_t st, int cap) {
 #define LIFEAPI_CONE(U, R) \
-  if (upw == U && rmax == R) return launch_cone<U, R, FIRST>(in, w, u, out, n, gens, cus, st, cap);
+  if (upw == U && rmax == R) return launch_cone<U, R, FIRST>(in, w, u, out, n, gens, cus, st, cap); \
+  if (upw == U && rmax == R + 100) return launch_cone<U, R, FIRST, OutT, true>(in, w, u, out, n, gens, cus, st, cap);
   LIFEAPI_CONE(8, 8)
   LIFEAPI_CONE(16, 4)
   LIFEAPI_CONE(16, 8)
@@ -32,7 +33,8 @@ int cone_by_shape(const uint64_t *in, const uint64_t *w, const uint64_t *u, OutT
 
 extern "C" {
 
-/* first != 0: the search filter (d_out uint32 first generations, any gens;
+/* rmax + 100: the pipelined pass (cone_wave PIPE).
+ * first != 0: the search filter (d_out uint32 first generations, any gens;
  * every window, the whole board included);
  * first == 0: Contains (d_out uint8).  upw universes per wave, rmax register
  * sets per pass; upw + 1000 * c: a grid of at most c blocks per CU looping
