@@ -83,7 +83,7 @@ def main():
                 ("filter1", "shipped", 516, lambda: hip.step_contains(x, dw, du, 1)),
                 ("filter2", "k_step_contains<8> (round 3)", 516, lambda: tune.step_contains_nat(x, dw, du, 2, 8, 0)),
                 ("filter2", "shipped", 516, lambda: hip.step_contains(x, dw, du, 2))]
-        for upw, rmax in ((16, 8), (32, 4), (32, 8), (32, 16), (64, 8), (64, 16), (32, 104), (64, 104), (64, 108)):
+        for upw, rmax in ((16, 8), (32, 4), (32, 8), (32, 16), (64, 8), (64, 16), (32, 104), (32, 108), (64, 108), (64, 116)):
             # rmax + 100: the pipelined pass (the next pass's loads before this pass's steps)
             label = f"k_cone<{upw},{rmax % 100}{' pipelined' if rmax > 100 else ''}>"
             rows.append(("contains", label, 513,
