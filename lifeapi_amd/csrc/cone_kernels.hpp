@@ -95,6 +95,40 @@ __global__ __launch_bounds__(kBlock) void k_cone(const uint64_t *in, const uint6
   else cone_wave<64, UPW, RMAX, FIRST, OutT, PIPE>(in, wanted, unwanted, out, n, u0, step, gens, xs, K, lane);
 }
 
+// k_cone with the chunk size chosen by the window: 64 universes per wave
+// chunk while P <= 8 lanes per universe (one pass), 16 for wider cones (one
+// pass of 16 / 4 / 1 universes per register set), on a grid of ceil(n / 16)
+// waves capped at the caller's blocks per CU, every wave looping over the
+// batch with its own chunk size.
+template <int RMAX, bool FIRST, typename OutT, bool A16 = false>
+__global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const uint64_t *__restrict__ wanted,
+                                                       const uint64_t *__restrict__ unwanted, OutT *__restrict__ out,
+                                                       uint64_t n, uint32_t gens, uint32_t kmax) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
+  if (wave * 16 >= n) return;
+  const uint32_t g = FIRST ? gens : 0u;
+  const uint64_t care_col = wanted[lane] | unwanted[lane];
+  uint32_t xs = 0, K = kWave;
+  if (!cone_whole(care_col, g)) cone_window(care_col, g, xs, K);
+  if (K > kmax) return;
+  if constexpr (!FIRST && A16) {
+    if (K == (uint32_t)kWave) return cone_wave_full16<16, RMAX>(in, wanted, unwanted, out, n, wave * 16, nw * 16, lane);
+  }
+  if (K <= 8) {
+    if (wave * 64 >= n) return;
+    if (K <= 4) cone_wave<4, 64, RMAX, FIRST>(in, wanted, unwanted, out, n, wave * 64, nw * 64, gens, xs, K, lane);
+    else cone_wave<8, 64, RMAX, FIRST>(in, wanted, unwanted, out, n, wave * 64, nw * 64, gens, xs, K, lane);
+  } else if (K <= 16) {
+    cone_wave<16, 16, RMAX, FIRST>(in, wanted, unwanted, out, n, wave * 16, nw * 16, gens, xs, K, lane);
+  } else if (K <= 32) {
+    cone_wave<32, 16, RMAX, FIRST>(in, wanted, unwanted, out, n, wave * 16, nw * 16, gens, xs, K, lane);
+  } else {
+    cone_wave<64, 16, RMAX, FIRST>(in, wanted, unwanted, out, n, wave * 16, nw * 16, gens, xs, K, lane);
+  }
+}
+
 // The shipped shape: 64 universes per wave, register sets 8 at a time, one-
 // shot grid.  Same process, 1M universes, each launch after a read-only scrub
 // (tools/ab/cone_grid_ab.py, profiles/r04/r04g/cone_grid_ab.jsonl): the
@@ -143,6 +177,27 @@ int launch_cone(const uint64_t *d_in, const uint64_t *d_wanted, const uint64_t *
   hipLaunchKernelGGL((k_cone<UPW, RMAX, FIRST, OutT, false, PIPE>), grid, dim3(kBlock), 0, stream, d_in, d_wanted,
                      d_unwanted, d_out, (uint64_t)n, gens, kmax);
   return launched("k_cone launch");
+}
+
+// Launches k_cone_adapt on ceil(n / 16) waves, at most blocks_per_cu blocks
+// per CU (0: no cap).
+template <int RMAX, bool FIRST, typename OutT>
+int launch_cone_adapt(const uint64_t *d_in, const uint64_t *d_wanted, const uint64_t *d_unwanted, OutT *d_out,
+                      size_t n, uint32_t gens, int cus, hipStream_t stream, int blocks_per_cu,
+                      uint32_t kmax = kWave) {
+  const dim3 grid(grid_for((n + 15) / 16, cus, blocks_per_cu));
+  bool a16 = false;
+  if constexpr (!FIRST) a16 = aligned16(d_in);
+  if (a16) {
+    if constexpr (!FIRST) {
+      hipLaunchKernelGGL((k_cone_adapt<RMAX, FIRST, OutT, true>), grid, dim3(kBlock), 0, stream, d_in, d_wanted,
+                         d_unwanted, d_out, (uint64_t)n, gens, kmax);
+      return launched("k_cone_adapt launch");
+    }
+  }
+  hipLaunchKernelGGL((k_cone_adapt<RMAX, FIRST, OutT, false>), grid, dim3(kBlock), 0, stream, d_in, d_wanted,
+                     d_unwanted, d_out, (uint64_t)n, gens, kmax);
+  return launched("k_cone_adapt launch");
 }
 
 }  // namespace

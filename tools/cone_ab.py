@@ -83,9 +83,13 @@ def main():
                 ("filter1", "shipped", 516, lambda: hip.step_contains(x, dw, du, 1)),
                 ("filter2", "k_step_contains<8> (round 3)", 516, lambda: tune.step_contains_nat(x, dw, du, 2, 8, 0)),
                 ("filter2", "shipped", 516, lambda: hip.step_contains(x, dw, du, 2))]
-        for upw, rmax in ((16, 8), (32, 4), (32, 8), (32, 16), (64, 8), (64, 16), (32, 104), (32, 108), (64, 108), (64, 116)):
+        for upw, rmax in ((16, 8), (32, 4), (32, 8), (32, 16), (64, 8), (64, 16), (32, 104), (32, 108), (64, 108), (64, 116),
+                           (0, 8), (4000, 8), (8000, 8), (16000, 8), (32000, 8), (8000, 16), (0, 16)):
+            # upw 0 + 1000 c: k_cone_adapt (chunk 64 / 16 by the window) capped at c blocks per CU
             # rmax + 100: the pipelined pass (the next pass's loads before this pass's steps)
             label = f"k_cone<{upw},{rmax % 100}{' pipelined' if rmax > 100 else ''}>"
+            if upw % 1000 == 0:
+                label = f"k_cone_adapt<{rmax}> cap {upw // 1000}"
             rows.append(("contains", label, 513,
                          lambda upw=upw, rmax=rmax: tune.cone(x, dw, du, 0, upw, rmax, first=False)))
             rows.append(("filter1", label, 516,
