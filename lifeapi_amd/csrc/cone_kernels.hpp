@@ -129,21 +129,20 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
   }
 }
 
-// The shipped shape: 64 universes per wave, register sets 8 at a time, one-
-// shot grid.  Same process, 1M universes, each launch after a read-only scrub
-// (tools/ab/cone_grid_ab.py, profiles/r04/r04g/cone_grid_ab.jsonl): the
-// 4-column target's filter 0.0270 against 0.0288 ms with 32 per wave (back to
-// back 0.0221 / 0.0240), Contains 0.0246 / 0.0256, a loaf box alike; the
-// whole-board filter 0.0933 / 0.0892 (back to back 0.0928 / 0.0940).  Capped
-// grids whose waves find the window once and loop over the batch: within
-// +-3 % of the one-shot grid for small targets, slower for the whole board.
-constexpr int kConeUniverses = 64, kConeSets = 8;
-// Contains (no generations) takes register sets 16 at a time: same process,
-// 1M universes, back to back (tools/cone_ab.py, profiles/r04/first and r04n):
-// the whole board 0.0804 against 0.0833 ms (16-byte loads, 32 in flight per
-// wave), a 14-column target 0.0407 / 0.0428, the small targets within 1 %.
-// (The filter keeps 8: 16 was 5 % slower on the whole board.)
-constexpr int kConeContainsSets = 16;
+// The shipped shape (round 4's last): k_cone_adapt, register sets 8 at a
+// time, at most 16 blocks per CU, for Contains and the 1-2 generation filter.
+// Same process, 1M universes, back to back (tools/cone_ab.py,
+// profiles/r04/r04x/cone_ab.jsonl), against k_cone with 64 universes per wave
+// on a one-shot grid (shipped before): filter 0.0223 / 0.0226 ms on the
+// 4-column target, 0.0436 / 0.0471 on 14 columns, 0.0658 / 0.0696 on 30, the
+// whole board 0.0884 / 0.0898; Contains 0.0199 / 0.0213, 0.0409 / 0.0411,
+// 0.0616 / 0.0626, 0.0790 / 0.0803.  Caps of 4 / 8 / 32 and no cap: slower
+// on some target each (32: +7 % on the 4-column filter; none: +40 %).
+// k_cone's fixed shapes, before: 64 per wave best for P <= 8 (0.0270 against
+// 0.0288 ms with 32 per wave, each launch after a scrub,
+// profiles/r04/r04g/cone_grid_ab.jsonl), 16 per wave best for 14-30 columns.
+constexpr int kConeSets = 8;
+constexpr int kConeAdaptBlocksPerCU = 16;
 // The iterated search loop (gens > 2, no final states) steps the light cone
 // while it spans at most this many columns (P <= 32 lanes per universe: at
 // most half the natural layout's work per universe-generation, against the

@@ -117,8 +117,8 @@ int lifeapi_contains_batch_dev(const uint64_t *d_states, const uint64_t *d_wante
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
   // only the columns holding the target's care cells (cone_kernels.hpp)
-  return launch_cone<kConeUniverses, kConeContainsSets, false>(d_states, d_wanted, d_unwanted, d_out, n, 0u, cus,
-                                                        (hipStream_t)stream);
+  return launch_cone_adapt<kConeSets, false>(d_states, d_wanted, d_unwanted, d_out, n, 0u, cus,
+                                             (hipStream_t)stream, kConeAdaptBlocksPerCU);
 }
 
 int lifeapi_fill_random_dev(uint64_t *d_out, size_t n, uint64_t seed, uint64_t first_universe,

@@ -179,8 +179,8 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
   } else if (!d_final) {
     // the search filter proper (first hits only): the target's light cone
     // (cone_kernels.hpp)
-    return launch_cone<kConeUniverses, kConeSets, true>(d_in, d_wanted, d_unwanted, d_first_gen, n, generations, cus,
-                                                         (hipStream_t)stream);
+    return launch_cone_adapt<kConeSets, true>(d_in, d_wanted, d_unwanted, d_first_gen, n, generations, cus,
+                                              (hipStream_t)stream, kConeAdaptBlocksPerCU);
   } else {
     // 8 universes per wave, every block slot (tools/ab/filter_ab.py,
     // profiles/r02/filter_ab.jsonl, 1M universes x 1 generation, same
