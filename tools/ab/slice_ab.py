@@ -40,7 +40,6 @@ def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 24
     a = hip.fill_random(n, seed=4)
     b = torch.empty_like(a)
-    want = hip.step(a, generations=1)
     gb = lambda ms: n * 1024 / (ms / 1e3) / 1e9  # noqa: E731
 
     def sliced(s, big):
@@ -58,6 +57,7 @@ def main():
         forms.append((f"slices of {s >> 10}K, product", sliced(s, False)))
         forms.append((f"slices of {s >> 10}K, large-batch code", sliced(s, True)))
     for name, fn in forms:
+        want = hip.step(a, generations=1)  # (the timings ping-pong a and b: a changes form to form)
         fn(a, b)
         torch.cuda.synchronize()
         same = bool((b == want).all().item())
