@@ -970,12 +970,13 @@ def main(argv=None):
                          "frac_kind": ("effective: algorithmic bytes / launch time; with the batch-keyed "
                                        "launch order and the plain-stored tail part of each launch's reads are "
                                        "served by the 256 MB memory-side Infinity Cache (DESIGN.md 3.1, 5.2); "
-                                       "cache_neutral is the HBM-only figure"
+                                       "cache_neutral reads from HBM alone (its last writes may still be in the cache at its end event: "
+                                       "DESIGN.md 5.2 counts those write-backs)"
                                        if n <= (1 << 22) else
                                        "effective: algorithmic bytes / launch time; above 4M universes per "
                                        "GPU the launch takes one order with every store nontemporal "
-                                       "(nothing is arranged for Infinity Cache reuse); cache_neutral is the "
-                                       "HBM-only figure"),
+                                       "(nothing is arranged for Infinity Cache reuse); cache_neutral reads from "
+                                       "HBM alone"),
                          "cache_neutral": ({"achieved": neu[0], "frac": neu[0] / HBM_PEAK_GBS,
                                             "kernel_ms": rank_figs[0][0],
                                             "method": "the shipped launch (lifeapi_step_batch_dev), same size, "
