@@ -32,9 +32,48 @@ int cone_by_shape(const uint64_t *in, const uint64_t *w, const uint64_t *u, OutT
   return fail(LIFEAPI_E_INVALID, "cone shapes: upw 16/32/64 x rmax 4/8/16/32%s");
 }
 
+// The light cone's access shape with nothing else: one 128-byte line (16
+// words) of each 512-byte universe, 4 universes per wave-instruction (lane
+// l: word 16 line + l % 16 of universe u0 + l / 16), 64 universes per wave in
+// 16 loads issued together, one uint32 out per universe (the OR of its
+// line), one coalesced store per wave; one-shot grid.  A ceiling for the
+// cone kernels on small targets.
+__global__ __launch_bounds__(kBlock) void k_line_read(const uint64_t *in, uint32_t *__restrict__ out, uint64_t n,
+                                                      uint32_t line) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint64_t u0 = wave * 64;
+  if (u0 >= n) return;
+  uint64_t v[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const uint64_t u = u0 + 4 * k + lane / 16;
+    v[k] = u < n ? __builtin_nontemporal_load(in + u * kWave + 16 * line + (lane & 15)) : 0ull;
+  }
+  uint32_t mine = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    // OR over the 16 lanes of each universe (DPP-free: a ballot of nonzero)
+    const uint64_t nz = __ballot(v[k] != 0ull);
+    const uint32_t rel = (uint32_t)lane - 4u * k;
+    if (rel < 4u) mine = (uint32_t)((nz >> (16 * rel)) & 0xFFFFu);
+  }
+  if (u0 + lane < n) out[u0 + lane] = mine;
+}
+
 }  // namespace
 
 extern "C" {
+
+int lifeapi_tune_line_read(const uint64_t *d_in, uint32_t *d_out, size_t n, int line, void *stream) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!d_in || !d_out || line < 0 || line > 3) return fail(LIFEAPI_E_INVALID, "bad argument to lifeapi_tune_line_read%s");
+  int cus = 0, rc = device_cus(cus);
+  if (rc != LIFEAPI_OK) return rc;
+  hipLaunchKernelGGL(k_line_read, dim3(grid_for((n + 63) / 64, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream, d_in,
+                     d_out, (uint64_t)n, (uint32_t)line);
+  return launched("k_line_read launch");
+}
 
 /* rmax + 100: the pipelined pass (cone_wave PIPE).
  * first != 0: the search filter (d_out uint32 first generations, any gens;

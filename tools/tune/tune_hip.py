@@ -319,3 +319,16 @@ def search_iter(states, wanted, unwanted, generations, cone_cap, split_cap, stre
     hip._check(lib.lifeapi_tune_search_iter(states.data_ptr(), wanted.data_ptr(), unwanted.data_ptr(), first.data_ptr(),
                                             n, generations, cone_cap, split_cap, hip._stream(stream)))
     return first
+
+
+lib.lifeapi_tune_line_read.argtypes = [_vp, _vp, _sz, _int, _vp]
+lib.lifeapi_tune_line_read.restype = _int
+
+
+def line_read(states, line, out=None, stream=None):
+    """one 128-byte line of each universe read, one uint32 written per universe"""
+    n = hip._universes(states)
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=states.device)
+    hip._check(lib.lifeapi_tune_line_read(states.data_ptr(), out.data_ptr(), n, line, hip._stream(stream)))
+    return out
