@@ -42,8 +42,9 @@ def main():
     bw[0, 10] = bw[0, 11] = 3 << 40
     bu[0, 9:13] = 15 << 39
     bu &= ~bw
-    rows = [("k_line_read line 0", 132, lambda a, b: tune.line_read(x, 0)),
-            ("k_line_read line 1", 132, lambda a, b: tune.line_read(x, 1)),
+    rows = [("k_line_read line 0, 16 lanes per universe", 132, lambda a, b: tune.line_read(x, 0)),
+            ("k_line_read line 0, 4 lanes per universe", 132, lambda a, b: tune.line_read(x, 4)),
+            ("k_line_read line 1, 4 lanes per universe", 132, lambda a, b: tune.line_read(x, 5)),
             ("Contains, block + ring (product)", 129, lambda a, b: hip.contains(x, bw, bu)),
             ("filter 1 gen, block + ring (product)", 132, lambda a, b: hip.step_contains(x, bw, bu, 1))]
     for name, nbytes, fn in rows:

@@ -32,31 +32,33 @@ int cone_by_shape(const uint64_t *in, const uint64_t *w, const uint64_t *u, OutT
   return fail(LIFEAPI_E_INVALID, "cone shapes: upw 16/32/64 x rmax 4/8/16/32%s");
 }
 
-// The light cone's access shape with nothing else: one 128-byte line (16
-// words) of each 512-byte universe, 4 universes per wave-instruction (lane
-// l: word 16 line + l % 16 of universe u0 + l / 16), 64 universes per wave in
-// 16 loads issued together, one uint32 out per universe (the OR of its
-// line), one coalesced store per wave; one-shot grid.  A ceiling for the
-// cone kernels on small targets.
+// The light cone's access shape with nothing else: LPU lanes per universe
+// read LPU consecutive words of one 128-byte line of each 512-byte universe
+// (16: the whole line; 4: words 8..11 of it, as the cone for a 4-column
+// target loads them), 64 universes per wave with every load issued
+// together, one uint32 out per universe (whether the words read are
+// nonzero), one coalesced store per wave; one-shot grid.
+template <int LPU>
 __global__ __launch_bounds__(kBlock) void k_line_read(const uint64_t *in, uint32_t *__restrict__ out, uint64_t n,
                                                       uint32_t line) {
+  constexpr int UPI = kWave / LPU, NL = 64 / UPI;  // universes per load instruction, loads per wave
   const int lane = threadIdx.x & (kWave - 1);
   const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint64_t u0 = wave * 64;
   if (u0 >= n) return;
-  uint64_t v[16];
+  const uint32_t word = 16 * line + (LPU == 16 ? 0u : 8u) + (uint32_t)(lane & (LPU - 1));
+  uint64_t v[NL];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const uint64_t u = u0 + 4 * k + lane / 16;
-    v[k] = u < n ? __builtin_nontemporal_load(in + u * kWave + 16 * line + (lane & 15)) : 0ull;
+  for (int k = 0; k < NL; ++k) {
+    const uint64_t u = u0 + (uint64_t)UPI * k + lane / LPU;
+    v[k] = u < n ? __builtin_nontemporal_load(in + u * kWave + word) : 0ull;
   }
   uint32_t mine = 0;
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    // OR over the 16 lanes of each universe (DPP-free: a ballot of nonzero)
+  for (int k = 0; k < NL; ++k) {
     const uint64_t nz = __ballot(v[k] != 0ull);
-    const uint32_t rel = (uint32_t)lane - 4u * k;
-    if (rel < 4u) mine = (uint32_t)((nz >> (16 * rel)) & 0xFFFFu);
+    const uint32_t rel = (uint32_t)lane - (uint32_t)(UPI * k);
+    if (rel < (uint32_t)UPI) mine = (uint32_t)((nz >> (LPU * rel)) & ((1ull << LPU) - 1)) != 0u;
   }
   if (u0 + lane < n) out[u0 + lane] = mine;
 }
@@ -67,11 +69,19 @@ extern "C" {
 
 int lifeapi_tune_line_read(const uint64_t *d_in, uint32_t *d_out, size_t n, int line, void *stream) {
   if (n == 0) return LIFEAPI_OK;
-  if (!d_in || !d_out || line < 0 || line > 3) return fail(LIFEAPI_E_INVALID, "bad argument to lifeapi_tune_line_read%s");
+  // line + 4 * k: k = 0 the whole line (16 lanes per universe), 1 words 8..11 of it (4 lanes)
+  const int lpu = (line >> 2) ? 4 : 16;
+  line &= 3;
+  if (!d_in || !d_out || line < 0) return fail(LIFEAPI_E_INVALID, "bad argument to lifeapi_tune_line_read%s");
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
-  hipLaunchKernelGGL(k_line_read, dim3(grid_for((n + 63) / 64, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream, d_in,
-                     d_out, (uint64_t)n, (uint32_t)line);
+  const dim3 grid(grid_for((n + 63) / 64, cus, 0));
+  if (lpu == 4)
+    hipLaunchKernelGGL(k_line_read<4>, grid, dim3(kBlock), 0, (hipStream_t)stream, d_in, d_out, (uint64_t)n,
+                       (uint32_t)line);
+  else
+    hipLaunchKernelGGL(k_line_read<16>, grid, dim3(kBlock), 0, (hipStream_t)stream, d_in, d_out, (uint64_t)n,
+                       (uint32_t)line);
   return launched("k_line_read launch");
 }
 
