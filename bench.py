@@ -123,11 +123,12 @@ class HipRuntime:
         self.device = torch.device("cuda", local_rank % ndev)
         torch.cuda.set_device(self.device)
         self.stream = torch.cuda.current_stream(self.device)
-        self.neutral, self.neutral_error = None, None
+        self.neutral, self.neutral_error, self.line_read = None, None, None
         try:  # the tuning build's streaming-step launcher (fixed order, explicit store policy)
             sys.path.insert(0, os.path.join(ROOT, "tools", "tune"))
             import tune_hip
             self.neutral = tune_hip.step_order
+            self.line_read = tune_hip.line_read  # the light cone's access shape alone
         except (ImportError, OSError) as e:
             self.neutral_error = str(e)
 
@@ -749,6 +750,18 @@ def secondary_filter(hip, rt):
                                     "definition": "the 128-byte lines of each universe that hold its light "
                                                   "cone (the fetch granularity) + the output, per launch"},
                        "full_read_equivalent_GBps": n * (512 + outb) / (ms / 1e3) / 1e9}
+            if lines == 1 and rt.line_read is not None:
+                # the same line of every universe read with as many lanes per
+                # universe as the cone uses, nothing computed (tuning build
+                # k_line_read): the ceiling of this access shape
+                lpu = 4 if k <= 4 else 8 if k <= 8 else 16
+                code = (xs // 16) + 4 * {16: 0, 4: 1, 8: 2}[lpu]
+                pm, _ = scrubbed_ms(rt, lambda a, b: rt.line_read(a, code, stream=rt.stream), x, x, scrub)
+                row[op]["access_shape"] = {"kernel": f"k_line_read<{lpu}> (tuning build)", "kernel_ms": pm,
+                                           "frac_of_shape": pm / ms,
+                                           "definition": "one 128-byte line of every universe read with the "
+                                                         "cone's lanes per universe and one uint32 written, "
+                                                         "nothing computed, timed as the kernel is"}
         out["targets"][name] = row
     del scrub, x
     torch.cuda.empty_cache()

@@ -69,8 +69,9 @@ extern "C" {
 
 int lifeapi_tune_line_read(const uint64_t *d_in, uint32_t *d_out, size_t n, int line, void *stream) {
   if (n == 0) return LIFEAPI_OK;
-  // line + 4 * k: k = 0 the whole line (16 lanes per universe), 1 words 8..11 of it (4 lanes)
-  const int lpu = (line >> 2) ? 4 : 16;
+  // line + 4 * k: k = 0 the whole line (16 lanes per universe), 1 words 8..11 of it (4 lanes),
+  // 2 words 8..15 (8 lanes)
+  const int lpu = (line >> 2) == 1 ? 4 : (line >> 2) == 2 ? 8 : 16;
   line &= 3;
   if (!d_in || !d_out || line < 0) return fail(LIFEAPI_E_INVALID, "bad argument to lifeapi_tune_line_read%s");
   int cus = 0, rc = device_cus(cus);
@@ -78,6 +79,9 @@ int lifeapi_tune_line_read(const uint64_t *d_in, uint32_t *d_out, size_t n, int 
   const dim3 grid(grid_for((n + 63) / 64, cus, 0));
   if (lpu == 4)
     hipLaunchKernelGGL(k_line_read<4>, grid, dim3(kBlock), 0, (hipStream_t)stream, d_in, d_out, (uint64_t)n,
+                       (uint32_t)line);
+  else if (lpu == 8)
+    hipLaunchKernelGGL(k_line_read<8>, grid, dim3(kBlock), 0, (hipStream_t)stream, d_in, d_out, (uint64_t)n,
                        (uint32_t)line);
   else
     hipLaunchKernelGGL(k_line_read<16>, grid, dim3(kBlock), 0, (hipStream_t)stream, d_in, d_out, (uint64_t)n,
