@@ -407,9 +407,9 @@ constexpr int kContainsNet = 6;  // tail network of the fused kernel (as k_step'
 // SIMD), where one shared pass took 84 (5), and 7 takes 62 (8 waves).
 constexpr int kContainsLo = 7, kContainsHi = 8;
 // the light-cone path of kContainsLo (cone_max below): universes per wave chunk
+// (16-universe chunks for cones of 9-32 columns: 6-8 % slower at 64K x 8-13
+// generations, +4 % at 1M x 3, equal at 1M x 8-13; profiles/r04/r04ag)
 constexpr int kConeLoUniverses = 8;
-// ... and for cones of 9-32 columns (P = 16, 32)
-constexpr int kConeLoUniversesWide = 16;
 constexpr uint32_t kLowRows = 4;  // tools/gen_split_asm.py LOW_H
 
 __device__ __forceinline__ uint64_t rotr64(uint64_t v, uint32_t k) {
@@ -600,11 +600,12 @@ __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *
       uint32_t cxs, cK;
       cone_window(care_col, gens, cxs, cK);  // cK <= cone_max (cone_fits)
       {
-        constexpr int U = kConeLoUniverses, UW = kConeLoUniversesWide;
-        const uint64_t wv = (uint64_t)blockIdx.x * kWavesPerBlock + wib, nw = (uint64_t)gridDim.x * kWavesPerBlock;
-        if (cK <= 8) cone_wave<8, U, 8, true>(in, wanted, unwanted, first, n, wv * U, nw * U, gens, cxs, cK, lane);
-        else if (cK <= 16) cone_wave<16, UW, 8, true>(in, wanted, unwanted, first, n, wv * UW, nw * UW, gens, cxs, cK, lane);
-        else cone_wave<32, UW, 8, true>(in, wanted, unwanted, first, n, wv * UW, nw * UW, gens, cxs, cK, lane);
+        constexpr int U = kConeLoUniverses;
+        const uint64_t u0 = ((uint64_t)blockIdx.x * kWavesPerBlock + wib) * U,
+                       step = (uint64_t)gridDim.x * kWavesPerBlock * U;
+        if (cK <= 8) cone_wave<8, U, 8, true>(in, wanted, unwanted, first, n, u0, step, gens, cxs, cK, lane);
+        else if (cK <= 16) cone_wave<16, U, 8, true>(in, wanted, unwanted, first, n, u0, step, gens, cxs, cK, lane);
+        else cone_wave<32, U, 8, true>(in, wanted, unwanted, first, n, u0, step, gens, cxs, cK, lane);
       }
     }
     return;
