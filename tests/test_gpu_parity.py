@@ -611,6 +611,44 @@ def test_stable_passes_chunked_grid_ragged(hip, port):
     assert (to_host(got) == port.stable_vulnerable(x)).all()
 
 
+def test_stable_passes_next_node_changed_lines(hip, port):
+    """The passes store only the 128-byte lines holding a changed column
+    (stable_kernels.hpp): on a search's next node -- _stable_cases propagated
+    to their fixpoint by the oracle, then one unknown cell decided (ON or OFF
+    by turns) -- a few columns change, so nearly every line is skipped, and a
+    change the kernel failed to record would leave its line stale.  Every
+    pass in place against the oracle, and the host-pointer form too."""
+    n = 1000
+    x, _ = port.stable_pass(_stable_cases(port, n, seed=21), 4)
+    x = x.reshape(n, 10, 64).copy()
+    decided = 0
+    for u in range(n):
+        cols = np.nonzero(x[u, 1])[0]
+        if len(cols) == 0:
+            continue
+        c = int(cols[len(cols) // 2])
+        low = x[u, 1, c] & (~x[u, 1, c] + np.uint64(1))
+        x[u, 1, c] &= ~low
+        if u % 2:
+            x[u, 0, c] |= low
+        decided += 1
+    assert decided > n // 2
+    x = x.reshape(n, 640)
+    for w, name in enumerate(hip.STABLE_PASSES):
+        want, wfl = port.stable_pass(x, w)
+        changed_cols = (want.reshape(n, 10, 64) != x.reshape(n, 10, 64)).any(axis=1).sum(axis=1)
+        d = to_dev(x).reshape(n, 640)
+        fl = hip.stable_pass(d, name).cpu().numpy()
+        assert (d.cpu().numpy().view(np.uint64) == want).all(), name
+        assert (fl == wfl).all(), name
+        if name == "propagate":
+            assert 0 < np.median(changed_cols) <= 16  # few columns change: most lines are skipped
+            h = np.ascontiguousarray(x).copy()
+            flags = np.zeros(n, np.uint8)
+            hip._check(hip.lib.lifeapi_stable_pass_batch(h.ctypes.data, flags.ctypes.data, n, w, 0, 0))
+            assert (h == want).all() and (flags == wfl).all()
+
+
 @pytest.mark.parametrize("density", [0.2, 0.5, 0.8])
 def test_stable_step_and_propagate_dense_counts(hip, port, density):
     """PropagateStep counts the state once and derives NeighbourCount(state |
