@@ -407,6 +407,10 @@ constexpr int kContainsNet = 6;  // tail network of the fused kernel (as k_step'
 // SIMD), where one shared pass took 84 (5), and 7 takes 62 (8 waves).
 constexpr int kContainsLo = 7, kContainsHi = 8;
 // the light-cone path of kContainsLo (cone_max below): universes per wave chunk
+// (Measured in the compiler's allocation, not shipped: the whole board in the
+// natural layout for wider cones at <= 4 generations -- 10-35 % faster there
+// -- costs kContainsLo 7 VGPRs (62 -> 69, any register-set count) or
+// kContainsHi 7 (70 -> 77), a wave per SIMD for every other target.)
 // (16-universe chunks for cones of 9-32 columns: 6-8 % slower at 64K x 8-13
 // generations, +4 % at 1M x 3, equal at 1M x 8-13; profiles/r04/r04ag)
 constexpr int kConeLoUniverses = 8;
