@@ -20,6 +20,13 @@
 // reads (after g generations the error has moved g columns in).  The care
 // columns are exact.  A window with K >= 64 loads the whole board from
 // column 0, where the rotate is the true torus.
+//
+// The pass over a wave's universes (cone_wave) and the window tests
+// (cone_window, cone_whole, cone_fits) live in step_kernels.hpp, shared with
+// the iterated search loop's kContainsLo.  This file holds the kernels that
+// launch them: k_cone_adapt (shipped: the chunk of universes per wave chosen
+// from the window), k_cone (fixed shapes, the tuning build's A/Bs) and the
+// whole-board Contains pass with 16-byte loads.
 #pragma once
 
 #include "step_kernels.hpp"
