@@ -44,12 +44,12 @@ def main():
     bu &= ~bw
     ww, wu = np.zeros(64, np.uint64), np.zeros(64, np.uint64)
     wu[0::3] = np.uint64(1 << 10)
-    caps = [(16, 32)]
+    caps = []
     for tname, (w, u) in (("block", (bw, bu)), ("whole", (ww, wu))):
         dw, du = (torch.from_numpy(v.view(np.int64)[None].copy()).cuda() for v in (w, u))
         for n in (1 << 16, 1 << 20):
             x = hip.fill_random(n, seed=3)
-            for gens in (3, 8, 13, 64):
+            for gens in (3, 4, 5, 6, 8, 13, 64):
                 ref = tune.step_contains(x, dw, du, gens, 7)  # both targets' windows are <= 4 rows
                 r = {"target": tname, "universes": n, "gens": gens}
                 for cc, sc in caps:
@@ -59,7 +59,9 @@ def main():
                 # round 3's launch (the uncapped split pair, no cone) and the product
                 forms = {"round3": lambda a, b, g=gens: tune.step_contains_pair(x, dw, du, g, 0, 0),
                          "product": lambda a, b, g=gens: hip.step_contains(x, dw, du, generations=g)[0],
-                         "cone8_alone": lambda a, b, g=gens: tune.cone(x, dw, du, g, 8, 8)}
+                         "cone8_alone": lambda a, b, g=gens: tune.cone(x, dw, du, g, 8, 8),
+                         # k_cone_adapt alone (the 1-2 generation filter's kernel), 16 blocks per CU
+                         "adapt_alone": lambda a, b, g=gens: tune.cone(x, dw, du, g, 16000, 8)}
                 for k, fn in forms.items():
                     r[k + "_equal"] = bool((fn(0, 0) == ref).all().item())
                     r[k + "_ms"] = bench.back_to_back_ms(rt, fn, x, x)
