@@ -91,7 +91,7 @@ int lifeapi_contains_batch_dev(const uint64_t *d_states, const uint64_t *d_wante
  * which Stepped(g) contains the target, or 0 if none; d_final (may be NULL)
  * receives Stepped(gens).  With d_final NULL (the search filter) only the
  * columns within gens of the target's care columns are read and stepped
- * when gens <= 2, or gens > 2 and those columns number at most 32.        */
+ * when gens <= 4, or when those columns number at most 32.                */
 int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
                                     const uint64_t *d_wanted, const uint64_t *d_unwanted,
                                     uint32_t *d_first_gen, size_t n, uint32_t generations,

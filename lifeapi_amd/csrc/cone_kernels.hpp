@@ -150,6 +150,9 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
 // profiles/r04/r04g/cone_grid_ab.jsonl), 16 per wave best for 14-30 columns.
 constexpr int kConeSets = 8;
 constexpr int kConeAdaptBlocksPerCU = 16;
+// The search filter without final states takes k_cone_adapt alone up to
+// this many generations (step.hip); beyond, the split-layout pair.
+constexpr uint32_t kConeAloneGens = 4;
 // The iterated search loop (gens > 2, no final states) steps the light cone
 // while it spans at most this many columns (P <= 32 lanes per universe: at
 // most half the natural layout's work per universe-generation, against the

@@ -148,6 +148,17 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
   }
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
+  if (!d_final && generations <= kConeAloneGens) {
+    // the search filter proper (first hits only) up to kConeAloneGens
+    // generations: the target's light cone, or the whole board, in the
+    // natural layout (cone_kernels.hpp k_cone_adapt).  At 3 and 4 generations
+    // it beats the split pair (below) on every target measured: 3-31 %
+    // (tools/ab/search_iter_caps_ab.py, profiles/r04/r04ak: a 4-column target
+    // and a whole-board one, 64K and 1M universes); from 5 on the split
+    // layout takes over for whole-board targets at 1M.
+    return launch_cone_adapt<kConeSets, true>(d_in, d_wanted, d_unwanted, d_first_gen, n, generations, cus,
+                                              (hipStream_t)stream, kConeAdaptBlocksPerCU);
+  }
   if (generations > 2) {  // the layout of the shipped step for gens > 2
     // Without final states, a target whose light cone over `generations`
     // spans at most kConeIterColumns columns is answered on that cone:
@@ -176,11 +187,6 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
       if (rc != LIFEAPI_OK) return rc;
     }
     return LIFEAPI_OK;
-  } else if (!d_final) {
-    // the search filter proper (first hits only): the target's light cone
-    // (cone_kernels.hpp)
-    return launch_cone_adapt<kConeSets, true>(d_in, d_wanted, d_unwanted, d_first_gen, n, generations, cus,
-                                              (hipStream_t)stream, kConeAdaptBlocksPerCU);
   } else {
     // 8 universes per wave, every block slot (tools/ab/filter_ab.py,
     // profiles/r02/filter_ab.jsonl, 1M universes x 1 generation, same
