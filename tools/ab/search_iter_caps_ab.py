@@ -47,9 +47,11 @@ def main():
     caps = []
     for tname, (w, u) in (("block", (bw, bu)), ("whole", (ww, wu))):
         dw, du = (torch.from_numpy(v.view(np.int64)[None].copy()).cuda() for v in (w, u))
-        for n in (1 << 16, 1 << 20):
+        sizes = [int(v) for v in sys.argv[1].split(",")] if len(sys.argv) > 1 else [1 << 16, 1 << 20]
+        gens_list = [int(v) for v in sys.argv[2].split(",")] if len(sys.argv) > 2 else [3, 4, 5, 6, 8, 13, 64]
+        for n in sizes:
             x = hip.fill_random(n, seed=3)
-            for gens in (3, 4, 5, 6, 8, 13, 64):
+            for gens in gens_list:
                 ref = tune.step_contains(x, dw, du, gens, 7)  # both targets' windows are <= 4 rows
                 r = {"target": tname, "universes": n, "gens": gens}
                 for cc, sc in caps:
