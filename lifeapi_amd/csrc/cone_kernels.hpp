@@ -151,8 +151,14 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
 constexpr int kConeSets = 8;
 constexpr int kConeAdaptBlocksPerCU = 16;
 // The search filter without final states takes k_cone_adapt alone up to
-// this many generations (step.hip); beyond, the split-layout pair.
-constexpr uint32_t kConeAloneGens = 4;
+// this many generations (step.hip); beyond, the split-layout pair.  Batches
+// of at most kConeAloneSmallUniverses take it up to kConeAloneGensSmall:
+// same process (tools/ab/search_iter_caps_ab.py, profiles/r04/r04an), at 5-6
+// generations k_cone_adapt / split pair = 0.65-0.94 on a 4-column and a
+// whole-board target at 64K-128K, 0.83-1.02 at 256K, but 1.07-1.14 on the
+// whole board at 512K.
+constexpr uint32_t kConeAloneGens = 4, kConeAloneGensSmall = 6;
+constexpr uint64_t kConeAloneSmallUniverses = 1u << 18;
 // The iterated search loop (gens > 2, no final states) steps the light cone
 // while it spans at most this many columns (P <= 32 lanes per universe: at
 // most half the natural layout's work per universe-generation, against the

@@ -148,14 +148,15 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
   }
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
-  if (!d_final && generations <= kConeAloneGens) {
+  if (!d_final && generations <= (n <= kConeAloneSmallUniverses ? kConeAloneGensSmall : kConeAloneGens)) {
     // the search filter proper (first hits only) up to kConeAloneGens
     // generations: the target's light cone, or the whole board, in the
     // natural layout (cone_kernels.hpp k_cone_adapt).  At 3 and 4 generations
     // it beats the split pair (below) on every target measured: 3-31 %
     // (tools/ab/search_iter_caps_ab.py, profiles/r04/r04ak: a 4-column target
     // and a whole-board one, 64K and 1M universes); from 5 on the split
-    // layout takes over for whole-board targets at 1M.
+    // layout takes over for whole-board targets at 1M; batches of <= 256K
+    // take it up to 6 generations (cone_kernels.hpp kConeAloneGensSmall).
     return launch_cone_adapt<kConeSets, true>(d_in, d_wanted, d_unwanted, d_first_gen, n, generations, cus,
                                               (hipStream_t)stream, kConeAdaptBlocksPerCU);
   }
