@@ -29,6 +29,8 @@
 // whole-board Contains pass with 16-byte loads.
 #pragma once
 
+#include <type_traits>
+
 #include "step_kernels.hpp"
 
 namespace lifeapi_impl {
@@ -94,12 +96,15 @@ __global__ __launch_bounds__(kBlock) void k_cone(const uint64_t *in, const uint6
     if (K == (uint32_t)kWave) return cone_wave_full16<UPW, RMAX>(in, wanted, unwanted, out, n, u0, step, lane);
   }
   // (a wave of UPW universes takes whole register sets: P >= 64 / UPW)
-  if (K <= 4 && UPW >= 16) cone_wave<UPW >= 16 ? 4 : 8, UPW, RMAX, FIRST, OutT, PIPE>(in, wanted, unwanted, out, n, u0, step, gens,
-                                                                         xs, K, lane);
-  else if (K <= 8) cone_wave<8, UPW, RMAX, FIRST, OutT, PIPE>(in, wanted, unwanted, out, n, u0, step, gens, xs, K, lane);
-  else if (K <= 16) cone_wave<16, UPW, RMAX, FIRST, OutT, PIPE>(in, wanted, unwanted, out, n, u0, step, gens, xs, K, lane);
-  else if (K <= 32) cone_wave<32, UPW, RMAX, FIRST, OutT, PIPE>(in, wanted, unwanted, out, n, u0, step, gens, xs, K, lane);
-  else cone_wave<64, UPW, RMAX, FIRST, OutT, PIPE>(in, wanted, unwanted, out, n, u0, step, gens, xs, K, lane);
+  auto pass = [&](auto p) __attribute__((always_inline)) {
+    cone_wave<decltype(p)::value, UPW, RMAX, FIRST, OutT, PIPE>(in, wanted, unwanted, out, n, u0, step, gens, xs, K,
+                                                                lane);
+  };
+  if (K <= 4 && UPW >= 16) pass(std::integral_constant<int, (UPW >= 16 ? 4 : 8)>{});
+  else if (K <= 8) pass(std::integral_constant<int, 8>{});
+  else if (K <= 16) pass(std::integral_constant<int, 16>{});
+  else if (K <= 32) pass(std::integral_constant<int, 32>{});
+  else pass(std::integral_constant<int, 64>{});
 }
 
 // k_cone with the chunk size chosen by the window: 64 universes per wave

@@ -130,11 +130,13 @@ int lifeapi_tune_search_iter(const uint64_t *d_in, const uint64_t *d_wanted, con
   const int upw = cone_cap < 0 ? -1 : cone_cap / 1000;
   cone_cap %= 1000;
   const hipStream_t st = (hipStream_t)stream;
-  if (upw == 16) rc = launch_cone<16, 8, true>(d_in, d_wanted, d_unwanted, d_first, n, gens, cus, st, cone_cap, kConeIterColumns);
-  else if (upw == 32) rc = launch_cone<32, 8, true>(d_in, d_wanted, d_unwanted, d_first, n, gens, cus, st, cone_cap, kConeIterColumns);
-  else if (upw == 8) rc = launch_cone<8, 8, true>(d_in, d_wanted, d_unwanted, d_first, n, gens, cus, st, cone_cap, kConeIterColumns);
-  else if (upw == 0) rc = launch_cone<kConeIterUniverses, kConeSets, true>(d_in, d_wanted, d_unwanted, d_first, n, gens,
-                                                                          cus, st, cone_cap, kConeIterColumns);
+  const uint64_t *w = d_wanted, *u = d_unwanted;
+  const uint32_t km = kConeIterColumns;
+  if (upw == 16) rc = launch_cone<16, 8, true>(d_in, w, u, d_first, n, gens, cus, st, cone_cap, km);
+  else if (upw == 32) rc = launch_cone<32, 8, true>(d_in, w, u, d_first, n, gens, cus, st, cone_cap, km);
+  else if (upw == 8) rc = launch_cone<8, 8, true>(d_in, w, u, d_first, n, gens, cus, st, cone_cap, km);
+  else if (upw == 0)
+    rc = launch_cone<kConeIterUniverses, kConeSets, true>(d_in, w, u, d_first, n, gens, cus, st, cone_cap, km);
   if (rc != LIFEAPI_OK) return rc;
   const dim3 grid(grid_for((n + 3) / 4, cus, split_cap));
   hipLaunchKernelGGL((k_step_contains_split<8, kContainsNet, kContainsLo>), grid, dim3(kBlock), 0, (hipStream_t)stream,
