@@ -173,8 +173,9 @@ constexpr uint64_t kConeAloneSmallUniverses = 1u << 18;
 // one wave per SIMD).
 constexpr uint32_t kConeIterColumns = 32;
 static_assert(kConeIterColumns <= 32, "kContainsLo's cone passes take P <= 32");
-// ... with both split kernels on grids of at most 32 blocks per CU looping
-// over the batch (step.hip): one of the two always idles.
+// The split kernels (step.hip, with or without final states) run on grids of
+// at most 32 blocks per CU looping over the batch: one of the two always
+// idles, and the working one is faster capped from 256K universes on.
 constexpr int kSplitIterBlocksPerCU = 32;
 // The tuning build's separate-launch form of the same (k_cone before the
 // pair): 8 universes per wave, at most 16 blocks per CU.

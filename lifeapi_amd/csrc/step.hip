@@ -164,13 +164,17 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
     // Without final states, a target whose light cone over `generations`
     // spans at most kConeIterColumns columns is answered on that cone:
     // kContainsLo's waves step only those columns in the natural layout
-    // (cone_wave) and kContainsHi's return.  Both grids are then capped
-    // (blocks per CU, looping over the batch), so that the idle kernel's
-    // waves cost a few microseconds instead of a wave launch per 4 universes
-    // (tools/ab/search_iter_caps_ab.py).
+    // (cone_wave) and kContainsHi's return.  Both grids are capped (blocks
+    // per CU, looping over the batch), so that the idle kernel's waves cost a
+    // few microseconds instead of a wave launch per 4 universes
+    // (tools/ab/search_iter_caps_ab.py).  With final states
+    // the capped grids help too: 1M universes x 8 / 64
+    // generations 0.467 -> 0.394-0.398 / 1.78-1.80 -> 1.70 ms, 256K 0.112 ->
+    // 0.101 ms; at config 3's 64K the cap does not bind (tools/ab/final_caps_ab.py,
+    // profiles/r04/r04ar).
+    const int split_cap = kSplitIterBlocksPerCU;
     uint32_t cone_max = 0;
-    int split_cap = 0;
-    if (!d_final) cone_max = kConeIterColumns, split_cap = kSplitIterBlocksPerCU;
+    if (!d_final) cone_max = kConeIterColumns;
     // two kernels, one per register layout (a target window of <= 4 rows in
     // 62 VGPRs, 8 waves per SIMD; the rest in 70, 7 waves): each wave finds
     // the window and only the matching kernel works (step_kernels.hpp

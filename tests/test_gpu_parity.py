@@ -611,6 +611,32 @@ def test_stable_passes_chunked_grid_ragged(hip, port):
     assert (to_host(got) == port.stable_vulnerable(x)).all()
 
 
+def test_step_contains_final_states_capped_grid(hip, port):
+    """With final states the split pair runs on grids of at most 32 blocks
+    per CU looping over the batch (step.hip kSplitIterBlocksPerCU): 200003
+    universes (more than one pass of the capped grid, ragged), 9 and 40
+    generations, first hits and final states against the oracle."""
+    n = 200003
+    x = port.fill(n, seed=77) & port.fill(n, seed=78)
+    w, u = np.zeros(64, np.uint64), np.zeros(64, np.uint64)
+    w[10] = w[11] = np.uint64(3 << 40)
+    for c in (9, 10, 11, 12):
+        u[c] = np.uint64(15 << 39)
+    u &= ~w
+    x[::5] = (x[::5] & ~(w | u)) | w
+    for gens in (9, 40):
+        fin = torch.empty((n, 64), dtype=torch.int64, device="cuda")
+        first, _ = hip.step_contains(to_dev(x).reshape(n, 64), to_dev(w[None]), to_dev(u[None]), gens, final=fin)
+        want, s = np.zeros(n, np.int64), x.copy()
+        for g in range(1, gens + 1):
+            s = port.step_batch(s, 1, nthreads=8)
+            hit = (((s ^ w) & (w | u)) == 0).all(axis=1)
+            want[(want == 0) & hit] = g
+        assert (first.cpu().numpy() == want).all(), gens
+        assert (to_host(fin) == s).all(), gens
+        assert (want > 0).sum() > n // 10
+
+
 def test_stable_passes_next_node_changed_lines(hip, port):
     """The passes store only the 128-byte lines holding a changed column
     (stable_kernels.hpp): on a search's next node -- _stable_cases propagated
