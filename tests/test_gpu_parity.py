@@ -634,7 +634,7 @@ def test_step_contains_final_states_capped_grid(hip, port):
             want[(want == 0) & hit] = g
         assert (first.cpu().numpy() == want).all(), gens
         assert (to_host(fin) == s).all(), gens
-        assert (want > 0).sum() > n // 10
+        assert (want > 0).sum() > 500  # hits (the planted blocks that survive their neighbours)
 
 
 def test_stable_passes_next_node_changed_lines(hip, port):
