@@ -136,11 +136,13 @@ int lifeapi_weld_step_batch_dev(uint64_t *d_welds, size_t n, uint32_t generation
     // with every slot (6: 0.458; 5: 0.472), same process, exact caps
     // (tools/ab/stencil_occupancy_ab.py, profiles/r03/stencil_caps.jsonl).
     // Round 4: two welds per wave (their 8 loads issued together) and each XCD
-    // a contiguous eighth of the batch: 1M welds in one order 0.4218 ms
-    // against 0.4680 with one weld per wave and 0.4505 for round 3's shipped
-    // launch with its alternating order (0.796 / 0.717 / 0.745 of 8 TB/s;
-    // after a read-only scrub 0.794 / 0.731 / 0.740); either change alone
-    // gains less (tools/ab/weld_u_ab.py, profiles/r04/r04b/weld_u_ab.jsonl).
+    // a contiguous eighth of the batch.  The A/B (profiles/r04/r04b/
+    // weld_u_ab.jsonl) ran the new shape in one fixed order: 0.4218 ms for 1M
+    // welds against 0.4680 with one weld per wave and 0.4505 for round 3's
+    // launch (0.796 / 0.717 / 0.745 of 8 TB/s).  What ships keeps the
+    // batch-keyed alternating order above; that exact launch, in place, back
+    // to back, measured 0.799-0.801 of 8 TB/s (0.791-0.795 after a read-only
+    // scrub) in tools/rows_bench.py (profiles/r04/r04u, r04e).
     constexpr int kWeldU = 2;
     unsigned lds = 0;
     rc = occupancy_lds(reinterpret_cast<const void *>(k_weld<true, kWeldU>), kWeldResidentBlocks, lds);

@@ -599,7 +599,8 @@ __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *
   // the cone test first: after the row window's, it costs kContainsHi 6
   // VGPRs, 70 -> 76)
   const uint64_t care_col = wanted[lane] | unwanted[lane];
-  if (cone_max && cone_max <= 32u && !fin && 2 * gens < cone_max && cone_fits(care_col, gens, cone_max)) {
+  // (2 gens in 64 bits: in 32 it wraps for gens >= 2^31)
+  if (cone_max && cone_max <= 32u && !fin && 2ull * gens < cone_max && cone_fits(care_col, gens, cone_max)) {
     if constexpr (ASM == kContainsLo) {
       uint32_t cxs, cK;
       cone_window(care_col, gens, cxs, cK);  // cK <= cone_max (cone_fits)

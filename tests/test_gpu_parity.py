@@ -675,6 +675,53 @@ def test_stable_passes_next_node_changed_lines(hip, port):
             assert (h == want).all() and (flags == wfl).all()
 
 
+def test_stable_sync_clears_unknown_without_reference_change(hip, port):
+    """SynchroniseStateKnown (LifeStable.hpp:526-556) clears `unknown` where
+    live2 and live3 are both ruled out (the cell becomes known-off), but the
+    reference's `changes` mask does not include those cells, so its flag says
+    "no change".  The kernel's changed-line stores must still write the
+    line: one such unknown cell per LifeStable, everything else
+    already synchronised, at every column of the board."""
+    n = 64 * 3
+    x = np.zeros((n, 10, 64), np.uint64)
+    x[:, 2] = x[:, 3] = ~np.uint64(0)  # live2 = live3 = 1 everywhere: known-off cells settled
+    for u in range(n):
+        c, r = u % 64, (7 * u) % 64
+        x[u, 1, c] = np.uint64(1) << np.uint64(r)
+    x = x.reshape(n, 640)
+    want, wfl = port.stable_pass(x, 0)
+    assert not want.reshape(n, 10, 64)[:, 1].any()  # the reference clears every unknown bit
+    assert (wfl == 1).all()  # ... and reports no change
+    for name in ("sync", "step", "propagate", "stabilise"):
+        if name not in hip.STABLE_PASSES:
+            continue
+        w = hip.STABLE_PASSES.index(name)
+        want, wfl = port.stable_pass(x, w)
+        d = to_dev(x).reshape(n, 640)
+        fl = hip.stable_pass(d, name).cpu().numpy()
+        assert (d.cpu().numpy().view(np.uint64) == want).all(), name
+        assert (fl == wfl).all(), name
+
+
+def test_stable_options_then_sync_on_device(hip, port):
+    """The sequence ADVICE r04 named: UpdateOptions then SynchroniseStateKnown,
+    both on the device in place, on _stable_cases with fresh options (the
+    sync clears unknown bits the options pass ruled live2 and live3 out of),
+    then PropagateStep on the result; planes and flags against the oracle
+    after every pass."""
+    n = 2000
+    x = _stable_cases(port, n, seed=33)
+    d = to_dev(x).reshape(n, 640)
+    cur = x
+    for name in ("options", "sync", "step", "options", "sync"):
+        w = hip.STABLE_PASSES.index(name)
+        want, wfl = port.stable_pass(cur, w)
+        fl = hip.stable_pass(d, name).cpu().numpy()
+        assert (d.cpu().numpy().view(np.uint64) == want).all(), name
+        assert (fl == wfl).all(), name
+        cur = want
+
+
 @pytest.mark.parametrize("density", [0.2, 0.5, 0.8])
 def test_stable_step_and_propagate_dense_counts(hip, port, density):
     """PropagateStep counts the state once and derives NeighbourCount(state |
