@@ -264,6 +264,45 @@ def scrubbed_ms(rt, fn, a, b, scrub, reps=10, warm=3):
     return float(np.median(ms)), ms
 
 
+def hbm_only_ms(rt, fn, a, b, scrub, reps=10, warm=3):
+    """The launch's HBM-only time, deferred write-backs included
+    (tools/writeback_ab.py's method): a launch timed alone
+    after a scrub reads from HBM, but can leave up to 256 MiB of its writes
+    dirty in the memory-side Infinity Cache, written back after its end
+    event.  Per rep: scrub; a scrub timed after that scrub (nothing dirty:
+    `clean`); the launch timed (`launch`); the next scrub timed (`after`: it
+    evicts what the launch left dirty, so it pays those write-backs).
+    inclusive = launch + after - clean.  Returns medians
+    {"launch_ms", "inclusive_ms", "scrub_clean_ms", "scrub_after_ms"}."""
+    bufs = [a, b]
+    launch, after, clean = [], [], []
+
+    def timed(f):
+        e0, e1 = rt.event(), rt.event()
+        e0.record(rt.stream)
+        f()
+        e1.record(rt.stream)
+        return e0, e1
+
+    for k in range(warm + reps):
+        x, y = bufs[k % 2], bufs[1 - k % 2]
+        scrub()
+        s = timed(scrub)
+        ln = timed(lambda: fn(x, y))
+        af = timed(scrub)
+        af[1].synchronize()
+        if k >= warm:
+            clean.append(s[0].elapsed_time(s[1]))
+            launch.append(ln[0].elapsed_time(ln[1]))
+            after.append(af[0].elapsed_time(af[1]))
+    lm, am, cm = (float(np.median(v)) for v in (launch, after, clean))
+    return {"launch_ms": lm, "inclusive_ms": lm + max(am - cm, 0.0), "scrub_clean_ms": cm, "scrub_after_ms": am}
+
+
+HBM_ONLY_METHOD = ("HBM only, deferred write-backs included: per rep a 768 MiB read scrub, a timed scrub (clean), "
+                   "the timed launch, a timed scrub (after); launch + after - clean, medians of 10")
+
+
 def side_fn(rt, gens, neutral):
     """A side launch of the shipped streaming kernel's code through the
     tuning build (tools/tune step_order, kernel k_step_ab: the same code as
@@ -313,10 +352,11 @@ def stream_figures(hip, rt, a, b, gens, reps=20):
     for key, g, neu in (("neutral_ms", gens, True), ("copy_ms", 0, False), ("copy_neutral_ms", 0, True)):
         fn = side_fn(rt, g, neu)
         out[key] = back_to_back_ms(rt, fn, a, b, reps) if fn is not None else None
-    # the shipped launch itself with a scrub before each launch: HBM only
+    # the shipped launch itself with a scrub before each launch, and the
+    # write-backs it leaves behind: HBM only
     scrub = Scrub(rt) if rt.kind == "hip" else (lambda: None)
-    out["scrubbed_ms"], _ = scrubbed_ms(rt, lambda x, y: hip.step(x, out=y, generations=gens, stream=rt.stream),
-                                        a, b, scrub)
+    h = hbm_only_ms(rt, lambda x, y: hip.step(x, out=y, generations=gens, stream=rt.stream), a, b, scrub)
+    out["scrubbed_ms"], out["hbm_only_ms"] = h["launch_ms"], h["inclusive_ms"]
     del scrub
     out["bytes"] = n * BYTES_PER_UNIVERSE_GEN
     return out
@@ -508,14 +548,18 @@ def expected_digests(cfg: int, seed: int, gens: int, world: int, n_rank: int, n_
     return [None] * world, None, None
 
 
+def _golden(key: str, field: str):
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "golden.json")) as f:
+            return json.load(f)["digests"][key][field]
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def golden_digest(key: str):
     """the reference-generated output digest of a full-size config
     (tests/golden/golden.json, tests/golden/make_golden.py via oracle/_ref)"""
-    try:
-        with open(os.path.join(ROOT, "tests", "golden", "golden.json")) as f:
-            return json.load(f)["digests"][key]["output_digest"]
-    except (OSError, ValueError, KeyError):
-        return None
+    return _golden(key, "output_digest")
 
 
 def _i64(u: int) -> int:
@@ -525,7 +569,7 @@ def _i64(u: int) -> int:
 def all_gather_ints(vals, world):
     """All-gather a short list of int64 bit patterns from every rank (rank order)."""
     t = torch.tensor([_i64(v) for v in vals], dtype=torch.int64, device=COLL_DEV)
-    if world == 1:
+    if not dist.is_initialized():
         return [[int(x) % (1 << 64) for x in t.tolist()]]
     parts = [torch.empty_like(t) for _ in range(world)]
     dist.all_gather(parts, t)
@@ -660,11 +704,10 @@ def secondary_config4_1gpu(hip, rt, steps=20, warm=20):
             "verified": digest == golden_digest("config4"),
             "roofline": {"bound": "hbm", "achieved": gb(b2b), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": gb(b2b) / HBM_PEAK_GBS,
-                         "cache_neutral": {"achieved": gb(figs["scrubbed_ms"]),
-                                           "frac": gb(figs["scrubbed_ms"]) / HBM_PEAK_GBS,
-                                           "kernel_ms": figs["scrubbed_ms"],
-                                           "method": "the shipped launch after a 768 MiB scrub, events "
-                                                     "around the launch only, median of 10"},
+                         "hbm_only": {"achieved": gb(figs["hbm_only_ms"]),
+                                      "frac": gb(figs["hbm_only_ms"]) / HBM_PEAK_GBS,
+                                      "kernel_ms": figs["hbm_only_ms"], "launch_ms": figs["scrubbed_ms"],
+                                      "method": HBM_ONLY_METHOD},
                          "fixed_order_nt_back_to_back": {"achieved": gb(figs["neutral_ms"]),
                                                          "kernel_ms": figs["neutral_ms"]},
                          "copy_same_shape_GBps": gb(figs["copy_ms"]),
@@ -787,11 +830,17 @@ def secondary_config5(hip, rt):
     # timed as the timed region is: launches back to back between one pair of events
     b2b = back_to_back_ms(rt, fn, planes, out)
     scrub = Scrub(rt)
-    scr, _ = scrubbed_ms(rt, fn, planes, out, scrub)
+    h = hbm_only_ms(rt, fn, planes, out, scrub)
     del scrub
     gb = lambda t: n * 7168 / (t / 1e3) / 1e9  # noqa: E731
+    digest = f"{batch_digest(hip.hashes(out.reshape(n * 3, 64), stream=rt.stream).cpu().numpy()):016x}"
+    want = _golden("config5", "output_digest")
     return {"workload": "config5: 256K universes, unknown_step_refined (11 planes in, 3 out)",
             "value": n / (b2b / 1e3), "unit": "universe-steps/s", "kernel_ms": b2b,
+            "output_digest": digest, "output_digest_expected": want,
+            "verified": (digest == want) if want else None,
+            "verified_against": "tests/golden/golden.json digests.config5 (the reference's "
+                                "unknown_step_refined.hpp fragment in its harness, via oracle/_ref)",
             "kernel_ms_single_launch_median": one, "kernel_ms_single_all": ms,
             "timing": "kernel_ms: 5 warm, then 3 runs of 20 launches back to back between one pair of events, "
                       "median (the timed region's method); single: one launch between events, median of 10",
@@ -799,9 +848,70 @@ def secondary_config5(hip, rt):
                          "unit": "GB/s", "frac": gb(b2b) / HBM_PEAK_GBS,
                          "algorithmic_bytes_per_universe": 7168,
                          "single_launch_frac": gb(one) / HBM_PEAK_GBS,
-                         "cache_neutral": {"achieved": gb(scr), "frac": gb(scr) / HBM_PEAK_GBS, "kernel_ms": scr,
-                                           "method": "one launch after a 768 MiB scrub, events around the "
-                                                     "launch only, median of 10"}}}
+                         "hbm_only": {"achieved": gb(h["inclusive_ms"]), "frac": gb(h["inclusive_ms"]) / HBM_PEAK_GBS,
+                                      "kernel_ms": h["inclusive_ms"], "launch_ms": h["launch_ms"],
+                                      "method": HBM_ONLY_METHOD}}}
+
+
+# ----------------------------------------------------------------------------
+# the printed line: compact, with a flat summary of the side measurements last
+# ----------------------------------------------------------------------------
+def compact_line(line: dict) -> dict:
+    """The printed line: the full one (written to the detail file) without
+    the per-launch series (lists longer than 8) and the long prose (strings
+    longer than 160 characters) below the top level."""
+    def walk(v, depth):
+        if isinstance(v, dict):
+            return {k: walk(x, depth + 1) for k, x in v.items()
+                    if not (depth > 0 and ((isinstance(x, list) and len(x) > 8)
+                                           or (isinstance(x, str) and len(x) > 160)))}
+        if isinstance(v, list):
+            return [walk(x, depth + 1) for x in v]
+        return v
+    return walk(line, 0)
+
+
+def _get(d, *keys):
+    for k in keys:
+        if not isinstance(d, dict) or d.get(k) is None:
+            return None
+        d = d[k]
+    return d
+
+
+def _r(x, nd=4):
+    return round(x, nd) if isinstance(x, float) else x
+
+
+def secondary_summary(line: dict, sec: dict | None, cpu: dict | None) -> dict:
+    """One flat dict of the figures a reader checks first: ms, roofline
+    fraction and reference check of every config and of the search filter."""
+    s = {"c2_kernel_ms": _r(line["kernel_ms_avg"]), "c2_frac": _r(_get(line, "roofline", "frac")),
+         "c2_frac_hbm_only": _r(_get(line, "roofline", "hbm_only", "frac")),
+         "c2_verified": _get(line, "verified", "ok")}
+    c1 = _get(cpu, "config1")
+    if c1:
+        s.update(c1_facade_ns_per_gen=c1.get("facade_ns_per_gen"), c1_reference_ns_per_gen=c1.get("reference_ns_per_gen"),
+                 c1_bit_exact=c1.get("bit_exact"), c1_pop_final=c1.get("pop_final"))
+    if sec:
+        c3, c4, c5, flt = (sec.get(k) for k in ("config3", "config4", "config5", "filter"))
+        if c3:
+            s.update(c3_kernel_ms=_r(c3["kernel_ms"]), c3_frac_valu=_r(_get(c3, "roofline", "frac")),
+                     c3_verified=c3["verified"], c3_search_ms=_r(_get(c3, "search_loop", "kernel_ms")),
+                     c3_search_verified=_get(c3, "search_loop", "verified"))
+        if c4:
+            s.update(c4_1gpu_kernel_ms=_r(c4["kernel_ms"]), c4_1gpu_frac=_r(_get(c4, "roofline", "frac")),
+                     c4_1gpu_frac_hbm_only=_r(_get(c4, "roofline", "hbm_only", "frac")),
+                     c4_1gpu_verified=c4["verified"])
+        if c5:
+            s.update(c5_kernel_ms=_r(c5["kernel_ms"]), c5_frac=_r(_get(c5, "roofline", "frac")),
+                     c5_frac_hbm_only=_r(_get(c5, "roofline", "hbm_only", "frac")), c5_verified=c5.get("verified"))
+        for name, row in ((flt or {}).get("targets") or {}).items():
+            for op in ("filter_1gen", "contains"):
+                s[f"{op}_{name}_ms"] = _r(_get(row, op, "kernel_ms"), 5)
+                s[f"{op}_{name}_frac"] = _r(_get(row, op, "roofline", "frac"))
+            s[f"filter_{name}_verified"] = row.get("verified")
+    return s
 
 
 # ----------------------------------------------------------------------------
@@ -820,7 +930,11 @@ def main(argv=None):
     hip, rt = load_kernels(backend, local, world)
     global COLL_DEV
     COLL_DEV = rt.device if backend == "nccl" else torch.device("cpu")
-    if world > 1:
+    # a process group whenever a launcher started this rank (torch.distributed.run
+    # sets WORLD_SIZE and MASTER_PORT), so one rank under the launcher runs the
+    # collective path of the N > 1 lines, RCCL included
+    dist_on = world > 1 or ("WORLD_SIZE" in os.environ and "MASTER_PORT" in os.environ)
+    if dist_on:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=rt.device)
         else:
@@ -860,17 +974,17 @@ def main(argv=None):
     rt.sync()
 
     # timed region: barrier + sync on both sides, max over ranks
-    if world > 1:
+    if dist_on:
         dist.barrier()
     rt.sync()
     t0 = time.perf_counter()
     evs, cur = timed_launches(hip, rt, bufs, args.steps, gens)
     rt.sync()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     span_ms = evs[0].elapsed_time(evs[1])   # GPU time of the K launches on their stream
-    if world > 1:
+    if dist_on:
         t = torch.tensor([elapsed], dtype=torch.float64, device=COLL_DEV)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -888,9 +1002,9 @@ def main(argv=None):
     # side figures on the rank's own buffers (after the hashes: they overwrite
     # both): cache-neutral step and live copy ceilings, gathered per rank
     figs = stream_figures(hip, rt, final, bufs[1 - cur], gens) if gens <= 2 else None
-    fig_keys = ("scrubbed_ms", "copy_ms", "copy_neutral_ms", "neutral_ms")
+    fig_keys = ("scrubbed_ms", "copy_ms", "copy_neutral_ms", "neutral_ms", "hbm_only_ms")
     fv = [(-1.0 if figs is None or figs[k] is None else figs[k]) for k in fig_keys]
-    if world > 1:
+    if dist_on:
         ft = torch.tensor(fv, dtype=torch.float64, device=COLL_DEV)
         fparts = [torch.empty_like(ft) for _ in range(world)]
         dist.all_gather(fparts, ft)
@@ -898,7 +1012,7 @@ def main(argv=None):
     else:
         rank_figs = [[(None if x < 0 else x) for x in fv]]
     collect = None
-    if world > 1:
+    if dist_on:
         dist.barrier()
         c0 = time.perf_counter()
         gathered = gather_hashes(h.to(COLL_DEV), world, [c for _, c in shards])
@@ -927,7 +1041,7 @@ def main(argv=None):
         cpu = cpu_baseline(x_cpu, args.cpu_seconds)
         cpu["config1"] = cpu_baseline_config1()
 
-    if world > 1:
+    if dist_on:
         dist.barrier()
     if rank == 0:
         total = n_total * gens * args.steps
@@ -944,13 +1058,17 @@ def main(argv=None):
         def copy_gbps(ms, c):
             return c * BYTES_PER_UNIVERSE_GEN / (ms / 1e3) / 1e9 if ms else None
 
-        neu = [gbps(f[0], c) for f, (_, c) in zip(rank_figs, per_rank)]
+        def frac(gb, peak=HBM_PEAK_GBS):
+            return gb / peak if gb else None
+
+        after_scrub = [gbps(f[0], c) for f, (_, c) in zip(rank_figs, per_rank)]
+        hbm = [gbps(f[4], c) for f, (_, c) in zip(rank_figs, per_rank)]
         cpy = [copy_gbps(f[1], c) for f, (_, c) in zip(rank_figs, per_rank)]
         cpy_neu = [copy_gbps(f[2], c) for f, (_, c) in zip(rank_figs, per_rank)]
         fixed = [gbps(f[3], c) for f, (_, c) in zip(rank_figs, per_rank)]
-        agg_neu = sum(neu) if all(v is not None for v in neu) else None
-        val_neu = (sum(c * gens / (f[0] / 1e3) for f, (_, c) in zip(rank_figs, per_rank))
-                   if all(f[0] for f in rank_figs) else None)
+        agg_hbm = sum(hbm) if all(v is not None for v in hbm) else None
+        val_hbm = (sum(c * gens / (f[4] / 1e3) for f, (_, c) in zip(rank_figs, per_rank))
+                   if all(f[4] for f in rank_figs) else None)
         line = {
             "metric": METRIC, "value": value, "unit": "universe-gen/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
@@ -968,63 +1086,48 @@ def main(argv=None):
             "kernel_timing": "HIP events on the launch stream around the K timed launches / K",
             "per_rank": [{"rank": r, "universes": c, "kernel_ms_avg": ms,
                           "GBps": c * gens * BYTES_PER_UNIVERSE_GEN / (ms / 1e3) / 1e9 if gens == 1 else None,
-                          "kernel_ms_cache_neutral": rank_figs[r][0], "GBps_cache_neutral": neu[r],
+                          "kernel_ms_hbm_only": rank_figs[r][4], "GBps_hbm_only": hbm[r],
+                          "GBps_launch_after_scrub": after_scrub[r],
                           "GBps_fixed_order_nt_back_to_back": fixed[r],
                           "copy_GBps": cpy[r], "copy_GBps_cache_neutral": cpy_neu[r]}
                          for r, (ms, c) in enumerate(per_rank)],
-            "value_cache_neutral": val_neu,
-            "value_cache_neutral_note": ("universe-gen/s if every rank ran its shard at its cache-neutral rate "
-                                         "(the shipped launch timed alone after a 768 MiB scrub of the "
-                                         "Infinity Cache, per rank after the timed region): the 8-vs-1 ratio "
-                                         "without Infinity Cache reuse on either side"),
+            "value_hbm_only": val_hbm,
+            "value_hbm_only_note": ("universe-gen/s if every rank ran its shard at its HBM-only rate (the shipped "
+                                    "launch after a 768 MiB scrub plus the write-backs it defers past its end event; "
+                                    "per rank, after the timed region): the 8-vs-1 ratio without cache reuse"),
             "collective_world_size": coll_world,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-                         "frac_kind": ("effective: algorithmic bytes / launch time; with the batch-keyed "
-                                       "launch order and the plain-stored tail part of each launch's reads are "
-                                       "served by the 256 MB memory-side Infinity Cache (DESIGN.md 3.1, 5.2); "
-                                       "cache_neutral reads from HBM alone (its last writes may still be in the cache at its end event: "
-                                       "DESIGN.md 5.2 counts those write-backs)"
+                         "frac": frac(achieved),
+                         "frac_kind": ("effective: algorithmic bytes / launch time, back-to-back launches; part of "
+                                       "each launch's reads is served by the 256 MB Infinity Cache (DESIGN.md 3.1)"
                                        if n <= (1 << 22) else
-                                       "effective: algorithmic bytes / launch time; above 4M universes per "
-                                       "GPU the launch takes one order with every store nontemporal "
-                                       "(nothing is arranged for Infinity Cache reuse); cache_neutral reads from "
-                                       "HBM alone"),
-                         "cache_neutral": ({"achieved": neu[0], "frac": neu[0] / HBM_PEAK_GBS,
-                                            "kernel_ms": rank_figs[0][0],
-                                            "method": "the shipped launch (lifeapi_step_batch_dev), same size, "
-                                                      "same process, rank 0, with a 768 MiB scrub (a read "
-                                                      "of an unrelated buffer) on the stream before each "
-                                                      "launch and events around the launch only: 3 warm, 10 "
-                                                      "timed ping-pong launches, median"}
-                                           if neu[0] else None),
-                         "fixed_order_nt_back_to_back": ({"achieved": fixed[0], "frac": fixed[0] / HBM_PEAK_GBS,
-                                                          "kernel_ms": rank_figs[0][3],
-                                                          "method": "round 3's cache-neutral form: the step "
-                                                                    "kernel's code (k_step_ab) in one fixed order, "
-                                                                    "every store nontemporal, 20 launches back to "
-                                                                    "back, median of 3 runs"}
-                                                         if fixed[0] else None),
-                         "cache_gain": (achieved / neu[0] - 1) if (achieved and neu[0]) else None,
+                                       "effective: algorithmic bytes / launch time, back-to-back launches; one "
+                                       "order, every store nontemporal (no Infinity Cache reuse arranged)"),
+                         "hbm_only": ({"achieved": hbm[0], "frac": frac(hbm[0]), "kernel_ms": rank_figs[0][4],
+                                       "launch_ms": rank_figs[0][0], "method": HBM_ONLY_METHOD}
+                                      if hbm[0] else None),
+                         "launch_after_scrub": ({"achieved": after_scrub[0], "frac": frac(after_scrub[0]),
+                                                 "kernel_ms": rank_figs[0][0],
+                                                 "note": "reads from HBM alone, but up to 256 MiB of its writes "
+                                                         "can still sit in the Infinity Cache at its end event"}
+                                                if after_scrub[0] else None),
+                         "fixed_order_nt_back_to_back": ({"achieved": fixed[0], "frac": frac(fixed[0]),
+                                                          "kernel_ms": rank_figs[0][3]} if fixed[0] else None),
+                         "cache_gain": (achieved / hbm[0] - 1) if (achieved and hbm[0]) else None,
                          "traffic": traffic, "traffic_source": tsrc,
-                         "traffic_note": "FETCH_SIZE/WRITE_SIZE count L2-to-fabric bytes, so reads the "
-                                         "memory-side Infinity Cache serves (the alternating launch order, "
-                                         "DESIGN.md 3.1) count as HBM bytes; achieved is algorithmic bytes / time",
+                         "traffic_note": "FETCH_SIZE x 2 + WRITE_SIZE (MI355X_MICROARCH.md); L2-to-fabric bytes, "
+                                         "so Infinity Cache hits count as HBM bytes",
                          "algorithmic_bytes_per_launch": bpl,
                          "aggregate_GBps": agg,
                          "aggregate_frac": (agg / (world * HBM_PEAK_GBS)) if agg else None,
-                         "aggregate_GBps_cache_neutral": agg_neu,
-                         "aggregate_frac_cache_neutral": (agg_neu / (world * HBM_PEAK_GBS)) if agg_neu else None,
+                         "aggregate_GBps_hbm_only": agg_hbm,
+                         "aggregate_frac_hbm_only": (agg_hbm / (world * HBM_PEAK_GBS)) if agg_hbm else None,
                          "read_only_GBps": achieved / 2 if achieved else None,
                          "copy_ceiling_GBps": cpy[0],
-                         "copy_ceiling_source": "live, rank 0: the step kernel's code with 0 generations (a copy "
-                                                "with the step's exact loads, stores, store policy and order), "
-                                                "5 warm ping-pong launches, then 3 runs of 20 back to back, "
-                                                "median (bench.py side_fn, kernel k_step_ab)",
+                         "copy_ceiling_source": "live, rank 0: the step kernel's code with 0 generations, same "
+                                                "store policy and order (bench.py side_fn, k_step_ab)",
                          "frac_of_copy_ceiling": (achieved / cpy[0]) if (achieved and cpy[0]) else None,
                          "copy_ceiling_cache_neutral_GBps": cpy_neu[0],
-                         "frac_of_copy_ceiling_cache_neutral": (neu[0] / cpy_neu[0])
-                         if (neu[0] and cpy_neu[0]) else None,
                          "copy_ceiling_recorded_GBps": ceiling, "copy_ceiling_recorded_source": ceiling_src},
             "cpu_baseline": cpu,
             "verified": verified,
@@ -1033,8 +1136,19 @@ def main(argv=None):
         }
         if rt.kind != "hip":
             line["kernel_backend"] = f"STUB {rt.kind} (CPU rank rehearsal, not a measurement)"
+        detail = os.environ.get("LIFEAPI_BENCH_DETAIL", os.path.join(ROOT, "gpurun_out", "bench_detail.json"))
+        try:
+            os.makedirs(os.path.dirname(detail), exist_ok=True)
+            with open(detail, "w") as f:
+                json.dump(line, f, indent=1)
+        except OSError as e:
+            detail = f"not written: {e}"
+        line = compact_line(line)
+        line["detail_file"] = os.path.relpath(detail, ROOT) if os.path.isabs(detail) else detail
+        # last, so the driver's 2000-character tail of stdout holds it whole
+        line["secondary_summary"] = secondary_summary(line, secondary, cpu)
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

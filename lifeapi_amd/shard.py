@@ -28,8 +28,10 @@ def gather_hashes(h: torch.Tensor, world: int, counts: list[int] | None = None) 
 
     Equal shard sizes use one all_gather_into_tensor; ragged shards (strong
     scaling with n_total % world != 0) pad to the largest shard and trim.
+    With a process group the collective runs at every world size (one rank
+    under the launcher included); without one, world 1 returns `h`.
     """
-    if world == 1:
+    if world == 1 and not dist.is_initialized():
         return h
     n = h.numel()
     if counts is None:

@@ -264,7 +264,29 @@ def filter_digests() -> dict:
     return out
 
 
+def config5_digest() -> dict:
+    """Config 5 at bench size: 256K universes of 11 planes (the seed-6
+    splitmix64 fill of 256K x 11 universes, bench.py secondary_config5)
+    through the reference's unknown_step_refined.hpp fragment in the
+    harness (ref_shim.cpp); batch digest of the 3 output planes taken as
+    3 x 256K consecutive 64-word blocks"""
+    n = 1 << 18
+    xin = P.fill(n * 11, seed=6).reshape(n, 11 * 64)
+    out = R.refined_step(xin)
+    return {"universes": n, "seed": 6, "planes_in": 11, "planes_out": 3,
+            "output_digest": f"{P.digest(P.hashes(out.reshape(n * 3, 64))):016x}"}
+
+
 def main():
+    if "--only-config5" in sys.argv:  # add / refresh digests.config5 alone
+        path = os.path.join(HERE, "golden.json")
+        with open(path) as f:
+            meta = json.load(f)
+        meta["digests"]["config5"] = config5_digest()
+        with open(path, "w") as f:
+            json.dump(meta, f, indent=1)
+        print(json.dumps(meta["digests"]["config5"], indent=1))
+        return
     if "--only-filter" in sys.argv:  # add / refresh digests.config2_filter alone
         path = os.path.join(HERE, "golden.json")
         with open(path) as f:
@@ -387,6 +409,7 @@ def main():
 
     meta["digests"] = batch_digests()
     meta["digests"]["config2_filter"] = filter_digests()
+    meta["digests"]["config5"] = config5_digest()
     with open(os.path.join(HERE, "golden.json"), "w") as f:
         json.dump(meta, f, indent=1)
     print(json.dumps(meta["digests"], indent=1))

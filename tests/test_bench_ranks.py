@@ -54,15 +54,15 @@ def test_bench_gpus2_strong_config4_spawns_two_ranks():
     assert "config4_small" in v["against"]
     assert line["value"] > 0 and line["ms_per_step"] > 0
     assert "STUB" in line["kernel_backend"]
-    # per rank: the shipped figure and the cache-neutral one (same kernel,
-    # fixed order, all stores nontemporal), and live copy ceilings
+    # per rank: the shipped figure, the HBM-only one (the launch after a scrub
+    # plus its deferred write-backs), and live copy ceilings
     for p in line["per_rank"]:
-        assert p["GBps"] > 0 and p["GBps_cache_neutral"] > 0
-        assert p["kernel_ms_cache_neutral"] > 0 and p["copy_GBps"] > 0 and p["copy_GBps_cache_neutral"] > 0
+        assert p["GBps"] > 0 and p["GBps_hbm_only"] > 0 and p["GBps_launch_after_scrub"] > 0
+        assert p["kernel_ms_hbm_only"] > 0 and p["copy_GBps"] > 0 and p["copy_GBps_cache_neutral"] > 0
     r = line["roofline"]
-    assert r["aggregate_GBps_cache_neutral"] > 0 and r["cache_neutral"]["achieved"] > 0
+    assert r["aggregate_GBps_hbm_only"] > 0 and r["hbm_only"]["achieved"] > 0
     assert r["frac_kind"].startswith("effective") and r["copy_ceiling_GBps"] > 0
-    assert line["value_cache_neutral"] > 0
+    assert line["value_hbm_only"] > 0
     # result collection: 1 warmup launch + (warmup-1) + steps generations in all
     c = line["collect"]
     assert c["universes_gathered"] == 1 << 14
@@ -83,8 +83,8 @@ def test_bench_gpus8_strong_config4_rehearsal():
     v = line["verified"]
     assert v["ok"] is True and v["per_rank_ok"] == [True] * 8 and v["global_ok"] is True
     assert "config4_small" in v["against"]
-    assert line["value"] > 0 and line["value_cache_neutral"] > 0
-    assert all(p["GBps_cache_neutral"] > 0 for p in line["per_rank"])
+    assert line["value"] > 0 and line["value_hbm_only"] > 0
+    assert all(p["GBps_hbm_only"] > 0 for p in line["per_rank"])
     c = line["collect"]
     assert c["universes_gathered"] == 1 << 14
     assert c["final_digest"] == _expected_collect(1 << 14, 4, 1 + 0 + 2)
@@ -113,8 +113,8 @@ def test_bench_gpus4_ragged_strong_split():
     P = Port()
     x = P.fill((1 << 14) + 4, seed=4)
     assert line["verified"]["global_digest"] == f"{batch_digest(P.hashes(P.step_batch(x, 1)).view(np.int64)):016x}"
-    assert len(line["per_rank"]) == 4 and all(p["GBps_cache_neutral"] > 0 for p in line["per_rank"])
-    assert line["roofline"]["aggregate_GBps_cache_neutral"] > 0
+    assert len(line["per_rank"]) == 4 and all(p["GBps_hbm_only"] > 0 for p in line["per_rank"])
+    assert line["roofline"]["aggregate_GBps_hbm_only"] > 0
     assert line["collect"]["final_digest"] == _expected_collect((1 << 14) + 4, 4, 2)
 
 
@@ -133,3 +133,54 @@ def test_bench_refuses_stub_marking(cfg):
     line, _ = _bench("--gpus", "1", "--config", cfg, "--universes", str(1 << 11 if cfg == "2" else 1 << 14),
                      "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-secondary")
     assert "STUB" in line["kernel_backend"]
+
+
+def test_bench_one_rank_under_launcher_takes_the_collective_path():
+    """One rank started by torch.distributed.run (WORLD_SIZE=1, MASTER_PORT set)
+    opens a process group and runs the N > 1 lines' collective code: barrier,
+    MAX of the timed region, the digest all-gather and the hash all-gather
+    (tests/test_rccl.py runs the same with the nccl backend on the GPU)."""
+    env = dict(os.environ, LIFEAPI_BENCH_BACKEND="gloo", HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="",
+               OMP_NUM_THREADS="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT", "MASTER_ADDR"):
+        env.pop(k, None)
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+                        "--master-addr=127.0.0.1", f"--master-port={port}",
+                        os.path.join(ROOT, "tests", "bench_rank_runner.py"), "--gpus", "1", "--config", "4",
+                        "--universes", str(1 << 14), "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
+                        "--no-secondary"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-4000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert line["n_gpus"] == 1 and line["collective_world_size"] == 1
+    assert line["verified"]["ok"] is True
+    c = line["collect"]
+    assert c["universes_gathered"] == 1 << 14 and "gloo" in c["op"]
+    assert c["final_digest"] == _expected_collect(1 << 14, 4, 1 + 0 + 2)
+
+
+def test_bench_line_is_compact_with_summary_last():
+    """The printed line leaves the per-launch series and long prose to the
+    detail file, and ends with the flat secondary_summary, so a 2000-character
+    tail of stdout holds the summary whole."""
+    import bench
+    sec = {"config3": {"kernel_ms": 1.3, "kernel_ms_all": [1.3] * 20, "verified": True,
+                       "roofline": {"frac": 0.66, "definition": "x" * 300},
+                       "search_loop": {"kernel_ms": 1.4, "verified": True, "kernel_ms_all": [1.4] * 20}},
+           "config5": {"kernel_ms": 0.3, "verified": True, "roofline": {"frac": 0.8, "hbm_only": {"frac": 0.7}}},
+           "filter": {"targets": {"block": {"verified": True, "filter_1gen": {"kernel_ms": 0.01,
+                                                                              "roofline": {"frac": 0.5}},
+                                            "contains": {"kernel_ms": 0.01, "roofline": {"frac": 0.6}}}}}}
+    line = {"metric": "m", "value": 1.0, "kernel_ms_avg": 0.16, "roofline": {"frac": 0.85, "hbm_only": {"frac": 0.7}},
+            "verified": {"ok": True}, "secondary": sec}
+    out = bench.compact_line(line)
+    assert "kernel_ms_all" not in out["secondary"]["config3"]
+    assert "definition" not in out["secondary"]["config3"]["roofline"]
+    out["secondary_summary"] = bench.secondary_summary(out, sec, {"config1": {"facade_ns_per_gen": 31.0}})
+    s = out["secondary_summary"]
+    assert s["c3_kernel_ms"] == 1.3 and s["c3_verified"] is True and s["c3_search_verified"] is True
+    assert s["c5_verified"] is True and s["c2_frac_hbm_only"] == 0.7 and s["filter_block_verified"] is True
+    assert list(out)[-1] == "secondary_summary" and len(json.dumps(s)) < 1900
