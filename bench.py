@@ -898,7 +898,8 @@ def secondary_summary(line: dict, sec: dict | None, cpu: dict | None) -> dict:
         if c3:
             s.update(c3_kernel_ms=_r(c3["kernel_ms"]), c3_frac_valu=_r(_get(c3, "roofline", "frac")),
                      c3_verified=c3["verified"], c3_search_ms=_r(_get(c3, "search_loop", "kernel_ms")),
-                     c3_search_verified=_get(c3, "search_loop", "verified"))
+                     c3_search_verified=_get(c3, "search_loop", "verified"),
+                     c3_cpu_universe_gen_per_s=_r(_get(c3, "cpu_baseline", "value"), 1))
         if c4:
             s.update(c4_1gpu_kernel_ms=_r(c4["kernel_ms"]), c4_1gpu_frac=_r(_get(c4, "roofline", "frac")),
                      c4_1gpu_frac_hbm_only=_r(_get(c4, "roofline", "hbm_only", "frac")),
@@ -921,6 +922,11 @@ def main(argv=None):
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus, argv))  # before any GPU call in this process
 
+    # stdout carries the one JSON line alone: everything else a rank prints to
+    # fd 1 (RCCL's version banner, gloo's peer notes, ...) goes to stderr
+    line_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -1143,11 +1149,13 @@ def main(argv=None):
                 json.dump(line, f, indent=1)
         except OSError as e:
             detail = f"not written: {e}"
-        line = compact_line(line)
+        # the side measurements in full stay in the detail file; the flat
+        # summary below carries their figures
+        line = compact_line({k: v for k, v in line.items() if k != "secondary"})
         line["detail_file"] = os.path.relpath(detail, ROOT) if os.path.isabs(detail) else detail
         # last, so the driver's 2000-character tail of stdout holds it whole
         line["secondary_summary"] = secondary_summary(line, secondary, cpu)
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=line_out, flush=True)
     if dist_on:
         dist.destroy_process_group()
 

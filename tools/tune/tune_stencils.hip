@@ -80,6 +80,23 @@ extern "C" {
 int lifeapi_tune_stable_pass(uint64_t *d_planes, uint8_t *d_flags, size_t n, int pass, uint32_t max_iters,
                              int blocks_per_cu, void *stream, int reverse) {
   if (n == 0) return LIFEAPI_OK;
+  if (pass >= 16 && pass <= 21) {  // k_stable_dma<pass - 16>: a grid of blocks_per_cu (0: all resident) per CU
+    if (!d_planes || !d_flags || !aligned8(d_planes)) return fail(LIFEAPI_E_INVALID, "bad argument%s");
+    int cus = 0, rc = device_cus(cus);
+    if (rc != LIFEAPI_OK) return rc;
+    using Fn = void (*)(uint64_t *, uint8_t *, uint64_t, uint32_t, uint32_t);
+    const Fn fns[6] = {k_stable_dma<0>, k_stable_dma<1>, k_stable_dma<2>,
+                       k_stable_dma<3>, k_stable_dma<4>, k_stable_dma<5>};
+    int res = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&res, fns[pass - 16], kBlock, 0);
+    if (e != hipSuccess || res < 1) return fail(LIFEAPI_E_INVALID, "k_stable_dma cannot be resident%s");
+    const int bpc = blocks_per_cu > 0 ? std::min(blocks_per_cu, res) : res;
+    uint64_t grid = std::min<uint64_t>((uint64_t)cus * bpc, (n + kWavesPerBlock - 1) / kWavesPerBlock);
+    grid = (grid + 7) & ~7ull;  // every XCD takes part: the eighths are dealt by blockIdx & 7
+    hipLaunchKernelGGL(fns[pass - 16], dim3((unsigned)grid), dim3(kBlock), 0, (hipStream_t)stream, d_planes,
+                       d_flags, (uint64_t)n, max_iters ? max_iters : 1u << 20, (uint32_t)reverse);
+    return launched("k_stable_dma (tuning) launch");
+  }
   // pass 8 + k: pass k with the prefetching loop (k_stable_pf<k>)
   if (!d_planes || !d_flags || !aligned8(d_planes) || pass < 0 || pass > 13 || (pass > 5 && pass < 8))
     return fail(LIFEAPI_E_INVALID, "bad argument to lifeapi_tune_stable_pass%s");
