@@ -6,6 +6,9 @@ shipped k_stable, same process, 1M LifeStables (--n), three inputs:
   next       rows_bench.stable_next_node: the same propagated, then one
              unknown cell decided (a search's next node; a few columns change);
   random     random planes (every pass changes most lines).
+Forms (nt fetch, waits counted so the stores stay in flight): dma_loop, the
+looping grid; dma_uU, a grid of n / U waves, each a contiguous run of U
+LifeStables; _capC: at most C blocks resident per CU.
 Per (input, pass, form): 4 launches back to back, each on its own fresh copy,
 between one pair of events (/ 4), median of 7; results checked bit for bit
 against the shipped pass (planes and flags).  One JSON line per row."""
@@ -41,7 +44,10 @@ def timed(run, src, works, reps=7):
 
 def main():
     n = int(sys.argv[sys.argv.index("--n") + 1]) if "--n" in sys.argv else 1 << 20
-    caps = [int(c) for c in sys.argv[sys.argv.index("--caps") + 1].split(",")] if "--caps" in sys.argv else [0, 6, 4]
+    # forms: label -> (tuning pass offset, blocks per CU cap, passes it exists for)
+    # forms: label -> (tuning pass offset, blocks per CU cap, LifeStables per wave (0: looping grid), passes)
+    forms = {"dma_loop": (16, 0, 0, range(6)), "dma_u2": (16, 0, 2, range(6)), "dma_u4": (16, 0, 4, range(6)),
+             "dma_u8": (16, 0, 8, range(6)), "dma_u4_cap4": (16, 4, 4, range(6))}
     passes = sys.argv[sys.argv.index("--passes") + 1].split(",") if "--passes" in sys.argv else list(hip.STABLE_PASSES)
     st = stable_inputs(n)
     inputs = {"still": st, "next": stable_next_node(st),
@@ -56,13 +62,15 @@ def main():
             want = chk.clone()
             row = {"input": iname, "pass": pname, "objects": n}
             row["shipped_ms"] = timed(lambda x: hip.stable_pass(x, pname), src, works)
-            for cap in caps:
+            for label, (off, cap, upw, which) in forms.items():
+                if w not in which:
+                    continue
                 chk.copy_(src)
-                f = tune_hip.stable_pass(chk, 16 + w, cap)
+                f = tune_hip.stable_pass(chk, off + w, cap, upw=upw)
                 torch.cuda.synchronize()
                 ok = bool(torch.equal(chk, want)) and bool(torch.equal(f, want_flags))
-                row[f"dma_cap{cap}_ms"] = timed(lambda x: tune_hip.stable_pass(x, 16 + w, cap), src, works)
-                row[f"dma_cap{cap}_exact"] = ok
+                row[f"{label}_ms"] = timed(lambda x: tune_hip.stable_pass(x, off + w, cap, upw=upw), src, works)
+                row[f"{label}_exact"] = ok
             print(json.dumps(row), flush=True)
 
 

@@ -80,20 +80,37 @@ extern "C" {
 int lifeapi_tune_stable_pass(uint64_t *d_planes, uint8_t *d_flags, size_t n, int pass, uint32_t max_iters,
                              int blocks_per_cu, void *stream, int reverse) {
   if (n == 0) return LIFEAPI_OK;
-  if (pass >= 16 && pass <= 21) {  // k_stable_dma<pass - 16>: a grid of blocks_per_cu (0: all resident) per CU
+  // k_stable_dma on a grid of blocks_per_cu (0: all resident) per CU:
+  // 16 + k: pass k, nt fetch, counted waits; 24 + k: plain fetch, counted;
+  // 32 + k: nt fetch, waits for every op (k in {0, 4} for the last two)
+  if (pass >= 16 && pass <= 37) {
     if (!d_planes || !d_flags || !aligned8(d_planes)) return fail(LIFEAPI_E_INVALID, "bad argument%s");
     int cus = 0, rc = device_cus(cus);
     if (rc != LIFEAPI_OK) return rc;
     using Fn = void (*)(uint64_t *, uint8_t *, uint64_t, uint32_t, uint32_t);
-    const Fn fns[6] = {k_stable_dma<0>, k_stable_dma<1>, k_stable_dma<2>,
-                       k_stable_dma<3>, k_stable_dma<4>, k_stable_dma<5>};
+    const Fn fns[22] = {k_stable_dma<0>, k_stable_dma<1>, k_stable_dma<2>, k_stable_dma<3>, k_stable_dma<4>,
+                        k_stable_dma<5>, nullptr, nullptr,
+                        k_stable_dma<0, 0>, nullptr, nullptr, nullptr, k_stable_dma<4, 0>, nullptr, nullptr, nullptr,
+                        k_stable_dma<0, 2, false>, nullptr, nullptr, nullptr, k_stable_dma<4, 2, false>, nullptr};
+    if (!fns[pass - 16]) return fail(LIFEAPI_E_INVALID, "no such k_stable_dma variant%s");
     int res = 0;
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&res, fns[pass - 16], kBlock, 0);
     if (e != hipSuccess || res < 1) return fail(LIFEAPI_E_INVALID, "k_stable_dma cannot be resident%s");
-    const int bpc = blocks_per_cu > 0 ? std::min(blocks_per_cu, res) : res;
-    uint64_t grid = std::min<uint64_t>((uint64_t)cus * bpc, (n + kWavesPerBlock - 1) / kWavesPerBlock);
-    grid = (grid + 7) & ~7ull;  // every XCD takes part: the eighths are dealt by blockIdx & 7
-    hipLaunchKernelGGL(fns[pass - 16], dim3((unsigned)grid), dim3(kBlock), 0, (hipStream_t)stream, d_planes,
+    // reverse >> 8 = U > 0: ceil(n / U) waves of U LifeStables each (blocks_per_cu
+    // then caps the resident blocks by unused LDS), else the looping grid
+    const uint32_t upw = (uint32_t)reverse >> 8;
+    uint64_t grid;
+    unsigned lds = 0;
+    if (upw) {
+      grid = grid_for((n + upw - 1) / upw, cus, 0);
+      if (blocks_per_cu > 0 && (rc = occupancy_lds((const void *)fns[pass - 16], blocks_per_cu, lds)) != LIFEAPI_OK)
+        return rc;
+    } else {
+      const int bpc = blocks_per_cu > 0 ? std::min(blocks_per_cu, res) : res;
+      grid = std::min<uint64_t>((uint64_t)cus * bpc, (n + kWavesPerBlock - 1) / kWavesPerBlock);
+      grid = (grid + 7) & ~7ull;  // every XCD takes part: the eighths are dealt by blockIdx & 7
+    }
+    hipLaunchKernelGGL(fns[pass - 16], dim3((unsigned)grid), dim3(kBlock), lds, (hipStream_t)stream, d_planes,
                        d_flags, (uint64_t)n, max_iters ? max_iters : 1u << 20, (uint32_t)reverse);
     return launched("k_stable_dma (tuning) launch");
   }
