@@ -86,6 +86,19 @@ int lifeapi_stable_pass_batch_dev(uint64_t *d_planes, uint8_t *d_flags, size_t n
   // signal 1.83 -> 1.72, PropagateStep 1.95 -> 1.86, StabiliseOptions
   // 1.79 -> 1.66.
   note_forward_write(d_planes, (uint64_t)n * 10 * 512);
+  if (pass == 2) {
+    // Round 5: SignalNeighbours reads its LifeStable into LDS by five
+    // 16-byte-per-lane global_load_lds and out to VGPRs by ds_read, one
+    // LifeStable per wave, every slot (k_stable_dma, U = 1): 0.78-0.80 ms
+    // against 1.10-1.15 for the 10 dwordx2 loads of k_stable on 1M
+    // LifeStables of all three families (0.82 of 8 TB/s on the 5131 bytes it
+    // moves).  The passes that write back most of their lines lose 1-11 %
+    // with it, so they keep k_stable (tools/stable_dma_ab.py,
+    // profiles/r05/stable_dma_ab.jsonl).
+    hipLaunchKernelGGL(k_stable_dma<2>, dim3(grid_for(n, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream,
+                       d_planes, d_flags, (uint64_t)n, max_iters ? max_iters : 1u << 20, 1u << 8);
+    return launched("k_stable_dma launch");
+  }
   hipLaunchKernelGGL(fns[pass], dim3(grid_for(n, cus, 0)), dim3(kBlock), lds, (hipStream_t)stream,
                      d_planes, d_flags, (uint64_t)n, max_iters ? max_iters : 1u << 20, 2u);
   return launched("k_stable launch");

@@ -247,3 +247,21 @@ def test_cone_shapes(tune, port, upw, rmax):
                 got = tune.cone(d, to_dev(tw[None]), to_dev(tu[None]), gens, upw, rmax).cpu().numpy()
             assert (got.astype(np.uint32) == want).all(), (w, x0, gens, np.nonzero(got != want)[0][:8])
             assert want[0] != 0
+
+
+# k_stable_dma (stable_kernels.hpp) on the tuning build's grids: the looping
+# grid (U = 0: each XCD an eighth, waves striding, the next LifeStable
+# prefetched into LDS), U LifeStables per wave (U = 2, 3: the prefetch within
+# a run), the wide stores (pass offset 32, U = 1) and a resident-block cap.
+# The shipped SignalNeighbours is the U = 1 form (tests/test_gpu_parity.py).
+@pytest.mark.parametrize("off,upw,cap", [(16, 0, 0), (16, 2, 0), (16, 3, 0), (16, 2, 3), (32, 1, 0), (32, 1, 5)])
+@pytest.mark.parametrize("n", [5, 20003])
+def test_stable_dma_forms(tune, hip, port, off, upw, cap, n):
+    from test_gpu_parity import _stable_cases
+    x = _stable_cases(port, n, seed=17 + n % 7)
+    for w, name in enumerate(hip.STABLE_PASSES):
+        want, wfl = port.stable_pass(x, w)
+        d = to_dev(x).reshape(n, 640)
+        fl = tune.stable_pass(d, off + w, cap, upw=upw).cpu().numpy()
+        assert (to_host(d).reshape(n, 640) == want).all(), (name, off, upw, cap)
+        assert (fl == wfl).all(), (name, off, upw, cap)

@@ -3,7 +3,16 @@
 must read and write per object; peak = 8 TB/s (MI355X_MICROARCH.md).  A timing is K launches back to back
 between two events (per launch: / K), median over 7 timings; `scrubbed`: the
 launch alone after a 768 MiB scrub of the Infinity Cache (bench.py Scrub),
-events around the launch only, median of 10 -- the HBM-only figure."""
+events around the launch only, median of 10.
+
+The LifeStable passes write back only the lines they change,
+so their rows are priced on the bytes each pass really moves, measured by
+PMC on the same inputs (profiles/r05/pmc_rows.json, tools/pmc_rows.py:
+FETCH_SIZE x 2 + WRITE_SIZE per LifeStable), and carry the VALU side beside
+it: SQ_INSTS_VALU per LifeStable / (1024 SIMDs x one wave64 instruction per
+2 clocks at 2.4 GHz = 1.2288e12 per second).  `bound_frac` = max(bytes time,
+VALU time) / measured time: how close the pass is to the larger of its two
+bounds."""
 import json
 import os
 import sys
@@ -49,6 +58,21 @@ def scrubbed(fn, prep=None):
     return sorted(ms)[len(ms) // 2]
 
 PEAK = 8000.0  # GB/s
+VALU_PEAK = 1024 * 2.4e9 / 2  # wave64 VALU instructions per second (MI355X_MICROARCH.md: 2 clocks each)
+PMC_ROWS = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "r05",
+                        "pmc_rows.json")
+
+
+def pmc_row(name):
+    """(bytes per object, VALU per object, source) measured for a LifeStable row, or None"""
+    try:
+        with open(PMC_ROWS) as f:
+            r = json.load(f)["rows"].get(name)
+    except (OSError, ValueError, KeyError):
+        return None
+    if not r:
+        return None
+    return r["hbm_bytes_per_object"], r["valu_per_object"], "profiles/r05/pmc_rows.json"
 
 
 K = 10  # launches per timing, back to back (the bench's own way: launch gaps hidden by the queue)
@@ -69,10 +93,21 @@ def timed(fn, reps=7):
     return sorted(ms)[len(ms) // 2]
 
 
-def report(name, n, nbytes, ms, extra=None, scrub_ms=None):
+def report(name, n, nbytes, ms, extra=None, scrub_ms=None, pmc=None):
+    """pmc: (measured bytes per object, VALU per object, source) -- the row
+    is then priced on the measured bytes, with its VALU fraction beside it"""
+    d = {"kernel": name, "objects": n, "algorithmic_bytes_per_object": nbytes}
+    if pmc:
+        nbytes, valu, src = pmc
+        d.update({"bytes_per_object": nbytes, "bytes_basis": f"measured: FETCH_SIZE x 2 + WRITE_SIZE ({src})",
+                  "valu_per_object": valu})
     gbs = n * nbytes / (ms / 1e3) / 1e9
-    d = {"kernel": name, "objects": n, "algorithmic_bytes_per_object": nbytes, "ms": ms,
-         "objects_per_s": n / ms * 1e3, "GBps": gbs, "hbm_frac": gbs / PEAK}
+    d.update({"ms": ms, "objects_per_s": n / ms * 1e3, "GBps": gbs, "hbm_frac": gbs / PEAK})
+    if pmc:
+        t_hbm = n * nbytes / (PEAK * 1e9) * 1e3
+        t_valu = n * valu / VALU_PEAK * 1e3
+        d.update({"valu_frac": t_valu / ms, "bound_ms": max(t_hbm, t_valu),
+                  "bound": "hbm" if t_hbm >= t_valu else "valu", "bound_frac": max(t_hbm, t_valu) / ms})
     if scrub_ms:
         d.update({"scrubbed_ms": scrub_ms, "scrubbed_objects_per_s": n / scrub_ms * 1e3,
                   "scrubbed_GBps": n * nbytes / (scrub_ms / 1e3) / 1e9,
@@ -191,9 +226,27 @@ def main():
             b.synchronize()
             ms.append(a.elapsed_time(b) / ks)
         sm = scrubbed(lambda: hip.stable_pass(works[0], name_run), prep=lambda: works[0].copy_(src))
-        report(f"k_stable {name}", n, 2 * 5120 + 1, sorted(ms)[len(ms) // 2], scrub_ms=sm)
+        label = f"k_stable {name_run} ({'next' if name.endswith('next node') else 'still'})"
+        report(f"k_stable {name}", n, 2 * 5120 + 1, sorted(ms)[len(ms) // 2], scrub_ms=sm,
+               pmc=pmc_row(label) if n == 1 << 20 else None)
+    for name in ("sync", "options", "signal", "step", "stabilise"):  # the single passes on the next node
+        ms = []
+        for _ in range(7):
+            for wk in works:
+                wk.copy_(nxt)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            for wk in works:
+                hip.stable_pass(wk, name)
+            b.record()
+            b.synchronize()
+            ms.append(a.elapsed_time(b) / ks)
+        report(f"k_stable {name} next node", n, 2 * 5120 + 1, sorted(ms)[len(ms) // 2],
+               pmc=pmc_row(f"k_stable {name} (next)") if n == 1 << 20 else None)
     del works, nxt
-    both("k_stable_vulnerable", n, 5120 + 512, lambda: hip.stable_vulnerable(st))
+    report("k_stable_vulnerable", n, 5120 + 512, timed(lambda: hip.stable_vulnerable(st)),
+           scrub_ms=scrubbed(lambda: hip.stable_vulnerable(st)),
+           pmc=pmc_row("k_stable_vulnerable (still)") if n == 1 << 20 else None)
     planes = hip.fill_random(11 * n, seed=21).view(n, 11 * 64)
     both("k_refined (config 5)", n, 7168, lambda: hip.refined_step(planes))
     n5 = 1 << 18

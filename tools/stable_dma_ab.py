@@ -8,7 +8,8 @@ shipped k_stable, same process, 1M LifeStables (--n), three inputs:
   random     random planes (every pass changes most lines).
 Forms (nt fetch, waits counted so the stores stay in flight): dma_loop, the
 looping grid; dma_uU, a grid of n / U waves, each a contiguous run of U
-LifeStables; _capC: at most C blocks resident per CU.
+LifeStables; wide_u1: U = 1 with the changed lines stored 16 bytes per lane
+through the LDS image; _capC: at most C blocks resident per CU.
 Per (input, pass, form): 4 launches back to back, each on its own fresh copy,
 between one pair of events (/ 4), median of 7; results checked bit for bit
 against the shipped pass (planes and flags).  One JSON line per row."""
@@ -46,8 +47,8 @@ def main():
     n = int(sys.argv[sys.argv.index("--n") + 1]) if "--n" in sys.argv else 1 << 20
     # forms: label -> (tuning pass offset, blocks per CU cap, passes it exists for)
     # forms: label -> (tuning pass offset, blocks per CU cap, LifeStables per wave (0: looping grid), passes)
-    forms = {"dma_loop": (16, 0, 0, range(6)), "dma_u2": (16, 0, 2, range(6)), "dma_u4": (16, 0, 4, range(6)),
-             "dma_u8": (16, 0, 8, range(6)), "dma_u4_cap4": (16, 4, 4, range(6))}
+    forms = {"dma_u1": (16, 0, 1, range(6)), "dma_u2": (16, 0, 2, range(6)),
+             "wide_u1": (32, 0, 1, range(6)), "wide_u1_cap3": (32, 3, 1, range(6)), "wide_u1_cap5": (32, 5, 1, range(6))}
     passes = sys.argv[sys.argv.index("--passes") + 1].split(",") if "--passes" in sys.argv else list(hip.STABLE_PASSES)
     st = stable_inputs(n)
     inputs = {"still": st, "next": stable_next_node(st),

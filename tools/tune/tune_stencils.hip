@@ -82,7 +82,8 @@ int lifeapi_tune_stable_pass(uint64_t *d_planes, uint8_t *d_flags, size_t n, int
   if (n == 0) return LIFEAPI_OK;
   // k_stable_dma on a grid of blocks_per_cu (0: all resident) per CU:
   // 16 + k: pass k, nt fetch, counted waits; 24 + k: plain fetch, counted;
-  // 32 + k: nt fetch, waits for every op (k in {0, 4} for the last two)
+  // 32 + k: nt fetch, counted, the changed lines stored 16 bytes per lane
+  // through the image (U = 1 only); k in {0, 4} for the plain fetch
   if (pass >= 16 && pass <= 37) {
     if (!d_planes || !d_flags || !aligned8(d_planes)) return fail(LIFEAPI_E_INVALID, "bad argument%s");
     int cus = 0, rc = device_cus(cus);
@@ -91,7 +92,9 @@ int lifeapi_tune_stable_pass(uint64_t *d_planes, uint8_t *d_flags, size_t n, int
     const Fn fns[22] = {k_stable_dma<0>, k_stable_dma<1>, k_stable_dma<2>, k_stable_dma<3>, k_stable_dma<4>,
                         k_stable_dma<5>, nullptr, nullptr,
                         k_stable_dma<0, 0>, nullptr, nullptr, nullptr, k_stable_dma<4, 0>, nullptr, nullptr, nullptr,
-                        k_stable_dma<0, 2, false>, nullptr, nullptr, nullptr, k_stable_dma<4, 2, false>, nullptr};
+                        k_stable_dma<0, 2, true, true>, k_stable_dma<1, 2, true, true>,
+                        k_stable_dma<2, 2, true, true>, k_stable_dma<3, 2, true, true>,
+                        k_stable_dma<4, 2, true, true>, k_stable_dma<5, 2, true, true>};
     if (!fns[pass - 16]) return fail(LIFEAPI_E_INVALID, "no such k_stable_dma variant%s");
     int res = 0;
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&res, fns[pass - 16], kBlock, 0);
