@@ -73,6 +73,82 @@ __device__ __forceinline__ void cone_wave_full16(const uint64_t *in, const uint6
   }
 }
 
+// The whole-board pass (K = 64) through LDS: each register set is one
+// universe, RB sets per pass; the RB universes of a pass (RB * 512
+// contiguous bytes) arrive by RB / 2 sixteen-byte-per-lane global_load_lds
+// (LDS-DMA, no VGPR destination: lanes 0-31 fill one universe, 32-63 the
+// next) and leave by ds_read_b64 with lane = column, and the next pass's are
+// fetched as soon as this pass has been read out, so that they stream in
+// while this pass steps.  Chunks of 2 RB universes per wave, u_step apart;
+// one coalesced store of answers per chunk.  `img`: this wave's RB * 512
+// bytes of LDS.  The batch must be 16-byte aligned.
+template <int RB, bool FIRST, typename OutT>
+__device__ __forceinline__ void cone_wave_full_dma(const uint64_t *in, const uint64_t *__restrict__ wanted,
+                                                   const uint64_t *__restrict__ unwanted, OutT *__restrict__ out,
+                                                   uint64_t n, uint64_t u_first, uint64_t u_step, uint32_t gens,
+                                                   int lane, uint64_t *img) {
+  static_assert(RB % 2 == 0 && 2 * RB <= kWave, "passes of pairs of universes, one answer per lane");
+  const uint64_t w64 = wanted[lane], m64 = w64 | unwanted[lane];
+  const W tw = split(w64), tm = split(m64);
+  auto clean = [&](W s) __attribute__((always_inline)) {
+    const uint32_t d = ((s.lo ^ tw.lo) & tm.lo) | ((s.hi ^ tw.hi) & tm.hi);
+    return __ballot(d != 0u) == 0ull;
+  };
+  // pass t: universes [base(t), base(t) + RB); chunk t / 2
+  auto base = [&](uint64_t t) { return u_first + (t >> 1) * u_step + (t & 1) * RB; };
+  auto fetch = [&](uint64_t ub) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < RB / 2; ++i) {
+      uint64_t u = ub + 2 * i + (lane >> 5);
+      if (u >= n) u = n - 1;  // (a valid address; the answer is never stored)
+      const char *src = reinterpret_cast<const char *>(in + u * kWave) + (lane & 31) * 16;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                       (__attribute__((address_space(3))) void *)(img + i * 2 * kWave), 16, 0, 2);
+    }
+  };
+  if (u_first >= n) return;
+  fetch(u_first);
+  uint32_t mine = 0;  // lane L: the answer for universe (chunk start) + L
+  int after = 0;      // vector-memory ops issued after the pending fetch (the chunk's answer store)
+  for (uint64_t t = 0;; ++t) {
+    const uint64_t ub = base(t);
+    if (ub >= n) break;
+    if (after) __builtin_amdgcn_s_waitcnt(kWaitVm1);
+    else __builtin_amdgcn_s_waitcnt(kWaitVm0);
+    W a[RB];
+#pragma unroll
+    for (int k = 0; k < RB; ++k) a[k] = split(img[k * kWave + lane]);
+    __builtin_amdgcn_s_waitcnt(kWaitLgkm0);  // read out before the next fetch lands
+    const uint64_t nb = base(t + 1);
+    if (nb < n) fetch(nb);
+    uint32_t res[RB];
+    if constexpr (FIRST) {
+#pragma unroll
+      for (int k = 0; k < RB; ++k) res[k] = 0;
+      for (uint32_t g = 1; g <= gens; ++g) {
+#pragma unroll
+        for (int k = 0; k < RB; ++k) {
+          a[k] = life_gen<XDPP, 3>(a[k], nullptr, lane);
+          if (res[k] == 0 && clean(a[k])) res[k] = g;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < RB; ++k) res[k] = clean(a[k]) ? 1u : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < RB; ++k)
+      if ((uint32_t)lane == (uint32_t)((t & 1) * RB + k)) mine = res[k];
+    after = 0;
+    if ((t & 1) || ub + RB >= n) {  // the chunk's last pass: store its answers
+      const uint64_t u0 = base(t & ~1ull);
+      if (lane < 2 * RB && u0 + lane < n) out[u0 + lane] = (OutT)mine;
+      mine = 0;
+      after = 1;
+    }
+  }
+}
+
 // UPW universes per wave (one-shot grid of ceil(n / UPW) waves), every wave
 // choosing its lane layout from the window (wave-uniform: the target is the
 // same for all).  Each choice runs its own copy of the pass.  A16: the batch
@@ -112,7 +188,9 @@ __global__ __launch_bounds__(kBlock) void k_cone(const uint64_t *in, const uint6
 // pass of 16 / 4 / 1 universes per register set), on a grid of ceil(n / 16)
 // waves capped at the caller's blocks per CU, every wave looping over the
 // batch with its own chunk size.
-template <int RMAX, bool FIRST, typename OutT, bool A16 = false>
+// DMA (a 16-byte aligned batch): the whole board (K = 64) through LDS
+// (cone_wave_full_dma, RMAX sets per pass, chunks of 2 RMAX universes).
+template <int RMAX, bool FIRST, typename OutT, bool A16 = false, bool DMA = false>
 __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const uint64_t *__restrict__ wanted,
                                                        const uint64_t *__restrict__ unwanted, OutT *__restrict__ out,
                                                        uint64_t n, uint32_t gens, uint32_t kmax) {
@@ -125,7 +203,16 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
   uint32_t xs = 0, K = kWave;
   if (!cone_whole(care_col, g)) cone_window(care_col, g, xs, K);
   if (K > kmax) return;
-  if constexpr (!FIRST && A16) {
+  if constexpr (DMA) {
+    __shared__ uint64_t img_all[kWavesPerBlock][RMAX * kWave];
+    if (K == (uint32_t)kWave) {
+      const uint64_t c = 2 * RMAX;
+      if (wave * c >= n) return;
+      return cone_wave_full_dma<RMAX, FIRST>(in, wanted, unwanted, out, n, wave * c, nw * c, gens, lane,
+                                             img_all[__builtin_amdgcn_readfirstlane(threadIdx.x / kWave)]);
+    }
+  }
+  if constexpr (!FIRST && A16 && !DMA) {
     if (K == (uint32_t)kWave) return cone_wave_full16<16, RMAX>(in, wanted, unwanted, out, n, wave * 16, nw * 16, lane);
   }
   if (K <= 8) {
@@ -201,12 +288,20 @@ int launch_cone(const uint64_t *d_in, const uint64_t *d_wanted, const uint64_t *
 }
 
 // Launches k_cone_adapt on ceil(n / 16) waves, at most blocks_per_cu blocks
-// per CU (0: no cap).
-template <int RMAX, bool FIRST, typename OutT>
+// per CU (0: no cap).  DMA: a whole-board window takes cone_wave_full_dma
+// when the batch is 16-byte aligned.
+template <int RMAX, bool FIRST, typename OutT, bool DMA = false>
 int launch_cone_adapt(const uint64_t *d_in, const uint64_t *d_wanted, const uint64_t *d_unwanted, OutT *d_out,
                       size_t n, uint32_t gens, int cus, hipStream_t stream, int blocks_per_cu,
                       uint32_t kmax = kWave) {
   const dim3 grid(grid_for((n + 15) / 16, cus, blocks_per_cu));
+  if constexpr (DMA) {
+    if (aligned16(d_in)) {
+      hipLaunchKernelGGL((k_cone_adapt<RMAX, FIRST, OutT, true, true>), grid, dim3(kBlock), 0, stream, d_in,
+                         d_wanted, d_unwanted, d_out, (uint64_t)n, gens, kmax);
+      return launched("k_cone_adapt launch");
+    }
+  }
   bool a16 = false;
   if constexpr (!FIRST) a16 = aligned16(d_in);
   if (a16) {

@@ -324,6 +324,13 @@ __device__ __forceinline__ uint64_t block_index() {
   else return blockIdx.x;
 }
 
+// s_waitcnt immediates (gfx9 encoding: vmcnt [3:0] + [15:14], expcnt [6:4],
+// lgkmcnt [11:8]): at most N vector-memory ops outstanding, or no LDS op.
+// Vector-memory ops retire in issue order, loads, LDS-DMA loads and stores
+// alike, so a wave waits for a global_load_lds by allowing the ops it issued
+// after it to remain.
+constexpr int kWaitVm0 = 0x0F70, kWaitVm1 = 0x0F71, kWaitVm6 = 0x0F76, kWaitVm11 = 0x0F7B, kWaitLgkm0 = 0xC07F;
+
 // Contains(LifeTarget) (LifeTarget.hpp:44-51): (s ^ w) & (w | u) == 0 on all columns
 __device__ __forceinline__ bool wave_contains(W s, W w, W u) {
   const uint32_t dlo = (s.lo ^ w.lo) & (w.lo | u.lo), dhi = (s.hi ^ w.hi) & (w.hi | u.hi);

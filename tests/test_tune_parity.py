@@ -213,7 +213,8 @@ def test_step_contains_pair_capped_grid(tune, hip, port, caps, kind):
 
 
 CONE_SHAPES = [(16, 4), (16, 8), (16, 16), (32, 4), (32, 8), (32, 16), (32, 32), (64, 8), (64, 16), (64, 32),
-               (1000 + 32, 8), (2000 + 64, 16), (8000 + 32, 8)]  # + 1000 c: at most c blocks per CU, grid-stride
+               (1000 + 32, 8), (2000 + 64, 16), (8000 + 32, 8),  # + 1000 c: at most c blocks per CU, grid-stride
+               (1, 4), (1, 8), (2000 + 1, 8)]  # upw 1: k_cone_adapt, the whole board through LDS (cone_wave_full_dma)
 
 
 @pytest.mark.parametrize("upw,rmax", CONE_SHAPES)
@@ -265,3 +266,28 @@ def test_stable_dma_forms(tune, hip, port, off, upw, cap, n):
         fl = tune.stable_pass(d, off + w, cap, upw=upw).cpu().numpy()
         assert (to_host(d).reshape(n, 640) == want).all(), (name, off, upw, cap)
         assert (fl == wfl).all(), (name, off, upw, cap)
+
+
+@pytest.mark.parametrize("rmax", [4, 8])
+@pytest.mark.parametrize("n", [1, 3, 17, 33, 100])
+def test_cone_full_dma_ragged(tune, port, rmax, n):
+    """cone_wave_full_dma on batches that end inside a pass or a chunk (its
+    loads clamp to the last universe, its stores stop at n): the whole-board
+    filter at 1 and 2 generations and whole-board Contains against the oracle"""
+    x = port.fill(n, seed=n + rmax)
+    x[::2] &= port.fill(n, seed=n + 99)[::2]
+    tw, tu = np.zeros(64, np.uint64), np.zeros(64, np.uint64)
+    tu[0::3] = np.uint64(1 << 10)  # row 10 of every third column dead: a 62-column window
+    d = to_dev(x)
+    for gens in (0, 1, 2):
+        if gens == 0:
+            want = (((x ^ tw) & (tw | tu)) == 0).all(axis=1).astype(np.uint8)
+            got = tune.cone(d, to_dev(tw[None]), to_dev(tu[None]), 0, 1, rmax, first=False).cpu().numpy()
+        else:
+            want, s = np.zeros(n, np.uint32), x.copy()
+            for g in range(1, gens + 1):
+                s = port.step_batch(s, 1)
+                hit = (((s ^ tw) & (tw | tu)) == 0).all(axis=1)
+                want[(want == 0) & hit] = g
+            got = tune.cone(d, to_dev(tw[None]), to_dev(tu[None]), gens, 1, rmax).cpu().numpy()
+        assert (got.astype(want.dtype) == want).all(), (gens, np.nonzero(got != want)[0][:8])

@@ -23,6 +23,7 @@ Both counters count L2-to-fabric bytes, so Infinity Cache hits count too; the
 scrub before every launch keeps those to the launch's own re-reads."""
 import csv
 import glob
+import re
 import json
 import os
 import statistics
@@ -58,12 +59,12 @@ def run():
                 w.copy_(src)
                 scrub()
                 hip.stable_pass(w, pname)
-            print(json.dumps({"workload": f"k_stable {pname} ({iname})", "match": "k_stable<",
+            print(json.dumps({"workload": f"k_stable {pname} ({iname})", "match": r"k_stable(_dma)?<",
                               "dispatches": REPS, "objects": N}), flush=True)
     for _ in range(REPS):
         scrub()
         hip.stable_vulnerable(st)
-    print(json.dumps({"workload": "k_stable_vulnerable (still)", "match": "k_stable_vulnerable",
+    print(json.dumps({"workload": "k_stable_vulnerable (still)", "match": r"k_stable_vulnerable",
                       "dispatches": REPS, "objects": N}), flush=True)
     torch.cuda.synchronize()
 
@@ -92,7 +93,7 @@ def _assign(rows, manifest):
                 raise SystemExit(f"ran out of dispatches at {m['workload']}")
             r = rows[i]
             i += 1
-            if m["match"] in r["name"]:
+            if re.search(m["match"], r["name"]):
                 got.append(r["ctr"])
         out.append(got)
     return out

@@ -17,6 +17,9 @@ int cone_by_shape(const uint64_t *in, const uint64_t *w, const uint64_t *u, OutT
   // upw 0: k_cone_adapt (64 universes per chunk for P <= 8, else 16), cap blocks per CU
   if (upw == 0 && rmax == 8) return launch_cone_adapt<8, FIRST>(in, w, u, out, n, gens, cus, st, cap);
   if (upw == 0 && rmax == 16) return launch_cone_adapt<16, FIRST>(in, w, u, out, n, gens, cus, st, cap);
+  // upw 1: k_cone_adapt with the whole board through LDS (cone_wave_full_dma, rmax sets per pass)
+  if (upw == 1 && rmax == 4) return launch_cone_adapt<4, FIRST, OutT, true>(in, w, u, out, n, gens, cus, st, cap);
+  if (upw == 1 && rmax == 8) return launch_cone_adapt<8, FIRST, OutT, true>(in, w, u, out, n, gens, cus, st, cap);
   LIFEAPI_CONE(8, 8)
   LIFEAPI_CONE(16, 4)
   LIFEAPI_CONE(16, 8)
