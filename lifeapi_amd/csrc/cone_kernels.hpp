@@ -197,7 +197,9 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
   const int lane = threadIdx.x & (kWave - 1);
   const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
-  if (wave * 16 >= n) return;
+  // (the smallest chunk any path takes: a wave starting past n has no work)
+  constexpr uint64_t kMinChunk = DMA && 2 * RMAX < 16 ? 2 * RMAX : 16;
+  if (wave * kMinChunk >= n) return;
   const uint32_t g = FIRST ? gens : 0u;
   const uint64_t care_col = wanted[lane] | unwanted[lane];
   uint32_t xs = 0, K = kWave;
