@@ -189,30 +189,45 @@ __global__ __launch_bounds__(kBlock) void k_cone(const uint64_t *in, const uint6
 // waves capped at the caller's blocks per CU, every wave looping over the
 // batch with its own chunk size.
 // DMA (a 16-byte aligned batch): the whole board (K = 64) through LDS
-// (cone_wave_full_dma, RMAX sets per pass, chunks of 2 RMAX universes).
+// (cone_wave_full_dma, RMAX sets per pass, chunks of 2 RMAX universes), on
+// the uncapped grid; every other window keeps the capped shape, the first
+// cap_waves waves looping over the batch and the rest returning after the
+// whole-board test (0: no cap).
 template <int RMAX, bool FIRST, typename OutT, bool A16 = false, bool DMA = false>
 __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const uint64_t *__restrict__ wanted,
                                                        const uint64_t *__restrict__ unwanted, OutT *__restrict__ out,
-                                                       uint64_t n, uint32_t gens, uint32_t kmax) {
+                                                       uint64_t n, uint32_t gens, uint32_t kmax, uint32_t cap_waves) {
   const int lane = threadIdx.x & (kWave - 1);
   const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
+  uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
   // (the smallest chunk any path takes: a wave starting past n has no work)
   constexpr uint64_t kMinChunk = DMA && 2 * RMAX < 16 ? 2 * RMAX : 16;
   if (wave * kMinChunk >= n) return;
   const uint32_t g = FIRST ? gens : 0u;
   const uint64_t care_col = wanted[lane] | unwanted[lane];
   uint32_t xs = 0, K = kWave;
-  if (!cone_whole(care_col, g)) cone_window(care_col, g, xs, K);
-  if (K > kmax) return;
+  const bool whole = cone_whole(care_col, g);
   if constexpr (DMA) {
     __shared__ uint64_t img_all[kWavesPerBlock][RMAX * kWave];
-    if (K == (uint32_t)kWave) {
-      const uint64_t c = 2 * RMAX;
-      if (wave * c >= n) return;
-      return cone_wave_full_dma<RMAX, FIRST>(in, wanted, unwanted, out, n, wave * c, nw * c, gens, lane,
-                                             img_all[__builtin_amdgcn_readfirstlane(threadIdx.x / kWave)]);
+    uint64_t *img = img_all[__builtin_amdgcn_readfirstlane(threadIdx.x / kWave)];
+    const uint64_t c = 2 * RMAX;
+    if (whole) {
+      if (kmax < (uint32_t)kWave || wave * c >= n) return;
+      return cone_wave_full_dma<RMAX, FIRST>(in, wanted, unwanted, out, n, wave * c, nw * c, gens, lane, img);
     }
+    if (cap_waves) {
+      if (wave >= cap_waves) return;
+      nw = nw < cap_waves ? nw : cap_waves;
+    }
+    cone_window(care_col, g, xs, K);
+    if (K > kmax) return;
+    if (K == (uint32_t)kWave) {
+      if (wave * c >= n) return;
+      return cone_wave_full_dma<RMAX, FIRST>(in, wanted, unwanted, out, n, wave * c, nw * c, gens, lane, img);
+    }
+  } else {
+    if (!whole) cone_window(care_col, g, xs, K);
+    if (K > kmax) return;
   }
   if constexpr (!FIRST && A16 && !DMA) {
     if (K == (uint32_t)kWave) return cone_wave_full16<16, RMAX>(in, wanted, unwanted, out, n, wave * 16, nw * 16, lane);
@@ -298,9 +313,11 @@ int launch_cone_adapt(const uint64_t *d_in, const uint64_t *d_wanted, const uint
                       uint32_t kmax = kWave) {
   const dim3 grid(grid_for((n + 15) / 16, cus, blocks_per_cu));
   if constexpr (DMA) {
-    if (aligned16(d_in)) {
-      hipLaunchKernelGGL((k_cone_adapt<RMAX, FIRST, OutT, true, true>), grid, dim3(kBlock), 0, stream, d_in,
-                         d_wanted, d_unwanted, d_out, (uint64_t)n, gens, kmax);
+    if (aligned16(d_in)) {  // the uncapped grid; the cap applies to the waves of a windowed target
+      const uint32_t cap_waves = blocks_per_cu > 0 ? (uint32_t)(cus * blocks_per_cu * kWavesPerBlock) : 0u;
+      hipLaunchKernelGGL((k_cone_adapt<RMAX, FIRST, OutT, true, true>), dim3(grid_for((n + 15) / 16, cus, 0)),
+                         dim3(kBlock), 0, stream, d_in, d_wanted, d_unwanted, d_out, (uint64_t)n, gens, kmax,
+                         cap_waves);
       return launched("k_cone_adapt launch");
     }
   }
@@ -309,12 +326,12 @@ int launch_cone_adapt(const uint64_t *d_in, const uint64_t *d_wanted, const uint
   if (a16) {
     if constexpr (!FIRST) {
       hipLaunchKernelGGL((k_cone_adapt<RMAX, FIRST, OutT, true>), grid, dim3(kBlock), 0, stream, d_in, d_wanted,
-                         d_unwanted, d_out, (uint64_t)n, gens, kmax);
+                         d_unwanted, d_out, (uint64_t)n, gens, kmax, 0u);
       return launched("k_cone_adapt launch");
     }
   }
   hipLaunchKernelGGL((k_cone_adapt<RMAX, FIRST, OutT, false>), grid, dim3(kBlock), 0, stream, d_in, d_wanted,
-                     d_unwanted, d_out, (uint64_t)n, gens, kmax);
+                     d_unwanted, d_out, (uint64_t)n, gens, kmax, 0u);
   return launched("k_cone_adapt launch");
 }
 

@@ -41,7 +41,7 @@ def main():
     n = gold["universes"]
     x = hip.fill_random(n, seed=gold["seed"])
     scrub = bench.Scrub(rt)
-    forms = {"shipped": None, "dma_r4": (1, 4), "dma_r8": (1, 8)}
+    forms = {"shipped": None, "dma_r8_cap16": (16001, 8), "dma_r4_cap16": (16001, 4), "dma_r8": (1, 8)}
     for name, t in gold["targets"].items():
         tw, tu = (torch.from_numpy(np.array([[int(v, 16) for v in t[k]]], dtype=np.uint64).view(np.int64)).cuda()
                   for k in ("wanted", "unwanted"))
