@@ -333,3 +333,16 @@ def line_read(states, line, out=None, stream=None):
         out = torch.empty(n, dtype=torch.int32, device=states.device)
     hip._check(lib.lifeapi_tune_line_read(states.data_ptr(), out.data_ptr(), n, line, hip._stream(stream)))
     return out
+
+
+lib.lifeapi_tune_stable_rep.argtypes = [_vp, _vp, _sz, _int, _u32, _vp]
+lib.lifeapi_tune_stable_rep.restype = _int
+
+
+def stable_rep(planes: torch.Tensor, which: int, reps: int, stream=None):
+    """the LifeStable pass `which` repeated `reps` times per LifeStable in
+    registers (k_stable_rep: a VALU probe; the planes get one result)"""
+    n = planes.numel() // (10 * 64)
+    flags = torch.empty(n, dtype=torch.uint8, device=planes.device)
+    hip._check(lib.lifeapi_tune_stable_rep(planes.data_ptr(), flags.data_ptr(), n, which, reps, hip._stream(stream)))
+    return flags

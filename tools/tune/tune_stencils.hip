@@ -73,9 +73,49 @@ __global__ __launch_bounds__(kBlock) void k_stable_pf(uint64_t *__restrict__ pla
   }
 }
 
+// The pass repeated `reps` times on each LifeStable's planes in VGPRs, each
+// repetition on the input again (so every repetition does the same work),
+// the last result stored: the pass's VALU side with its memory side paid
+// once (a probe of the issue rate, tools/stable_valu_probe.py).
+template <int PASS>
+__global__ __launch_bounds__(kBlock) void k_stable_rep(uint64_t *__restrict__ planes, uint8_t *__restrict__ flags,
+                                                       uint64_t n, uint32_t max_iters, uint32_t reps) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const uint64_t u = xcd_chunk_block() * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  if (u >= n) return;
+  uint64_t *q = planes + u * 10 * kWave + lane;
+  W p0[10], p[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) p0[k] = ld<true>(q + k * kWave);
+  int r = 0;
+  for (uint32_t i = 0; i < reps; ++i) {
+#pragma unroll
+    for (int k = 0; k < 10; ++k) p[k] = p0[k];
+    r = stable_run<PASS>(p, max_iters);
+    // (keep p0 live and the repetitions distinct)
+    p0[0].lo ^= (uint32_t)__builtin_amdgcn_readfirstlane((int)(r & 0x100));
+  }
+#pragma unroll
+  for (int k = 0; k < 10; ++k) st<true>(q + k * kWave, p[k]);
+  if (lane == 0) flags[u] = (uint8_t)r;
+}
+
 }  // namespace
 
 extern "C" {
+
+int lifeapi_tune_stable_rep(uint64_t *d_planes, uint8_t *d_flags, size_t n, int pass, uint32_t reps, void *stream) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!d_planes || !d_flags || pass < 0 || pass > 5) return fail(LIFEAPI_E_INVALID, "bad argument%s");
+  int cus = 0, rc = device_cus(cus);
+  if (rc != LIFEAPI_OK) return rc;
+  using Fn = void (*)(uint64_t *, uint8_t *, uint64_t, uint32_t, uint32_t);
+  const Fn fns[6] = {k_stable_rep<0>, k_stable_rep<1>, k_stable_rep<2>, k_stable_rep<3>, k_stable_rep<4>,
+                     k_stable_rep<5>};
+  hipLaunchKernelGGL(fns[pass], dim3(grid_for(n, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream, d_planes, d_flags,
+                     (uint64_t)n, 1u << 20, reps);
+  return launched("k_stable_rep launch");
+}
 
 int lifeapi_tune_stable_pass(uint64_t *d_planes, uint8_t *d_flags, size_t n, int pass, uint32_t max_iters,
                              int blocks_per_cu, void *stream, int reverse) {
