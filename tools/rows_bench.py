@@ -182,10 +182,13 @@ def main():
     bw[0, 10] = bw[0, 11] = 3 << 40
     bu[0, 9:13] = 15 << 39
     bu &= ~bw
-    both("k_cone Contains, 2x2 block + ring (4 columns)", n, 513, lambda: hip.contains(x, bw, bu),
-         {"lines_128B_per_object": 1})
-    both("k_cone 1 gen (first hit only), 2x2 block + ring", n, 516, lambda: hip.step_contains(x, bw, bu, 1),
-         {"lines_128B_per_object": 1})
+    # the light cone of this target (columns 9-12, +-1 for a generation) lies in
+    # one 128-byte line of each universe: the bytes the kernel must move are
+    # that line and the answer (PMC: FETCH_SIZE x 2 = 128 B per universe)
+    both("k_cone Contains, 2x2 block + ring (4 columns)", n, 128 + 1, lambda: hip.contains(x, bw, bu),
+         {"lines_128B_per_object": 1, "full_read_equivalent_bytes": 513})
+    both("k_cone 1 gen (first hit only), 2x2 block + ring", n, 128 + 4, lambda: hip.step_contains(x, bw, bu, 1),
+         {"lines_128B_per_object": 1, "full_read_equivalent_bytes": 516})
     fp = [x.clone(), y]
 
     def filter_pingpong():  # a loop stepping its batch with the filter: final states ping-ponged
