@@ -7,6 +7,7 @@ reference on fresh seeded inputs.
 """
 import json
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -169,7 +170,11 @@ def test_refined_truth_table_fixture(port, meta):
                                          ("stable_vulnerable_circuit.inc", "stable_vulnerable_tt.npz")])
 def test_generated_circuit_is_the_table(inc, ttfile):
     """A generated bitop3 network (lifeapi_amd/csrc/*.inc), simulated on every
-    input combination, is exactly the reference fragment's truth table."""
+    input combination, is exactly the reference fragment's truth table -- on
+    every row, or, for a network generated on the reachable rows
+    (tools/cgp_stable.py, its header says so), on every row that
+    NeighbourCount-derived inputs can take (test_reachable_rows_cover_every_
+    neighbourhood checks that set)."""
     import re
     d = load(ttfile)
     tt = d["tt"].astype(bool)
@@ -190,7 +195,57 @@ def test_generated_circuit_is_the_table(inc, ttfile):
     for nm in (str(s) for s in d["outputs"]):
         m = re.search(rf"\b{nm} = (~(t\d+)|(t\d+|x\[\d+\]));", src)
         outs.append(~val[m[2]] if m[2] else val[m[3]])
-    assert (np.stack(outs) == tt).all()
+    got = np.stack(outs)
+    if "reachable_rows" in src:
+        sys.path.insert(0, os.path.join(os.path.dirname(GOLD), "..", "tools"))
+        from cgp_stable import reachable_rows
+        rows = reachable_rows(inc.split("_")[1])
+        assert (got[:, rows] == tt[:, rows]).all()
+    else:
+        assert (got == tt).all()
+
+
+def _inclusive_count(plane: np.ndarray) -> np.ndarray:
+    """NeighbourCount (NeighbourCount.hpp:40-70) per cell of a (64, 64) bool
+    plane on the torus: the 3x3 block's population, centre included"""
+    p = plane.astype(np.int64)
+    return sum(np.roll(np.roll(p, dx, 0), dy, 1) for dx in (-1, 0, 1) for dy in (-1, 0, 1))
+
+
+def test_reachable_rows_cover_every_neighbourhood():
+    """The care sets of the resynthesised LifeStable networks
+    (tools/cgp_stable.py reachable_rows) contain every input row the passes
+    form from real planes: random state / unknown / option planes of many
+    densities, state and unknown overlapping too, every cell of every board
+    (the kernels compute the same counts, stable_kernels.hpp)."""
+    sys.path.insert(0, os.path.join(os.path.dirname(GOLD), "..", "tools"))
+    from cgp_stable import reachable_rows
+    care = {k: set(reachable_rows(k).tolist()) for k in ("count", "signal", "vulnerable")}
+    rng = np.random.default_rng(2024)
+
+    def rowint(cols):
+        return sum(c.astype(np.int64) << i for i, c in enumerate(cols))
+
+    def bits(v, hi):
+        return [(v >> k) & 1 for k in range(hi, -1, -1)]
+    seen = {k: set() for k in care}
+    for dens_s, dens_u in [(0.1, 0.1), (0.5, 0.5), (0.9, 0.05), (0.05, 0.9), (0.3, 0.0), (0.0, 0.3), (0.7, 0.7)]:
+        for _ in range(3):
+            st = rng.random((64, 64)) < dens_s
+            un = rng.random((64, 64)) < dens_u
+            opt = [rng.random((64, 64)) < 0.5 for _ in range(8)]
+            off = ~un & ~st
+            on_c, off_c = _inclusive_count(st), _inclusive_count(off)
+            m_c, u_c = _inclusive_count(st | un), _inclusive_count(un)
+            r = rowint(bits(on_c % 8, 2) + bits(off_c, 3) + [st, off])
+            seen["count"] |= set(r.ravel().tolist())
+            r = rowint(opt + bits(on_c % 8, 2) + bits(m_c, 3) + [st, un])
+            seen["signal"] |= set(r.ravel().tolist())
+            r = rowint(opt + bits(on_c % 8, 2) + bits(u_c, 3))
+            seen["vulnerable"] |= set(r.ravel().tolist())
+    for k in care:
+        assert seen[k] <= care[k], k
+        assert len(seen[k]) > len(care[k]) // 10  # the sample reaches a good part of the set
 
 
 def test_rule3_network_truth():
