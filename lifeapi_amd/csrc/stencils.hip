@@ -25,6 +25,8 @@ constexpr int kWeldResidentBlocks = 7;  // k_weld (below 12 generations)
 // StabiliseOptions 4 (3 and 4 within 1 %).  Round 2's "3" had been 2 (its
 // LDS share was rounded up).
 constexpr int kStablePassResident[6] = {3, 3, 3, 3, 0, kStableResidentBlocks};
+// the LDS-DMA passes (below): at most 5 blocks resident per CU
+constexpr int kStableDmaResident = 5;
 
 static int counts_launch(const uint64_t *d_in, uint64_t *d_out, size_t n, int mode, void *stream) {
   if (n == 0) return LIFEAPI_OK;
@@ -86,17 +88,29 @@ int lifeapi_stable_pass_batch_dev(uint64_t *d_planes, uint8_t *d_flags, size_t n
   // signal 1.83 -> 1.72, PropagateStep 1.95 -> 1.86, StabiliseOptions
   // 1.79 -> 1.66.
   note_forward_write(d_planes, (uint64_t)n * 10 * 512);
-  if (pass == 2) {
-    // Round 5: SignalNeighbours reads its LifeStable into LDS by five
-    // 16-byte-per-lane global_load_lds and out to VGPRs by ds_read, one
-    // LifeStable per wave, every slot (k_stable_dma, U = 1): 0.78-0.80 ms
-    // against 1.10-1.15 for the 10 dwordx2 loads of k_stable on 1M
-    // LifeStables of all three families (0.82 of 8 TB/s on the 5131 bytes it
-    // moves).  The passes that write back most of their lines lose 1-11 %
-    // with it, so they keep k_stable (tools/stable_dma_ab.py,
-    // profiles/r05/stable_dma_ab.jsonl).
-    hipLaunchKernelGGL(k_stable_dma<2>, dim3(grid_for(n, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream,
-                       d_planes, d_flags, (uint64_t)n, max_iters ? max_iters : 1u << 20, 1u << 8);
+  if ((pass == 0 || pass == 2 || pass == 3) && aligned16(d_planes)) {
+    // Round 5: SynchroniseStateKnown, SignalNeighbours and PropagateStep
+    // move their LifeStable through LDS (k_stable_dma, U = 1, WIDE): five
+    // 16-byte-per-lane global_load_lds in, ds_read_b64 out to lane =
+    // column; the changed lines back through the image, 16 bytes per lane;
+    // at most 5 blocks resident per CU.  Same process, 1M LifeStables of
+    // three families, ms (tools/stable_dma_ab.py, profiles/r05/
+    // stable_dma_ab_r05m.jsonl; fresh options / a search's next node /
+    // random planes): signal 0.791 / 0.786 / 0.790 against 0.802 / 0.798 /
+    // 0.802 for k_stable (round 4: 1.10-1.15); PropagateStep 1.654 / 1.074
+    // / 1.645 against 1.697 / 1.368 / 1.631; sync 1.649 / 1.058 / 1.649
+    // against 1.625 / 1.142 / 1.632.  UpdateOptions loses 6 % on the
+    // inputs where every column changes, Propagate and StabiliseOptions
+    // gain nothing: they keep k_stable.  The loads and
+    // stores are 16 bytes wide: an 8-byte aligned batch keeps k_stable.
+    using DFn = void (*)(uint64_t *, uint8_t *, uint64_t, uint32_t, uint32_t);
+    const DFn dma = pass == 0 ? (DFn)k_stable_dma<0, 2, true, true>
+                    : pass == 2 ? (DFn)k_stable_dma<2, 2, true, true> : (DFn)k_stable_dma<3, 2, true, true>;
+    unsigned dlds = 0;
+    rc = occupancy_lds(reinterpret_cast<const void *>(dma), kStableDmaResident, dlds);
+    if (rc != LIFEAPI_OK) return rc;
+    hipLaunchKernelGGL(dma, dim3(grid_for(n, cus, 0)), dim3(kBlock), dlds, (hipStream_t)stream, d_planes, d_flags,
+                       (uint64_t)n, max_iters ? max_iters : 1u << 20, 1u << 8);
     return launched("k_stable_dma launch");
   }
   hipLaunchKernelGGL(fns[pass], dim3(grid_for(n, cus, 0)), dim3(kBlock), lds, (hipStream_t)stream,

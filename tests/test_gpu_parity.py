@@ -787,3 +787,33 @@ def test_refined_step_full_size_sample(hip, port):
     idx = np.r_[0:512, 511 * np.arange(1, 500)]
     x = d.cpu().numpy().view(np.uint64)[idx]
     assert (got.cpu().numpy().view(np.uint64)[idx] == port.refined_step(x)).all()
+
+
+def test_stable_passes_8_byte_aligned_batch(hip, port):
+    """SynchroniseStateKnown, SignalNeighbours and PropagateStep move a
+    16-byte aligned batch through LDS with 16-byte accesses (stencils.hip,
+    k_stable_dma); a batch that is only 8-byte aligned (the ABI's
+    requirement) takes k_stable.  Both forms, every pass, against the oracle,
+    on a search's next node and on fresh options."""
+    n = 777
+    fresh = _stable_cases(port, n, seed=41)
+    nxt, _ = port.stable_pass(fresh, 4)
+    nxt = nxt.reshape(n, 10, 64).copy()
+    for u in range(n):
+        cols = np.nonzero(nxt[u, 1])[0]
+        if len(cols):
+            c = int(cols[0])
+            low = nxt[u, 1, c] & (~nxt[u, 1, c] + np.uint64(1))
+            nxt[u, 1, c] &= ~low
+            nxt[u, 0, c] |= low
+    for x in (fresh, nxt.reshape(n, 640)):
+        for w, name in enumerate(hip.STABLE_PASSES):
+            want, wfl = port.stable_pass(x, w)
+            for offset in (0, 1):  # int64 words: 16-byte aligned, then 8-byte aligned only
+                buf = torch.empty(n * 640 + 2, dtype=torch.int64, device="cuda")
+                d = buf[offset: offset + n * 640].view(n, 640)
+                assert (d.data_ptr() % 16 == 0) == (offset == 0)
+                d.copy_(to_dev(x).reshape(n, 640))
+                fl = hip.stable_pass(d, name).cpu().numpy()
+                assert (to_host(d).reshape(n, 640) == want).all(), (name, offset)
+                assert (fl == wfl).all(), (name, offset)
