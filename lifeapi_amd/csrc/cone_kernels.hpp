@@ -196,10 +196,15 @@ __global__ __launch_bounds__(kBlock) void k_cone(const uint64_t *in, const uint6
 template <int RMAX, bool FIRST, typename OutT, bool A16 = false, bool DMA = false>
 __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const uint64_t *__restrict__ wanted,
                                                        const uint64_t *__restrict__ unwanted, OutT *__restrict__ out,
-                                                       uint64_t n, uint32_t gens, uint32_t kmax, uint32_t cap_waves) {
+                                                       uint64_t n, uint32_t gens, uint32_t kmax, uint32_t cap_waves,
+                                                       int32_t *cls) {
   const int lane = threadIdx.x & (kWave - 1);
   const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
+  // the first wave reports the window K to the host (host.hpp cone_class_slot)
+  auto report = [&](uint32_t k) __attribute__((always_inline)) {
+    if (cls && wave == 0 && lane == 0) *reinterpret_cast<volatile int32_t *>(cls) = (int32_t)k;
+  };
   // (the smallest chunk any path takes: a wave starting past n has no work)
   constexpr uint64_t kMinChunk = DMA && 2 * RMAX < 16 ? 2 * RMAX : 16;
   if (wave * kMinChunk >= n) return;
@@ -212,6 +217,7 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
     uint64_t *img = img_all[__builtin_amdgcn_readfirstlane(threadIdx.x / kWave)];
     const uint64_t c = 2 * RMAX;
     if (whole) {
+      report(kWave);
       if (kmax < (uint32_t)kWave || wave * c >= n) return;
       return cone_wave_full_dma<RMAX, FIRST>(in, wanted, unwanted, out, n, wave * c, nw * c, gens, lane, img);
     }
@@ -220,6 +226,7 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
       nw = nw < cap_waves ? nw : cap_waves;
     }
     cone_window(care_col, g, xs, K);
+    report(K);
     if (K > kmax) return;
     if (K == (uint32_t)kWave) {
       if (wave * c >= n) return;
@@ -227,6 +234,7 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
     }
   } else {
     if (!whole) cone_window(care_col, g, xs, K);
+    report(K);
     if (K > kmax) return;
   }
   if constexpr (!FIRST && A16 && !DMA) {
@@ -306,18 +314,30 @@ int launch_cone(const uint64_t *d_in, const uint64_t *d_wanted, const uint64_t *
 
 // Launches k_cone_adapt on ceil(n / 16) waves, at most blocks_per_cu blocks
 // per CU (0: no cap).  DMA: a whole-board window takes cone_wave_full_dma
-// when the batch is 16-byte aligned.
-template <int RMAX, bool FIRST, typename OutT, bool DMA = false>
+// when the batch is 16-byte aligned (the uncapped grid; the cap then applies
+// to the waves of a windowed target).  AUTO (the product's search filter):
+// the DMA form exactly when the last launch on this target reported a
+// whole-board window (host.hpp cone_class_slot), else the capped form; both
+// compute the same answers for any target.
+template <int RMAX, bool FIRST, typename OutT, bool DMA = false, bool AUTO = false>
 int launch_cone_adapt(const uint64_t *d_in, const uint64_t *d_wanted, const uint64_t *d_unwanted, OutT *d_out,
                       size_t n, uint32_t gens, int cus, hipStream_t stream, int blocks_per_cu,
                       uint32_t kmax = kWave) {
   const dim3 grid(grid_for((n + 15) / 16, cus, blocks_per_cu));
-  if constexpr (DMA) {
-    if (aligned16(d_in)) {  // the uncapped grid; the cap applies to the waves of a windowed target
+  int32_t *cls = nullptr;
+  bool dma = DMA;
+  if constexpr (AUTO) {
+    int last_k = -1;
+    const int rc = cone_class_slot(d_wanted, d_unwanted, gens, cls, last_k);
+    if (rc != LIFEAPI_OK) return rc;
+    dma = last_k == kWave && kmax >= (uint32_t)kWave;
+  }
+  if constexpr (DMA || AUTO) {
+    if (dma && aligned16(d_in)) {  // the uncapped grid; the cap applies to the waves of a windowed target
       const uint32_t cap_waves = blocks_per_cu > 0 ? (uint32_t)(cus * blocks_per_cu * kWavesPerBlock) : 0u;
       hipLaunchKernelGGL((k_cone_adapt<RMAX, FIRST, OutT, true, true>), dim3(grid_for((n + 15) / 16, cus, 0)),
                          dim3(kBlock), 0, stream, d_in, d_wanted, d_unwanted, d_out, (uint64_t)n, gens, kmax,
-                         cap_waves);
+                         cap_waves, cls);
       return launched("k_cone_adapt launch");
     }
   }
@@ -326,12 +346,12 @@ int launch_cone_adapt(const uint64_t *d_in, const uint64_t *d_wanted, const uint
   if (a16) {
     if constexpr (!FIRST) {
       hipLaunchKernelGGL((k_cone_adapt<RMAX, FIRST, OutT, true>), grid, dim3(kBlock), 0, stream, d_in, d_wanted,
-                         d_unwanted, d_out, (uint64_t)n, gens, kmax, 0u);
+                         d_unwanted, d_out, (uint64_t)n, gens, kmax, 0u, cls);
       return launched("k_cone_adapt launch");
     }
   }
   hipLaunchKernelGGL((k_cone_adapt<RMAX, FIRST, OutT, false>), grid, dim3(kBlock), 0, stream, d_in, d_wanted,
-                     d_unwanted, d_out, (uint64_t)n, gens, kmax, 0u);
+                     d_unwanted, d_out, (uint64_t)n, gens, kmax, 0u, cls);
   return launched("k_cone_adapt launch");
 }
 

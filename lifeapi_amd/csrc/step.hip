@@ -157,8 +157,16 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
     // and a whole-board one, 64K and 1M universes); from 5 on the split
     // layout takes over for whole-board targets at 1M; batches of <= 256K
     // take it up to 6 generations (cone_kernels.hpp kConeAloneGensSmall).
-    return launch_cone_adapt<kConeSets, true>(d_in, d_wanted, d_unwanted, d_first_gen, n, generations, cus,
-                                              (hipStream_t)stream, kConeAdaptBlocksPerCU);
+    // A whole-board target takes the universes through LDS (cone_wave_full_dma,
+    // chunks of 16, 8 per pass by global_load_lds, the next pass fetched
+    // while this one steps) on the uncapped grid; the form is chosen by what
+    // the last launch on this target reported (launch_cone_adapt AUTO), so the
+    // first call on a target, and every small target, takes the capped form.
+    // 1M universes, 1 generation, alone after a scrub: 0.0816-0.0849 ms against
+    // 0.0874-0.0889 (tools/filter_dma_ab.py, profiles/r05/filter_dma_ab_r05*.jsonl).
+    return launch_cone_adapt<kConeSets, true, uint32_t, false, true>(d_in, d_wanted, d_unwanted, d_first_gen, n,
+                                                                     generations, cus, (hipStream_t)stream,
+                                                                     kConeAdaptBlocksPerCU);
   }
   if (generations > 2) {  // the layout of the shipped step for gens > 2
     // Without final states, a target whose light cone over `generations`

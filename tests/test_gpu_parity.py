@@ -817,3 +817,40 @@ def test_stable_passes_8_byte_aligned_batch(hip, port):
                 fl = hip.stable_pass(d, name).cpu().numpy()
                 assert (to_host(d).reshape(n, 640) == want).all(), (name, offset)
                 assert (fl == wfl).all(), (name, offset)
+
+
+def test_filter_launch_form_follows_the_target(hip, port):
+    """The search filter picks its launch form by what the last launch on the
+    same target pointers reported (cone_kernels.hpp launch_cone_adapt AUTO):
+    the first call on a whole-board target runs the capped form, the next ones
+    the LDS form on the uncapped grid; rewriting the target in place to a
+    small one leaves one call on the stale form, which must still be exact.
+    Every call against the oracle, at 1 and 2 generations, ragged n."""
+    n = 70001
+    x = port.fill(n, seed=91) & port.fill(n, seed=92)
+    d = to_dev(x)
+    whole_u = np.zeros(64, np.uint64)
+    whole_u[0::3] = np.uint64(1 << 10)
+    small_w, small_u = np.zeros(64, np.uint64), np.zeros(64, np.uint64)
+    small_w[10] = small_w[11] = np.uint64(3 << 40)
+    small_u[9:13] = np.uint64(15 << 39)
+    small_u &= ~small_w
+    tw = torch.zeros((1, 64), dtype=torch.int64, device="cuda")
+    tu = torch.zeros((1, 64), dtype=torch.int64, device="cuda")
+
+    def want(w, u, gens):
+        res, s = np.zeros(n, np.uint32), x.copy()
+        for g in range(1, gens + 1):
+            s = port.step_batch(s, 1, nthreads=8)
+            hit = (((s ^ w) & (w | u)) == 0).all(axis=1)
+            res[(res == 0) & hit] = g
+        return res
+    for gens in (1, 2):
+        for w, u in ((np.zeros(64, np.uint64), whole_u), (small_w, small_u)):
+            tw.copy_(to_dev(w[None]).reshape(1, 64))
+            tu.copy_(to_dev(u[None]).reshape(1, 64))
+            exp = want(w, u, gens)
+            for _ in range(3):  # first call: the last report is stale or absent; then the target's own form
+                first, _ = hip.step_contains(d, tw, tu, gens)
+                torch.cuda.synchronize()
+                assert (first.cpu().numpy().astype(np.uint32) == exp).all(), (gens, int(w.any()))
