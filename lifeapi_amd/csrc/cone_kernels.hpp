@@ -197,13 +197,16 @@ template <int RMAX, bool FIRST, typename OutT, bool A16 = false, bool DMA = fals
 __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const uint64_t *__restrict__ wanted,
                                                        const uint64_t *__restrict__ unwanted, OutT *__restrict__ out,
                                                        uint64_t n, uint32_t gens, uint32_t kmax, uint32_t cap_waves,
-                                                       int32_t *cls) {
+                                                       int32_t *cls, int32_t cls_last) {
   const int lane = threadIdx.x & (kWave - 1);
   const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
   // the first wave reports the window K to the host (host.hpp cone_class_slot)
+  // when it differs from what the host last read there: a write to host
+  // memory holds the launch's end by a PCIe round trip, so a target that
+  // keeps its window costs it once
   auto report = [&](uint32_t k) __attribute__((always_inline)) {
-    if (cls && wave == 0 && lane == 0) *reinterpret_cast<volatile int32_t *>(cls) = (int32_t)k;
+    if (cls && wave == 0 && lane == 0 && (int32_t)k != cls_last) *reinterpret_cast<volatile int32_t *>(cls) = (int32_t)k;
   };
   // (the smallest chunk any path takes: a wave starting past n has no work)
   constexpr uint64_t kMinChunk = DMA && 2 * RMAX < 16 ? 2 * RMAX : 16;
@@ -325,9 +328,9 @@ int launch_cone_adapt(const uint64_t *d_in, const uint64_t *d_wanted, const uint
                       uint32_t kmax = kWave) {
   const dim3 grid(grid_for((n + 15) / 16, cus, blocks_per_cu));
   int32_t *cls = nullptr;
+  int last_k = -1;
   bool dma = DMA;
   if constexpr (AUTO) {
-    int last_k = -1;
     const int rc = cone_class_slot(d_wanted, d_unwanted, gens, cls, last_k);
     if (rc != LIFEAPI_OK) return rc;
     dma = last_k == kWave && kmax >= (uint32_t)kWave;
@@ -337,7 +340,7 @@ int launch_cone_adapt(const uint64_t *d_in, const uint64_t *d_wanted, const uint
       const uint32_t cap_waves = blocks_per_cu > 0 ? (uint32_t)(cus * blocks_per_cu * kWavesPerBlock) : 0u;
       hipLaunchKernelGGL((k_cone_adapt<RMAX, FIRST, OutT, true, true>), dim3(grid_for((n + 15) / 16, cus, 0)),
                          dim3(kBlock), 0, stream, d_in, d_wanted, d_unwanted, d_out, (uint64_t)n, gens, kmax,
-                         cap_waves, cls);
+                         cap_waves, cls, (int32_t)last_k);
       return launched("k_cone_adapt launch");
     }
   }
@@ -346,12 +349,12 @@ int launch_cone_adapt(const uint64_t *d_in, const uint64_t *d_wanted, const uint
   if (a16) {
     if constexpr (!FIRST) {
       hipLaunchKernelGGL((k_cone_adapt<RMAX, FIRST, OutT, true>), grid, dim3(kBlock), 0, stream, d_in, d_wanted,
-                         d_unwanted, d_out, (uint64_t)n, gens, kmax, 0u, cls);
+                         d_unwanted, d_out, (uint64_t)n, gens, kmax, 0u, cls, (int32_t)last_k);
       return launched("k_cone_adapt launch");
     }
   }
   hipLaunchKernelGGL((k_cone_adapt<RMAX, FIRST, OutT, false>), grid, dim3(kBlock), 0, stream, d_in, d_wanted,
-                     d_unwanted, d_out, (uint64_t)n, gens, kmax, 0u, cls);
+                     d_unwanted, d_out, (uint64_t)n, gens, kmax, 0u, cls, (int32_t)last_k);
   return launched("k_cone_adapt launch");
 }
 
