@@ -185,6 +185,75 @@ __global__ __launch_bounds__(kBlock) void k_step_ab(const uint64_t *in, uint64_t
   step_body<X, U, NT, RULE, NTS>(in, out, n, gens, plain_from);
 }
 
+// step_body with the wave's U universes moved through LDS (the LifeStable
+// passes' LDS-DMA form, stable_kernels.hpp k_stable_dma): U / 2
+// sixteen-byte-per-lane global_load_lds in (lanes 0-31 one universe, 32-63 the
+// next), ds_read_b64 out to lane = column; WIDE: the results back through the
+// image, 16 bytes per lane (ds_write_b64, ds_read_b128, global_store_dwordx4),
+// else 8-byte stores from the lanes.  Order, plain-stored tail and XCD
+// chunking as step_body.  The batch must be 16-byte aligned.
+template <int U, int RULE, bool NTS, bool WIDE>
+__device__ __forceinline__ void step_body_dma(const uint64_t *in, uint64_t *out, uint64_t n, uint32_t gens,
+                                              uint64_t plain_from) {
+  static_assert(U % 2 == 0, "pairs of universes per 16-byte load");
+  __shared__ uint64_t img_all[kWavesPerBlock][U * kWave];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  uint64_t *img = img_all[wib];
+  const bool rev = (gens & kReverse) != 0;
+  const uint64_t blk = (gens & kXcdChunk) ? xcd_chunk_block() : (uint64_t)blockIdx.x;
+  gens &= ~(kReverse | kXcdChunk);
+  const uint64_t groups = (n + U - 1) / U, wstride = (uint64_t)gridDim.x * kWavesPerBlock;
+  for (uint64_t grp = blk * kWavesPerBlock + wib; grp < groups; grp += wstride) {
+    const uint64_t u0 = (rev ? groups - 1 - grp : grp) * U;
+#pragma unroll
+    for (int i = 0; i < U / 2; ++i) {
+      uint64_t u = u0 + 2 * i + (lane >> 5);
+      if (u >= n) u = n - 1;  // (a valid address; the result is not stored)
+      const char *src = reinterpret_cast<const char *>(in + u * kWave) + (lane & 31) * 16;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                       (__attribute__((address_space(3))) void *)(img + i * 2 * kWave), 16, 0, 2);
+    }
+    __builtin_amdgcn_s_waitcnt(kWaitVm0);
+    W a[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) a[k] = split(img[k * kWave + lane]);
+    for (uint32_t g = 0; g < gens; ++g) {
+#pragma unroll
+      for (int k = 0; k < U; ++k) a[k] = life_gen<XDPP, RULE>(a[k], nullptr, lane);
+    }
+    const bool nt = NTS && grp < plain_from;
+    if constexpr (WIDE) {
+#pragma unroll
+      for (int k = 0; k < U; ++k) img[k * kWave + lane] = join(a[k]);
+      const u64x2 *src = reinterpret_cast<const u64x2 *>(img) + lane;
+#pragma unroll
+      for (int i = 0; i < U / 2; ++i) {
+        const uint64_t u = u0 + 2 * i + (lane >> 5);
+        const u64x2 v = src[i * kWave];
+        u64x2 *dst = reinterpret_cast<u64x2 *>(out + u * kWave) + (lane & 31);
+        if (u < n) {
+          if (nt) __builtin_nontemporal_store(v, dst);
+          else *dst = v;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < U; ++k)
+        if (u0 + k < n) {
+          if (nt) st<true>(out + (u0 + k) * kWave + lane, a[k]);
+          else st<false>(out + (u0 + k) * kWave + lane, a[k]);
+        }
+    }
+  }
+}
+
+template <int U, int RULE, bool NTS, bool WIDE>
+__global__ __launch_bounds__(kBlock) void k_step_dma(const uint64_t *in, uint64_t *out, uint64_t n, uint32_t gens,
+                                                     uint64_t plain_from) {
+  step_body_dma<U, RULE, NTS, WIDE>(in, out, n, gens, plain_from);
+}
+
 // k_step for the split layouts: wave w takes G groups of P = S/2
 // consecutive universes, grid-strided; all branches wave-uniform.  NET: the
 // tail network (7 = RULE 3's, 6 = life_tail6); D: registers exchanged by DPP

@@ -659,6 +659,11 @@ int lifeapi_tune_step_order(const uint64_t *d_in, uint64_t *d_out, size_t n, uin
   const StepFn fn = upw == 2 ? order_fn<2>(nts) : upw == 4 ? order_fn<4>(nts) : upw == 8 ? order_fn<8>(nts)
                   : upw == 36 ? (nts ? (StepFn)k_step_pairnat<4, true> : (StepFn)k_step_pairnat<4, false>)
                   : upw == 40 ? (nts ? (StepFn)k_step_pairnat<8, true> : (StepFn)k_step_pairnat<8, false>)
+                  // upw 64 + U / 96 + U: through LDS (k_step_dma<U>, 8-byte / 16-byte stores; 16-byte-aligned batches)
+                  : upw == 68 ? (nts ? (StepFn)k_step_dma<4, 3, true, false> : (StepFn)k_step_dma<4, 3, false, false>)
+                  : upw == 72 ? (nts ? (StepFn)k_step_dma<8, 3, true, false> : (StepFn)k_step_dma<8, 3, false, false>)
+                  : upw == 100 ? (nts ? (StepFn)k_step_dma<4, 3, true, true> : (StepFn)k_step_dma<4, 3, false, true>)
+                  : upw == 104 ? (nts ? (StepFn)k_step_dma<8, 3, true, true> : (StepFn)k_step_dma<8, 3, false, true>)
                   : nullptr;
   if (!fn) return fail(LIFEAPI_E_INVALID, "universes per wave: 2, 4 or 8%s");
   upw &= 31;
