@@ -73,6 +73,22 @@ __device__ __forceinline__ void cone_wave_full16(const uint64_t *in, const uint6
   }
 }
 
+// One pass of the whole-board LDS form: the RB universes from ub on (RB * 512
+// contiguous bytes; past n, universe n - 1 again: a valid address whose
+// answer is never stored) into img by RB / 2 sixteen-byte-per-lane
+// global_load_lds (lanes 0-31 one universe, 32-63 the next).
+template <int RB>
+__device__ __forceinline__ void dma_fetch_pass(const uint64_t *in, uint64_t n, uint64_t ub, int lane, uint64_t *img) {
+#pragma unroll
+  for (int i = 0; i < RB / 2; ++i) {
+    uint64_t u = ub + 2 * i + (lane >> 5);
+    if (u >= n) u = n - 1;
+    const char *src = reinterpret_cast<const char *>(in + u * kWave) + (lane & 31) * 16;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                     (__attribute__((address_space(3))) void *)(img + i * 2 * kWave), 16, 0, 2);
+  }
+}
+
 // The whole-board pass (K = 64) through LDS: each register set is one
 // universe, RB sets per pass; the RB universes of a pass (RB * 512
 // contiguous bytes) arrive by RB / 2 sixteen-byte-per-lane global_load_lds
@@ -83,12 +99,11 @@ __device__ __forceinline__ void cone_wave_full16(const uint64_t *in, const uint6
 // one coalesced store of answers per chunk.  `img`: this wave's RB * 512
 // bytes of LDS.  The batch must be 16-byte aligned.
 template <int RB, bool FIRST, typename OutT>
-__device__ __forceinline__ void cone_wave_full_dma(const uint64_t *in, const uint64_t *__restrict__ wanted,
-                                                   const uint64_t *__restrict__ unwanted, OutT *__restrict__ out,
-                                                   uint64_t n, uint64_t u_first, uint64_t u_step, uint32_t gens,
-                                                   int lane, uint64_t *img) {
+__device__ __forceinline__ void cone_wave_full_dma(const uint64_t *in, uint64_t w64, uint64_t m64,
+                                                   OutT *__restrict__ out, uint64_t n, uint64_t u_first,
+                                                   uint64_t u_step, uint32_t gens, int lane, uint64_t *img,
+                                                   bool prefetched) {
   static_assert(RB % 2 == 0 && 2 * RB <= kWave, "passes of pairs of universes, one answer per lane");
-  const uint64_t w64 = wanted[lane], m64 = w64 | unwanted[lane];
   const W tw = split(w64), tm = split(m64);
   auto clean = [&](W s) __attribute__((always_inline)) {
     const uint32_t d = ((s.lo ^ tw.lo) & tm.lo) | ((s.hi ^ tw.hi) & tm.hi);
@@ -96,18 +111,9 @@ __device__ __forceinline__ void cone_wave_full_dma(const uint64_t *in, const uin
   };
   // pass t: universes [base(t), base(t) + RB); chunk t / 2
   auto base = [&](uint64_t t) { return u_first + (t >> 1) * u_step + (t & 1) * RB; };
-  auto fetch = [&](uint64_t ub) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < RB / 2; ++i) {
-      uint64_t u = ub + 2 * i + (lane >> 5);
-      if (u >= n) u = n - 1;  // (a valid address; the answer is never stored)
-      const char *src = reinterpret_cast<const char *>(in + u * kWave) + (lane & 31) * 16;
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
-                                       (__attribute__((address_space(3))) void *)(img + i * 2 * kWave), 16, 0, 2);
-    }
-  };
+  auto fetch = [&](uint64_t ub) __attribute__((always_inline)) { dma_fetch_pass<RB>(in, n, ub, lane, img); };
   if (u_first >= n) return;
-  fetch(u_first);
+  if (!prefetched) fetch(u_first);  // (else the caller issued it)
   uint32_t mine = 0;  // lane L: the answer for universe (chunk start) + L
   int after = 0;      // vector-memory ops issued after the pending fetch (the chunk's answer store)
   for (uint64_t t = 0;; ++t) {
@@ -147,6 +153,109 @@ __device__ __forceinline__ void cone_wave_full_dma(const uint64_t *in, const uin
       after = 1;
     }
   }
+}
+
+// The whole-board pass of the filter (FIRST, gens >= 1) when the target's care
+// rows, widened by the light cone, fit FW = 32 / PK rows: rows y0 .. y0 + FW - 1
+// of each universe's column are cut out by one v_alignbit (WRAP: the window
+// crosses row 63), PK universes share one 32-bit register (v_perm, universe j
+// of the word in bits j FW .. j FW + FW - 1), and the generation runs on the
+// packed words with 1-bit shifts for the vertical neighbours.  The bits
+// shifted in at a field's edges (the next field's, or zero) are wrong, and the
+// error moves one row inwards per generation -- never onto a care row, which
+// lies at least `gens` rows inside its field (cone_rows).  Columns are whole
+// (the DPP rotate is the torus), so the care cells are exact.  Same passes,
+// LDS image and answers as cone_wave_full_dma; a universe costs one cut, a
+// share of the pack, 1 / PK of the network and its field's test.
+template <int RB, int PK, bool WRAP, typename OutT>
+__device__ __forceinline__ void cone_wave_rows_dma(const uint64_t *in, uint64_t w64, uint64_t m64,
+                                                   OutT *__restrict__ out, uint64_t n, uint64_t u_first,
+                                                   uint64_t u_step, uint32_t gens, uint32_t y0, int lane,
+                                                   uint64_t *img, bool prefetched) {
+  static_assert(RB % 2 == 0 && RB % PK == 0 && 2 * RB <= kWave, "passes of whole words and pairs of universes");
+  static_assert(PK == 1 || PK == 2 || PK == 4, "fields of 32, 16 or 8 rows");
+  constexpr int FW = 32 / PK, NW = RB / PK;
+  constexpr uint32_t fmask = FW == 32 ? ~0u : (1u << FW) - 1u;
+  constexpr uint32_t rep = PK == 1 ? 1u : PK == 2 ? 0x00010001u : 0x01010101u;
+  const uint32_t sh = y0 & 31u;
+  auto cut = [&](uint64_t v) __attribute__((always_inline)) {
+    const W w = split(v);
+    return WRAP ? __builtin_amdgcn_alignbit(w.lo, w.hi, sh) : __builtin_amdgcn_alignbit(w.hi, w.lo, sh);
+  };
+  const uint32_t tw = (cut(w64) & fmask) * rep, tm = (cut(m64) & fmask) * rep;
+  constexpr uint32_t kDiff = ((TA ^ TB) & TC) & 0xFF;  // (s ^ wanted) & care
+  auto base = [&](uint64_t t) { return u_first + (t >> 1) * u_step + (t & 1) * RB; };
+  auto fetch = [&](uint64_t ub) __attribute__((always_inline)) { dma_fetch_pass<RB>(in, n, ub, lane, img); };
+  if (u_first >= n) return;
+  if (!prefetched) fetch(u_first);  // (else the caller issued it)
+  uint32_t mine = 0;  // lane L: the answer for universe (chunk start) + L
+  int after = 0;      // vector-memory ops issued after the pending fetch (the chunk's answer store)
+  for (uint64_t t = 0;; ++t) {
+    const uint64_t ub = base(t);
+    if (ub >= n) break;
+    if (after) __builtin_amdgcn_s_waitcnt(kWaitVm1);
+    else __builtin_amdgcn_s_waitcnt(kWaitVm0);
+    uint32_t a[NW];
+#pragma unroll
+    for (int m = 0; m < NW; ++m) {
+      uint32_t e[PK];
+#pragma unroll
+      for (int j = 0; j < PK; ++j) e[j] = cut(img[(m * PK + j) * kWave + lane]);
+      if constexpr (PK == 1) {
+        a[m] = e[0];
+      } else if constexpr (PK == 2) {
+        a[m] = __builtin_amdgcn_perm(e[1], e[0], 0x05040100u);  // low halves: e0 | e1 << 16
+      } else {
+        const uint32_t p01 = __builtin_amdgcn_perm(e[1], e[0], 0x0C0C0400u);  // e0.b0, e1.b0
+        const uint32_t p23 = __builtin_amdgcn_perm(e[3], e[2], 0x0C0C0400u);  // e2.b0, e3.b0
+        a[m] = __builtin_amdgcn_perm(p23, p01, 0x05040100u);
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(kWaitLgkm0);  // read out before the next fetch lands
+    const uint64_t nb = base(t + 1);
+    if (nb < n) fetch(nb);
+    uint32_t res[RB];
+#pragma unroll
+    for (int k = 0; k < RB; ++k) res[k] = 0;
+    for (uint32_t g = 1; g <= gens; ++g) {
+#pragma unroll
+      for (int m = 0; m < NW; ++m) {
+        const uint32_t L = dpp_prev(a[m]), R = dpp_next(a[m]);
+        const uint32_t h0 = lut3<kXor3>(L, a[m], R), h1 = lut3<kMaj>(L, a[m], R);
+        a[m] = life_tail6(h0 << 1, h0, h0 >> 1, h1 << 1, h1, h1 >> 1, a[m]);
+        const uint32_t d = lut3<kDiff>(a[m], tw, tm);
+#pragma unroll
+        for (int j = 0; j < PK; ++j) {
+          const bool clean = __ballot((d & (fmask << (j * FW))) != 0u) == 0ull;
+          if (res[m * PK + j] == 0 && clean) res[m * PK + j] = g;
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < RB; ++k)
+      if ((uint32_t)lane == (uint32_t)((t & 1) * RB + k)) mine = res[k];
+    after = 0;
+    if ((t & 1) || ub + RB >= n) {  // the chunk's last pass: store its answers
+      const uint64_t u0 = base(t & ~1ull);
+      if (lane < 2 * RB && u0 + lane < n) out[u0 + lane] = (OutT)mine;
+      mine = 0;
+      after = 1;
+    }
+  }
+}
+
+// The row window of a filter's whole-board pass (cone_wave_rows_dma): the
+// smallest cyclic window of the target's care rows, widened by `gens` rows on
+// either side, and the most universes per 32-bit word whose field holds it
+// (PK = 4, 2, 1: fields of 8, 16, 32 rows); 0 when it needs more than 32 rows.
+__device__ __forceinline__ int cone_rows(uint64_t care_col, uint32_t gens, uint32_t &y0) {
+  const uint32_t lo = wave_or_u32_dpp((uint32_t)care_col), hi = wave_or_u32_dpp((uint32_t)(care_col >> 32));
+  uint32_t cy0, h;
+  care_window((uint64_t)lo | (uint64_t)hi << 32, cy0, h);
+  if (gens >= 16u) return 0;
+  const uint32_t need = h + 2u * gens;
+  y0 = (cy0 - gens) & 63u;
+  return need <= 8u ? 4 : need <= 16u ? 2 : need <= 32u ? 1 : 0;
 }
 
 // UPW universes per wave (one-shot grid of ceil(n / UPW) waves), every wave
@@ -193,8 +302,8 @@ __global__ __launch_bounds__(kBlock) void k_cone(const uint64_t *in, const uint6
 // the uncapped grid; every other window keeps the capped shape, the first
 // cap_waves waves looping over the batch and the rest returning after the
 // whole-board test (0: no cap).
-template <int RMAX, bool FIRST, typename OutT, bool A16 = false, bool DMA = false>
-__global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const uint64_t *__restrict__ wanted,
+template <int RMAX, bool FIRST, typename OutT, bool A16 = false, bool DMA = false, bool ROWS = true>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DMA ? 10 : 1))) void k_cone_adapt(const uint64_t *in, const uint64_t *__restrict__ wanted,
                                                        const uint64_t *__restrict__ unwanted, OutT *__restrict__ out,
                                                        uint64_t n, uint32_t gens, uint32_t kmax, uint32_t cap_waves,
                                                        int32_t *cls, int32_t cls_last) {
@@ -212,31 +321,56 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
   constexpr uint64_t kMinChunk = DMA && 2 * RMAX < 16 ? 2 * RMAX : 16;
   if (wave * kMinChunk >= n) return;
   const uint32_t g = FIRST ? gens : 0u;
-  const uint64_t care_col = wanted[lane] | unwanted[lane];
+  const uint64_t w64 = wanted[lane], m64 = w64 | unwanted[lane], care_col = m64;
   uint32_t xs = 0, K = kWave;
-  const bool whole = cone_whole(care_col, g);
   if constexpr (DMA) {
     __shared__ uint64_t img_all[kWavesPerBlock][RMAX * kWave];
     uint64_t *img = img_all[__builtin_amdgcn_readfirstlane(threadIdx.x / kWave)];
     const uint64_t c = 2 * RMAX;
-    if (whole) {
+    // the last launch on this target reported a whole board: the wave's first
+    // pass is fetched before the window tests, which then run under it (a
+    // wave that turns out not to need it waits for it before leaving: LDS-DMA
+    // still in flight must not outlive the wave's LDS)
+    const bool early = cls_last == kWave && wave * c < n;
+    if (early) dma_fetch_pass<RMAX>(in, n, wave * c, lane, img);
+    auto leave = [&]() __attribute__((always_inline)) {
+      if (early) __builtin_amdgcn_s_waitcnt(kWaitVm0);
+    };
+    if (cone_whole(care_col, g)) {
       report(kWave);
-      if (kmax < (uint32_t)kWave || wave * c >= n) return;
-      return cone_wave_full_dma<RMAX, FIRST>(in, wanted, unwanted, out, n, wave * c, nw * c, gens, lane, img);
+      if (kmax < (uint32_t)kWave || wave * c >= n) return leave();
+      if constexpr (FIRST && ROWS) {
+        uint32_t y0 = 0;
+        const int pk = cone_rows(care_col, gens, y0);
+        auto rows = [&](auto pk_c, auto wrap_c) __attribute__((always_inline)) {
+          cone_wave_rows_dma<RMAX, decltype(pk_c)::value, decltype(wrap_c)::value>(
+              in, w64, m64, out, n, wave * c, nw * c, gens, y0, lane, img, early);
+        };
+        using T = std::true_type;
+        using F = std::false_type;
+        using P1 = std::integral_constant<int, 1>;
+        using P2 = std::integral_constant<int, 2>;
+        using P4 = std::integral_constant<int, 4>;
+        if (pk == 4) return y0 >= 32u ? rows(P4{}, T{}) : rows(P4{}, F{});
+        if (pk == 2) return y0 >= 32u ? rows(P2{}, T{}) : rows(P2{}, F{});
+        if (pk == 1) return y0 >= 32u ? rows(P1{}, T{}) : rows(P1{}, F{});
+      }
+      return cone_wave_full_dma<RMAX, FIRST>(in, w64, m64, out, n, wave * c, nw * c, gens, lane, img, early);
     }
     if (cap_waves) {
-      if (wave >= cap_waves) return;
+      if (wave >= cap_waves) return leave();
       nw = nw < cap_waves ? nw : cap_waves;
     }
     cone_window(care_col, g, xs, K);
     report(K);
-    if (K > kmax) return;
+    if (K > kmax) return leave();
     if (K == (uint32_t)kWave) {
-      if (wave * c >= n) return;
-      return cone_wave_full_dma<RMAX, FIRST>(in, wanted, unwanted, out, n, wave * c, nw * c, gens, lane, img);
+      if (wave * c >= n) return leave();
+      return cone_wave_full_dma<RMAX, FIRST>(in, w64, m64, out, n, wave * c, nw * c, gens, lane, img, early);
     }
+    leave();
   } else {
-    if (!whole) cone_window(care_col, g, xs, K);
+    if (!cone_whole(care_col, g)) cone_window(care_col, g, xs, K);
     report(K);
     if (K > kmax) return;
   }
@@ -322,13 +456,13 @@ int launch_cone(const uint64_t *d_in, const uint64_t *d_wanted, const uint64_t *
 // the DMA form exactly when the last launch on this target reported a
 // whole-board window (host.hpp cone_class_slot), else the capped form; both
 // compute the same answers for any target.
-template <int RMAX, bool FIRST, typename OutT, bool DMA = false, bool AUTO = false>
+template <int RMAX, bool FIRST, typename OutT, bool DMA = false, bool AUTO = false, bool ROWS = true>
 int launch_cone_adapt(const uint64_t *d_in, const uint64_t *d_wanted, const uint64_t *d_unwanted, OutT *d_out,
                       size_t n, uint32_t gens, int cus, hipStream_t stream, int blocks_per_cu,
-                      uint32_t kmax = kWave) {
+                      uint32_t kmax = kWave, int dma_blocks_per_cu = 0, int hint_k = -1) {
   const dim3 grid(grid_for((n + 15) / 16, cus, blocks_per_cu));
   int32_t *cls = nullptr;
-  int last_k = -1;
+  int last_k = hint_k;  // (the tuning build's stand-in for a report)
   bool dma = DMA;
   if constexpr (AUTO) {
     const int rc = cone_class_slot(d_wanted, d_unwanted, gens, cls, last_k);
@@ -338,7 +472,7 @@ int launch_cone_adapt(const uint64_t *d_in, const uint64_t *d_wanted, const uint
   if constexpr (DMA || AUTO) {
     if (dma && aligned16(d_in)) {  // the uncapped grid; the cap applies to the waves of a windowed target
       const uint32_t cap_waves = blocks_per_cu > 0 ? (uint32_t)(cus * blocks_per_cu * kWavesPerBlock) : 0u;
-      hipLaunchKernelGGL((k_cone_adapt<RMAX, FIRST, OutT, true, true>), dim3(grid_for((n + 15) / 16, cus, 0)),
+      hipLaunchKernelGGL((k_cone_adapt<RMAX, FIRST, OutT, true, true, ROWS>), dim3(grid_for((n + 15) / 16, cus, dma_blocks_per_cu)),
                          dim3(kBlock), 0, stream, d_in, d_wanted, d_unwanted, d_out, (uint64_t)n, gens, kmax,
                          cap_waves, cls, (int32_t)last_k);
       return launched("k_cone_adapt launch");

@@ -854,3 +854,56 @@ def test_filter_launch_form_follows_the_target(hip, port):
                 first, _ = hip.step_contains(d, tw, tu, gens)
                 torch.cuda.synchronize()
                 assert (first.cpu().numpy().astype(np.uint32) == exp).all(), (gens, int(w.any()))
+
+
+def _rows_target(rows, cols, wanted_at=None):
+    """care cells at `rows` of every column in `cols` (unwanted), and one
+    wanted cell (row, column) if given"""
+    w, u = np.zeros(64, np.uint64), np.zeros(64, np.uint64)
+    m = np.uint64(0)
+    for r in rows:
+        m |= np.uint64(1) << np.uint64(r % 64)
+    for c in cols:
+        u[c] = m
+    if wanted_at is not None:
+        r, c = wanted_at
+        w[c] = np.uint64(1) << np.uint64(r)
+        u[c] &= ~w[c]
+    return w, u
+
+
+@pytest.mark.parametrize("rows,gens_list", [
+    ((10,), (1, 2, 3, 4, 6)),              # 8-row fields up to 3 generations, then 16
+    ((61, 62, 63, 0, 1), (1, 2, 5)),       # a window across row 63 (8, 16, 32 rows)
+    ((30, 31, 32, 33), (1, 2, 6)),         # across the two 32-bit halves
+    (tuple(range(40, 54)), (1, 2, 3, 4)),  # 16-row fields at 1, then 32, then the full pass
+    (tuple(range(64)), (1, 2)),            # every row: the full pass
+])
+def test_filter_whole_board_row_windows(hip, port, rows, gens_list):
+    """A whole-board target whose care rows, widened by the light cone, fit 8,
+    16 or 32 rows takes the packed row-window pass (cone_kernels.hpp
+    cone_wave_rows_dma: 4, 2 or 1 universes per 32-bit register, shifts for
+    the vertical neighbours) in the LDS form; windows across row 63 and across
+    the 32-bit halves; every call against the oracle (first call the capped
+    form, the next two the LDS form), ragged n."""
+    n = 70001
+    x = port.fill(n, seed=93) & port.fill(n, seed=94) & port.fill(n, seed=95)
+    d = to_dev(x)
+    tw = torch.zeros((1, 64), dtype=torch.int64, device="cuda")
+    tu = torch.zeros((1, 64), dtype=torch.int64, device="cuda")
+    targets = [_rows_target(rows, range(0, 64, 3)),
+               _rows_target(rows, range(0, 64, 2), wanted_at=(rows[len(rows) // 2] % 64, 8))]
+    for gens in gens_list:
+        for w, u in targets:
+            tw.copy_(to_dev(w[None]).reshape(1, 64))
+            tu.copy_(to_dev(u[None]).reshape(1, 64))
+            res, s = np.zeros(n, np.uint32), x.copy()
+            for g in range(1, gens + 1):
+                s = port.step_batch(s, 1, nthreads=8)
+                hit = (((s ^ w) & (w | u)) == 0).all(axis=1)
+                res[(res == 0) & hit] = g
+            for call in range(3):
+                first, _ = hip.step_contains(d, tw, tu, gens)
+                torch.cuda.synchronize()
+                got = first.cpu().numpy().astype(np.uint32)
+                assert (got == res).all(), (rows, gens, call, int(w.any()), int((got != res).sum()))

@@ -1,9 +1,12 @@
-"""A/B: the whole-board search filter and Contains with the universes fetched
-into LDS by global_load_lds (k_cone_adapt DMA form, cone_wave_full_dma;
-tuning build cone shape upw 1, rmax = sets per pass) against the shipped
-k_cone_adapt, same process, 1M config-2 universes (seed 2), bench.py's two
-targets (golden.json digests.config2_filter: block = 4 care columns, whole
-board).  Per (target, op, form): back to back (20 launches between one pair
+"""A/B: the search filter and Contains, shipped (launch form by the target's
+last report) against the tuning build's fixed forms, same process, 1M
+config-2 universes (seed 2), bench.py's two targets (golden.json
+digests.config2_filter: block = 4 care columns; whole board = row 10 of every
+third column) and a whole-board target with five care rows spread over the
+column (rows 0, 12, 29, 46, 63: no row window).  Forms: dma_r8 = the LDS form
+on the uncapped grid (cone shape upw 1), dma_r8_norows = the same without
+the packed row-window pass (upw 2), capped = the capped form (upw 0, 16 blocks
+per CU).  Per (target, op, form): back to back (20 launches between one pair
 of events, median of 7) and each launch alone after a 768 MiB scrub (median
 of 10, bench.py's secondary.filter timing); answers checked against the
 shipped kernel's.  One JSON line per row."""
@@ -41,11 +44,20 @@ def main():
     n = gold["universes"]
     x = hip.fill_random(n, seed=gold["seed"])
     scrub = bench.Scrub(rt)
-    forms = {"shipped": None, "dma_r8_cap16": (16001, 8), "dma_r4_cap16": (16001, 4), "dma_r8": (1, 8)}
-    for name, t in gold["targets"].items():
-        tw, tu = (torch.from_numpy(np.array([[int(v, 16) for v in t[k]]], dtype=np.uint64).view(np.int64)).cuda()
-                  for k in ("wanted", "unwanted"))
-        for op, gens in (("filter_1gen", 1), ("filter_2gen", 2), ("contains", 0)):
+    forms = {"shipped": None, "dma_r8": (1, 8), "dma_r8_norows": (2, 8), "capped": (16000, 8)}
+    targets = {k: tuple(np.array([int(v, 16) for v in t[k2]], dtype=np.uint64) for k2 in ("wanted", "unwanted"))
+               for k, t in gold["targets"].items()}
+    full_u = np.zeros(64, np.uint64)
+    full_u[0::3] = np.uint64(0x8000400020001001)  # five care rows spread over the column: the full pass
+    targets["whole_board_5rows"] = (np.zeros(64, np.uint64), full_u)
+    ops = [("filter_1gen", 1), ("filter_2gen", 2), ("filter_4gen", 4), ("contains", 0)]
+    if os.environ.get("FILTER_AB_OPS"):
+        ops = [o for o in ops if o[0] in os.environ["FILTER_AB_OPS"].split(",")]
+    for name, (w, u) in targets.items():
+        if os.environ.get("FILTER_AB_TARGETS") and name not in os.environ["FILTER_AB_TARGETS"].split(","):
+            continue
+        tw, tu = (torch.from_numpy(v.view(np.int64)[None].copy()).cuda() for v in (w, u))
+        for op, gens in ops:
             row = {"target": name, "op": op, "universes": n}
             ref = None
             for form, shape in forms.items():

@@ -20,6 +20,15 @@ int cone_by_shape(const uint64_t *in, const uint64_t *w, const uint64_t *u, OutT
   // upw 1: k_cone_adapt with the whole board through LDS (cone_wave_full_dma, rmax sets per pass)
   if (upw == 1 && rmax == 4) return launch_cone_adapt<4, FIRST, OutT, true>(in, w, u, out, n, gens, cus, st, cap);
   if (upw == 1 && rmax == 8) return launch_cone_adapt<8, FIRST, OutT, true>(in, w, u, out, n, gens, cus, st, cap);
+  // upw 3: upw 1 with the whole-board grid capped at `cap` blocks per CU
+  if (upw == 3 && rmax == 8)
+    return launch_cone_adapt<8, FIRST, OutT, true>(in, w, u, out, n, gens, cus, st, 0, kWave, cap);
+  // upw 4: upw 1 told that the target is a whole board (the first pass fetched before the window tests)
+  if (upw == 4 && rmax == 8)
+    return launch_cone_adapt<8, FIRST, OutT, true>(in, w, u, out, n, gens, cus, st, cap, kWave, 0, kWave);
+  // upw 2: upw 1 without the packed row-window pass (cone_wave_rows_dma): every whole-board target full
+  if (upw == 2 && rmax == 8)
+    return launch_cone_adapt<8, FIRST, OutT, true, false, false>(in, w, u, out, n, gens, cus, st, cap);
   LIFEAPI_CONE(8, 8)
   LIFEAPI_CONE(16, 4)
   LIFEAPI_CONE(16, 8)
