@@ -745,7 +745,8 @@ def _lines_touched(xs: int, k: int, line: int = 128) -> int:
 def secondary_filter(hip, rt):
     """The search filter as loops consume Step (SURVEY 8(f) row 1,
     LifeTarget.hpp:44-51): 1M config-2 universes, Step() then
-    Contains(target), first hits only -- and batched Contains alone -- on the
+    Contains(target) at 1 and 2 generations, first hits only -- and batched
+    Contains alone -- on the
     light-cone kernels (cone_kernels.hpp), which read only the columns within
     one generation of the target's care columns.  Each launch is timed alone
     after a 768 MiB scrub (the cone of a small target fits in the Infinity
@@ -760,8 +761,8 @@ def secondary_filter(hip, rt):
     n = gold["universes"]
     x = hip.fill_random(n, seed=gold["seed"], device=rt.device, stream=rt.stream)
     scrub = Scrub(rt)
-    out = {"workload": f"config2 input: {n} universes, Step() then Contains(target) (first hits only), "
-                       "and Contains(target) alone",
+    out = {"workload": f"config2 input: {n} universes, Step() then Contains(target) at 1 and 2 generations "
+                       "(first hits only), and Contains(target) alone",
            "timing": "3 warm, 10 timed launches, each after a 768 MiB scrub, events around the launch only, "
                      "median; b2b: 20 launches back to back on the same input (Infinity Cache warm)",
            "targets": {}}
@@ -769,15 +770,19 @@ def secondary_filter(hip, rt):
         w, u = (np.array([int(v, 16) for v in t[k]], dtype=np.uint64) for k in ("wanted", "unwanted"))
         tw, tu = (torch.from_numpy(v.view(np.int64)[None].copy()).to(rt.device) for v in (w, u))
         first, _ = hip.step_contains(x, tw, tu, 1, stream=rt.stream)
+        first2, _ = hip.step_contains(x, tw, tu, 2, stream=rt.stream)
         cont = hip.contains(x, tw, tu, stream=rt.stream)
         rt.sync()
         fd = f"{batch_digest(first.cpu().numpy().astype(np.uint64)):016x}"
+        fd2 = f"{batch_digest(first2.cpu().numpy().astype(np.uint64)):016x}"
         cd = f"{batch_digest(cont.cpu().numpy().astype(np.uint64)):016x}"
-        hits = int((first > 0).sum().item())
-        row = {"verified": fd == t["first_digest"] and hits == t["hits"] and cd == t["contains_digest"],
-               "hits": hits}
+        hits, hits2 = int((first > 0).sum().item()), int((first2 > 0).sum().item())
+        row = {"verified": fd == t["first_digest"] and hits == t["hits"] and cd == t["contains_digest"]
+               and fd2 == t.get("first_digest_2gen") and hits2 == t.get("hits_2gen"),
+               "hits": hits, "hits_2gen": hits2}
         for op, gens, outb, fn in (
                 ("filter_1gen", 1, 4, lambda a, b: hip.step_contains(a, tw, tu, 1, stream=rt.stream)),
+                ("filter_2gen", 2, 4, lambda a, b: hip.step_contains(a, tw, tu, 2, stream=rt.stream)),
                 ("contains", 0, 1, lambda a, b: hip.contains(a, tw, tu, stream=rt.stream))):
             xs, k = _cone_columns(w, u, gens)
             lines = _lines_touched(xs, k)
@@ -908,7 +913,7 @@ def secondary_summary(line: dict, sec: dict | None, cpu: dict | None) -> dict:
             s.update(c5_kernel_ms=_r(c5["kernel_ms"]), c5_frac=_r(_get(c5, "roofline", "frac")),
                      c5_frac_hbm_only=_r(_get(c5, "roofline", "hbm_only", "frac")), c5_verified=c5.get("verified"))
         for name, row in ((flt or {}).get("targets") or {}).items():
-            for op in ("filter_1gen", "contains"):
+            for op in ("filter_1gen", "filter_2gen", "contains"):
                 s[f"{op}_{name}_ms"] = _r(_get(row, op, "kernel_ms"), 5)
                 s[f"{op}_{name}_frac"] = _r(_get(row, op, "roofline", "frac"))
             s[f"filter_{name}_verified"] = row.get("verified")

@@ -303,7 +303,7 @@ __global__ __launch_bounds__(kBlock) void k_cone(const uint64_t *in, const uint6
 // cap_waves waves looping over the batch and the rest returning after the
 // whole-board test (0: no cap).
 template <int RMAX, bool FIRST, typename OutT, bool A16 = false, bool DMA = false, bool ROWS = true>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DMA ? 10 : 1))) void k_cone_adapt(const uint64_t *in, const uint64_t *__restrict__ wanted,
+__global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const uint64_t *__restrict__ wanted,
                                                        const uint64_t *__restrict__ unwanted, OutT *__restrict__ out,
                                                        uint64_t n, uint32_t gens, uint32_t kmax, uint32_t cap_waves,
                                                        int32_t *cls, int32_t cls_last) {

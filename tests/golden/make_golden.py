@@ -249,17 +249,19 @@ def filter_targets():
 
 
 def filter_digests() -> dict:
-    """The 1-generation search filter and batched Contains on the config-2
+    """The 1- and 2-generation search filter and batched Contains on the config-2
     input (1M universes, seed 2): the reference's own Step() + Contains and
     Contains (ref_shim.cpp), as digests of the per-universe answers"""
     x = P.fill(1 << 20, seed=2)
     out = {"universes": 1 << 20, "seed": 2, "generations": 1, "targets": {}}
     for name, (w, u) in filter_targets().items():
         first, _ = R.step_contains_batch(x, w, u, 1, nthreads=8)
+        first2, _ = R.step_contains_batch(x, w, u, 2, nthreads=8)
         cont = R.contains_batch(x, w, u)
         out["targets"][name] = {
             "wanted": [f"{int(v):016x}" for v in w], "unwanted": [f"{int(v):016x}" for v in u],
             "first_digest": f"{P.digest(first.astype(np.uint64)):016x}", "hits": int((first > 0).sum()),
+            "first_digest_2gen": f"{P.digest(first2.astype(np.uint64)):016x}", "hits_2gen": int((first2 > 0).sum()),
             "contains_digest": f"{P.digest(cont.astype(np.uint64)):016x}", "contained": int(cont.sum())}
     return out
 
