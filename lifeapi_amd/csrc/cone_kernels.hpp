@@ -258,6 +258,34 @@ __device__ __forceinline__ int cone_rows(uint64_t care_col, uint32_t gens, uint3
   return need <= 8u ? 4 : need <= 16u ? 2 : need <= 32u ? 1 : 0;
 }
 
+// The filter's report word for a target (host.hpp cone_class_slot): the
+// window K (64: the whole board), and for a whole board the row-window class
+// (cone_rows: 4, 2, 1 universes per register, 0 none) in bits 8-15.
+constexpr int32_t kReportWhole = kWave;
+__device__ __forceinline__ bool report_whole(int32_t word) { return (word & 0xFF) == kReportWhole; }
+__device__ __forceinline__ int32_t report_word(uint32_t K, int pk) { return (int32_t)K | (pk << 8); }
+
+// The report of a target the split pair answers (step.hip: more generations
+// than k_cone_adapt takes unless the last report allows it): one wave
+// computes what k_cone_adapt's first wave would report and writes it, so
+// that the next call on this target can choose.
+__global__ __launch_bounds__(kWave) void k_cone_classify(const uint64_t *__restrict__ wanted,
+                                                         const uint64_t *__restrict__ unwanted, uint32_t gens,
+                                                         int32_t *cls) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const uint64_t care_col = wanted[lane] | unwanted[lane];
+  int32_t word;
+  if (cone_whole(care_col, gens)) {
+    uint32_t y0 = 0;
+    word = report_word(kWave, cone_rows(care_col, gens, y0));
+  } else {
+    uint32_t xs = 0, K = kWave;
+    cone_window(care_col, gens, xs, K);
+    word = report_word(K, 0);
+  }
+  if (lane == 0) *reinterpret_cast<volatile int32_t *>(cls) = word;
+}
+
 // UPW universes per wave (one-shot grid of ceil(n / UPW) waves), every wave
 // choosing its lane layout from the window (wave-uniform: the target is the
 // same for all).  Each choice runs its own copy of the pass.  A16: the batch
@@ -314,8 +342,8 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
   // when it differs from what the host last read there: a write to host
   // memory holds the launch's end by a PCIe round trip, so a target that
   // keeps its window costs it once
-  auto report = [&](uint32_t k) __attribute__((always_inline)) {
-    if (cls && wave == 0 && lane == 0 && (int32_t)k != cls_last) *reinterpret_cast<volatile int32_t *>(cls) = (int32_t)k;
+  auto report = [&](int32_t word) __attribute__((always_inline)) {
+    if (cls && wave == 0 && lane == 0 && word != cls_last) *reinterpret_cast<volatile int32_t *>(cls) = word;
   };
   // (the smallest chunk any path takes: a wave starting past n has no work)
   constexpr uint64_t kMinChunk = DMA && 2 * RMAX < 16 ? 2 * RMAX : 16;
@@ -331,17 +359,18 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
     // pass is fetched before the window tests, which then run under it (a
     // wave that turns out not to need it waits for it before leaving: LDS-DMA
     // still in flight must not outlive the wave's LDS)
-    const bool early = cls_last == kWave && wave * c < n;
+    const bool early = (cls_last & 0xFF) == kReportWhole && wave * c < n;
     if (early) dma_fetch_pass<RMAX>(in, n, wave * c, lane, img);
     auto leave = [&]() __attribute__((always_inline)) {
       if (early) __builtin_amdgcn_s_waitcnt(kWaitVm0);
     };
     if (cone_whole(care_col, g)) {
-      report(kWave);
+      uint32_t y0 = 0;
+      int pk = 0;
+      if constexpr (FIRST) pk = cone_rows(care_col, gens, y0);
+      report(report_word(kWave, pk));
       if (kmax < (uint32_t)kWave || wave * c >= n) return leave();
       if constexpr (FIRST && ROWS) {
-        uint32_t y0 = 0;
-        const int pk = cone_rows(care_col, gens, y0);
         auto rows = [&](auto pk_c, auto wrap_c) __attribute__((always_inline)) {
           cone_wave_rows_dma<RMAX, decltype(pk_c)::value, decltype(wrap_c)::value>(
               in, w64, m64, out, n, wave * c, nw * c, gens, y0, lane, img, early);
@@ -362,7 +391,7 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
       nw = nw < cap_waves ? nw : cap_waves;
     }
     cone_window(care_col, g, xs, K);
-    report(K);
+    report(report_word(K, 0));
     if (K > kmax) return leave();
     if (K == (uint32_t)kWave) {
       if (wave * c >= n) return leave();
@@ -370,8 +399,14 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
     }
     leave();
   } else {
-    if (!cone_whole(care_col, g)) cone_window(care_col, g, xs, K);
-    report(K);
+    int pk = 0;
+    if (!cone_whole(care_col, g)) {
+      cone_window(care_col, g, xs, K);
+    } else if constexpr (FIRST) {
+      uint32_t y0 = 0;
+      if (cls && wave == 0) pk = cone_rows(care_col, gens, y0);  // (only the report needs it)
+    }
+    report(report_word(K, pk));
     if (K > kmax) return;
   }
   if constexpr (!FIRST && A16 && !DMA) {
@@ -412,6 +447,9 @@ constexpr int kConeAdaptBlocksPerCU = 16;
 // whole-board target at 64K-128K, 0.83-1.02 at 256K, but 1.07-1.14 on the
 // whole board at 512K.
 constexpr uint32_t kConeAloneGens = 4, kConeAloneGensSmall = 6;
+// Beyond those, up to this many generations (exclusive), a whole-board target
+// whose row window fits 32 rows (cone_rows) keeps k_cone_adapt (step.hip).
+constexpr uint32_t kConeRowsMaxGens = 16;
 constexpr uint64_t kConeAloneSmallUniverses = 1u << 18;
 // The iterated search loop (gens > 2, no final states) steps the light cone
 // while it spans at most this many columns (P <= 32 lanes per universe: at
@@ -467,7 +505,7 @@ int launch_cone_adapt(const uint64_t *d_in, const uint64_t *d_wanted, const uint
   if constexpr (AUTO) {
     const int rc = cone_class_slot(d_wanted, d_unwanted, gens, cls, last_k);
     if (rc != LIFEAPI_OK) return rc;
-    dma = last_k == kWave && kmax >= (uint32_t)kWave;
+    dma = (last_k & 0xFF) == kReportWhole && kmax >= (uint32_t)kWave;
   }
   if constexpr (DMA || AUTO) {
     if (dma && aligned16(d_in)) {  // the uncapped grid; the cap applies to the waves of a windowed target

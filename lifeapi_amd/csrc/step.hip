@@ -168,6 +168,30 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
                                                                      generations, cus, (hipStream_t)stream,
                                                                      kConeAdaptBlocksPerCU);
   }
+  // More generations without final states: a whole-board target whose care
+  // rows, widened by the light cone, fit 32 rows (as the last report on this
+  // target says: launch_cone_adapt) keeps k_cone_adapt's packed row-window
+  // pass, which is 1.5-2x the split pair below on a one-row target (1M
+  // universes at 5 / 8 / 12 generations: 0.116 / 0.190 / 0.269 ms against
+  // 0.234 / 0.297 / 0.400; tools/filter_gens_ab.py, profiles/r05/gens/).  A
+  // target with no report yet takes the split pair, and one wave of
+  // k_cone_classify writes its report for the next call.
+  if (!d_final && generations < kConeRowsMaxGens && aligned16(d_in)) {
+    int32_t *slot = nullptr;
+    int last = -1;
+    rc = cone_class_slot(d_wanted, d_unwanted, generations, slot, last);
+    if (rc != LIFEAPI_OK) return rc;
+    if (last >= 0 && (last & 0xFF) == kWave && (last >> 8) > 0)
+      return launch_cone_adapt<kConeSets, true, uint32_t, false, true>(d_in, d_wanted, d_unwanted, d_first_gen, n,
+                                                                       generations, cus, (hipStream_t)stream,
+                                                                       kConeAdaptBlocksPerCU);
+    if (slot && last < 0) {
+      hipLaunchKernelGGL(k_cone_classify, dim3(1), dim3(kWave), 0, (hipStream_t)stream, d_wanted, d_unwanted,
+                         generations, slot);
+      rc = launched("k_cone_classify launch");
+      if (rc != LIFEAPI_OK) return rc;
+    }
+  }
   if (generations > 2) {  // the layout of the shipped step for gens > 2
     // Without final states, a target whose light cone over `generations`
     // spans at most kConeIterColumns columns is answered on that cone:

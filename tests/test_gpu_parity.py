@@ -873,10 +873,10 @@ def _rows_target(rows, cols, wanted_at=None):
 
 
 @pytest.mark.parametrize("rows,gens_list", [
-    ((10,), (1, 2, 3, 4, 6)),              # 8-row fields up to 3 generations, then 16
-    ((61, 62, 63, 0, 1), (1, 2, 5)),       # a window across row 63 (8, 16, 32 rows)
-    ((30, 31, 32, 33), (1, 2, 6)),         # across the two 32-bit halves
-    (tuple(range(40, 54)), (1, 2, 3, 4)),  # 16-row fields at 1, then 32, then the full pass
+    ((10,), (1, 2, 3, 4, 6, 8, 12, 15, 16)),  # 8-row fields up to 3 generations, 16 to 7, 32 to 15
+    ((61, 62, 63, 0, 1), (1, 2, 5, 8)),       # a window across row 63 (8, 16, 32 rows)
+    ((30, 31, 32, 33), (1, 2, 6, 10)),        # across the two 32-bit halves
+    (tuple(range(40, 54)), (1, 2, 3, 9, 10)),  # 16-row fields at 1, 32 to 9 (no slack), then the full pass
     (tuple(range(64)), (1, 2)),            # every row: the full pass
 ])
 def test_filter_whole_board_row_windows(hip, port, rows, gens_list):
@@ -885,7 +885,9 @@ def test_filter_whole_board_row_windows(hip, port, rows, gens_list):
     cone_wave_rows_dma: 4, 2 or 1 universes per 32-bit register, shifts for
     the vertical neighbours) in the LDS form; windows across row 63 and across
     the 32-bit halves; every call against the oracle (first call the capped
-    form, the next two the LDS form), ragged n."""
+    form, the next two the LDS form), ragged n.  Beyond k_cone_adapt's own
+    generation limit the first call takes the split pair and classifies the
+    target (k_cone_classify), the next ones the row-window pass (step.hip)."""
     n = 70001
     x = port.fill(n, seed=93) & port.fill(n, seed=94) & port.fill(n, seed=95)
     d = to_dev(x)

@@ -179,13 +179,17 @@ def main():
     both("k_cone Contains, whole-board target", n, 513, lambda: hip.contains(x, w, w))
     both("k_cone 1 gen (first hit only), whole-board target", n, 516, lambda: hip.step_contains(x, w, w, 1))
     # bench.py's whole-board target (row 10 of every third column must be dead):
-    # its care rows, widened by the light cone, fit 8 rows up to 3 generations,
-    # so the filter runs the packed row-window pass
+    # its care rows, widened by the light cone, fit 8 rows up to 3 generations
+    # (16 to 7, 32 to 15), so the filter runs the packed row-window pass
+    # (DESIGN.md 3.2), beyond 4 generations too
     rw, ru = torch.zeros_like(w), torch.zeros_like(w)
     ru[0, 0::3] = 1 << 10
-    for gens in (1, 2, 4):
-        both(f"k_cone {gens} gen (first hit only), whole-board target of one care row", n, 516,
+    for gens in (1, 2, 3, 5, 8):
+        both(f"filter {gens} gen (first hit only), whole-board target of one care row", n, 516,
              lambda g=gens: hip.step_contains(x, rw, ru, g))
+    for gens in (3, 5, 8):  # every row cares: the full pass to 4 generations, then the split pair
+        both(f"filter {gens} gen (first hit only), whole-board target, every row", n, 516,
+             lambda g=gens: hip.step_contains(x, w, w, g))
     bw, bu = torch.zeros_like(w), torch.zeros_like(w)
     bw[0, 10] = bw[0, 11] = 3 << 40
     bu[0, 9:13] = 15 << 39
