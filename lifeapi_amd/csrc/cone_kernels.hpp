@@ -259,11 +259,14 @@ __device__ __forceinline__ int cone_rows(uint64_t care_col, uint32_t gens, uint3
 }
 
 // The filter's report word for a target (host.hpp cone_class_slot): the
-// window K (64: the whole board), and for a whole board the row-window class
-// (cone_rows: 4, 2, 1 universes per register, 0 none) in bits 8-15.
+// window K (64: the whole board) in bits 0-7, and for a whole board the
+// row-window class (cone_rows: 4, 2, 1 universes per register, 0 none) in
+// bits 8-15 and its first row y0 in bits 16-21.
 constexpr int32_t kReportWhole = kWave;
 __device__ __forceinline__ bool report_whole(int32_t word) { return (word & 0xFF) == kReportWhole; }
-__device__ __forceinline__ int32_t report_word(uint32_t K, int pk) { return (int32_t)K | (pk << 8); }
+__device__ __forceinline__ int32_t report_word(uint32_t K, int pk, uint32_t y0 = 0) {
+  return (int32_t)K | (pk << 8) | (pk ? (int32_t)(y0 & 63u) << 16 : 0);
+}
 
 // The report of a target the split pair answers (step.hip: more generations
 // than k_cone_adapt takes unless the last report allows it): one wave
@@ -277,7 +280,8 @@ __global__ __launch_bounds__(kWave) void k_cone_classify(const uint64_t *__restr
   int32_t word;
   if (cone_whole(care_col, gens)) {
     uint32_t y0 = 0;
-    word = report_word(kWave, cone_rows(care_col, gens, y0));
+    const int pk = cone_rows(care_col, gens, y0);
+    word = report_word(kWave, pk, y0);
   } else {
     uint32_t xs = 0, K = kWave;
     cone_window(care_col, gens, xs, K);
@@ -364,11 +368,30 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
     auto leave = [&]() __attribute__((always_inline)) {
       if (early) __builtin_amdgcn_s_waitcnt(kWaitVm0);
     };
-    if (cone_whole(care_col, g)) {
-      uint32_t y0 = 0;
-      int pk = 0;
-      if constexpr (FIRST) pk = cone_rows(care_col, gens, y0);
-      report(report_word(kWave, pk));
+    // the row window: every wave but the first takes the one the last report
+    // on this target gave, once one ballot shows the care rows inside its
+    // exact interior (the row-window pass is exact for any columns, so the
+    // whole-board test is not needed then); the first wave, and every wave
+    // without such a report, find it themselves
+    int pk = 0;
+    uint32_t y0 = 0;
+    bool whole = false, hinted = false;
+    if constexpr (FIRST && ROWS) {
+      const int hpk = (cls_last >> 8) & 0xFF;
+      if (wave != 0 && report_whole(cls_last) && hpk && gens < 16u && 2u * gens < 32u / (uint32_t)hpk) {
+        const uint32_t hy0 = ((uint32_t)cls_last >> 16) & 63u, inner_w = 32u / (uint32_t)hpk - 2u * gens;
+        const uint64_t inner = rotr64((1ull << inner_w) - 1ull, (64u - ((hy0 + gens) & 63u)) & 63u);
+        if (__ballot((care_col & ~inner) != 0ull) == 0ull) pk = hpk, y0 = hy0, whole = hinted = true;
+      }
+    }
+    if (!hinted) {
+      whole = cone_whole(care_col, g);
+      if (whole) {
+        if constexpr (FIRST) pk = cone_rows(care_col, gens, y0);
+        report(report_word(kWave, pk, y0));
+      }
+    }
+    if (whole) {
       if (kmax < (uint32_t)kWave || wave * c >= n) return leave();
       if constexpr (FIRST && ROWS) {
         auto rows = [&](auto pk_c, auto wrap_c) __attribute__((always_inline)) {
@@ -400,13 +423,13 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
     leave();
   } else {
     int pk = 0;
+    uint32_t y0 = 0;
     if (!cone_whole(care_col, g)) {
       cone_window(care_col, g, xs, K);
     } else if constexpr (FIRST) {
-      uint32_t y0 = 0;
       if (cls && wave == 0) pk = cone_rows(care_col, gens, y0);  // (only the report needs it)
     }
-    report(report_word(K, pk));
+    report(report_word(K, pk, y0));
     if (K > kmax) return;
   }
   if constexpr (!FIRST && A16 && !DMA) {

@@ -26,6 +26,9 @@ int cone_by_shape(const uint64_t *in, const uint64_t *w, const uint64_t *u, OutT
   // upw 4: upw 1 told that the target is a whole board (the first pass fetched before the window tests)
   if (upw == 4 && rmax == 8)
     return launch_cone_adapt<8, FIRST, OutT, true>(in, w, u, out, n, gens, cus, st, cap, kWave, 0, kWave);
+  // upw 5: upw 4 with rmax >> 8 as the last report word (the row-window hint: K | class << 8 | y0 << 16)
+  if (upw == 5 && (rmax & 0xFF) == 8)
+    return launch_cone_adapt<8, FIRST, OutT, true>(in, w, u, out, n, gens, cus, st, cap, kWave, 0, rmax >> 8);
   // upw 2: upw 1 without the packed row-window pass (cone_wave_rows_dma): every whole-board target full
   if (upw == 2 && rmax == 8)
     return launch_cone_adapt<8, FIRST, OutT, true, false, false>(in, w, u, out, n, gens, cus, st, cap);
