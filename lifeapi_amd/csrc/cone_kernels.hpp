@@ -258,6 +258,16 @@ __device__ __forceinline__ int cone_rows(uint64_t care_col, uint32_t gens, uint3
   return need <= 8u ? 4 : need <= 16u ? 2 : need <= 32u ? 1 : 0;
 }
 
+// Waves after the first take the row window from the last report from this
+// many generations on.  1M universes, bench.py's whole-board target, each
+// launch alone after a scrub, interleaved with the same launch finding the
+// window itself (tools/filter_interleave.py rows_hint / rows_early,
+// profiles/r05/hint/): 3 / 4 / 5 / 8 generations 0.081 / 0.096 / 0.109 /
+// 0.188 ms against 0.095 / 0.108 / 0.122 / 0.194; at 1 generation no
+// difference (0.083-0.085 both), at 2 it costs 4 % (0.086 against 0.082,
+// unexplained; every series on the box agreed).
+constexpr uint32_t kConeHintGens = 3;
+
 // The filter's report word for a target (host.hpp cone_class_slot): the
 // window K (64: the whole board) in bits 0-7, and for a whole board the
 // row-window class (cone_rows: 4, 2, 1 universes per register, 0 none) in
@@ -368,17 +378,19 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
     auto leave = [&]() __attribute__((always_inline)) {
       if (early) __builtin_amdgcn_s_waitcnt(kWaitVm0);
     };
-    // the row window: every wave but the first takes the one the last report
-    // on this target gave, once one ballot shows the care rows inside its
-    // exact interior (the row-window pass is exact for any columns, so the
-    // whole-board test is not needed then); the first wave, and every wave
-    // without such a report, find it themselves
+    // the row window: from kConeHintGens generations on, every wave but the
+    // first takes the one the last report on this target gave, once one
+    // ballot shows the care rows inside its exact interior (the row-window
+    // pass is exact for any columns, so the whole-board test is not needed
+    // then); the first wave, and every wave without such a report, find it
+    // themselves
     int pk = 0;
     uint32_t y0 = 0;
     bool whole = false, hinted = false;
     if constexpr (FIRST && ROWS) {
       const int hpk = (cls_last >> 8) & 0xFF;
-      if (wave != 0 && report_whole(cls_last) && hpk && gens < 16u && 2u * gens < 32u / (uint32_t)hpk) {
+      if (wave != 0 && gens >= kConeHintGens && report_whole(cls_last) && hpk && gens < 16u &&
+          2u * gens < 32u / (uint32_t)hpk) {
         const uint32_t hy0 = ((uint32_t)cls_last >> 16) & 63u, inner_w = 32u / (uint32_t)hpk - 2u * gens;
         const uint64_t inner = rotr64((1ull << inner_w) - 1ull, (64u - ((hy0 + gens) & 63u)) & 63u);
         if (__ballot((care_col & ~inner) != 0ull) == 0ull) pk = hpk, y0 = hy0, whole = hinted = true;
