@@ -825,7 +825,11 @@ def test_filter_launch_form_follows_the_target(hip, port):
     the first call on a whole-board target runs the capped form, the next ones
     the LDS form on the uncapped grid; rewriting the target in place to a
     small one leaves one call on the stale form, which must still be exact.
-    Every call against the oracle, at 1 and 2 generations, ragged n."""
+    From 3 generations the waves after the first take the row window from the
+    report (cone_kernels.hpp kConeHintGens): a small target in the whole-board
+    target's rows runs on that stale window in those waves and on its own
+    window in the first -- overlapping chunks, both exact.  Every call against
+    the oracle, at 1, 2, 3 and 5 generations, ragged n."""
     n = 70001
     x = port.fill(n, seed=91) & port.fill(n, seed=92)
     d = to_dev(x)
@@ -845,15 +849,18 @@ def test_filter_launch_form_follows_the_target(hip, port):
             hit = (((s ^ w) & (w | u)) == 0).all(axis=1)
             res[(res == 0) & hit] = g
         return res
-    for gens in (1, 2):
-        for w, u in ((np.zeros(64, np.uint64), whole_u), (small_w, small_u)):
+    row10_u = np.zeros(64, np.uint64)  # care row 10 in four columns: fits a whole-board report's row window
+    row10_u[20:24] = np.uint64(1 << 10)
+    zero = np.zeros(64, np.uint64)
+    for gens in (1, 2, 3, 5):
+        for w, u in ((zero, whole_u), (small_w, small_u), (zero, whole_u), (zero, row10_u), (zero, whole_u)):
             tw.copy_(to_dev(w[None]).reshape(1, 64))
             tu.copy_(to_dev(u[None]).reshape(1, 64))
             exp = want(w, u, gens)
             for _ in range(3):  # first call: the last report is stale or absent; then the target's own form
                 first, _ = hip.step_contains(d, tw, tu, gens)
                 torch.cuda.synchronize()
-                assert (first.cpu().numpy().astype(np.uint32) == exp).all(), (gens, int(w.any()))
+                assert (first.cpu().numpy().astype(np.uint32) == exp).all(), (gens, int(w.any()), int(np.count_nonzero(u)))
 
 
 def _rows_target(rows, cols, wanted_at=None):
