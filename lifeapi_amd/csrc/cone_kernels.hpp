@@ -167,7 +167,7 @@ __device__ __forceinline__ void cone_wave_full_dma(const uint64_t *in, uint64_t 
 // (the DPP rotate is the torus), so the care cells are exact.  Same passes,
 // LDS image and answers as cone_wave_full_dma; a universe costs one cut, a
 // share of the pack, 1 / PK of the network and its field's test.
-template <int RB, int PK, bool WRAP, typename OutT>
+template <int RB, int PK, bool WRAP, typename OutT, int SLEEP = 0>
 __device__ __forceinline__ void cone_wave_rows_dma(const uint64_t *in, uint64_t w64, uint64_t m64,
                                                    OutT *__restrict__ out, uint64_t n, uint64_t u_first,
                                                    uint64_t u_step, uint32_t gens, uint32_t y0, int lane,
@@ -214,6 +214,7 @@ __device__ __forceinline__ void cone_wave_rows_dma(const uint64_t *in, uint64_t 
     __builtin_amdgcn_s_waitcnt(kWaitLgkm0);  // read out before the next fetch lands
     const uint64_t nb = base(t + 1);
     if (nb < n) fetch(nb);
+    if constexpr (SLEEP > 0) __builtin_amdgcn_s_sleep(SLEEP);  // (the tuning build's pacing probe)
     uint32_t res[RB];
 #pragma unroll
     for (int k = 0; k < RB; ++k) res[k] = 0;

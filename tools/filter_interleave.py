@@ -12,7 +12,9 @@ most C blocks per CU looping over the batch), rows_early (upw 4: rows with
 the first pass fetched before the window tests, as the shipped launch does
 after a whole-board report), rows_hint (upw 5: rows_early given the report
 word the shipped launch gets, so that all waves but the first take the row
-window from it after one ballot), capped (upw 0, 16 blocks per CU), and
+window from it after one ballot), probe_sS (with PROBE=1: the pass with no
+window search and s_sleep(S) after each next-pass fetch, tune_cone.hip
+k_rows_probe), capped (upw 0, 16 blocks per CU), and
 Contains (shipped, and the LDS form).  One JSON line per generation count:
 median, 10th and 90th percentile per form, answers checked against the
 shipped form."""
@@ -77,6 +79,8 @@ def main():
             "rows_cap16": lambda: tune.cone(x, tw, tu, gens, 16003, 8, first=True),
             "norows": lambda: tune.cone(x, tw, tu, gens, 2, 8, first=True),
             "capped": lambda: tune.cone(x, tw, tu, gens, 16000, 8, first=True),
+            **({f"probe_s{sl}": (lambda sl=sl: tune.rows_probe(x, tw, tu, gens, (r - gens) & 63, sl))
+                for sl in (0, 2, 8)} if pk == 4 and os.environ.get("PROBE") else {}),
             "contains": lambda: hip.contains(x, tw, tu),
             "contains_lds": lambda: tune.cone(x, tw, tu, 0, 1, 8, first=False),
         }

@@ -78,9 +78,51 @@ __global__ __launch_bounds__(kBlock) void k_line_read(const uint64_t *in, uint32
   if (u0 + lane < n) out[u0 + lane] = mine;
 }
 
+// Pacing probe: the row-window pass (cone_wave_rows_dma, 4 universes per
+// register) with no window search -- y0 given, the first pass fetched at
+// once -- and s_sleep(SLEEP) after each next-pass fetch; uncapped grid of
+// chunks of 16 universes.  For targets whose care rows, widened by gens, lie
+// in rows y0 + gens .. y0 + 7 - gens (the caller's to ensure).
+template <int SLEEP>
+__global__ __launch_bounds__(kBlock) void k_rows_probe(const uint64_t *in, const uint64_t *__restrict__ wanted,
+                                                       const uint64_t *__restrict__ unwanted, uint32_t *out,
+                                                       uint64_t n, uint32_t gens, uint32_t y0) {
+  __shared__ uint64_t img_all[kWavesPerBlock][8 * kWave];
+  const int lane = threadIdx.x & (kWave - 1);
+  const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
+  if (wave * 16 >= n) return;
+  uint64_t *img = img_all[__builtin_amdgcn_readfirstlane(threadIdx.x / kWave)];
+  dma_fetch_pass<8>(in, n, wave * 16, lane, img);
+  const uint64_t w64 = wanted[lane], m64 = w64 | unwanted[lane];
+  if (y0 >= 32u)
+    cone_wave_rows_dma<8, 4, true, uint32_t, SLEEP>(in, w64, m64, out, n, wave * 16, nw * 16, gens, y0, lane, img,
+                                                      true);
+  else
+    cone_wave_rows_dma<8, 4, false, uint32_t, SLEEP>(in, w64, m64, out, n, wave * 16, nw * 16, gens, y0, lane, img,
+                                                       true);
+}
+
 }  // namespace
 
 extern "C" {
+
+/* k_rows_probe with s_sleep `sleep` (0, 1, 2, 4, 8, 16) */
+int lifeapi_tune_rows_probe(const uint64_t *d_in, const uint64_t *d_wanted, const uint64_t *d_unwanted,
+                            uint32_t *d_out, size_t n, uint32_t gens, uint32_t y0, int sleep, void *stream) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!d_in || !d_wanted || !d_unwanted || !d_out || !aligned16(d_in) || y0 > 63)
+    return fail(LIFEAPI_E_INVALID, "bad argument to lifeapi_tune_rows_probe%s");
+  int cus = 0, rc = device_cus(cus);
+  if (rc != LIFEAPI_OK) return rc;
+  const dim3 grid(grid_for((n + 15) / 16, cus, 0));
+  using Fn = void (*)(const uint64_t *, const uint64_t *, const uint64_t *, uint32_t *, uint64_t, uint32_t, uint32_t);
+  Fn fn = sleep == 1 ? k_rows_probe<1> : sleep == 2 ? k_rows_probe<2> : sleep == 4 ? k_rows_probe<4>
+        : sleep == 8 ? k_rows_probe<8> : sleep == 16 ? k_rows_probe<16> : k_rows_probe<0>;
+  hipLaunchKernelGGL(fn, grid, dim3(kBlock), 0, (hipStream_t)stream, d_in, d_wanted, d_unwanted, d_out, (uint64_t)n,
+                     gens, y0);
+  return launched("k_rows_probe launch");
+}
 
 int lifeapi_tune_line_read(const uint64_t *d_in, uint32_t *d_out, size_t n, int line, void *stream) {
   if (n == 0) return LIFEAPI_OK;

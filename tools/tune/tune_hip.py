@@ -346,3 +346,18 @@ def stable_rep(planes: torch.Tensor, which: int, reps: int, stream=None):
     flags = torch.empty(n, dtype=torch.uint8, device=planes.device)
     hip._check(lib.lifeapi_tune_stable_rep(planes.data_ptr(), flags.data_ptr(), n, which, reps, hip._stream(stream)))
     return flags
+
+
+lib.lifeapi_tune_rows_probe.argtypes = [_vp, _vp, _vp, _vp, _sz, _u32, _u32, _int, _vp]
+lib.lifeapi_tune_rows_probe.restype = _int
+
+
+def rows_probe(states, wanted, unwanted, generations, y0, sleep=0, out=None, stream=None):
+    """the row-window filter pass, window given, s_sleep(sleep) after each
+    next-pass fetch (tune_cone.hip k_rows_probe)"""
+    n = hip._universes(states)
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=states.device)
+    hip._check(lib.lifeapi_tune_rows_probe(states.data_ptr(), wanted.data_ptr(), unwanted.data_ptr(), out.data_ptr(),
+                                           n, generations, y0, sleep, hip._stream(stream)))
+    return out
