@@ -301,50 +301,6 @@ __global__ __launch_bounds__(kWave) void k_cone_classify(const uint64_t *__restr
   if (lane == 0) *reinterpret_cast<volatile int32_t *>(cls) = word;
 }
 
-// The search filter (first hits, 1 <= gens < 16) on a target whose last
-// report gave a row window (`hint`, launch_cone_adapt AUTO): every wave
-// fetches its first pass at once, takes the row-window pass when one ballot
-// finds the care rows inside the window's exact interior, else the
-// whole-board pass (exact for any target, only slower); the first wave also
-// reports the target's own window.  Only these two passes, so it fits 10
-// waves per SIMD, all the LDS holds (k_cone_adapt's LDS form: 9).
-template <int RMAX>
-__global__ __launch_bounds__(kBlock) void k_cone_rows(const uint64_t *in, const uint64_t *__restrict__ wanted,
-                                                      const uint64_t *__restrict__ unwanted, uint32_t *out,
-                                                      uint64_t n, uint32_t gens, int32_t *cls, int32_t hint) {
-  __shared__ uint64_t img_all[kWavesPerBlock][RMAX * kWave];
-  const int lane = threadIdx.x & (kWave - 1);
-  const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock, c = 2 * RMAX;
-  if (wave * c >= n) return;
-  uint64_t *img = img_all[__builtin_amdgcn_readfirstlane(threadIdx.x / kWave)];
-  dma_fetch_pass<RMAX>(in, n, wave * c, lane, img);
-  const uint64_t w64 = wanted[lane], m64 = w64 | unwanted[lane];
-  if (cls && wave == 0) {
-    const int32_t word = cone_report(m64, gens);
-    if (lane == 0 && word != hint) *reinterpret_cast<volatile int32_t *>(cls) = word;
-  }
-  const int pk = (hint >> 8) & 0xFF;
-  const uint32_t y0 = ((uint32_t)hint >> 16) & 63u;
-  bool fits = (pk == 1 || pk == 2 || pk == 4) && gens < 16u && 2u * gens < 32u / (uint32_t)pk;
-  if (fits) {
-    const uint64_t inner = rotr64((1ull << (32u / (uint32_t)pk - 2u * gens)) - 1ull, (64u - ((y0 + gens) & 63u)) & 63u);
-    fits = __ballot((m64 & ~inner) != 0ull) == 0ull;
-  }
-  if (fits) {
-    auto rows = [&](auto pk_c, auto wrap_c) __attribute__((always_inline)) {
-      cone_wave_rows_dma<RMAX, decltype(pk_c)::value, decltype(wrap_c)::value>(in, w64, m64, out, n, wave * c, nw * c,
-                                                                               gens, y0, lane, img, true);
-    };
-    using T = std::true_type;
-    using F = std::false_type;
-    if (pk == 4) return y0 >= 32u ? rows(std::integral_constant<int, 4>{}, T{}) : rows(std::integral_constant<int, 4>{}, F{});
-    if (pk == 2) return y0 >= 32u ? rows(std::integral_constant<int, 2>{}, T{}) : rows(std::integral_constant<int, 2>{}, F{});
-    return y0 >= 32u ? rows(std::integral_constant<int, 1>{}, T{}) : rows(std::integral_constant<int, 1>{}, F{});
-  }
-  cone_wave_full_dma<RMAX, true>(in, w64, m64, out, n, wave * c, nw * c, gens, lane, img, true);
-}
-
 // UPW universes per wave (one-shot grid of ceil(n / UPW) waves), every wave
 // choosing its lane layout from the window (wave-uniform: the target is the
 // same for all).  Each choice runs its own copy of the pass.  A16: the batch
@@ -565,15 +521,6 @@ int launch_cone(const uint64_t *d_in, const uint64_t *d_wanted, const uint64_t *
   hipLaunchKernelGGL((k_cone<UPW, RMAX, FIRST, OutT, false, PIPE>), grid, dim3(kBlock), 0, stream, d_in, d_wanted,
                      d_unwanted, d_out, (uint64_t)n, gens, kmax);
   return launched("k_cone launch");
-}
-
-// Launches k_cone_rows on ceil(n / 2 RMAX) waves (a 16-byte aligned batch).
-template <int RMAX>
-int launch_cone_rows(const uint64_t *d_in, const uint64_t *d_wanted, const uint64_t *d_unwanted, uint32_t *d_out,
-                     size_t n, uint32_t gens, int cus, hipStream_t stream, int32_t *cls, int32_t hint) {
-  hipLaunchKernelGGL(k_cone_rows<RMAX>, dim3(grid_for((n + 2 * RMAX - 1) / (2 * RMAX), cus, 0)), dim3(kBlock), 0,
-                     stream, d_in, d_wanted, d_unwanted, d_out, (uint64_t)n, gens, cls, hint);
-  return launched("k_cone_rows launch");
 }
 
 // Launches k_cone_adapt on ceil(n / 16) waves, at most blocks_per_cu blocks

@@ -12,9 +12,7 @@ most C blocks per CU looping over the batch), rows_early (upw 4: rows with
 the first pass fetched before the window tests, as the shipped launch does
 after a whole-board report), rows_hint (upw 5: rows_early given the report
 word the shipped launch gets, so that all waves but the first take the row
-window from it after one ballot), rows_lean (upw 6: k_cone_rows, the
-row-window and whole-board passes alone, given the same report word),
-probe_sS (with PROBE=1: the pass with no
+window from it after one ballot), probe_sS (with PROBE=1: the pass with no
 window search and s_sleep(S) after each next-pass fetch, tune_cone.hip
 k_rows_probe), capped (upw 0, 16 blocks per CU), and
 Contains (shipped, and the LDS form).  One JSON line per generation count:
@@ -78,7 +76,6 @@ def main():
             "rows": lambda: tune.cone(x, tw, tu, gens, 1, 8, first=True),
             "rows_early": lambda: tune.cone(x, tw, tu, gens, 4, 8, first=True),
             "rows_hint": lambda: tune.cone(x, tw, tu, gens, 5, 8 | (hint << 8), first=True),
-            "rows_lean": lambda: tune.cone(x, tw, tu, gens, 6, 8 | (hint << 8), first=True),
             "rows_cap16": lambda: tune.cone(x, tw, tu, gens, 16003, 8, first=True),
             "norows": lambda: tune.cone(x, tw, tu, gens, 2, 8, first=True),
             "capped": lambda: tune.cone(x, tw, tu, gens, 16000, 8, first=True),
