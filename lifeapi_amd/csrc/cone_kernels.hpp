@@ -268,6 +268,9 @@ __device__ __forceinline__ int cone_rows(uint64_t care_col, uint32_t gens, uint3
 // difference (0.083-0.085 both), at 2 it costs 4 % (0.086 against 0.082,
 // unexplained; every series on the box agreed).
 constexpr uint32_t kConeHintGens = 3;
+// A column window (5-32 columns) takes the row window too from this many
+// generations on (cone_wave_rows; below it the pass is not VALU-bound).
+constexpr uint32_t kConeRowsWindowGens = 3;
 
 // The filter's report word for a target (host.hpp cone_class_slot): the
 // window K (64: the whole board) in bits 0-7, and for a whole board the
@@ -289,9 +292,9 @@ __device__ __forceinline__ int32_t cone_report(uint64_t care_col, uint32_t gens)
     const int pk = cone_rows(care_col, gens, y0);
     return report_word(kWave, pk, y0);
   }
-  uint32_t xs = 0, K = kWave;
+  uint32_t xs = 0, K = kWave, y0 = 0;
   cone_window(care_col, gens, xs, K);
-  return report_word(K, 0);
+  return report_word(K, cone_rows(care_col, gens, y0), y0);
 }
 __global__ __launch_bounds__(kWave) void k_cone_classify(const uint64_t *__restrict__ wanted,
                                                          const uint64_t *__restrict__ unwanted, uint32_t gens,
@@ -427,7 +430,14 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
       nw = nw < cap_waves ? nw : cap_waves;
     }
     cone_window(care_col, g, xs, K);
-    report(report_word(K, 0));
+    {
+      int wpk = 0;
+      uint32_t wy0 = 0;
+      if constexpr (FIRST) {
+        if (cls && wave == 0) wpk = cone_rows(care_col, gens, wy0);  // (only the report needs it)
+      }
+      report(report_word(K, wpk, wy0));
+    }
     if (K > kmax) return leave();
     if (K == (uint32_t)kWave) {
       if (wave * c >= n) return leave();
@@ -439,11 +449,47 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
     uint32_t y0 = 0;
     if (!cone_whole(care_col, g)) {
       cone_window(care_col, g, xs, K);
+      // (the row window of a column window: cone_wave_rows, below)
+      if constexpr (FIRST && ROWS) {
+        if (gens >= kConeRowsWindowGens || (cls && wave == 0)) pk = cone_rows(care_col, gens, y0);
+      }
     } else if constexpr (FIRST) {
       if (cls && wave == 0) pk = cone_rows(care_col, gens, y0);  // (only the report needs it)
     }
     report(report_word(K, pk, y0));
     if (K > kmax) return;
+    if constexpr (FIRST && ROWS) {
+      // a column window of 5-32 columns whose rows, widened by the cone, fit
+      // 32 (16) rows: 1 (2) universes per register and lane, rows cut to the
+      // window (cone_wave_rows)
+      if (pk > 0 && K > 4u && K <= 32u && gens >= kConeRowsWindowGens) {
+        auto rw = [&](auto p_c, auto upw_c, auto pk_c, auto wrap_c) __attribute__((always_inline)) {
+          constexpr int UPWc = decltype(upw_c)::value;
+          if (wave * UPWc >= n) return;
+          cone_wave_rows<decltype(p_c)::value, UPWc, RMAX, decltype(pk_c)::value, decltype(wrap_c)::value>(
+              in, wanted, unwanted, out, n, wave * UPWc, nw * UPWc, gens, xs, K, y0, lane);
+        };
+        using I8 = std::integral_constant<int, 8>;
+        using I16 = std::integral_constant<int, 16>;
+        using I32 = std::integral_constant<int, 32>;
+        using I64 = std::integral_constant<int, 64>;
+        using K1 = std::integral_constant<int, 1>;
+        using K2 = std::integral_constant<int, 2>;
+        using T = std::true_type;
+        using F = std::false_type;
+        const bool wrap = y0 >= 32u, two = pk >= 2;
+        if (K <= 8u) {
+          if (two) return wrap ? rw(I8{}, I64{}, K2{}, T{}) : rw(I8{}, I64{}, K2{}, F{});
+          return wrap ? rw(I8{}, I64{}, K1{}, T{}) : rw(I8{}, I64{}, K1{}, F{});
+        }
+        if (K <= 16u) {
+          if (two) return wrap ? rw(I16{}, I16{}, K2{}, T{}) : rw(I16{}, I16{}, K2{}, F{});
+          return wrap ? rw(I16{}, I16{}, K1{}, T{}) : rw(I16{}, I16{}, K1{}, F{});
+        }
+        if (two) return wrap ? rw(I32{}, I16{}, K2{}, T{}) : rw(I32{}, I16{}, K2{}, F{});
+        return wrap ? rw(I32{}, I16{}, K1{}, T{}) : rw(I32{}, I16{}, K1{}, F{});
+      }
+    }
   }
   if constexpr (!FIRST && A16 && !DMA) {
     if (K == (uint32_t)kWave) return cone_wave_full16<16, RMAX>(in, wanted, unwanted, out, n, wave * 16, nw * 16, lane);
@@ -486,6 +532,8 @@ constexpr uint32_t kConeAloneGens = 4, kConeAloneGensSmall = 6;
 // Beyond those, up to this many generations (exclusive), a whole-board target
 // whose row window fits 32 rows (cone_rows) keeps k_cone_adapt (step.hip).
 constexpr uint32_t kConeRowsMaxGens = 16;
+// ... and so does a column window of 5-32 columns whose rows fit (cone_wave_rows).
+constexpr bool kConeRowsWindowRoute = false;
 constexpr uint64_t kConeAloneSmallUniverses = 1u << 18;
 // The iterated search loop (gens > 2, no final states) steps the light cone
 // while it spans at most this many columns (P <= 32 lanes per universe: at
@@ -546,9 +594,9 @@ int launch_cone_adapt(const uint64_t *d_in, const uint64_t *d_wanted, const uint
   if constexpr (DMA || AUTO) {
     if (dma && aligned16(d_in)) {  // the uncapped grid; the cap applies to the waves of a windowed target
       const uint32_t cap_waves = blocks_per_cu > 0 ? (uint32_t)(cus * blocks_per_cu * kWavesPerBlock) : 0u;
-      hipLaunchKernelGGL((k_cone_adapt<RMAX, FIRST, OutT, true, true, ROWS>), dim3(grid_for((n + 15) / 16, cus, dma_blocks_per_cu)),
-                         dim3(kBlock), 0, stream, d_in, d_wanted, d_unwanted, d_out, (uint64_t)n, gens, kmax,
-                         cap_waves, cls, (int32_t)last_k);
+      hipLaunchKernelGGL((k_cone_adapt<RMAX, FIRST, OutT, true, true, ROWS>),
+                         dim3(grid_for((n + 15) / 16, cus, dma_blocks_per_cu)), dim3(kBlock), 0, stream, d_in,
+                         d_wanted, d_unwanted, d_out, (uint64_t)n, gens, kmax, cap_waves, cls, (int32_t)last_k);
       return launched("k_cone_adapt launch");
     }
   }
@@ -556,13 +604,13 @@ int launch_cone_adapt(const uint64_t *d_in, const uint64_t *d_wanted, const uint
   if constexpr (!FIRST) a16 = aligned16(d_in);
   if (a16) {
     if constexpr (!FIRST) {
-      hipLaunchKernelGGL((k_cone_adapt<RMAX, FIRST, OutT, true>), grid, dim3(kBlock), 0, stream, d_in, d_wanted,
-                         d_unwanted, d_out, (uint64_t)n, gens, kmax, 0u, cls, (int32_t)last_k);
+      hipLaunchKernelGGL((k_cone_adapt<RMAX, FIRST, OutT, true, false, ROWS>), grid, dim3(kBlock), 0, stream, d_in,
+                         d_wanted, d_unwanted, d_out, (uint64_t)n, gens, kmax, 0u, cls, (int32_t)last_k);
       return launched("k_cone_adapt launch");
     }
   }
-  hipLaunchKernelGGL((k_cone_adapt<RMAX, FIRST, OutT, false>), grid, dim3(kBlock), 0, stream, d_in, d_wanted,
-                     d_unwanted, d_out, (uint64_t)n, gens, kmax, 0u, cls, (int32_t)last_k);
+  hipLaunchKernelGGL((k_cone_adapt<RMAX, FIRST, OutT, false, false, ROWS>), grid, dim3(kBlock), 0, stream, d_in,
+                     d_wanted, d_unwanted, d_out, (uint64_t)n, gens, kmax, 0u, cls, (int32_t)last_k);
   return launched("k_cone_adapt launch");
 }
 

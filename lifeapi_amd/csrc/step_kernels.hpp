@@ -649,6 +649,103 @@ __device__ __forceinline__ void cone_wave(const uint64_t *in, const uint64_t *__
   }
 }
 
+// cone_wave with the rows cut to the light cone too (the column window's
+// counterpart of cone_kernels.hpp cone_wave_rows_dma): each lane's column is
+// cut to rows y0 .. y0 + FW - 1 (FW = 32 / PK) by one v_alignbit (WRAP: the
+// window crosses row 63), PK universes share one 32-bit register (universe
+// field f in bits f FW ..), and the generation runs with 1-bit shifts for the
+// vertical neighbours: the bits shifted in at a field's edges are wrong and
+// move one row inwards per generation, never onto a care row, which lies at
+// least `gens` rows inside its field (FIRST only; gens < 16).  Lanes as
+// cone_wave: P per universe, GPS = 64 / P universes per register set, so one
+// register holds PK GPS universes: register k, field f, group q is universe
+// u0 + k PK GPS + f GPS + q.
+template <int P, int UPW, int RMAX, int PK, bool WRAP, typename OutT>
+__device__ __forceinline__ void cone_wave_rows(const uint64_t *in, const uint64_t *__restrict__ wanted,
+                                               const uint64_t *__restrict__ unwanted, OutT *__restrict__ out,
+                                               uint64_t n, uint64_t u_first, uint64_t u_step, uint32_t gens,
+                                               uint32_t xs, uint32_t K, uint32_t y0, int lane) {
+  constexpr int GPS = kWave / P, FW = 32 / PK, UPR = GPS * PK;
+  static_assert(PK == 1 || PK == 2 || PK == 4, "fields of 32, 16 or 8 rows");
+  static_assert(UPW % UPR == 0 && UPW <= kWave, "a wave takes whole registers, one result per lane");
+  constexpr int R = UPW / UPR;
+  constexpr int RB = R < RMAX ? R : RMAX;
+  static_assert(R % RB == 0, "passes of RB registers");
+  constexpr uint32_t fmask = FW == 32 ? ~0u : (1u << FW) - 1u;
+  constexpr uint32_t rep = PK == 1 ? 1u : PK == 2 ? 0x00010001u : 0x01010101u;
+  constexpr uint32_t kDiff = ((TA ^ TB) & TC) & 0xFF;  // (s ^ wanted) & care
+  const uint32_t j = (uint32_t)lane & (P - 1), q = (uint32_t)lane / P;
+  const uint32_t col = (xs + j) & (kWave - 1);
+  const bool live = j < K;
+  const uint32_t sh = y0 & 31u, gsh = q * P;
+  auto cut = [&](uint64_t v) __attribute__((always_inline)) {
+    const W w = split(v);
+    return WRAP ? __builtin_amdgcn_alignbit(w.lo, w.hi, sh) : __builtin_amdgcn_alignbit(w.hi, w.lo, sh);
+  };
+  const uint64_t w64 = live ? wanted[col] : 0ull, m64 = live ? (w64 | unwanted[col]) : 0ull;
+  const uint32_t tw = (cut(w64) & fmask) * rep, tm = (cut(m64) & fmask) * rep;
+  for (uint64_t u0 = u_first; u0 < n; u0 += u_step) {
+    uint32_t mine = 0;  // lane L: the result of universe u0 + L
+#pragma unroll 1
+    for (int pass = 0; pass < R / RB; ++pass) {
+      const uint64_t ub = u0 + (uint64_t)pass * RB * UPR + q;
+      uint32_t a[RB];
+#pragma unroll
+      for (int k = 0; k < RB; ++k) {
+        uint32_t e[PK];
+#pragma unroll
+        for (int f = 0; f < PK; ++f) {
+          const uint64_t u = ub + (uint64_t)(k * UPR + f * GPS);
+          e[f] = (live && u < n) ? cut(__builtin_nontemporal_load(in + u * kWave + col)) : 0u;
+        }
+        if constexpr (PK == 1) {
+          a[k] = e[0];
+        } else if constexpr (PK == 2) {
+          a[k] = __builtin_amdgcn_perm(e[1], e[0], 0x05040100u);
+        } else {
+          const uint32_t p01 = __builtin_amdgcn_perm(e[1], e[0], 0x0C0C0400u);
+          const uint32_t p23 = __builtin_amdgcn_perm(e[3], e[2], 0x0C0C0400u);
+          a[k] = __builtin_amdgcn_perm(p23, p01, 0x05040100u);
+        }
+      }
+      uint32_t res[RB][PK];
+#pragma unroll
+      for (int k = 0; k < RB; ++k)
+#pragma unroll
+        for (int f = 0; f < PK; ++f) res[k][f] = 0;
+      for (uint32_t g = 1; g <= gens; ++g) {
+#pragma unroll
+        for (int k = 0; k < RB; ++k) {
+          const uint32_t L = dpp_prev(a[k]), Rt = dpp_next(a[k]);
+          const uint32_t h0 = lut3<kXor3>(L, a[k], Rt), h1 = lut3<kMaj>(L, a[k], Rt);
+          a[k] = life_tail6(h0 << 1, h0, h0 >> 1, h1 << 1, h1, h1 >> 1, a[k]);
+          const uint32_t d = lut3<kDiff>(a[k], tw, tm);
+#pragma unroll
+          for (int f = 0; f < PK; ++f) {
+            const uint64_t bad = __ballot((d & (fmask << (f * FW))) != 0u);
+            bool clean;
+            if constexpr (P == kWave) clean = bad == 0ull;
+            else clean = ((bad >> gsh) & ((1ull << P) - 1)) == 0ull;
+            if (res[k][f] == 0 && clean) res[k][f] = g;
+          }
+        }
+      }
+      // register k, field f, group q is universe u0 + (pass RB + k) UPR + f GPS + q:
+      // its result (uniform over the group) moves to that lane
+#pragma unroll
+      for (int k = 0; k < RB; ++k)
+#pragma unroll
+        for (int f = 0; f < PK; ++f) {
+          const uint32_t first = (uint32_t)((pass * RB + k) * UPR + f * GPS), rel = (uint32_t)lane - first;
+          uint32_t v = res[k][f];
+          if constexpr (GPS > 1) v = (uint32_t)__shfl((int)v, (int)((rel & (GPS - 1)) * P));
+          if (rel < (uint32_t)GPS) mine = v;
+        }
+    }
+    if (lane < UPW && u0 + lane < n) out[u0 + lane] = (OutT)mine;
+  }
+}
+
 // cone_max: with no final states, a target whose light cone spans at most
 // cone_max columns (0 = never) is answered on that cone: kContainsLo's waves
 // step only those columns in the natural layout (cone_wave, 8 universes per

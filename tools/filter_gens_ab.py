@@ -4,8 +4,11 @@ batches <= 256K; beyond, the split-layout pair) against the natural layout
 at every generation count (tuning build k_cone_adapt, LDS form: `rows` =
 with the packed row-window pass, `norows` = the full pass).  1M config-2
 universes (seed 2); targets: bench.py's whole-board one (row 10 of every third
-column must be dead: one care row) and one with five care rows spread over
-the column (0, 12, 29, 46, 63 of every third column: no row window).  Per
+column must be dead: one care row), one with five care rows spread over
+the column (0, 12, 29, 46, 63 of every third column: no row window), and
+bench.py's block target (4 columns x 4 rows).  `capped` / `capped_norows`:
+the capped form (cone shape upw 0 / 7, 16 blocks per CU) with and without
+the row-window passes (for a column window: cone_wave_rows).  Per
 rep every form in turn, each launch alone after a 768 MiB scrub; medians.
 Answers checked against the shipped path."""
 import json
@@ -47,13 +50,24 @@ def main():
         u[0::3] = np.uint64(rowmask)
         targets[name] = (torch.zeros((1, 64), dtype=torch.int64, device="cuda"),
                          torch.from_numpy(u.view(np.int64)[None].copy()).cuda())
+    # bench.py's block target: a 2x2 block and its ring, columns 9-12, rows 39-42
+    bw, bu = np.zeros(64, np.uint64), np.zeros(64, np.uint64)
+    bw[10] = bw[11] = np.uint64(3 << 40)
+    bu[9:13] = np.uint64(15 << 39)
+    bu &= ~bw
+    targets["block"] = tuple(torch.from_numpy(v.view(np.int64)[None].copy()).cuda() for v in (bw, bu))
+    only = os.environ.get("TARGETS")
     gens_list = [int(v) for v in os.environ.get("GENS", "3,4,5,6,8,12").split(",")]
     for tname, (tw, tu) in targets.items():
+        if only and tname not in only.split(","):
+            continue
         for gens in gens_list:
             forms = {
                 "shipped": lambda: hip.step_contains(x, tw, tu, gens)[0],
                 "rows": lambda: tune.cone(x, tw, tu, gens, 1, 8, first=True),
                 "norows": lambda: tune.cone(x, tw, tu, gens, 2, 8, first=True),
+                "capped": lambda: tune.cone(x, tw, tu, gens, 16000, 8, first=True),
+                "capped_norows": lambda: tune.cone(x, tw, tu, gens, 16007, 8, first=True),
             }
             ref = forms["shipped"]().clone()
             torch.cuda.synchronize()

@@ -29,6 +29,9 @@ int cone_by_shape(const uint64_t *in, const uint64_t *w, const uint64_t *u, OutT
   // upw 5: upw 4 with rmax >> 8 as the last report word (the row-window hint: K | class << 8 | y0 << 16)
   if (upw == 5 && (rmax & 0xFF) == 8)
     return launch_cone_adapt<8, FIRST, OutT, true>(in, w, u, out, n, gens, cus, st, cap, kWave, 0, rmax >> 8);
+  // upw 7: upw 0 (the capped form) without the row-window passes
+  if (upw == 7 && rmax == 8)
+    return launch_cone_adapt<8, FIRST, OutT, false, false, false>(in, w, u, out, n, gens, cus, st, cap);
   // upw 2: upw 1 without the packed row-window pass (cone_wave_rows_dma): every whole-board target full
   if (upw == 2 && rmax == 8)
     return launch_cone_adapt<8, FIRST, OutT, true, false, false>(in, w, u, out, n, gens, cus, st, cap);
