@@ -459,10 +459,10 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
     report(report_word(K, pk, y0));
     if (K > kmax) return;
     if constexpr (FIRST && ROWS) {
-      // a column window of 5-32 columns whose rows, widened by the cone, fit
+      // a column window of 5-63 columns whose rows, widened by the cone, fit
       // 32 (16) rows: 1 (2) universes per register and lane, rows cut to the
       // window (cone_wave_rows)
-      if (pk > 0 && K > 4u && K <= 32u && gens >= kConeRowsWindowGens) {
+      if (pk > 0 && K > 4u && K < (uint32_t)kWave && gens >= kConeRowsWindowGens) {
         auto rw = [&](auto p_c, auto upw_c, auto pk_c, auto wrap_c) __attribute__((always_inline)) {
           constexpr int UPWc = decltype(upw_c)::value;
           if (wave * UPWc >= n) return;
@@ -486,8 +486,12 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
           if (two) return wrap ? rw(I16{}, I16{}, K2{}, T{}) : rw(I16{}, I16{}, K2{}, F{});
           return wrap ? rw(I16{}, I16{}, K1{}, T{}) : rw(I16{}, I16{}, K1{}, F{});
         }
-        if (two) return wrap ? rw(I32{}, I16{}, K2{}, T{}) : rw(I32{}, I16{}, K2{}, F{});
-        return wrap ? rw(I32{}, I16{}, K1{}, T{}) : rw(I32{}, I16{}, K1{}, F{});
+        if (K <= 32u) {
+          if (two) return wrap ? rw(I32{}, I16{}, K2{}, T{}) : rw(I32{}, I16{}, K2{}, F{});
+          return wrap ? rw(I32{}, I16{}, K1{}, T{}) : rw(I32{}, I16{}, K1{}, F{});
+        }
+        if (two) return wrap ? rw(I64{}, I16{}, K2{}, T{}) : rw(I64{}, I16{}, K2{}, F{});
+        return wrap ? rw(I64{}, I16{}, K1{}, T{}) : rw(I64{}, I16{}, K1{}, F{});
       }
     }
   }
@@ -532,7 +536,7 @@ constexpr uint32_t kConeAloneGens = 4, kConeAloneGensSmall = 6;
 // Beyond those, up to this many generations (exclusive), a whole-board target
 // whose row window fits 32 rows (cone_rows) keeps k_cone_adapt (step.hip).
 constexpr uint32_t kConeRowsMaxGens = 16;
-// ... and so does a column window of 5-32 columns whose rows fit (cone_wave_rows).
+// ... and so does a column window of 5-63 columns whose rows fit (cone_wave_rows).
 constexpr bool kConeRowsWindowRoute = false;
 constexpr uint64_t kConeAloneSmallUniverses = 1u << 18;
 // The iterated search loop (gens > 2, no final states) steps the light cone

@@ -183,7 +183,7 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
     if (rc != LIFEAPI_OK) return rc;
     const int last_k = last & 0xFF, last_pk = (last >> 8) & 0xFF;
     if (last >= 0 && last_pk > 0 &&
-        (last_k == kWave || (kConeRowsWindowRoute && last_k > 4 && last_k <= (int)kConeIterColumns)))
+        (last_k == kWave || (kConeRowsWindowRoute && last_k > 4)))
       return launch_cone_adapt<kConeSets, true, uint32_t, false, true>(d_in, d_wanted, d_unwanted, d_first_gen, n,
                                                                        generations, cus, (hipStream_t)stream,
                                                                        kConeAdaptBlocksPerCU);

@@ -6,7 +6,7 @@ with the packed row-window pass, `norows` = the full pass).  1M config-2
 universes (seed 2); targets: bench.py's whole-board one (row 10 of every third
 column must be dead: one care row), one with five care rows spread over
 the column (0, 12, 29, 46, 63 of every third column: no row window), and
-bench.py's block target (4 columns x 4 rows).  `capped` / `capped_norows`:
+bench.py's block target (4 columns x 4 rows), and 40 columns x 3 rows.  `capped` / `capped_norows`:
 the capped form (cone shape upw 0 / 7, 16 blocks per CU) with and without
 the row-window passes (for a column window: cone_wave_rows).  Per
 rep every form in turn, each launch alone after a 768 MiB scrub; medians.
@@ -56,6 +56,11 @@ def main():
     bu[9:13] = np.uint64(15 << 39)
     bu &= ~bw
     targets["block"] = tuple(torch.from_numpy(v.view(np.int64)[None].copy()).cuda() for v in (bw, bu))
+    # 40 columns x 3 rows (rows 20-22 must be dead): a column window wider than 32
+    wu = np.zeros(64, np.uint64)
+    wu[:40] = np.uint64(7 << 20)
+    targets["wide"] = (torch.zeros((1, 64), dtype=torch.int64, device="cuda"),
+                       torch.from_numpy(wu.view(np.int64)[None].copy()).cuda())
     only = os.environ.get("TARGETS")
     gens_list = [int(v) for v in os.environ.get("GENS", "3,4,5,6,8,12").split(",")]
     for tname, (tw, tu) in targets.items():
