@@ -536,8 +536,13 @@ constexpr uint32_t kConeAloneGens = 4, kConeAloneGensSmall = 6;
 // Beyond those, up to this many generations (exclusive), a whole-board target
 // whose row window fits 32 rows (cone_rows) keeps k_cone_adapt (step.hip).
 constexpr uint32_t kConeRowsMaxGens = 16;
-// ... and so does a column window of 5-63 columns whose rows fit (cone_wave_rows).
-constexpr bool kConeRowsWindowRoute = false;
+// ... and so does a column window of 5-63 columns whose rows fit
+// (cone_wave_rows, the capped form): 1M universes, bench.py's block target
+// (4 x 4) at 5 / 8 / 13 generations 0.060 / 0.151 / 0.225 ms against 0.096 /
+// 0.231 / 0.363 on the split pair, 40 x 3 columns at 5 / 8 0.159 / 0.228
+// against 0.229 / 0.300 (tools/filter_gens_ab.py,
+// profiles/r05/gens/gens_ab_window_rows.jsonl).
+constexpr bool kConeRowsWindowRoute = true;
 constexpr uint64_t kConeAloneSmallUniverses = 1u << 18;
 // The iterated search loop (gens > 2, no final states) steps the light cone
 // while it spans at most this many columns (P <= 32 lanes per universe: at

@@ -168,14 +168,17 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
                                                                      generations, cus, (hipStream_t)stream,
                                                                      kConeAdaptBlocksPerCU);
   }
-  // More generations without final states: a whole-board target whose care
-  // rows, widened by the light cone, fit 32 rows (as the last report on this
-  // target says: launch_cone_adapt) keeps k_cone_adapt's packed row-window
-  // pass, which is 1.5-2x the split pair below on a one-row target (1M
-  // universes at 5 / 8 / 12 generations: 0.116 / 0.190 / 0.269 ms against
-  // 0.234 / 0.297 / 0.400; tools/filter_gens_ab.py, profiles/r05/gens/).  A
-  // target with no report yet takes the split pair, and one wave of
-  // k_cone_classify writes its report for the next call.
+  // More generations without final states: a target whose care rows,
+  // widened by the light cone, fit 32 rows (as the last report on this
+  // target says: launch_cone_adapt) keeps k_cone_adapt's row-window passes
+  // -- whole board (cone_wave_rows_dma) or a column window of more than 4
+  // columns (cone_wave_rows, kConeRowsWindowRoute) -- which are 1.3-2x the
+  // split pair below (1M universes, a one-row whole-board target at 5 / 8 /
+  // 12 generations: 0.116 / 0.190 / 0.269 ms against 0.234 / 0.297 / 0.400;
+  // the 4 x 4 block at 5 / 8 / 13: 0.060 / 0.151 / 0.225 against 0.096 /
+  // 0.231 / 0.363; tools/filter_gens_ab.py, profiles/r05/gens/).  A target
+  // with no report yet takes the split pair, and one wave of k_cone_classify
+  // writes its report for the next call.
   if (!d_final && generations < kConeRowsMaxGens && aligned16(d_in)) {
     int32_t *slot = nullptr;
     int last = -1;
