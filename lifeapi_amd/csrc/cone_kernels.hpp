@@ -454,15 +454,16 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
         if (gens >= kConeRowsWindowGens || (cls && wave == 0)) pk = cone_rows(care_col, gens, y0);
       }
     } else if constexpr (FIRST) {
-      if (cls && wave == 0) pk = cone_rows(care_col, gens, y0);  // (only the report needs it)
+      if ((ROWS && gens >= kConeRowsWindowGens) || (cls && wave == 0)) pk = cone_rows(care_col, gens, y0);
     }
     report(report_word(K, pk, y0));
     if (K > kmax) return;
     if constexpr (FIRST && ROWS) {
-      // a column window of 5-63 columns whose rows, widened by the cone, fit
-      // 32 (16) rows: 1 (2) universes per register and lane, rows cut to the
-      // window (cone_wave_rows)
-      if (pk > 0 && K > 4u && K < (uint32_t)kWave && gens >= kConeRowsWindowGens) {
+      // a column window of more than 4 columns (the whole board too, in this
+      // capped form) whose rows, widened by the cone, fit 32 (16) rows: 1 (2)
+      // universes per register and lane, rows cut to the window
+      // (cone_wave_rows)
+      if (pk > 0 && K > 4u && gens >= kConeRowsWindowGens) {
         auto rw = [&](auto p_c, auto upw_c, auto pk_c, auto wrap_c) __attribute__((always_inline)) {
           constexpr int UPWc = decltype(upw_c)::value;
           if (wave * UPWc >= n) return;

@@ -201,6 +201,11 @@ def main():
          {"lines_128B_per_object": 1, "full_read_equivalent_bytes": 513})
     both("k_cone 1 gen (first hit only), 2x2 block + ring", n, 128 + 4, lambda: hip.step_contains(x, bw, bu, 1),
          {"lines_128B_per_object": 1, "full_read_equivalent_bytes": 516})
+    for gens in (5, 8, 13):  # the column and row window widen with the generations (cone_wave_rows)
+        xs = (9 - gens) % 64
+        lines = len({((xs + c) % 64) // 16 for c in range(4 + 2 * gens)})
+        both(f"filter {gens} gen (first hit only), 2x2 block + ring", n, 128 * lines + 4,
+             lambda g=gens: hip.step_contains(x, bw, bu, g), {"lines_128B_per_object": lines})
     fp = [x.clone(), y]
 
     def filter_pingpong():  # a loop stepping its batch with the filter: final states ping-ponged
