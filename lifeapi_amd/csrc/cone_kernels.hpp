@@ -296,7 +296,7 @@ __device__ __forceinline__ int32_t cone_report(uint64_t care_col, uint32_t gens)
   cone_window(care_col, gens, xs, K);
   return report_word(K, cone_rows(care_col, gens, y0), y0);
 }
-__global__ __launch_bounds__(kWave) void k_cone_classify(const uint64_t *__restrict__ wanted,
+__global__ __launch_bounds__(kWave) __attribute__((unused)) void k_cone_classify(const uint64_t *__restrict__ wanted,
                                                          const uint64_t *__restrict__ unwanted, uint32_t gens,
                                                          int32_t *cls) {
   const int lane = threadIdx.x & (kWave - 1);
