@@ -329,7 +329,8 @@ __device__ __forceinline__ uint64_t block_index() {
 // Vector-memory ops retire in issue order, loads, LDS-DMA loads and stores
 // alike, so a wave waits for a global_load_lds by allowing the ops it issued
 // after it to remain.
-constexpr int kWaitVm0 = 0x0F70, kWaitVm1 = 0x0F71, kWaitVm6 = 0x0F76, kWaitVm11 = 0x0F7B, kWaitLgkm0 = 0xC07F;
+constexpr int kWaitVm0 = 0x0F70, kWaitVm1 = 0x0F71, kWaitVm5 = 0x0F75, kWaitVm6 = 0x0F76, kWaitVm9 = 0x0F79,
+              kWaitVm11 = 0x0F7B, kWaitLgkm0 = 0xC07F;
 
 // Contains(LifeTarget) (LifeTarget.hpp:44-51): (s ^ w) & (w | u) == 0 on all columns
 __device__ __forceinline__ bool wave_contains(W s, W w, W u) {

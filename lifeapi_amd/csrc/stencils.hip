@@ -88,9 +88,9 @@ int lifeapi_stable_pass_batch_dev(uint64_t *d_planes, uint8_t *d_flags, size_t n
   // signal 1.83 -> 1.72, PropagateStep 1.95 -> 1.86, StabiliseOptions
   // 1.79 -> 1.66.
   note_forward_write(d_planes, (uint64_t)n * 10 * 512);
-  if ((pass == 0 || pass == 2 || pass == 3) && aligned16(d_planes)) {
-    // Round 5: SynchroniseStateKnown, SignalNeighbours and PropagateStep
-    // move their LifeStable through LDS (k_stable_dma, U = 1, WIDE): five
+  if ((pass == 0 || pass == 1 || pass == 2 || pass == 3) && aligned16(d_planes)) {
+    // Round 5: SynchroniseStateKnown, UpdateOptions, SignalNeighbours and
+    // PropagateStep move their LifeStable through LDS (k_stable_dma, U = 1, WIDE): five
     // 16-byte-per-lane global_load_lds in, ds_read_b64 out to lane =
     // column; the changed lines back through the image, 16 bytes per lane;
     // at most 5 blocks resident per CU.  Same process, 1M LifeStables of
@@ -99,13 +99,18 @@ int lifeapi_stable_pass_batch_dev(uint64_t *d_planes, uint8_t *d_flags, size_t n
     // random planes): signal 0.791 / 0.786 / 0.790 against 0.802 / 0.798 /
     // 0.802 for k_stable (round 4: 1.10-1.15); PropagateStep 1.654 / 1.074
     // / 1.645 against 1.697 / 1.368 / 1.631; sync 1.649 / 1.058 / 1.649
-    // against 1.625 / 1.142 / 1.632.  UpdateOptions loses 6 % on the
-    // inputs where every column changes, Propagate and StabiliseOptions
-    // gain nothing: they keep k_stable.  The loads and
-    // stores are 16 bytes wide: an 8-byte aligned batch keeps k_stable.
+    // against 1.625 / 1.142 / 1.632; UpdateOptions, which stores only the
+    // option planes, 1.491 / 1.042 / 1.491 against 1.551 / 1.210 / 1.560
+    // (profiles/r05/stall/options_dma_ab.jsonl; storing state and unknown
+    // too, as the image holds them, it lost 6 % where every column
+    // changes).  Propagate and StabiliseOptions gain nothing: they keep
+    // k_stable.  The loads and stores are 16 bytes wide: an
+    // 8-byte aligned batch keeps k_stable.
     using DFn = void (*)(uint64_t *, uint8_t *, uint64_t, uint32_t, uint32_t);
-    const DFn dma = pass == 0 ? (DFn)k_stable_dma<0, 2, true, true>
-                    : pass == 2 ? (DFn)k_stable_dma<2, 2, true, true> : (DFn)k_stable_dma<3, 2, true, true>;
+    const DFn dma = pass == 0   ? (DFn)k_stable_dma<0, 2, true, true>
+                    : pass == 1 ? (DFn)k_stable_dma<1, 2, true, true>
+                    : pass == 2 ? (DFn)k_stable_dma<2, 2, true, true>
+                                : (DFn)k_stable_dma<3, 2, true, true>;
     unsigned dlds = 0;
     rc = occupancy_lds(reinterpret_cast<const void *>(dma), kStableDmaResident, dlds);
     if (rc != LIFEAPI_OK) return rc;
