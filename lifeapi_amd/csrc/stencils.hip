@@ -88,7 +88,7 @@ int lifeapi_stable_pass_batch_dev(uint64_t *d_planes, uint8_t *d_flags, size_t n
   // signal 1.83 -> 1.72, PropagateStep 1.95 -> 1.86, StabiliseOptions
   // 1.79 -> 1.66.
   note_forward_write(d_planes, (uint64_t)n * 10 * 512);
-  if ((pass == 0 || pass == 1 || pass == 2 || pass == 3) && aligned16(d_planes)) {
+  if ((pass == 0 || pass == 1 || pass == 2 || pass == 3 || pass == 5) && aligned16(d_planes)) {
     // Round 5: SynchroniseStateKnown, UpdateOptions, SignalNeighbours and
     // PropagateStep move their LifeStable through LDS (k_stable_dma, U = 1, WIDE): five
     // 16-byte-per-lane global_load_lds in, ds_read_b64 out to lane =
@@ -103,17 +103,25 @@ int lifeapi_stable_pass_batch_dev(uint64_t *d_planes, uint8_t *d_flags, size_t n
     // option planes, 1.491 / 1.042 / 1.491 against 1.551 / 1.210 / 1.560
     // (profiles/r05/stall/options_dma_ab.jsonl; storing state and unknown
     // too, as the image holds them, it lost 6 % where every column
-    // changes).  Propagate and StabiliseOptions gain nothing: they keep
-    // k_stable.  The loads and stores are 16 bytes wide: an
-    // 8-byte aligned batch keeps k_stable.
+    // changes).  SynchroniseStateKnown, UpdateOptions and StabiliseOptions
+    // store only the planes that changed: sync 1.499 / 0.929 / 1.494,
+    // UpdateOptions 1.496 / 0.940 / 1.495, StabiliseOptions (uncapped grid:
+    // at most 5 blocks per CU it loses on the next node, 1.22) 1.553 /
+    // 1.068 / 1.555 against 1.711 / 1.103 / 1.708 (profiles/r05/stall/
+    // skip_planes_ab*.jsonl).  Propagate gains nothing: it keeps k_stable
+    // (DESIGN.md 3.5).  The loads and stores are 16 bytes wide: an 8-byte
+    // aligned batch keeps k_stable.
     using DFn = void (*)(uint64_t *, uint8_t *, uint64_t, uint32_t, uint32_t);
     const DFn dma = pass == 0   ? (DFn)k_stable_dma<0, 2, true, true>
                     : pass == 1 ? (DFn)k_stable_dma<1, 2, true, true>
                     : pass == 2 ? (DFn)k_stable_dma<2, 2, true, true>
-                                : (DFn)k_stable_dma<3, 2, true, true>;
+                    : pass == 3 ? (DFn)k_stable_dma<3, 2, true, true>
+                                : (DFn)k_stable_dma<5, 2, true, true>;
     unsigned dlds = 0;
-    rc = occupancy_lds(reinterpret_cast<const void *>(dma), kStableDmaResident, dlds);
-    if (rc != LIFEAPI_OK) return rc;
+    if (pass != 5) {  // (StabiliseOptions: every block the LDS holds)
+      rc = occupancy_lds(reinterpret_cast<const void *>(dma), kStableDmaResident, dlds);
+      if (rc != LIFEAPI_OK) return rc;
+    }
     hipLaunchKernelGGL(dma, dim3(grid_for(n, cus, 0)), dim3(kBlock), dlds, (hipStream_t)stream, d_planes, d_flags,
                        (uint64_t)n, max_iters ? max_iters : 1u << 20, 1u << 8);
     return launched("k_stable_dma launch");
