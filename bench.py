@@ -836,6 +836,86 @@ def secondary_filter(hip, rt):
     return out
 
 
+def _cone_cells(wanted: np.ndarray, unwanted: np.ndarray, gens: int) -> int:
+    """cell-updates the iterated filter cannot avoid per universe: at
+    generation g (1..gens) the cells within Chebyshev distance gens - g of the
+    target's care cells on the torus (the ones a later test reads)"""
+    care = np.zeros((64, 64), bool)  # [column, row]
+    for x in range(64):
+        v = int(wanted[x]) | int(unwanted[x])
+        care[x] = [(v >> y) & 1 for y in range(64)]
+    total, cur = 0, care.copy()
+    reach = [care.sum()]
+    for _ in range(gens - 1):
+        cur = cur | np.roll(cur, 1, 0) | np.roll(cur, -1, 0)
+        cur = cur | np.roll(cur, 1, 1) | np.roll(cur, -1, 1)
+        reach.append(cur.sum())
+    for g in range(1, gens + 1):
+        total += int(reach[gens - g])
+    return total
+
+
+def secondary_filter_iter(hip, rt):
+    """The iterated search filter (LifeTarget.hpp:44-51,
+    LifeAPI.hpp:877-881): 1M config-2 universes, Step() then Contains(target)
+    after every generation up to 3-13 generations, first hits only, on three
+    targets: bench's block + ring (a 4 x 4 care window), its one-row
+    whole-board target, and a full-height one (16 dead cells, one in every
+    fourth row: no window of any kind).  Each call is timed alone after a 768
+    MiB scrub (median of 10) and back to back; the answers of the first and
+    the second call on each target (the first call has no launch report yet)
+    are checked against the reference's own loop (tests/golden/golden.json
+    digests.config2_filter_iter, make_golden.py).  Bounds per call: bytes =
+    the 128-byte lines of each universe holding the light cone + the 4-byte
+    answer at 8 TB/s; VALU = the cells each generation must update (those
+    within gens - g of a care cell) at 16 wave64 issue slots per 4096 cells
+    (config 3's fixed network bound) at 1.2288e12 slots/s."""
+    gold = _golden("config2_filter_iter", "targets")
+    if not gold:
+        return None
+    n = 1 << 20
+    x = hip.fill_random(n, seed=2, device=rt.device, stream=rt.stream)
+    scrub = Scrub(rt)
+    out = {"workload": f"config2 input: {n} universes, the search loop Step() then Contains(target) up to "
+                       "3-13 generations, first hits only",
+           "timing": "alone: 3 warm, 10 timed calls each after a 768 MiB scrub, events around the call, "
+                     "median; b2b: 20 calls back to back",
+           "targets": {}}
+    for name, t in gold.items():
+        w, u = (np.array([int(v, 16) for v in t[k]], dtype=np.uint64) for k in ("wanted", "unwanted"))
+        tw, tu = (torch.from_numpy(v.view(np.int64)[None].copy()).to(rt.device) for v in (w, u))
+        rows = {}
+        for gs, want in t["gens"].items():
+            g = int(gs)
+            ok = True
+            for _ in range(2):  # the first call on a target, then the reported form
+                first, _ = hip.step_contains(x, tw, tu, g, stream=rt.stream)
+                rt.sync()
+                d = f"{batch_digest(first.cpu().numpy().astype(np.uint64)):016x}"
+                ok = ok and d == want["first_digest"] and int((first > 0).sum().item()) == want["hits"]
+            fn = lambda a, b, g=g: hip.step_contains(a, tw, tu, g, stream=rt.stream)  # noqa: E731
+            ms, allms = scrubbed_ms(rt, fn, x, x, scrub)
+            b2b = back_to_back_ms(rt, fn, x, x)
+            xs, k = _cone_columns(w, u, g)
+            lines = _lines_touched(xs, k)
+            bytes_ms = n * (lines * 128 + 4) / (HBM_PEAK_GBS * 1e9) * 1e3
+            cells = _cone_cells(w, u, g)
+            valu_ms = n * cells * C3_SLOTS_PER_UNIVERSE_GEN / 4096 / VALU_PEAK_SLOTS * 1e3
+            board_ms = n * g * C3_SLOTS_PER_UNIVERSE_GEN / VALU_PEAK_SLOTS * 1e3
+            bound = max(bytes_ms, valu_ms)
+            rows[gs] = {"verified": ok, "hits": want["hits"], "kernel_ms": ms, "kernel_ms_all": allms,
+                        "kernel_ms_b2b": b2b, "universes_per_s": n / (ms / 1e3),
+                        "lines_128B_per_universe": lines, "cone_cells": cells,
+                        "bound": {"bytes_ms": bytes_ms, "valu_ms": valu_ms,
+                                  "bound": "hbm" if bytes_ms >= valu_ms else "valu", "bound_ms": bound,
+                                  "bound_frac": bound / ms, "whole_board_valu_ms": board_ms,
+                                  "whole_board_valu_frac": board_ms / ms}}
+        out["targets"][name] = rows
+    del scrub, x
+    torch.cuda.empty_cache()
+    return out
+
+
 def secondary_config5(hip, rt):
     """Config 5: unknown_step_refined ternary step, 256K universes, one launch."""
     n = 1 << 18
@@ -937,6 +1017,11 @@ def secondary_summary(line: dict, sec: dict | None, cpu: dict | None) -> dict:
                 s[f"{op}_{name}_ms"] = _r(_get(row, op, "kernel_ms"), 5)
                 s[f"{op}_{name}_frac"] = _r(_get(row, op, "roofline", "frac"))
             s[f"filter_{name}_verified"] = row.get("verified")
+        for name, rows in ((sec.get("filter_iter") or {}).get("targets") or {}).items():
+            for g, row in rows.items():
+                s[f"iter_{name}_{g}gen_ms"] = _r(row.get("kernel_ms"), 5)
+                s[f"iter_{name}_{g}gen_bound_frac"] = _r(_get(row, "bound", "bound_frac"))
+                s[f"iter_{name}_{g}gen_verified"] = row.get("verified")
     return s
 
 
@@ -1060,7 +1145,8 @@ def main(argv=None):
         csec = 0.0 if args.no_cpu_baseline else args.cpu_seconds / 3
         secondary = {"config3": secondary_config3(hip, rt, csec),
                      "config5": secondary_config5(hip, rt),
-                     "filter": secondary_filter(hip, rt)}
+                     "filter": secondary_filter(hip, rt),
+                     "filter_iter": secondary_filter_iter(hip, rt)}
         if cfg == 2:
             del a, b, bufs, final
             torch.cuda.empty_cache()

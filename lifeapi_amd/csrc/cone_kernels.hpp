@@ -31,7 +31,7 @@
 
 #include <type_traits>
 
-#include "step_kernels.hpp"
+#include "cone_split.hpp"
 
 namespace lifeapi_impl {
 namespace {
@@ -348,7 +348,10 @@ __global__ __launch_bounds__(kBlock) void k_cone(const uint64_t *in, const uint6
 // the uncapped grid; every other window keeps the capped shape, the first
 // cap_waves waves looping over the batch and the rest returning after the
 // whole-board test (0: no cap).
-template <int RMAX, bool FIRST, typename OutT, bool A16 = false, bool DMA = false, bool ROWS = true>
+// WIN: from kConeRowsWindowGens generations on, a target whose rows fit
+// 32 (16) takes the window split layout (cone_split.hpp cone_wave_split) on
+// the capped grid instead of the packed row-window passes.
+template <int RMAX, bool FIRST, typename OutT, bool A16 = false, bool DMA = false, bool ROWS = true, bool WIN = false>
 __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const uint64_t *__restrict__ wanted,
                                                        const uint64_t *__restrict__ unwanted, OutT *__restrict__ out,
                                                        uint64_t n, uint32_t gens, uint32_t kmax, uint32_t cap_waves,
@@ -369,6 +372,33 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
   const uint32_t g = FIRST ? gens : 0u;
   const uint64_t w64 = wanted[lane], m64 = w64 | unwanted[lane], care_col = m64;
   uint32_t xs = 0, K = kWave;
+  // the window split layout (WIN): R = 32 rows for row class 1, 16 for 2 and
+  // 4; P = the lanes per universe the column window needs (>= 16 for R = 16:
+  // one answer per lane), universes u_first + k (64 / P) (256 / R)
+  auto split_pass = [&](int pk_, uint32_t y0_, uint64_t nw_) __attribute__((always_inline)) {
+    auto run = [&](auto p_c, auto r_c) __attribute__((always_inline)) {
+      constexpr int Pc = decltype(p_c)::value, Rc = decltype(r_c)::value;
+      constexpr uint64_t UPS = (uint64_t)(kWave / Pc) * (256 / Rc);
+      if (wave * UPS >= n) return;
+      if (y0_ >= 32u)
+        cone_wave_split<Pc, Rc, true>(in, wanted, unwanted, out, n, wave * UPS, nw_ * UPS, gens, xs, K, y0_, lane);
+      else
+        cone_wave_split<Pc, Rc, false>(in, wanted, unwanted, out, n, wave * UPS, nw_ * UPS, gens, xs, K, y0_, lane);
+    };
+    using I8 = std::integral_constant<int, 8>;
+    using I16 = std::integral_constant<int, 16>;
+    using I32 = std::integral_constant<int, 32>;
+    using I64 = std::integral_constant<int, 64>;
+    if (pk_ == 1) {
+      if (K <= 8u) return run(I8{}, I32{});
+      if (K <= 16u) return run(I16{}, I32{});
+      if (K <= 32u) return run(I32{}, I32{});
+      return run(I64{}, I32{});
+    }
+    if (K <= 16u) return run(I16{}, I16{});
+    if (K <= 32u) return run(I32{}, I16{});
+    return run(I64{}, I16{});
+  };
   if constexpr (DMA) {
     __shared__ uint64_t img_all[kWavesPerBlock][RMAX * kWave];
     uint64_t *img = img_all[__builtin_amdgcn_readfirstlane(threadIdx.x / kWave)];
@@ -377,7 +407,11 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
     // pass is fetched before the window tests, which then run under it (a
     // wave that turns out not to need it waits for it before leaving: LDS-DMA
     // still in flight must not outlive the wave's LDS)
-    const bool early = (cls_last & 0xFF) == kReportWhole && wave * c < n;
+    // (WIN: a whole board whose report carries a row class from
+    // kConeRowsWindowGens generations on takes the split window, which loads
+    // by itself)
+    const bool win_hint = WIN && FIRST && gens >= kConeRowsWindowGens && ((cls_last >> 8) & 0xFF) != 0;
+    const bool early = (cls_last & 0xFF) == kReportWhole && !win_hint && wave * c < n;
     if (early) dma_fetch_pass<RMAX>(in, n, wave * c, lane, img);
     auto leave = [&]() __attribute__((always_inline)) {
       if (early) __builtin_amdgcn_s_waitcnt(kWaitVm0);
@@ -409,6 +443,16 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
     }
     if (whole) {
       if (kmax < (uint32_t)kWave || wave * c >= n) return leave();
+      if constexpr (FIRST && WIN) {
+        if (pk > 0 && gens >= kConeRowsWindowGens) {
+          leave();
+          if (cap_waves) {
+            if (wave >= cap_waves) return;
+            nw = nw < cap_waves ? nw : cap_waves;
+          }
+          return split_pass(pk, y0, nw);
+        }
+      }
       if constexpr (FIRST && ROWS) {
         auto rows = [&](auto pk_c, auto wrap_c) __attribute__((always_inline)) {
           cone_wave_rows_dma<RMAX, decltype(pk_c)::value, decltype(wrap_c)::value>(
@@ -463,6 +507,9 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
       // capped form) whose rows, widened by the cone, fit 32 (16) rows: 1 (2)
       // universes per register and lane, rows cut to the window
       // (cone_wave_rows)
+      if constexpr (WIN) {
+        if (pk > 0 && K > 4u && gens >= kConeRowsWindowGens) return split_pass(pk, y0, nw);
+      }
       if (pk > 0 && K > 4u && gens >= kConeRowsWindowGens) {
         auto rw = [&](auto p_c, auto upw_c, auto pk_c, auto wrap_c) __attribute__((always_inline)) {
           constexpr int UPWc = decltype(upw_c)::value;
@@ -588,7 +635,8 @@ int launch_cone(const uint64_t *d_in, const uint64_t *d_wanted, const uint64_t *
 // the DMA form exactly when the last launch on this target reported a
 // whole-board window (host.hpp cone_class_slot), else the capped form; both
 // compute the same answers for any target.
-template <int RMAX, bool FIRST, typename OutT, bool DMA = false, bool AUTO = false, bool ROWS = true>
+template <int RMAX, bool FIRST, typename OutT, bool DMA = false, bool AUTO = false, bool ROWS = true,
+          bool WIN = false>
 int launch_cone_adapt(const uint64_t *d_in, const uint64_t *d_wanted, const uint64_t *d_unwanted, OutT *d_out,
                       size_t n, uint32_t gens, int cus, hipStream_t stream, int blocks_per_cu,
                       uint32_t kmax = kWave, int dma_blocks_per_cu = 0, int hint_k = -1) {
@@ -604,7 +652,7 @@ int launch_cone_adapt(const uint64_t *d_in, const uint64_t *d_wanted, const uint
   if constexpr (DMA || AUTO) {
     if (dma && aligned16(d_in)) {  // the uncapped grid; the cap applies to the waves of a windowed target
       const uint32_t cap_waves = blocks_per_cu > 0 ? (uint32_t)(cus * blocks_per_cu * kWavesPerBlock) : 0u;
-      hipLaunchKernelGGL((k_cone_adapt<RMAX, FIRST, OutT, true, true, ROWS>),
+      hipLaunchKernelGGL((k_cone_adapt<RMAX, FIRST, OutT, true, true, ROWS, WIN>),
                          dim3(grid_for((n + 15) / 16, cus, dma_blocks_per_cu)), dim3(kBlock), 0, stream, d_in,
                          d_wanted, d_unwanted, d_out, (uint64_t)n, gens, kmax, cap_waves, cls, (int32_t)last_k);
       return launched("k_cone_adapt launch");
@@ -614,12 +662,12 @@ int launch_cone_adapt(const uint64_t *d_in, const uint64_t *d_wanted, const uint
   if constexpr (!FIRST) a16 = aligned16(d_in);
   if (a16) {
     if constexpr (!FIRST) {
-      hipLaunchKernelGGL((k_cone_adapt<RMAX, FIRST, OutT, true, false, ROWS>), grid, dim3(kBlock), 0, stream, d_in,
+      hipLaunchKernelGGL((k_cone_adapt<RMAX, FIRST, OutT, true, false, ROWS, WIN>), grid, dim3(kBlock), 0, stream, d_in,
                          d_wanted, d_unwanted, d_out, (uint64_t)n, gens, kmax, 0u, cls, (int32_t)last_k);
       return launched("k_cone_adapt launch");
     }
   }
-  hipLaunchKernelGGL((k_cone_adapt<RMAX, FIRST, OutT, false, false, ROWS>), grid, dim3(kBlock), 0, stream, d_in,
+  hipLaunchKernelGGL((k_cone_adapt<RMAX, FIRST, OutT, false, false, ROWS, WIN>), grid, dim3(kBlock), 0, stream, d_in,
                      d_wanted, d_unwanted, d_out, (uint64_t)n, gens, kmax, 0u, cls, (int32_t)last_k);
   return launched("k_cone_adapt launch");
 }

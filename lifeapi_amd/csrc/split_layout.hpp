@@ -90,18 +90,33 @@ struct SplitNet<16> {  // R_j: j = row bits 3..0, 8 universes
   static constexpr __device__ int reg(int j) { return ((j & 7) << 1) | (j >> 3); }
 };
 
+// One swap stage.  Stages 0 and 1 (16- and 8-bit shifts) move whole bytes:
+// each register of a pair is one v_perm of the pair (the delta swap's five
+// VALU -- shift, masked xor, xor, shift, xor -- become two).  Stages 2-4 write
+// each register as a bit select between itself and its partner shifted into
+// place: new B = (A >> s) & m | B & ~m, new A = (B << s) & (m << s) | A &
+// ~(m << s) -- a shift and a v_bitop3 each, four VALU per pair.
 template <int S>
 __device__ __forceinline__ void split_swap(uint32_t (&x)[S], int stage) {
   constexpr uint32_t masks[5] = {0x0000FFFFu, 0x00FF00FFu, 0x0F0F0F0Fu, 0x33333333u, 0x55555555u};
+  constexpr uint32_t kSel = ((TA & TC) | (TB & ~TC)) & 0xFF;  // c ? a : b, bit by bit
   const int a = SplitNet<S>::a[stage], sh = 16 >> stage;
   const uint32_t m = masks[stage];
 #pragma unroll
   for (int i = 0; i < S; ++i) {
     if ((i >> a) & 1) continue;
     const int k = i | (1 << a);
-    const uint32_t t = ((x[i] >> sh) ^ x[k]) & m;
-    x[k] ^= t;
-    x[i] ^= t << sh;
+    const uint32_t xi = x[i], xk = x[k];
+    if (sh == 16) {  // A.hi16 <-> B.lo16
+      x[i] = __builtin_amdgcn_perm(xk, xi, 0x05040100u);
+      x[k] = __builtin_amdgcn_perm(xk, xi, 0x07060302u);
+    } else if (sh == 8) {  // A bytes 1, 3 <-> B bytes 0, 2
+      x[i] = __builtin_amdgcn_perm(xk, xi, 0x06020400u);
+      x[k] = __builtin_amdgcn_perm(xk, xi, 0x07030501u);
+    } else {
+      x[k] = lut3<kSel>(xi >> sh, xk, m);
+      x[i] = lut3<kSel>(xk << sh, xi, m << sh);
+    }
   }
 }
 

@@ -475,6 +475,11 @@ constexpr int kContainsNet = 6;  // tail network of the fused kernel (as k_step'
 // sees one assembly loop's pins at a time: 8 takes 70 VGPRs (7 waves per
 // SIMD), where one shared pass took 84 (5), and 7 takes 62 (8 waves).
 constexpr int kContainsLo = 7, kContainsHi = 8;
+// 9: both in one kernel (each wave takes the loop its window calls for), so
+// that one launch answers any target; the kernel takes kContainsHi's 72
+// VGPRs (7 waves per SIMD), which costs the low layout nothing measurable
+// (6 above: the low layout's occupancy alone gained nothing)
+constexpr int kContainsAll = 9;
 // the light-cone path of kContainsLo (cone_max below): universes per wave chunk
 // (Measured in the compiler's allocation, not shipped: the whole board in the
 // natural layout for wider cones at <= 4 generations -- 10-35 % faster there
@@ -750,7 +755,13 @@ __device__ __forceinline__ void cone_wave_rows(const uint64_t *in, const uint64_
 // cone_max columns (0 = never) is answered on that cone: kContainsLo's waves
 // step only those columns in the natural layout (cone_wave, 8 universes per
 // wave chunk, looping over the batch), every other ASM's waves return at once.
-template <int S, int NET, int ASM = 0>
+// PF (16-byte aligned batch, no final states): the wave's next group of P
+// universes is fetched into LDS by P / 2 sixteen-byte-per-lane
+// global_load_lds (LDS-DMA: no VGPR destination, so the assembly loops keep
+// their registers) as soon as the current group has been read out, and
+// streams in while the current group steps; the generation loops' own LDS
+// traffic is the exchange area, a different 2 KiB.
+template <int S, int NET, int ASM = 0, bool PF = false>
 __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *in, uint64_t *fin,
                                                                 const uint64_t *__restrict__ wanted,
                                                                 const uint64_t *__restrict__ unwanted,
@@ -759,6 +770,7 @@ __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *
   constexpr int P = S / 2;
   constexpr uint32_t every = P == 1 ? ~0u : P == 2 ? 0x55555555u : P == 4 ? 0x11111111u : 0x01010101u;
   __shared__ uint32_t lds[kWavesPerBlock * S * kWave];
+  __shared__ uint64_t stage_all[PF ? kWavesPerBlock : 1][PF ? P * kWave : 1];  // (PF's fetch)
   const int lane = threadIdx.x & (kWave - 1);
   const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   // the target's care cells in this lane's column (both windows read it;
@@ -767,7 +779,7 @@ __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *
   const uint64_t care_col = wanted[lane] | unwanted[lane];
   // (2 gens in 64 bits: in 32 it wraps for gens >= 2^31)
   if (cone_max && cone_max <= 32u && !fin && 2ull * gens < cone_max && cone_fits(care_col, gens, cone_max)) {
-    if constexpr (ASM == kContainsLo) {
+    if constexpr (ASM == kContainsLo || ASM == kContainsAll) {
       uint32_t cxs, cK;
       cone_window(care_col, gens, cxs, cK);  // cK <= cone_max (cone_fits)
       {
@@ -809,7 +821,75 @@ __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *
   // as the generation loop; every wave-uniform choice of loop (below) gets
   // its own copy of this pass, so that each assembly loop's pinned registers
   // are all the register allocator sees around it
+  auto universes_pf = [&](auto &&gens_loop) __attribute__((always_inline)) {
+    static_assert(P % 2 == 0, "pairs of universes per 16-byte load");
+    uint64_t *img = stage_all[PF ? wib : 0];
+    const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock * P;
+    auto fetch = [&](uint64_t ub) __attribute__((always_inline)) {
+      const uint32_t ln = lane_id_fresh();
+#pragma unroll
+      for (int i = 0; i < P / 2; ++i) {
+        uint64_t u = ub + 2 * i + (ln >> 5);
+        if (u >= n) u = n - 1;  // (a valid address; its answer is not stored)
+        const char *src = reinterpret_cast<const char *>(in + u * kWave) + (ln & 31) * 16;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                         (__attribute__((address_space(3))) void *)(img + i * 2 * kWave), 16, 0, 2);
+      }
+    };
+    uint64_t u0 = ((uint64_t)blockIdx.x * kWavesPerBlock + wib) * P;
+    if (u0 >= n) return;
+    fetch(u0);
+    bool stored = false;  // an answer store was issued after the pending fetch
+    for (; u0 < n; u0 += stride) {
+      const uint64_t left = n - u0;
+      const uint32_t avail = (left >> 2) ? (uint32_t)P : (uint32_t)left;
+      // the fetch is the only older vector-memory op but the answer store
+      // (in issue order: MI355X_MICROARCH.md, s_waitcnt vmcnt)
+      if (stored) __builtin_amdgcn_s_waitcnt(kWaitVm1);
+      else __builtin_amdgcn_s_waitcnt(kWaitVm0);
+      uint32_t r[S];
+      {
+        // the P columns of this lane, read in one assembly block: a compiled
+        // LDS read after an LDS-DMA makes the compiler wait for every
+        // outstanding vector-memory op (vmcnt(0)), the last answer store
+        // included; the counted wait above is the one this read needs
+        static_assert(P == 4, "four universes per group");
+        const uint32_t at = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)img +
+                            lane_id_fresh() * 8u;
+        uint64_t v0, v1, v2, v3;
+        asm volatile(
+            "ds_read_b64 %0, %4\n"
+            "ds_read_b64 %1, %4 offset:512\n"
+            "ds_read_b64 %2, %4 offset:1024\n"
+            "ds_read_b64 %3, %4 offset:1536\n"
+            "s_waitcnt lgkmcnt(0)\n"
+            : "=&v"(v0), "=&v"(v1), "=&v"(v2), "=&v"(v3)
+            : "v"(at)
+            : "memory");
+        W c[P] = {split(v0), split(v1), split(v2), split(v3)};
+        if (y0) {  // (wave-uniform)
+#pragma unroll
+          for (int u = 0; u < P; ++u) c[u] = split(rotr64(join(c[u]), y0));
+        }
+        if (u0 + stride < n) fetch(u0 + stride);  // (the stage is read out: the next group may land)
+        Split<S>::load(c, r);
+      }
+      uint32_t hit[P];
+#pragma unroll
+      for (int u = 0; u < P; ++u) hit[u] = 0;
+      gens_loop(r, hit);
+      const uint32_t ln2 = lane_id_fresh();
+      uint32_t h = hit[0];
+#pragma unroll
+      for (int u = 1; u < P; ++u) h = ln2 == (uint32_t)u ? hit[u] : h;
+      if (ln2 < avail) first[u0 + ln2] = h;  // one store instruction
+      stored = true;
+    }
+  };
   auto universes = [&](auto &&gens_loop) __attribute__((always_inline)) {
+    if constexpr (PF) {
+      if (!fin) return universes_pf(gens_loop);
+    }
     const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock * P;
     for (uint64_t u0 = ((uint64_t)blockIdx.x * kWavesPerBlock + wib) * P; u0 < n; u0 += stride) {
       // the wave's universes u0 .. u0 + avail - 1 from scalar bases: a 64-bit
@@ -822,8 +902,11 @@ __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *
       uint32_t r[S];
       W c[P];
 #pragma unroll
-      for (int u = 0; u < P; ++u)
-        c[u] = (uint32_t)u < avail ? split(rotr64(src[u * kWave + ln], y0)) : W{0u, 0u};
+      for (int u = 0; u < P; ++u) c[u] = (uint32_t)u < avail ? split(src[u * kWave + ln]) : W{0u, 0u};
+      if (y0) {  // (wave-uniform: the row window's rotation, none for a window of 8 rows from row 0)
+#pragma unroll
+        for (int u = 0; u < P; ++u) c[u] = split(rotr64(join(c[u]), y0));
+      }
       Split<S>::load(c, r);
       uint32_t hit[P];
 #pragma unroll
@@ -835,7 +918,7 @@ __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *
         uint64_t *dst = fin + u0 * kWave;
 #pragma unroll
         for (int u = 0; u < P; ++u)
-          if ((uint32_t)u < avail) dst[u * kWave + ln2] = rotr64(join(c[u]), (64 - y0) & 63);
+          if ((uint32_t)u < avail) dst[u * kWave + ln2] = y0 ? rotr64(join(c[u]), 64 - y0) : join(c[u]);
       }
       if (ln2 == 0) {
 #pragma unroll
@@ -869,6 +952,12 @@ __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *
       LIFEAPI_RUN(split_contains_asm_lean);
     } else if constexpr (ASM == 8) {
       if (h == 5) LIFEAPI_RUN(split_contains_asm_batch_h5);
+      else if (h == 6) LIFEAPI_RUN(split_contains_asm_batch_h6);
+      else if (h == 7) LIFEAPI_RUN(split_contains_asm_batch_h7);
+      else LIFEAPI_RUN(split_contains_asm_lean);
+    } else if constexpr (ASM == kContainsAll) {
+      if (h <= kLowRows) LIFEAPI_RUN(split_contains_asm_batch_lo);
+      else if (h == 5) LIFEAPI_RUN(split_contains_asm_batch_h5);
       else if (h == 6) LIFEAPI_RUN(split_contains_asm_batch_h6);
       else if (h == 7) LIFEAPI_RUN(split_contains_asm_batch_h7);
       else LIFEAPI_RUN(split_contains_asm_lean);

@@ -266,6 +266,42 @@ def filter_digests() -> dict:
     return out
 
 
+def full_height_target():
+    """A whole-board target whose care cells sit in every fourth row, one per
+    row at column 3y mod 64, all required dead: no column window, no row
+    window (its care rows leave no run of 4 empty rows), so the iterated
+    filter runs the full board in the split layout; 16 dead cells are
+    found in about 0.3 % of stepped random universes, so the answers carry
+    first hits at every generation count"""
+    w, u = np.zeros(64, np.uint64), np.zeros(64, np.uint64)
+    for y in range(0, 64, 4):
+        u[(3 * y) % 64] |= np.uint64(1 << y)
+    return w, u
+
+
+FILTER_ITER_GENS = {"block": (5, 8, 13), "whole_board": (5, 8), "full_height": (3, 5, 8)}
+
+
+def filter_iter_digests() -> dict:
+    """The iterated search filter (first hits only, 3-13 generations) on the
+    config-2 input (1M universes, seed 2): the reference's own loop of Step()
+    then Contains(LifeTarget) after every generation (ref_shim.cpp
+    ref_step_contains_batch), as digests of the per-universe first-hit
+    generations -- bench.py secondary_filter_iter's check"""
+    x = P.fill(1 << 20, seed=2)
+    tg = dict(filter_targets())
+    tg["full_height"] = full_height_target()
+    out = {"universes": 1 << 20, "seed": 2, "targets": {}}
+    for name, (w, u) in tg.items():
+        row = {"wanted": [f"{int(v):016x}" for v in w], "unwanted": [f"{int(v):016x}" for v in u], "gens": {}}
+        for g in FILTER_ITER_GENS[name]:
+            first, _ = R.step_contains_batch(x, w, u, g, nthreads=8)
+            row["gens"][str(g)] = {"first_digest": f"{P.digest(first.astype(np.uint64)):016x}",
+                                   "hits": int((first > 0).sum())}
+        out["targets"][name] = row
+    return out
+
+
 def config5_digest() -> dict:
     """Config 5 at bench size: 256K universes of 11 planes (the seed-6
     splitmix64 fill of 256K x 11 universes, bench.py secondary_config5)
@@ -288,6 +324,15 @@ def main():
         with open(path, "w") as f:
             json.dump(meta, f, indent=1)
         print(json.dumps(meta["digests"]["config5"], indent=1))
+        return
+    if "--only-filter-iter" in sys.argv:  # add / refresh digests.config2_filter_iter alone
+        path = os.path.join(HERE, "golden.json")
+        with open(path) as f:
+            meta = json.load(f)
+        meta["digests"]["config2_filter_iter"] = filter_iter_digests()
+        with open(path, "w") as f:
+            json.dump(meta, f, indent=1)
+        print(json.dumps(meta["digests"]["config2_filter_iter"]["targets"], indent=1))
         return
     if "--only-filter" in sys.argv:  # add / refresh digests.config2_filter alone
         path = os.path.join(HERE, "golden.json")
@@ -411,6 +456,7 @@ def main():
 
     meta["digests"] = batch_digests()
     meta["digests"]["config2_filter"] = filter_digests()
+    meta["digests"]["config2_filter_iter"] = filter_iter_digests()
     meta["digests"]["config5"] = config5_digest()
     with open(os.path.join(HERE, "golden.json"), "w") as f:
         json.dump(meta, f, indent=1)

@@ -790,10 +790,11 @@ def test_refined_step_full_size_sample(hip, port):
 
 
 def test_stable_passes_8_byte_aligned_batch(hip, port):
-    """SynchroniseStateKnown, SignalNeighbours and PropagateStep move a
-    16-byte aligned batch through LDS with 16-byte accesses (stencils.hip,
-    k_stable_dma); a batch that is only 8-byte aligned (the ABI's
-    requirement) takes k_stable.  Both forms, every pass, against the oracle,
+    """SynchroniseStateKnown, UpdateOptions, SignalNeighbours, PropagateStep
+    and StabiliseOptions (passes 0, 1, 2, 3, 5) move a 16-byte aligned batch
+    through LDS with 16-byte accesses (stencils.hip, k_stable_dma); Propagate
+    keeps k_stable, and a batch that is only 8-byte aligned (the ABI's
+    requirement) takes k_stable for every pass.  Both forms, every pass, against the oracle,
     on a search's next node and on fresh options."""
     n = 777
     fresh = _stable_cases(port, n, seed=41)

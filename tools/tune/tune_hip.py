@@ -361,3 +361,19 @@ def rows_probe(states, wanted, unwanted, generations, y0, sleep=0, out=None, str
     hip._check(lib.lifeapi_tune_rows_probe(states.data_ptr(), wanted.data_ptr(), unwanted.data_ptr(), out.data_ptr(),
                                            n, generations, y0, sleep, hip._stream(stream)))
     return out
+
+
+lib.lifeapi_tune_filter_iter.argtypes = [_vp, _vp, _vp, _vp, _sz, _u32, _int, _vp]
+lib.lifeapi_tune_filter_iter.restype = _int
+# tools/filter_iter_probe.py's forms of the round-6 A/B: blocks per CU | PF | Hi / Lo alone
+FILTER_ITER_FORMS = {"pair32": 32, "pair32_pf": 32 | 0x100, "pair7_pf": 7 | 0x100,
+                     "all32": 32 | 0x800, "all32_pf": 32 | 0x900, "all7_pf": 7 | 0x900, "all14_pf": 14 | 0x900}
+
+
+def filter_iter(states, wanted, unwanted, generations, variant, stream=None):
+    """the split pair without final states, round 6 variants (tune_step.hip)"""
+    n = hip._universes(states)
+    first = torch.empty(n, dtype=torch.int32, device=states.device)
+    hip._check(lib.lifeapi_tune_filter_iter(states.data_ptr(), wanted.data_ptr(), unwanted.data_ptr(),
+                                            first.data_ptr(), n, generations, variant, hip._stream(stream)))
+    return first

@@ -620,6 +620,46 @@ int lifeapi_tune_step_contains_pair(const uint64_t *d_in, uint64_t *d_final, con
   return launched("k_step_contains_split (tuning) launch");
 }
 
+/* the iterated search filter without final states on the split pair
+ * (round 6 A/B, tools/filter_iter_probe.py): variant bits 0-7 = blocks per
+ * CU of both grids (0: one-shot), bit 8 = the LDS-DMA prefetch form (PF),
+ * bit 9 = kContainsHi alone (the Lo kernel not launched: answers only for
+ * targets whose row window exceeds 4 rows), bit 10 = kContainsLo alone,
+ * bit 11 = the merged kernel (kContainsAll) alone: one launch, any target */
+int lifeapi_tune_filter_iter(const uint64_t *d_in, const uint64_t *d_wanted, const uint64_t *d_unwanted,
+                             uint32_t *d_first_gen, size_t n, uint32_t generations, int variant, void *stream) {
+  if (n == 0) return LIFEAPI_OK;
+  if (!d_in || !d_wanted || !d_unwanted || !d_first_gen || generations <= 2 || variant < 0 ||
+      ((variant & 0x100) && !aligned16(d_in)))
+    return fail(LIFEAPI_E_INVALID, "bad argument%s");
+  int cus = 0, rc = device_cus(cus);
+  if (rc != LIFEAPI_OK) return rc;
+  const int cap = variant & 0xFF;
+  const bool pf = (variant & 0x100) != 0, hi_only = (variant & 0x200) != 0, lo_only = (variant & 0x400) != 0;
+  using Fn = void (*)(const uint64_t *, uint64_t *, const uint64_t *, const uint64_t *, uint32_t *, uint64_t, uint32_t,
+                      uint32_t);
+  const Fn lo = pf ? k_step_contains_split<8, kContainsNet, kContainsLo, true>
+                   : k_step_contains_split<8, kContainsNet, kContainsLo>;
+  const Fn hi = pf ? k_step_contains_split<8, kContainsNet, kContainsHi, true>
+                   : k_step_contains_split<8, kContainsNet, kContainsHi>;
+  const dim3 grid(grid_for((n + 3) / 4, cus, cap));
+  if (variant & 0x800) {
+    const Fn all = pf ? k_step_contains_split<8, kContainsNet, kContainsAll, true>
+                      : k_step_contains_split<8, kContainsNet, kContainsAll>;
+    hipLaunchKernelGGL(all, grid, dim3(kBlock), 0, (hipStream_t)stream, d_in, nullptr, d_wanted, d_unwanted,
+                       d_first_gen, (uint64_t)n, generations, 32u);
+    return launched("k_step_contains_split (tuning) launch");
+  }
+  for (int k = 0; k < 2; ++k) {
+    if ((k == 0 && hi_only) || (k == 1 && lo_only)) continue;
+    hipLaunchKernelGGL(k == 0 ? lo : hi, grid, dim3(kBlock), 0, (hipStream_t)stream, d_in, nullptr, d_wanted,
+                       d_unwanted, d_first_gen, (uint64_t)n, generations, 32u);  // (cone_max: cone_kernels.hpp kConeIterColumns)
+    rc = launched("k_step_contains_split (tuning) launch");
+    if (rc != LIFEAPI_OK) return rc;
+  }
+  return LIFEAPI_OK;
+}
+
 /* the pair layout (k_step_pair), schedule `variant` 0..5 */
 int lifeapi_tune_step_pair(const uint64_t *d_in, uint64_t *d_out, size_t n, uint32_t generations, int variant,
                            void *stream) {
