@@ -31,7 +31,7 @@
 
 #include <type_traits>
 
-#include "cone_split.hpp"
+#include "step_kernels.hpp"
 
 namespace lifeapi_impl {
 namespace {
@@ -73,21 +73,7 @@ __device__ __forceinline__ void cone_wave_full16(const uint64_t *in, const uint6
   }
 }
 
-// One pass of the whole-board LDS form: the RB universes from ub on (RB * 512
-// contiguous bytes; past n, universe n - 1 again: a valid address whose
-// answer is never stored) into img by RB / 2 sixteen-byte-per-lane
-// global_load_lds (lanes 0-31 one universe, 32-63 the next).
-template <int RB>
-__device__ __forceinline__ void dma_fetch_pass(const uint64_t *in, uint64_t n, uint64_t ub, int lane, uint64_t *img) {
-#pragma unroll
-  for (int i = 0; i < RB / 2; ++i) {
-    uint64_t u = ub + 2 * i + (lane >> 5);
-    if (u >= n) u = n - 1;
-    const char *src = reinterpret_cast<const char *>(in + u * kWave) + (lane & 31) * 16;
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
-                                     (__attribute__((address_space(3))) void *)(img + i * 2 * kWave), 16, 0, 2);
-  }
-}
+// (dma_fetch_pass: cone_split.hpp)
 
 // The whole-board pass (K = 64) through LDS: each register set is one
 // universe, RB sets per pass; the RB universes of a pass (RB * 512
@@ -155,147 +141,10 @@ __device__ __forceinline__ void cone_wave_full_dma(const uint64_t *in, uint64_t 
   }
 }
 
-// The whole-board pass of the filter (FIRST, gens >= 1) when the target's care
-// rows, widened by the light cone, fit FW = 32 / PK rows: rows y0 .. y0 + FW - 1
-// of each universe's column are cut out by one v_alignbit (WRAP: the window
-// crosses row 63), PK universes share one 32-bit register (v_perm, universe j
-// of the word in bits j FW .. j FW + FW - 1), and the generation runs on the
-// packed words with 1-bit shifts for the vertical neighbours.  The bits
-// shifted in at a field's edges (the next field's, or zero) are wrong, and the
-// error moves one row inwards per generation -- never onto a care row, which
-// lies at least `gens` rows inside its field (cone_rows).  Columns are whole
-// (the DPP rotate is the torus), so the care cells are exact.  Same passes,
-// LDS image and answers as cone_wave_full_dma; a universe costs one cut, a
-// share of the pack, 1 / PK of the network and its field's test.
-template <int RB, int PK, bool WRAP, typename OutT, int SLEEP = 0>
-__device__ __forceinline__ void cone_wave_rows_dma(const uint64_t *in, uint64_t w64, uint64_t m64,
-                                                   OutT *__restrict__ out, uint64_t n, uint64_t u_first,
-                                                   uint64_t u_step, uint32_t gens, uint32_t y0, int lane,
-                                                   uint64_t *img, bool prefetched) {
-  static_assert(RB % 2 == 0 && RB % PK == 0 && 2 * RB <= kWave, "passes of whole words and pairs of universes");
-  static_assert(PK == 1 || PK == 2 || PK == 4, "fields of 32, 16 or 8 rows");
-  constexpr int FW = 32 / PK, NW = RB / PK;
-  constexpr uint32_t fmask = FW == 32 ? ~0u : (1u << FW) - 1u;
-  constexpr uint32_t rep = PK == 1 ? 1u : PK == 2 ? 0x00010001u : 0x01010101u;
-  const uint32_t sh = y0 & 31u;
-  auto cut = [&](uint64_t v) __attribute__((always_inline)) {
-    const W w = split(v);
-    return WRAP ? __builtin_amdgcn_alignbit(w.lo, w.hi, sh) : __builtin_amdgcn_alignbit(w.hi, w.lo, sh);
-  };
-  const uint32_t tw = (cut(w64) & fmask) * rep, tm = (cut(m64) & fmask) * rep;
-  constexpr uint32_t kDiff = ((TA ^ TB) & TC) & 0xFF;  // (s ^ wanted) & care
-  auto base = [&](uint64_t t) { return u_first + (t >> 1) * u_step + (t & 1) * RB; };
-  auto fetch = [&](uint64_t ub) __attribute__((always_inline)) { dma_fetch_pass<RB>(in, n, ub, lane, img); };
-  if (u_first >= n) return;
-  if (!prefetched) fetch(u_first);  // (else the caller issued it)
-  uint32_t mine = 0;  // lane L: the answer for universe (chunk start) + L
-  int after = 0;      // vector-memory ops issued after the pending fetch (the chunk's answer store)
-  for (uint64_t t = 0;; ++t) {
-    const uint64_t ub = base(t);
-    if (ub >= n) break;
-    if (after) __builtin_amdgcn_s_waitcnt(kWaitVm1);
-    else __builtin_amdgcn_s_waitcnt(kWaitVm0);
-    uint32_t a[NW];
-#pragma unroll
-    for (int m = 0; m < NW; ++m) {
-      uint32_t e[PK];
-#pragma unroll
-      for (int j = 0; j < PK; ++j) e[j] = cut(img[(m * PK + j) * kWave + lane]);
-      if constexpr (PK == 1) {
-        a[m] = e[0];
-      } else if constexpr (PK == 2) {
-        a[m] = __builtin_amdgcn_perm(e[1], e[0], 0x05040100u);  // low halves: e0 | e1 << 16
-      } else {
-        const uint32_t p01 = __builtin_amdgcn_perm(e[1], e[0], 0x0C0C0400u);  // e0.b0, e1.b0
-        const uint32_t p23 = __builtin_amdgcn_perm(e[3], e[2], 0x0C0C0400u);  // e2.b0, e3.b0
-        a[m] = __builtin_amdgcn_perm(p23, p01, 0x05040100u);
-      }
-    }
-    __builtin_amdgcn_s_waitcnt(kWaitLgkm0);  // read out before the next fetch lands
-    const uint64_t nb = base(t + 1);
-    if (nb < n) fetch(nb);
-    if constexpr (SLEEP > 0) __builtin_amdgcn_s_sleep(SLEEP);  // (the tuning build's pacing probe)
-    uint32_t res[RB];
-#pragma unroll
-    for (int k = 0; k < RB; ++k) res[k] = 0;
-    for (uint32_t g = 1; g <= gens; ++g) {
-#pragma unroll
-      for (int m = 0; m < NW; ++m) {
-        const uint32_t L = dpp_prev(a[m]), R = dpp_next(a[m]);
-        const uint32_t h0 = lut3<kXor3>(L, a[m], R), h1 = lut3<kMaj>(L, a[m], R);
-        a[m] = life_tail6(h0 << 1, h0, h0 >> 1, h1 << 1, h1, h1 >> 1, a[m]);
-        const uint32_t d = lut3<kDiff>(a[m], tw, tm);
-#pragma unroll
-        for (int j = 0; j < PK; ++j) {
-          const bool clean = __ballot((d & (fmask << (j * FW))) != 0u) == 0ull;
-          if (res[m * PK + j] == 0 && clean) res[m * PK + j] = g;
-        }
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < RB; ++k)
-      if ((uint32_t)lane == (uint32_t)((t & 1) * RB + k)) mine = res[k];
-    after = 0;
-    if ((t & 1) || ub + RB >= n) {  // the chunk's last pass: store its answers
-      const uint64_t u0 = base(t & ~1ull);
-      if (lane < 2 * RB && u0 + lane < n) out[u0 + lane] = (OutT)mine;
-      mine = 0;
-      after = 1;
-    }
-  }
-}
+// (cone_wave_rows_dma: cone_split.hpp)
 
-// The row window of a filter's whole-board pass (cone_wave_rows_dma): the
-// smallest cyclic window of the target's care rows, widened by `gens` rows on
-// either side, and the most universes per 32-bit word whose field holds it
-// (PK = 4, 2, 1: fields of 8, 16, 32 rows); 0 when it needs more than 32 rows.
-__device__ __forceinline__ int cone_rows(uint64_t care_col, uint32_t gens, uint32_t &y0) {
-  const uint32_t lo = wave_or_u32_dpp((uint32_t)care_col), hi = wave_or_u32_dpp((uint32_t)(care_col >> 32));
-  uint32_t cy0, h;
-  care_window((uint64_t)lo | (uint64_t)hi << 32, cy0, h);
-  if (gens >= 16u) return 0;
-  const uint32_t need = h + 2u * gens;
-  y0 = (cy0 - gens) & 63u;
-  return need <= 8u ? 4 : need <= 16u ? 2 : need <= 32u ? 1 : 0;
-}
-
-// Waves after the first take the row window from the last report from this
-// many generations on.  1M universes, bench.py's whole-board target, each
-// launch alone after a scrub, interleaved with the same launch finding the
-// window itself (tools/filter_interleave.py rows_hint / rows_early,
-// profiles/r05/hint/): 3 / 4 / 5 / 8 generations 0.081 / 0.096 / 0.109 /
-// 0.188 ms against 0.095 / 0.108 / 0.122 / 0.194; at 1 generation no
-// difference (0.083-0.085 both), at 2 it costs 4 % (0.086 against 0.082,
-// unexplained; every series on the box agreed).
-constexpr uint32_t kConeHintGens = 3;
-// A column window (5-32 columns) takes the row window too from this many
-// generations on (cone_wave_rows; below it the pass is not VALU-bound).
-constexpr uint32_t kConeRowsWindowGens = 3;
-
-// The filter's report word for a target (host.hpp cone_class_slot): the
-// window K (64: the whole board) in bits 0-7, and for a whole board the
-// row-window class (cone_rows: 4, 2, 1 universes per register, 0 none) in
-// bits 8-15 and its first row y0 in bits 16-21.
-constexpr int32_t kReportWhole = kWave;
-__device__ __forceinline__ bool report_whole(int32_t word) { return (word & 0xFF) == kReportWhole; }
-__device__ __forceinline__ int32_t report_word(uint32_t K, int pk, uint32_t y0 = 0) {
-  return (int32_t)K | (pk << 8) | (pk ? (int32_t)(y0 & 63u) << 16 : 0);
-}
-
-// The report of a target the split pair answers (step.hip: more generations
-// than k_cone_adapt takes unless the last report allows it): one wave
-// computes what k_cone_adapt's first wave would report and writes it, so
-// that the next call on this target can choose.
-__device__ __forceinline__ int32_t cone_report(uint64_t care_col, uint32_t gens) {
-  if (cone_whole(care_col, gens)) {
-    uint32_t y0 = 0;
-    const int pk = cone_rows(care_col, gens, y0);
-    return report_word(kWave, pk, y0);
-  }
-  uint32_t xs = 0, K = kWave, y0 = 0;
-  cone_window(care_col, gens, xs, K);
-  return report_word(K, cone_rows(care_col, gens, y0), y0);
-}
+// (cone_rows, kConeHintGens, kConeRowsWindowGens and the report word:
+// step_kernels.hpp)
 __global__ __launch_bounds__(kWave) __attribute__((unused)) void k_cone_classify(const uint64_t *__restrict__ wanted,
                                                          const uint64_t *__restrict__ unwanted, uint32_t gens,
                                                          int32_t *cls) {
@@ -367,37 +216,16 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
     if (cls && wave == 0 && lane == 0 && word != cls_last) *reinterpret_cast<volatile int32_t *>(cls) = word;
   };
   // (the smallest chunk any path takes: a wave starting past n has no work)
-  constexpr uint64_t kMinChunk = DMA && 2 * RMAX < 16 ? 2 * RMAX : 16;
+  // (WIN: the window split layout's sets are as small as 8 universes, 64
+  // lanes x 32 rows)
+  constexpr uint64_t kMinChunk = WIN ? 8 : DMA && 2 * RMAX < 16 ? 2 * RMAX : 16;
   if (wave * kMinChunk >= n) return;
   const uint32_t g = FIRST ? gens : 0u;
   const uint64_t w64 = wanted[lane], m64 = w64 | unwanted[lane], care_col = m64;
   uint32_t xs = 0, K = kWave;
-  // the window split layout (WIN): R = 32 rows for row class 1, 16 for 2 and
-  // 4; P = the lanes per universe the column window needs (>= 16 for R = 16:
-  // one answer per lane), universes u_first + k (64 / P) (256 / R)
+  // the window split layout (WIN, cone_split.hpp)
   auto split_pass = [&](int pk_, uint32_t y0_, uint64_t nw_) __attribute__((always_inline)) {
-    auto run = [&](auto p_c, auto r_c) __attribute__((always_inline)) {
-      constexpr int Pc = decltype(p_c)::value, Rc = decltype(r_c)::value;
-      constexpr uint64_t UPS = (uint64_t)(kWave / Pc) * (256 / Rc);
-      if (wave * UPS >= n) return;
-      if (y0_ >= 32u)
-        cone_wave_split<Pc, Rc, true>(in, wanted, unwanted, out, n, wave * UPS, nw_ * UPS, gens, xs, K, y0_, lane);
-      else
-        cone_wave_split<Pc, Rc, false>(in, wanted, unwanted, out, n, wave * UPS, nw_ * UPS, gens, xs, K, y0_, lane);
-    };
-    using I8 = std::integral_constant<int, 8>;
-    using I16 = std::integral_constant<int, 16>;
-    using I32 = std::integral_constant<int, 32>;
-    using I64 = std::integral_constant<int, 64>;
-    if (pk_ == 1) {
-      if (K <= 8u) return run(I8{}, I32{});
-      if (K <= 16u) return run(I16{}, I32{});
-      if (K <= 32u) return run(I32{}, I32{});
-      return run(I64{}, I32{});
-    }
-    if (K <= 16u) return run(I16{}, I16{});
-    if (K <= 32u) return run(I32{}, I16{});
-    return run(I64{}, I16{});
+    cone_split_pass(in, wanted, unwanted, out, n, wave, nw_, gens, xs, K, pk_, y0_, lane);
   };
   if constexpr (DMA) {
     __shared__ uint64_t img_all[kWavesPerBlock][RMAX * kWave];
@@ -410,7 +238,7 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
     // (WIN: a whole board whose report carries a row class from
     // kConeRowsWindowGens generations on takes the split window, which loads
     // by itself)
-    const bool win_hint = WIN && FIRST && gens >= kConeRowsWindowGens && ((cls_last >> 8) & 0xFF) != 0;
+    const bool win_hint = WIN && FIRST && gens >= kConeWholeWinGens && ((cls_last >> 8) & 0xFF) != 0;
     const bool early = (cls_last & 0xFF) == kReportWhole && !win_hint && wave * c < n;
     if (early) dma_fetch_pass<RMAX>(in, n, wave * c, lane, img);
     auto leave = [&]() __attribute__((always_inline)) {
@@ -442,9 +270,9 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
       }
     }
     if (whole) {
-      if (kmax < (uint32_t)kWave || wave * c >= n) return leave();
+      if (kmax < (uint32_t)kWave) return leave();
       if constexpr (FIRST && WIN) {
-        if (pk > 0 && gens >= kConeRowsWindowGens) {
+        if (pk > 0 && gens >= kConeWholeWinGens) {  // (its sets may be 8 universes: before the chunk test)
           leave();
           if (cap_waves) {
             if (wave >= cap_waves) return;
@@ -453,6 +281,7 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
           return split_pass(pk, y0, nw);
         }
       }
+      if (wave * c >= n) return leave();
       if constexpr (FIRST && ROWS) {
         auto rows = [&](auto pk_c, auto wrap_c) __attribute__((always_inline)) {
           cone_wave_rows_dma<RMAX, decltype(pk_c)::value, decltype(wrap_c)::value>(
@@ -580,7 +409,13 @@ constexpr int kConeAdaptBlocksPerCU = 16;
 // generations k_cone_adapt / split pair = 0.65-0.94 on a 4-column and a
 // whole-board target at 64K-128K, 0.83-1.02 at 256K, but 1.07-1.14 on the
 // whole board at 512K.
-constexpr uint32_t kConeAloneGens = 4, kConeAloneGensSmall = 6;
+constexpr uint32_t kConeAloneGens = 4, kConeAloneGensSmall = 6;  // (round 5's routing; the tuning build's A/Bs)
+// Round 6: the merged split kernel (step.hip, 3+ generations without final
+// states) on a grid of at most this many blocks per CU looping over the
+// batch (1M universes: 16 and 32 within 1-3 % of each other on every
+// target, 8 up to 9 % slower on the one-row whole board; profiles/r06/ab/)
+constexpr int kFilterIterBlocksPerCU = 16;
+// (kConeWholeWinGens: step_kernels.hpp)
 // Beyond those, up to this many generations (exclusive), a whole-board target
 // whose row window fits 32 rows (cone_rows) keeps k_cone_adapt (step.hip).
 constexpr uint32_t kConeRowsMaxGens = 16;

@@ -41,10 +41,118 @@
 // clean generation of every universe not yet found.
 #pragma once
 
-#include "step_kernels.hpp"
+#include <type_traits>
+
+#include "device.hpp"
 
 namespace lifeapi_impl {
 namespace {
+
+// One pass of the whole-board LDS form: the RB universes from ub on (RB * 512
+// contiguous bytes; past n, universe n - 1 again: a valid address whose
+// answer is never stored) into img by RB / 2 sixteen-byte-per-lane
+// global_load_lds (lanes 0-31 one universe, 32-63 the next).
+template <int RB>
+__device__ __forceinline__ void dma_fetch_pass(const uint64_t *in, uint64_t n, uint64_t ub, int lane, uint64_t *img) {
+#pragma unroll
+  for (int i = 0; i < RB / 2; ++i) {
+    uint64_t u = ub + 2 * i + (lane >> 5);
+    if (u >= n) u = n - 1;
+    const char *src = reinterpret_cast<const char *>(in + u * kWave) + (lane & 31) * 16;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                     (__attribute__((address_space(3))) void *)(img + i * 2 * kWave), 16, 0, 2);
+  }
+}
+
+// The whole-board pass of the filter (FIRST, gens >= 1) when the target's care
+// rows, widened by the light cone, fit FW = 32 / PK rows: rows y0 .. y0 + FW - 1
+// of each universe's column are cut out by one v_alignbit (WRAP: the window
+// crosses row 63), PK universes share one 32-bit register (v_perm, universe j
+// of the word in bits j FW .. j FW + FW - 1), and the generation runs on the
+// packed words with 1-bit shifts for the vertical neighbours.  The bits
+// shifted in at a field's edges (the next field's, or zero) are wrong, and the
+// error moves one row inwards per generation -- never onto a care row, which
+// lies at least `gens` rows inside its field (cone_rows).  Columns are whole
+// (the DPP rotate is the torus), so the care cells are exact.  Same passes,
+// LDS image and answers as cone_wave_full_dma; a universe costs one cut, a
+// share of the pack, 1 / PK of the network and its field's test.
+template <int RB, int PK, bool WRAP, typename OutT, int SLEEP = 0>
+__device__ __forceinline__ void cone_wave_rows_dma(const uint64_t *in, uint64_t w64, uint64_t m64,
+                                                   OutT *__restrict__ out, uint64_t n, uint64_t u_first,
+                                                   uint64_t u_step, uint32_t gens, uint32_t y0, int lane,
+                                                   uint64_t *img, bool prefetched) {
+  static_assert(RB % 2 == 0 && RB % PK == 0 && 2 * RB <= kWave, "passes of whole words and pairs of universes");
+  static_assert(PK == 1 || PK == 2 || PK == 4, "fields of 32, 16 or 8 rows");
+  constexpr int FW = 32 / PK, NW = RB / PK;
+  constexpr uint32_t fmask = FW == 32 ? ~0u : (1u << FW) - 1u;
+  constexpr uint32_t rep = PK == 1 ? 1u : PK == 2 ? 0x00010001u : 0x01010101u;
+  const uint32_t sh = y0 & 31u;
+  auto cut = [&](uint64_t v) __attribute__((always_inline)) {
+    const W w = split(v);
+    return WRAP ? __builtin_amdgcn_alignbit(w.lo, w.hi, sh) : __builtin_amdgcn_alignbit(w.hi, w.lo, sh);
+  };
+  const uint32_t tw = (cut(w64) & fmask) * rep, tm = (cut(m64) & fmask) * rep;
+  constexpr uint32_t kDiff = ((TA ^ TB) & TC) & 0xFF;  // (s ^ wanted) & care
+  auto base = [&](uint64_t t) { return u_first + (t >> 1) * u_step + (t & 1) * RB; };
+  auto fetch = [&](uint64_t ub) __attribute__((always_inline)) { dma_fetch_pass<RB>(in, n, ub, lane, img); };
+  if (u_first >= n) return;
+  if (!prefetched) fetch(u_first);  // (else the caller issued it)
+  uint32_t mine = 0;  // lane L: the answer for universe (chunk start) + L
+  int after = 0;      // vector-memory ops issued after the pending fetch (the chunk's answer store)
+  for (uint64_t t = 0;; ++t) {
+    const uint64_t ub = base(t);
+    if (ub >= n) break;
+    if (after) __builtin_amdgcn_s_waitcnt(kWaitVm1);
+    else __builtin_amdgcn_s_waitcnt(kWaitVm0);
+    uint32_t a[NW];
+#pragma unroll
+    for (int m = 0; m < NW; ++m) {
+      uint32_t e[PK];
+#pragma unroll
+      for (int j = 0; j < PK; ++j) e[j] = cut(img[(m * PK + j) * kWave + lane]);
+      if constexpr (PK == 1) {
+        a[m] = e[0];
+      } else if constexpr (PK == 2) {
+        a[m] = __builtin_amdgcn_perm(e[1], e[0], 0x05040100u);  // low halves: e0 | e1 << 16
+      } else {
+        const uint32_t p01 = __builtin_amdgcn_perm(e[1], e[0], 0x0C0C0400u);  // e0.b0, e1.b0
+        const uint32_t p23 = __builtin_amdgcn_perm(e[3], e[2], 0x0C0C0400u);  // e2.b0, e3.b0
+        a[m] = __builtin_amdgcn_perm(p23, p01, 0x05040100u);
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(kWaitLgkm0);  // read out before the next fetch lands
+    const uint64_t nb = base(t + 1);
+    if (nb < n) fetch(nb);
+    if constexpr (SLEEP > 0) __builtin_amdgcn_s_sleep(SLEEP);  // (the tuning build's pacing probe)
+    uint32_t res[RB];
+#pragma unroll
+    for (int k = 0; k < RB; ++k) res[k] = 0;
+    for (uint32_t g = 1; g <= gens; ++g) {
+#pragma unroll
+      for (int m = 0; m < NW; ++m) {
+        const uint32_t L = dpp_prev(a[m]), R = dpp_next(a[m]);
+        const uint32_t h0 = lut3<kXor3>(L, a[m], R), h1 = lut3<kMaj>(L, a[m], R);
+        a[m] = life_tail6(h0 << 1, h0, h0 >> 1, h1 << 1, h1, h1 >> 1, a[m]);
+        const uint32_t d = lut3<kDiff>(a[m], tw, tm);
+#pragma unroll
+        for (int j = 0; j < PK; ++j) {
+          const bool clean = __ballot((d & (fmask << (j * FW))) != 0u) == 0ull;
+          if (res[m * PK + j] == 0 && clean) res[m * PK + j] = g;
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < RB; ++k)
+      if ((uint32_t)lane == (uint32_t)((t & 1) * RB + k)) mine = res[k];
+    after = 0;
+    if ((t & 1) || ub + RB >= n) {  // the chunk's last pass: store its answers
+      const uint64_t u0 = base(t & ~1ull);
+      if (lane < 2 * RB && u0 + lane < n) out[u0 + lane] = (OutT)mine;
+      mine = 0;
+      after = 1;
+    }
+  }
+}
 
 // the three index swaps of the window layout (register bit b <-> position
 // bit b), as split_swap's select form
@@ -223,6 +331,39 @@ __device__ __forceinline__ void cone_wave_split(const uint64_t *in, const uint64
     }
     if (lane < UPS && u0 + (uint64_t)lane < n) out[u0 + lane] = (OutT)mine;
   }
+}
+
+// The pass for a window (R = 32 rows for row class 1, 16 for classes 2 and
+// 4; P = the lanes per universe the K columns need, >= 16 for R = 16: one
+// answer per lane), this wave's sets from wave index `wave` of `nw`, sets of
+// (64 / P) (256 / R) universes.
+template <typename OutT>
+__device__ __forceinline__ void cone_split_pass(const uint64_t *in, const uint64_t *__restrict__ wanted,
+                                                const uint64_t *__restrict__ unwanted, OutT *__restrict__ out,
+                                                uint64_t n, uint64_t wave, uint64_t nw, uint32_t gens, uint32_t xs,
+                                                uint32_t K, int pk, uint32_t y0, int lane) {
+  auto run = [&](auto p_c, auto r_c) __attribute__((always_inline)) {
+    constexpr int Pc = decltype(p_c)::value, Rc = decltype(r_c)::value;
+    constexpr uint64_t UPS = (uint64_t)(kWave / Pc) * (256 / Rc);
+    if (wave * UPS >= n) return;
+    if (y0 >= 32u)
+      cone_wave_split<Pc, Rc, true>(in, wanted, unwanted, out, n, wave * UPS, nw * UPS, gens, xs, K, y0, lane);
+    else
+      cone_wave_split<Pc, Rc, false>(in, wanted, unwanted, out, n, wave * UPS, nw * UPS, gens, xs, K, y0, lane);
+  };
+  using I8 = std::integral_constant<int, 8>;
+  using I16 = std::integral_constant<int, 16>;
+  using I32 = std::integral_constant<int, 32>;
+  using I64 = std::integral_constant<int, 64>;
+  if (pk == 1) {
+    if (K <= 8u) return run(I8{}, I32{});
+    if (K <= 16u) return run(I16{}, I32{});
+    if (K <= 32u) return run(I32{}, I32{});
+    return run(I64{}, I32{});
+  }
+  if (K <= 16u) return run(I16{}, I16{});
+  if (K <= 32u) return run(I32{}, I16{});
+  return run(I64{}, I16{});
 }
 
 }  // namespace

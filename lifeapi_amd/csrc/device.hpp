@@ -324,6 +324,31 @@ __device__ __forceinline__ uint64_t block_index() {
   else return blockIdx.x;
 }
 
+__device__ __forceinline__ uint64_t rotr64(uint64_t v, uint32_t k) {
+  return (v >> k) | (v << ((64 - k) & 63));
+}
+// the smallest cyclic window [y0, y0 + h) of rows holding every set bit of
+// rm (wave-uniform; h = 1 for an empty mask): the complement of the longest
+// cyclic run of empty rows, found by binary lifting (run_k bit p = rows
+// p .. p + k - 1 all empty) in a few dozen scalar instructions
+__device__ __forceinline__ void care_window(uint64_t rm, uint32_t &y0, uint32_t &h) {
+  y0 = 0;
+  h = 1;
+  if (rm == 0) return;
+  uint64_t run[6];
+  run[0] = ~rm;  // runs of 1
+#pragma unroll
+  for (int k = 1; k < 6; ++k) run[k] = run[k - 1] & rotr64(run[k - 1], 1u << (k - 1));  // runs of 2^k
+  uint64_t cur = ~0ull;  // starts of runs of length len
+  uint32_t len = 0;
+#pragma unroll
+  for (int k = 5; k >= 0; --k) {
+    const uint64_t t = cur & rotr64(run[k], len);
+    if (t) cur = t, len += 1u << k;
+  }
+  h = 64 - len;
+  y0 = len ? ((uint32_t)__builtin_ctzll(cur) + len) & 63 : 0;
+}
 // s_waitcnt immediates (gfx9 encoding: vmcnt [3:0] + [15:14], expcnt [6:4],
 // lgkmcnt [11:8]): at most N vector-memory ops outstanding, or no LDS op.
 // "s_waitcnt vmcnt(N) waits until all but the wave's N youngest

@@ -148,54 +148,48 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
   }
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
-  if (!d_final && generations <= (n <= kConeAloneSmallUniverses ? kConeAloneGensSmall : kConeAloneGens)) {
-    // the search filter proper (first hits only) up to kConeAloneGens
-    // generations: the target's light cone, or the whole board, in the
-    // natural layout (cone_kernels.hpp k_cone_adapt).  At 3 and 4 generations
-    // it beats the split pair (below) on every target measured: 3-31 %
-    // (tools/ab/search_iter_caps_ab.py, profiles/r04/r04ak: a 4-column target
-    // and a whole-board one, 64K and 1M universes); from 5 on the split
-    // layout takes over for whole-board targets at 1M; batches of <= 256K
-    // take it up to 6 generations (cone_kernels.hpp kConeAloneGensSmall).
-    // A whole-board target takes the universes through LDS (cone_wave_full_dma,
-    // chunks of 16, 8 per pass by global_load_lds, the next pass fetched
-    // while this one steps) on the uncapped grid; the form is chosen by what
-    // the last launch on this target reported (launch_cone_adapt AUTO), so the
-    // first call on a target, and every small target, takes the capped form.
-    // 1M universes, 1 generation, alone after a scrub: 0.0816-0.0849 ms against
-    // 0.0874-0.0889 (tools/filter_dma_ab.py, profiles/r05/filter_dma_ab_r05*.jsonl).
+  if (!d_final && generations <= 2) {
+    // the search filter proper (first hits only) at 1-2 generations: the
+    // target's light cone, or the whole board, in the natural layout
+    // (cone_kernels.hpp k_cone_adapt).  A whole-board target takes the
+    // universes through LDS (cone_wave_full_dma, chunks of 16, 8 per pass by
+    // global_load_lds, the next pass fetched while this one steps) on the
+    // uncapped grid; the form is chosen by what the last launch on this target
+    // reported (launch_cone_adapt AUTO), so the first call on a target, and
+    // every small target, takes the capped form.  1M universes, 1 generation,
+    // alone after a scrub: 0.0816-0.0849 ms against 0.0874-0.0889
+    // (tools/filter_dma_ab.py, profiles/r05/filter_dma_ab_r05*.jsonl).
     return launch_cone_adapt<kConeSets, true, uint32_t, false, true>(d_in, d_wanted, d_unwanted, d_first_gen, n,
                                                                      generations, cus, (hipStream_t)stream,
                                                                      kConeAdaptBlocksPerCU);
   }
-  // More generations without final states: a target whose care rows,
-  // widened by the light cone, fit 32 rows (as the last report on this
-  // target says: launch_cone_adapt) keeps k_cone_adapt's row-window passes
-  // -- whole board (cone_wave_rows_dma) or a column window of more than 4
-  // columns (cone_wave_rows, kConeRowsWindowRoute) -- which are 1.3-2x the
-  // split pair below (1M universes, a one-row whole-board target at 5 / 8 /
-  // 12 generations: 0.116 / 0.190 / 0.269 ms against 0.234 / 0.297 / 0.400;
-  // the 4 x 4 block at 5 / 8 / 13: 0.060 / 0.151 / 0.225 against 0.096 /
-  // 0.231 / 0.363; tools/filter_gens_ab.py, profiles/r05/gens/).  A target
-  // with no report yet takes the split pair, and one wave of k_cone_classify
-  // writes its report for the next call.
-  if (!d_final && generations < kConeRowsMaxGens && aligned16(d_in)) {
-    int32_t *slot = nullptr;
-    int last = -1;
-    rc = cone_class_slot(d_wanted, d_unwanted, generations, slot, last);
-    if (rc != LIFEAPI_OK) return rc;
-    const int last_k = last & 0xFF, last_pk = (last >> 8) & 0xFF;
-    if (last >= 0 && last_pk > 0 &&
-        (last_k == kWave || (kConeRowsWindowRoute && last_k > 4)))
-      return launch_cone_adapt<kConeSets, true, uint32_t, false, true>(d_in, d_wanted, d_unwanted, d_first_gen, n,
-                                                                       generations, cus, (hipStream_t)stream,
-                                                                       kConeAdaptBlocksPerCU);
-    if (slot && last < 0) {
-      hipLaunchKernelGGL(k_cone_classify, dim3(1), dim3(kWave), 0, (hipStream_t)stream, d_wanted, d_unwanted,
-                         generations, slot);
-      rc = launched("k_cone_classify launch");
-      if (rc != LIFEAPI_OK) return rc;
-    }
+  if (!d_final) {
+    // 3+ generations, first hits only (round 6): one launch of the merged
+    // split kernel (step_kernels.hpp k_step_contains_split, kContainsAll),
+    // whose waves take the pass their target calls for -- no report, so a
+    // loop that rewrites its target buffers loses nothing:
+    // * care rows that fit 32 with the light cone (cone_rows): on a whole
+    //   board below kConeWholeWinGens generations the packed LDS-DMA pass
+    //   (cone_wave_rows_dma), else the window split layout (cone_split.hpp)
+    //   on the column window;
+    // * else a cone of <= 32 columns: the natural layout on the cone
+    //   (cone_wave);
+    // * else the 8-way row split with the test fused (the loop its row
+    //   window picks), the next group of universes fetched into LDS while
+    //   this one steps.
+    // 1M universes, median of 5 x 10 back to back (tools/filter_iter_probe.py,
+    // profiles/r06/): block + ring at 3 / 5 / 8 / 13 generations 0.036 / 0.053
+    // / 0.110 / 0.153 ms (round 5: 0.047 / 0.057 / 0.154 / 0.222), a
+    // full-height target 0.176 / 0.237 / 0.327 / 0.465 (0.18 / 0.24 / 0.32 /
+    // 0.47 on the split pair).
+    using Fn = void (*)(const uint64_t *, uint64_t *, const uint64_t *, const uint64_t *, uint32_t *, uint64_t,
+                        uint32_t, uint32_t, int32_t *, int32_t);
+    const Fn fn = aligned16(d_in) ? k_step_contains_split<8, kContainsNet, kContainsAll, true, true>
+                                  : k_step_contains_split<8, kContainsNet, kContainsAll, false, true>;
+    hipLaunchKernelGGL(fn, dim3(grid_for((n + 3) / 4, cus, kFilterIterBlocksPerCU)), dim3(kBlock), 0,
+                       (hipStream_t)stream, d_in, (uint64_t *)nullptr, d_wanted, d_unwanted, d_first_gen, (uint64_t)n,
+                       generations, kConeIterColumns, (int32_t *)nullptr, -1);
+    return launched("k_step_contains_split launch");
   }
   if (generations > 2) {  // the layout of the shipped step for gens > 2
     // Without final states, a target whose light cone over `generations`
@@ -210,21 +204,20 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
     // 0.101 ms; at config 3's 64K the cap does not bind (tools/ab/final_caps_ab.py,
     // profiles/r04/r04ar).
     const int split_cap = kSplitIterBlocksPerCU;
-    uint32_t cone_max = 0;
-    if (!d_final) cone_max = kConeIterColumns;
+    const uint32_t cone_max = 0;  // (final states: every universe steps the whole board)
     // two kernels, one per register layout (a target window of <= 4 rows in
     // 62 VGPRs, 8 waves per SIMD; the rest in 70, 7 waves): each wave finds
     // the window and only the matching kernel works (step_kernels.hpp
     // kContainsLo / kContainsHi)
     using Fn = void (*)(const uint64_t *, uint64_t *, const uint64_t *, const uint64_t *, uint32_t *, uint64_t,
-                        uint32_t, uint32_t);
+                        uint32_t, uint32_t, int32_t *, int32_t);
     const Fn fns[2] = {k_step_contains_split<8, kContainsNet, kContainsLo>,
                        k_step_contains_split<8, kContainsNet, kContainsHi>};
     const dim3 grid(grid_for((n + 3) / 4, cus, split_cap));
     if (d_final) note_forward_write(d_final, (uint64_t)n * 512);
     for (const Fn fn : fns) {
       hipLaunchKernelGGL(fn, grid, dim3(kBlock), 0, (hipStream_t)stream, d_in, d_final, d_wanted, d_unwanted,
-                         d_first_gen, (uint64_t)n, generations, cone_max);
+                         d_first_gen, (uint64_t)n, generations, cone_max, (int32_t *)nullptr, -1);
       rc = launched("k_step_contains_split launch");
       if (rc != LIFEAPI_OK) return rc;
     }

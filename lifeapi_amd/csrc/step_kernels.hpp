@@ -9,6 +9,7 @@
 #include "host.hpp"
 #include "split_layout.hpp"
 #include "split_asm.inc"
+#include "cone_split.hpp"
 
 namespace lifeapi_impl {
 // internal linkage: every library that includes this header gets its own
@@ -490,31 +491,7 @@ constexpr int kContainsAll = 9;
 constexpr int kConeLoUniverses = 8;
 constexpr uint32_t kLowRows = 4;  // tools/gen_split_asm.py LOW_H
 
-__device__ __forceinline__ uint64_t rotr64(uint64_t v, uint32_t k) {
-  return (v >> k) | (v << ((64 - k) & 63));
-}
-// the smallest cyclic window [y0, y0 + h) of rows holding every set bit of
-// rm (wave-uniform; h = 1 for an empty mask): the complement of the longest
-// cyclic run of empty rows, found by binary lifting (run_k bit p = rows
-// p .. p + k - 1 all empty) in a few dozen scalar instructions
-__device__ __forceinline__ void care_window(uint64_t rm, uint32_t &y0, uint32_t &h) {
-  y0 = 0;
-  h = 1;
-  if (rm == 0) return;
-  uint64_t run[6];
-  run[0] = ~rm;  // runs of 1
-#pragma unroll
-  for (int k = 1; k < 6; ++k) run[k] = run[k - 1] & rotr64(run[k - 1], 1u << (k - 1));  // runs of 2^k
-  uint64_t cur = ~0ull;  // starts of runs of length len
-  uint32_t len = 0;
-#pragma unroll
-  for (int k = 5; k >= 0; --k) {
-    const uint64_t t = cur & rotr64(run[k], len);
-    if (t) cur = t, len += 1u << k;
-  }
-  h = 64 - len;
-  y0 = len ? ((uint32_t)__builtin_ctzll(cur) + len) & 63 : 0;
-}
+// (rotr64, care_window: device.hpp)
 // The column window of a target's care cells, widened by the light cone of
 // `gens` generations: xs = first column, K = columns (64: the whole board
 // from column 0; also for gens >= 32, whatever the window).  The light-cone
@@ -568,6 +545,65 @@ __device__ __forceinline__ void cone_window(const uint64_t *__restrict__ wanted,
   cone_window(wanted[lane] | unwanted[lane], gens, xs, K);
 }
 
+// The row window of a filter's whole-board pass (cone_kernels.hpp
+// cone_wave_rows_dma) and of the window split layout (cone_split.hpp): the
+// smallest cyclic window of the target's care rows, widened by `gens` rows on
+// either side, and the most universes per 32-bit word whose field holds it
+// (PK = 4, 2, 1: fields of 8, 16, 32 rows); 0 when it needs more than 32 rows.
+__device__ __forceinline__ int cone_rows(uint64_t care_col, uint32_t gens, uint32_t &y0) {
+  const uint32_t lo = wave_or_u32_dpp((uint32_t)care_col), hi = wave_or_u32_dpp((uint32_t)(care_col >> 32));
+  uint32_t cy0, h;
+  care_window((uint64_t)lo | (uint64_t)hi << 32, cy0, h);
+  if (gens >= 16u) return 0;
+  const uint32_t need = h + 2u * gens;
+  y0 = (cy0 - gens) & 63u;
+  return need <= 8u ? 4 : need <= 16u ? 2 : need <= 32u ? 1 : 0;
+}
+
+// Waves after the first take the row window from the last report from this
+// many generations on.  1M universes, bench.py's whole-board target, each
+// launch alone after a scrub, interleaved with the same launch finding the
+// window itself (tools/filter_interleave.py rows_hint / rows_early,
+// profiles/r05/hint/): 3 / 4 / 5 / 8 generations 0.081 / 0.096 / 0.109 /
+// 0.188 ms against 0.095 / 0.108 / 0.122 / 0.194; at 1 generation no
+// difference (0.083-0.085 both), at 2 it costs 4 % (0.086 against 0.082,
+// unexplained; every series on the box agreed).
+constexpr uint32_t kConeHintGens = 3;
+// A column window (5-32 columns) takes the row window too from this many
+// generations on (cone_wave_rows; below it the pass is not VALU-bound).
+constexpr uint32_t kConeRowsWindowGens = 3;
+// A whole board whose report carries a row window takes k_cone_adapt's
+// LDS-DMA packed form (cone_wave_rows_dma) below this many generations, the
+// window split layout (cone_split.hpp) from it on (one-row target, 1M
+// universes: 3 / 5 generations 0.080 / 0.116 ms against 0.102 / 0.113 for
+// the split window; 8 / 13: 0.203 / 0.289 against 0.199 / 0.279;
+// profiles/r06/ab/)
+constexpr uint32_t kConeWholeWinGens = 8;
+
+// The filter's report word for a target (host.hpp cone_class_slot): the
+// window K (64: the whole board) in bits 0-7, and for a whole board the
+// row-window class (cone_rows: 4, 2, 1 universes per register, 0 none) in
+// bits 8-15 and its first row y0 in bits 16-21.
+constexpr int32_t kReportWhole = kWave;
+__device__ __forceinline__ bool report_whole(int32_t word) { return (word & 0xFF) == kReportWhole; }
+__device__ __forceinline__ int32_t report_word(uint32_t K, int pk, uint32_t y0 = 0) {
+  return (int32_t)K | (pk << 8) | (pk ? (int32_t)(y0 & 63u) << 16 : 0);
+}
+
+// The report of a target the split pair answers (step.hip: more generations
+// than k_cone_adapt takes unless the last report allows it): one wave
+// computes what k_cone_adapt's first wave would report and writes it, so
+// that the next call on this target can choose.
+__device__ __forceinline__ int32_t cone_report(uint64_t care_col, uint32_t gens) {
+  if (cone_whole(care_col, gens)) {
+    uint32_t y0 = 0;
+    const int pk = cone_rows(care_col, gens, y0);
+    return report_word(kWave, pk, y0);
+  }
+  uint32_t xs = 0, K = kWave, y0 = 0;
+  cone_window(care_col, gens, xs, K);
+  return report_word(K, cone_rows(care_col, gens, y0), y0);
+}
 // The light-cone pass (cone_kernels.hpp; here for the iterated search
 // loop's low-layout kernel, below).  One wave's chunks of UPW universes u0 .. u0 + UPW - 1, u0 = u_first,
 // u_first + u_step, ... (< n), under the window (xs = first loaded column,
@@ -761,22 +797,70 @@ __device__ __forceinline__ void cone_wave_rows(const uint64_t *in, const uint64_
 // their registers) as soon as the current group has been read out, and
 // streams in while the current group steps; the generation loops' own LDS
 // traffic is the exchange area, a different 2 KiB.
-template <int S, int NET, int ASM = 0, bool PF = false>
+// WIN (no final states, 3 <= gens < 16): a target whose care rows, widened
+// by the light cone, fit 32 rows (cone_rows) takes the window split layout
+// (cone_split.hpp) on its column window; cls: the report word of this
+// target (host.hpp cone_class_slot), written by wave 0 when it differs from
+// cls_last (what the host last read), so that the next call can choose.
+template <int S, int NET, int ASM = 0, bool PF = false, bool WIN = false>
 __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *in, uint64_t *fin,
                                                                 const uint64_t *__restrict__ wanted,
                                                                 const uint64_t *__restrict__ unwanted,
                                                                 uint32_t *__restrict__ first, uint64_t n,
-                                                                uint32_t gens, uint32_t cone_max) {
+                                                                uint32_t gens, uint32_t cone_max, int32_t *cls,
+                                                                int32_t cls_last) {
   constexpr int P = S / 2;
   constexpr uint32_t every = P == 1 ? ~0u : P == 2 ? 0x55555555u : P == 4 ? 0x11111111u : 0x01010101u;
-  __shared__ uint32_t lds[kWavesPerBlock * S * kWave];
-  __shared__ uint64_t stage_all[PF ? kWavesPerBlock : 1][PF ? P * kWave : 1];  // (PF's fetch)
+  // 4 KiB of LDS per wave: the exchange area of the generation loops
+  // (S words per lane), then PF's fetch stage (P universes); the whole-board
+  // row-window pass (WIN) takes all of it as its image (8 universes)
+  static_assert(S * kWave * 4 + P * kWave * 8 <= 4096, "4 KiB per wave");
+  __shared__ uint64_t wave_lds[kWavesPerBlock][512];
   const int lane = threadIdx.x & (kWave - 1);
   const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  uint32_t *const lds = reinterpret_cast<uint32_t *>(wave_lds[0]);  // (wave w's area: lds + w * 1024)
   // the target's care cells in this lane's column (both windows read it;
   // the cone test first: after the row window's, it costs kContainsHi 6
   // VGPRs, 70 -> 76)
   const uint64_t care_col = wanted[lane] | unwanted[lane];
+  if (cls && blockIdx.x == 0 && wib == 0) {
+    const int32_t word = cone_report(care_col, gens);
+    if (lane == 0 && word != cls_last) *reinterpret_cast<volatile int32_t *>(cls) = word;
+  }
+  if constexpr (WIN) {
+    if (!fin && gens >= kConeRowsWindowGens && gens < 16u) {
+      uint32_t y0w = 0;
+      const int pk = cone_rows(care_col, gens, y0w);
+      if (pk > 0) {
+        const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerBlock + wib, nw = (uint64_t)gridDim.x * kWavesPerBlock;
+        uint32_t xs = 0, K = kWave;
+        const bool whole = cone_whole(care_col, gens);
+        if (!whole) cone_window(care_col, gens, xs, K);
+        if constexpr (PF) {  // (a 16-byte aligned batch)
+          if (whole && gens < kConeWholeWinGens) {
+            // the whole board's row window below kConeWholeWinGens: the
+            // packed LDS-DMA pass (cone_split.hpp cone_wave_rows_dma, chunks
+            // of 16 universes, 8 per pass fetched while the last steps)
+            const uint64_t w64 = wanted[lane], m64 = w64 | unwanted[lane];
+            uint64_t *img = wave_lds[wib];
+            auto rows = [&](auto pk_c, auto wrap_c) __attribute__((always_inline)) {
+              cone_wave_rows_dma<8, decltype(pk_c)::value, decltype(wrap_c)::value>(
+                  in, w64, m64, first, n, wave * 16, nw * 16, gens, y0w, lane, img, false);
+            };
+            using T = std::true_type;
+            using F = std::false_type;
+            using P1 = std::integral_constant<int, 1>;
+            using P2 = std::integral_constant<int, 2>;
+            using P4 = std::integral_constant<int, 4>;
+            if (pk == 4) return y0w >= 32u ? rows(P4{}, T{}) : rows(P4{}, F{});
+            if (pk == 2) return y0w >= 32u ? rows(P2{}, T{}) : rows(P2{}, F{});
+            return y0w >= 32u ? rows(P1{}, T{}) : rows(P1{}, F{});
+          }
+        }
+        return cone_split_pass(in, wanted, unwanted, first, n, wave, nw, gens, xs, K, pk, y0w, lane);
+      }
+    }
+  }
   // (2 gens in 64 bits: in 32 it wraps for gens >= 2^31)
   if (cone_max && cone_max <= 32u && !fin && 2ull * gens < cone_max && cone_fits(care_col, gens, cone_max)) {
     if constexpr (ASM == kContainsLo || ASM == kContainsAll) {
@@ -823,7 +907,7 @@ __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *
   // are all the register allocator sees around it
   auto universes_pf = [&](auto &&gens_loop) __attribute__((always_inline)) {
     static_assert(P % 2 == 0, "pairs of universes per 16-byte load");
-    uint64_t *img = stage_all[PF ? wib : 0];
+    uint64_t *img = wave_lds[wib] + S * kWave / 2;  // (after the exchange area)
     const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock * P;
     auto fetch = [&](uint64_t ub) __attribute__((always_inline)) {
       const uint32_t ln = lane_id_fresh();
@@ -929,8 +1013,7 @@ __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *
   };
   if constexpr (ASM) {  // split_asm.inc: the default generation loop with the test fused in
     static_assert(S == 8 && NET == 6 && P == 4, "split_contains_asm is rule 11");
-    const uint32_t base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)(
-        lds + wib * S * kWave);
+    const uint32_t base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)(lds + wib * 1024);
     const uint32_t self = base + lane * 16u, prev = base + ((lane + kWave - 1) & (kWave - 1)) * 16u,
                    next = base + ((lane + 1) & (kWave - 1)) * 16u;
 #define LIFEAPI_RUN(fn)                                                                          \
@@ -980,7 +1063,7 @@ __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *
     universes([&](uint32_t(&r)[S], uint32_t(&hit)[P]) __attribute__((always_inline)) {
       uint32_t found = 0;
       for (uint32_t g = 1; g <= gens; ++g) {
-        gen_split<S, NET>(r, lds + wib * S * kWave, lane);
+        gen_split<S, NET>(r, lds + wib * 1024, lane);
         uint32_t d = 0;
 #pragma unroll
         for (int j = 0; j < S; ++j) d |= lut3<kDiff>(r[j], tw[j], tu[j]);

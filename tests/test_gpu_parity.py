@@ -893,9 +893,11 @@ def test_filter_whole_board_row_windows(hip, port, rows, gens_list):
     cone_wave_rows_dma: 4, 2 or 1 universes per 32-bit register, shifts for
     the vertical neighbours) in the LDS form; windows across row 63 and across
     the 32-bit halves; every call against the oracle (first call the capped
-    form, the next two the LDS form), ragged n.  Beyond k_cone_adapt's own
-    generation limit the first call takes the split pair and classifies the
-    target (k_cone_classify), the next ones the row-window pass (step.hip)."""
+    form, the next two the LDS form), ragged n.  From 3 generations the first
+    call takes the merged split kernel (step.hip: its waves run the window
+    split layout, cone_split.hpp, and wave 0 writes the target's report), the
+    next ones k_cone_adapt (the LDS-DMA packed form below kConeWholeWinGens,
+    the window split layout from it on)."""
     n = 70001
     x = port.fill(n, seed=93) & port.fill(n, seed=94) & port.fill(n, seed=95)
     d = to_dev(x)

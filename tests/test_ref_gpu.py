@@ -164,8 +164,11 @@ def test_config3_search_loop_vs_reference_digest(hip):
 
 
 def test_step_contains_random_windows_vs_reference(hip, R, port):
-    """the shipped pair on 48 targets with random row windows (1..12 rows,
-    also 20 and 64, anywhere including across the row seam) and columns:
+    """the shipped filter (round 6: the merged split kernel on the first call
+    on a target, k_cone_adapt's window split layout once a report carries a
+    row window -- and the target buffers are reused, so calls read the last
+    target's report) on 48 targets with random row windows (1..12 rows, also
+    20 and 64, anywhere including across the row seam) and columns:
     each target is universe 0's box after 3 generations, so universe 0 hits;
     first-hit generations and final states against the reference's loop"""
     rng = np.random.default_rng(4242)
@@ -348,14 +351,20 @@ def test_iterated_search_loop_cone_and_split_vs_reference(hip, R, port, w, gens)
 
 @pytest.mark.parametrize("w,h,gens", [(2, 1, 3), (2, 2, 8), (4, 4, 13), (4, 5, 13), (6, 7, 9), (6, 8, 3),
                                       (20, 3, 5), (20, 6, 5), (27, 2, 3), (28, 4, 3), (4, 3, 15), (4, 6, 16),
-                                      (12, 4, 24), (12, 6, 24)])
+                                      (12, 4, 24), (12, 6, 24),
+                                      # round 6: the window split layout's shapes (cone_split.hpp):
+                                      # P = 8 / 16 / 32 / 64 lanes x R = 32 / 16 rows
+                                      (2, 20, 3), (1, 12, 3), (6, 14, 5), (14, 4, 6), (30, 1, 15),
+                                      (40, 2, 4), (40, 12, 7), (64, 3, 14)])
 def test_iterated_search_loop_short_targets_vs_reference(hip, R, port, w, h, gens):
     """gens > 2, no final states, targets of w columns x h rows (cyclic, at
-    the seams): the cone test comes first in both split kernels, so a cone
-    target of <= 4 rows (the low layout's) and one of more rows (the high
-    layout's) both go to kContainsLo's cone pass and kContainsHi returns;
-    wider cones (w + 2 gens > 32) go to the layout their height picks.
-    Against the reference's Step() + Contains loop."""
+    the seams), each called twice (no report, then the form the report
+    picks): rows that fit 32 with the light cone take the window split
+    layout (cone_split.hpp; the round-6 shapes cover P = 8 / 16 / 32 / 64
+    lanes x R = 32 / 16 rows), narrower cones of taller targets the natural
+    layout's cone pass, the rest the 8-way row split that their height
+    picks (step_kernels.hpp kContainsAll).  Against the reference's Step() +
+    Contains loop."""
     rng = np.random.default_rng(100 * w + 10 * h + gens)
     n = 777
     x = port.fill(n, seed=700 + w) & port.fill(n, seed=800 + h)

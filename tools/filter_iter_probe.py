@@ -104,6 +104,9 @@ def forms(x, tw, tu, gens):
         fs["hi_only"] = lambda: tune.step_contains(x, tw, tu, gens, 8)
     # k_cone_adapt's capped form (16 / 32 blocks per CU): the packed row-window
     # passes (cone_wave_rows) against the window split layout (cone_split.hpp)
+    # the 1-2 generation filter's LDS form on the capped grid (no report needed)
+    fs["dma_capped16"] = lambda: tune.cone(x, tw, tu, gens, 16003, 8, first=True)
+    fs["dma_capped8"] = lambda: tune.cone(x, tw, tu, gens, 8003, 8, first=True)
     fs["rows_capped"] = lambda: tune.cone(x, tw, tu, gens, 16000, 8, first=True)
     fs["win_capped"] = lambda: tune.cone(x, tw, tu, gens, 16008, 8, first=True)
     fs["win_capped32"] = lambda: tune.cone(x, tw, tu, gens, 32008, 8, first=True)
@@ -229,6 +232,7 @@ def summarize(manifest, *dirs):
             per_row[i].update({c: v / m["calls"] for c, v in tot.items()})
             per_row[i].setdefault("kernels", names)
             per_row[i]["dispatches_per_call"] = len(kern) / m["calls"]
+    keyed = {}
     for m, c in zip(rows, per_row):
         out = dict(m)
         out.update(c)
@@ -245,6 +249,16 @@ def summarize(manifest, *dirs):
                 if k in c:
                     out[k.lower() + "_frac"] = c[k] / c["SQ_WAVE_CYCLES"]
         print(json.dumps(out))
+        if m["form"] == "shipped":
+            keyed[f"{m['target']} {m['gens']}"] = out
+    if os.environ.get("PMC_JSON"):  # the table tools/rows_bench.py prices the filter rows on
+        with open(os.environ["PMC_JSON"], "w") as f:
+            json.dump({"source": "tools/filter_iter_probe.py pmc + summarize (rocprofv3 --pmc, one counter "
+                                 "group per run; each call after a 768 MiB scrub, 3 calls per row, per-call "
+                                 "counters over every dispatch of the call)",
+                       "corrections": {"FETCH_SIZE": 2.0, "why": "MI355X_MICROARCH.md HBM: FETCH_SIZE reads "
+                                                                 "half the bytes of wide streaming reads"},
+                       "rows": keyed}, f, indent=1)
 
 
 if __name__ == "__main__":

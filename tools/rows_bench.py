@@ -99,7 +99,8 @@ def report(name, n, nbytes, ms, extra=None, scrub_ms=None, pmc=None):
     d = {"kernel": name, "objects": n, "algorithmic_bytes_per_object": nbytes}
     if pmc:
         nbytes, valu, src = pmc
-        d.update({"bytes_per_object": nbytes, "bytes_basis": f"measured: FETCH_SIZE x 2 + WRITE_SIZE ({src})",
+        d.update({"bytes_per_object": nbytes, "bytes_basis": f"measured: FETCH_SIZE x 2 + WRITE_SIZE ({src})"
+                  if "pmc_rows" in src else f"max(algorithmic, FETCH_SIZE x 2 + 4) ({src})",
                   "valu_per_object": valu})
     gbs = n * nbytes / (ms / 1e3) / 1e9
     d.update({"ms": ms, "objects_per_s": n / ms * 1e3, "GBps": gbs, "hbm_frac": gbs / PEAK})
@@ -116,8 +117,29 @@ def report(name, n, nbytes, ms, extra=None, scrub_ms=None, pmc=None):
     print(json.dumps(d), flush=True)
 
 
-def both(name, n, nbytes, fn, extra=None):
-    report(name, n, nbytes, timed(fn), extra, scrubbed(fn))
+def both(name, n, nbytes, fn, extra=None, pmc=None):
+    report(name, n, nbytes, timed(fn), extra, scrubbed(fn), pmc=pmc)
+
+
+PMC_FILTER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "r06",
+                          "pmc_filter.json")
+
+
+def pmc_filter_row(target, gens, algo_bytes):
+    """(bytes per universe, VALU per universe, source) of the shipped filter
+    on this target at this many generations (tools/filter_iter_probe.py pmc +
+    summarize), or None.  The bytes are the algorithmic ones (the cone's lines
+    + the answer) unless the measured fetch exceeds them."""
+    try:
+        with open(PMC_FILTER) as f:
+            rows = json.load(f)["rows"]
+    except (OSError, ValueError, KeyError):
+        return None
+    r = rows.get(f"{target} {gens}")
+    if not r or "valu_per_universe" not in r:
+        return None
+    fetched = r.get("fetch_bytes_per_universe", 0.0) + 4
+    return max(algo_bytes, fetched), r["valu_per_universe"], "profiles/r06/pmc_filter.json"
 
 
 def stable_inputs(n):
@@ -184,12 +206,24 @@ def main():
     # (DESIGN.md 3.2), beyond 4 generations too
     rw, ru = torch.zeros_like(w), torch.zeros_like(w)
     ru[0, 0::3] = 1 << 10
-    for gens in (1, 2, 3, 5, 8):
+    for gens in (1, 2):
         both(f"filter {gens} gen (first hit only), whole-board target of one care row", n, 516,
              lambda g=gens: hip.step_contains(x, rw, ru, g))
-    for gens in (3, 5, 8):  # every row cares: the full pass to 4 generations, then the split pair
-        both(f"filter {gens} gen (first hit only), whole-board target, every row", n, 516,
-             lambda g=gens: hip.step_contains(x, w, w, g))
+    # the iterated filter (3+ generations): VALU-bound, so priced on the
+    # larger of its bytes and its measured VALU (PMC, tools/filter_iter_probe.py
+    # summarize -> profiles/r06/pmc_filter.json), as the LifeStable rows
+    fu = torch.zeros_like(w)  # bench.py's full-height target: 16 dead cells, one in every fourth row
+    for yy in range(0, 64, 4):
+        fu[0, (3 * yy) % 64] |= 1 << yy
+    iters = [("one_row", "whole-board target of one care row", rw, ru, (3, 5, 8, 13)),
+             ("full_height", "full-height target (16 cells, every fourth row)", torch.zeros_like(w), fu,
+              (3, 5, 8, 13)),
+             ("full", "whole-board target, every row (a random universe)", w, w, (3, 5, 8))]
+    for key, label, tw_, tu_, gl in iters:
+        for gens in gl:
+            both(f"filter {gens} gen (first hit only), {label}", n, 516,
+                 lambda g=gens, a=tw_, b=tu_: hip.step_contains(x, a, b, g),
+                 pmc=pmc_filter_row(key, gens, 512 + 4))
     bw, bu = torch.zeros_like(w), torch.zeros_like(w)
     bw[0, 10] = bw[0, 11] = 3 << 40
     bu[0, 9:13] = 15 << 39
@@ -201,11 +235,12 @@ def main():
          {"lines_128B_per_object": 1, "full_read_equivalent_bytes": 513})
     both("k_cone 1 gen (first hit only), 2x2 block + ring", n, 128 + 4, lambda: hip.step_contains(x, bw, bu, 1),
          {"lines_128B_per_object": 1, "full_read_equivalent_bytes": 516})
-    for gens in (5, 8, 13):  # the column and row window widen with the generations (cone_wave_rows)
+    for gens in (3, 5, 8, 13):  # the column and row window widen with the generations (cone_split.hpp)
         xs = (9 - gens) % 64
         lines = len({((xs + c) % 64) // 16 for c in range(4 + 2 * gens)})
         both(f"filter {gens} gen (first hit only), 2x2 block + ring", n, 128 * lines + 4,
-             lambda g=gens: hip.step_contains(x, bw, bu, g), {"lines_128B_per_object": lines})
+             lambda g=gens: hip.step_contains(x, bw, bu, g), {"lines_128B_per_object": lines},
+             pmc=pmc_filter_row("block", gens, 128 * lines + 4))
     fp = [x.clone(), y]
 
     def filter_pingpong():  # a loop stepping its batch with the filter: final states ping-ponged

@@ -207,11 +207,13 @@ int lifeapi_tune_search_iter(const uint64_t *d_in, const uint64_t *d_wanted, con
   if (rc != LIFEAPI_OK) return rc;
   const dim3 grid(grid_for((n + 3) / 4, cus, split_cap));
   hipLaunchKernelGGL((k_step_contains_split<8, kContainsNet, kContainsLo>), grid, dim3(kBlock), 0, (hipStream_t)stream,
-                     d_in, (uint64_t *)nullptr, d_wanted, d_unwanted, d_first, (uint64_t)n, gens, kConeIterColumns);
+                     d_in, (uint64_t *)nullptr, d_wanted, d_unwanted, d_first, (uint64_t)n, gens, kConeIterColumns,
+                     (int32_t *)nullptr, -1);
   rc = launched("k_step_contains_split (tuning) launch");
   if (rc != LIFEAPI_OK) return rc;
   hipLaunchKernelGGL((k_step_contains_split<8, kContainsNet, kContainsHi>), grid, dim3(kBlock), 0, (hipStream_t)stream,
-                     d_in, (uint64_t *)nullptr, d_wanted, d_unwanted, d_first, (uint64_t)n, gens, kConeIterColumns);
+                     d_in, (uint64_t *)nullptr, d_wanted, d_unwanted, d_first, (uint64_t)n, gens, kConeIterColumns,
+                     (int32_t *)nullptr, -1);
   return launched("k_step_contains_split (tuning) launch");
 }
 

@@ -366,8 +366,9 @@ def rows_probe(states, wanted, unwanted, generations, y0, sleep=0, out=None, str
 lib.lifeapi_tune_filter_iter.argtypes = [_vp, _vp, _vp, _vp, _sz, _u32, _int, _vp]
 lib.lifeapi_tune_filter_iter.restype = _int
 # tools/filter_iter_probe.py's forms of the round-6 A/B: blocks per CU | PF | Hi / Lo alone
-FILTER_ITER_FORMS = {"pair32": 32, "pair32_pf": 32 | 0x100, "pair7_pf": 7 | 0x100,
-                     "all32": 32 | 0x800, "all32_pf": 32 | 0x900, "all7_pf": 7 | 0x900, "all14_pf": 14 | 0x900}
+FILTER_ITER_FORMS = {"pair32": 32, "all32_pf": 32 | 0x900, "all14_pf": 14 | 0x900,
+                     "all16_pf_win": 16 | 0x1900, "all32_pf_win": 32 | 0x1900, "all8_pf_win": 8 | 0x1900,
+                     "all16_win": 16 | 0x1800}
 
 
 def filter_iter(states, wanted, unwanted, generations, variant, stream=None):
