@@ -145,13 +145,6 @@ __device__ __forceinline__ void cone_wave_full_dma(const uint64_t *in, uint64_t 
 
 // (cone_rows, kConeHintGens, kConeRowsWindowGens and the report word:
 // step_kernels.hpp)
-__global__ __launch_bounds__(kWave) __attribute__((unused)) void k_cone_classify(const uint64_t *__restrict__ wanted,
-                                                         const uint64_t *__restrict__ unwanted, uint32_t gens,
-                                                         int32_t *cls) {
-  const int lane = threadIdx.x & (kWave - 1);
-  const int32_t word = cone_report(wanted[lane] | unwanted[lane], gens);
-  if (lane == 0) *reinterpret_cast<volatile int32_t *>(cls) = word;
-}
 
 // UPW universes per wave (one-shot grid of ceil(n / UPW) waves), every wave
 // choosing its lane layout from the window (wave-uniform: the target is the
@@ -465,27 +458,20 @@ int launch_cone(const uint64_t *d_in, const uint64_t *d_wanted, const uint64_t *
 
 // Launches k_cone_adapt on ceil(n / 16) waves, at most blocks_per_cu blocks
 // per CU (0: no cap).  DMA: a whole-board window takes cone_wave_full_dma
-// when the batch is 16-byte aligned (the uncapped grid; the cap then applies
-// to the waves of a windowed target).  AUTO (the product's search filter):
-// the DMA form exactly when the last launch on this target reported a
-// whole-board window (host.hpp cone_class_slot), else the capped form; both
-// compute the same answers for any target.
-template <int RMAX, bool FIRST, typename OutT, bool DMA = false, bool AUTO = false, bool ROWS = true,
-          bool WIN = false>
+// when the batch is 16-byte aligned, on a grid of at most dma_blocks_per_cu
+// blocks per CU (0: uncapped; blocks_per_cu then caps the waves of a
+// windowed target).  hint_k: the tuning build's stand-in for round 5's
+// launch report (the last launch's window word: a whole board fetches its
+// first pass before the window tests; -1 none).
+template <int RMAX, bool FIRST, typename OutT, bool DMA = false, bool ROWS = true, bool WIN = false>
 int launch_cone_adapt(const uint64_t *d_in, const uint64_t *d_wanted, const uint64_t *d_unwanted, OutT *d_out,
                       size_t n, uint32_t gens, int cus, hipStream_t stream, int blocks_per_cu,
                       uint32_t kmax = kWave, int dma_blocks_per_cu = 0, int hint_k = -1) {
   const dim3 grid(grid_for((n + 15) / 16, cus, blocks_per_cu));
-  int32_t *cls = nullptr;
-  int last_k = hint_k;  // (the tuning build's stand-in for a report)
-  bool dma = DMA;
-  if constexpr (AUTO) {
-    const int rc = cone_class_slot(d_wanted, d_unwanted, gens, cls, last_k);
-    if (rc != LIFEAPI_OK) return rc;
-    dma = (last_k & 0xFF) == kReportWhole && kmax >= (uint32_t)kWave;
-  }
-  if constexpr (DMA || AUTO) {
-    if (dma && aligned16(d_in)) {  // the uncapped grid; the cap applies to the waves of a windowed target
+  int32_t *const cls = nullptr;
+  const int last_k = hint_k;
+  if constexpr (DMA) {
+    if (aligned16(d_in)) {
       const uint32_t cap_waves = blocks_per_cu > 0 ? (uint32_t)(cus * blocks_per_cu * kWavesPerBlock) : 0u;
       hipLaunchKernelGGL((k_cone_adapt<RMAX, FIRST, OutT, true, true, ROWS, WIN>),
                          dim3(grid_for((n + 15) / 16, cus, dma_blocks_per_cu)), dim3(kBlock), 0, stream, d_in,

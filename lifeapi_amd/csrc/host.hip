@@ -189,60 +189,6 @@ void note_forward_write(const void *d_out, uint64_t bytes) {
   order_record(*b, (uintptr_t)d_out, bytes, false);
 }
 
-// ---- the search filter's launch form by its target (host.hpp cone_class_slot) ----
-namespace {
-constexpr int kConeClassSlots = 32;
-struct ConeClassBook {
-  std::mutex mu;
-  int32_t *host = nullptr, *dev = nullptr;  // kConeClassSlots words of pinned, device-mapped memory
-  uintptr_t w[kConeClassSlots] = {}, u[kConeClassSlots] = {};
-  uint32_t g[kConeClassSlots] = {};
-  uint64_t tick[kConeClassSlots] = {}, now = 0;
-  bool failed = false;
-};
-ConeClassBook g_cone_class[kOrderDevices];
-}  // namespace
-
-int cone_class_slot(const void *wanted, const void *unwanted, uint32_t gens, int32_t *&dev_slot, int &last_k) {
-  dev_slot = nullptr;
-  last_k = -1;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kOrderDevices) return LIFEAPI_OK;
-  ConeClassBook &b = g_cone_class[dev];
-  std::lock_guard<std::mutex> lk(b.mu);
-  if (!b.host && !b.failed) {
-    void *h = nullptr, *d = nullptr;
-    if (hipHostMalloc(&h, kConeClassSlots * sizeof(int32_t), hipHostMallocMapped) != hipSuccess ||
-        hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
-      (void)hipGetLastError();
-      if (h) (void)hipHostFree(h);
-      b.failed = true;  // (the filter then always takes its default form)
-      return LIFEAPI_OK;
-    }
-    b.host = static_cast<int32_t *>(h);
-    b.dev = static_cast<int32_t *>(d);
-    for (int i = 0; i < kConeClassSlots; ++i) b.host[i] = -1;
-  }
-  if (!b.host) return LIFEAPI_OK;
-  int victim = 0;
-  for (int i = 0; i < kConeClassSlots; ++i) {
-    if (b.tick[i] && b.w[i] == (uintptr_t)wanted && b.u[i] == (uintptr_t)unwanted && b.g[i] == gens) {
-      b.tick[i] = ++b.now;
-      last_k = reinterpret_cast<volatile int32_t *>(b.host)[i];
-      dev_slot = b.dev + i;
-      return LIFEAPI_OK;
-    }
-    if (b.tick[i] < b.tick[victim]) victim = i;
-  }
-  b.w[victim] = (uintptr_t)wanted;
-  b.u[victim] = (uintptr_t)unwanted;
-  b.g[victim] = gens;
-  b.tick[victim] = ++b.now;
-  reinterpret_cast<volatile int32_t *>(b.host)[victim] = -1;
-  dev_slot = b.dev + victim;
-  return LIFEAPI_OK;
-}
-
 bool aligned8(const void *p) { return ((uintptr_t)p & 7u) == 0; }
 
 int check_batch(const void *in, const void *out, size_t n) {

@@ -36,17 +36,6 @@ bool launch_reverse(const void *d_in, const void *d_out, uint64_t bytes);
 // Records d_out (bytes) as written in forward order by a launch that does not
 // alternate (so a stale entry for that range cannot reverse a later reader).
 void note_forward_write(const void *d_out, uint64_t bytes);
-// The search filter's launch form by its target (cone_kernels.hpp
-// launch_cone_adapt): a word of pinned, device-mapped host memory per
-// (device, target pointers, generations) -- a few dozen remembered, the least
-// recently used replaced -- into which the filter's first wave writes the
-// target's light-cone width K.  Returns that word's device pointer (null if
-// the memory could not be had) and the K the last launch on this target
-// wrote, if it has landed (-1: none yet).  A hint: it picks between launch
-// forms that compute the same answers, so a stale value (the target's
-// contents changed at the same pointers) costs one launch's speed, never a
-// result.
-int cone_class_slot(const void *wanted, const void *unwanted, uint32_t gens, int32_t *&dev_slot, int &last_k);
 bool aligned8(const void *p);
 inline bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
 // n universes in / out: non-null, 8-byte aligned, equal or disjoint

@@ -151,17 +151,22 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
   if (!d_final && generations <= 2) {
     // the search filter proper (first hits only) at 1-2 generations: the
     // target's light cone, or the whole board, in the natural layout
-    // (cone_kernels.hpp k_cone_adapt).  A whole-board target takes the
-    // universes through LDS (cone_wave_full_dma, chunks of 16, 8 per pass by
-    // global_load_lds, the next pass fetched while this one steps) on the
-    // uncapped grid; the form is chosen by what the last launch on this target
-    // reported (launch_cone_adapt AUTO), so the first call on a target, and
-    // every small target, takes the capped form.  1M universes, 1 generation,
-    // alone after a scrub: 0.0816-0.0849 ms against 0.0874-0.0889
-    // (tools/filter_dma_ab.py, profiles/r05/filter_dma_ab_r05*.jsonl).
-    return launch_cone_adapt<kConeSets, true, uint32_t, false, true>(d_in, d_wanted, d_unwanted, d_first_gen, n,
-                                                                     generations, cus, (hipStream_t)stream,
-                                                                     kConeAdaptBlocksPerCU);
+    // (cone_kernels.hpp k_cone_adapt, DMA form): a whole-board target takes
+    // the universes through LDS (cone_wave_full_dma / cone_wave_rows_dma, 8
+    // per pass by global_load_lds, the next pass fetched while this one
+    // steps), every other window its cone (cone_wave); every wave decides,
+    // on a grid of at most kConeAdaptBlocksPerCU blocks per CU looping over
+    // the batch.  Round 6: no launch report -- round 5 chose the grid per
+    // target pointers from the last call's report, which a loop that rewrites
+    // its target buffers read stale (+13 % per call, tools/report_loop_probe.py,
+    // profiles/r06/).  1M universes, median of 5 x 10 back to back
+    // (tools/filter_iter_probe.py, profiles/r06/): the one-row whole board
+    // 0.083 / 0.086 ms at 1 / 2 generations against 0.082 / 0.081 on the
+    // reported uncapped grid, the full-height and random whole boards 5-9 %
+    // faster, the block + ring unchanged (0.023 / 0.026).
+    return launch_cone_adapt<kConeSets, true, uint32_t, true>(d_in, d_wanted, d_unwanted, d_first_gen, n,
+                                                              generations, cus, (hipStream_t)stream,
+                                                              kConeAdaptBlocksPerCU, kWave, kConeAdaptBlocksPerCU);
   }
   if (!d_final) {
     // 3+ generations, first hits only (round 6): one launch of the merged
@@ -183,12 +188,12 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
     // full-height target 0.176 / 0.237 / 0.327 / 0.465 (0.18 / 0.24 / 0.32 /
     // 0.47 on the split pair).
     using Fn = void (*)(const uint64_t *, uint64_t *, const uint64_t *, const uint64_t *, uint32_t *, uint64_t,
-                        uint32_t, uint32_t, int32_t *, int32_t);
+                        uint32_t, uint32_t);
     const Fn fn = aligned16(d_in) ? k_step_contains_split<8, kContainsNet, kContainsAll, true, true>
                                   : k_step_contains_split<8, kContainsNet, kContainsAll, false, true>;
     hipLaunchKernelGGL(fn, dim3(grid_for((n + 3) / 4, cus, kFilterIterBlocksPerCU)), dim3(kBlock), 0,
                        (hipStream_t)stream, d_in, (uint64_t *)nullptr, d_wanted, d_unwanted, d_first_gen, (uint64_t)n,
-                       generations, kConeIterColumns, (int32_t *)nullptr, -1);
+                       generations, kConeIterColumns);
     return launched("k_step_contains_split launch");
   }
   if (generations > 2) {  // the layout of the shipped step for gens > 2
@@ -210,14 +215,14 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
     // the window and only the matching kernel works (step_kernels.hpp
     // kContainsLo / kContainsHi)
     using Fn = void (*)(const uint64_t *, uint64_t *, const uint64_t *, const uint64_t *, uint32_t *, uint64_t,
-                        uint32_t, uint32_t, int32_t *, int32_t);
+                        uint32_t, uint32_t);
     const Fn fns[2] = {k_step_contains_split<8, kContainsNet, kContainsLo>,
                        k_step_contains_split<8, kContainsNet, kContainsHi>};
     const dim3 grid(grid_for((n + 3) / 4, cus, split_cap));
     if (d_final) note_forward_write(d_final, (uint64_t)n * 512);
     for (const Fn fn : fns) {
       hipLaunchKernelGGL(fn, grid, dim3(kBlock), 0, (hipStream_t)stream, d_in, d_final, d_wanted, d_unwanted,
-                         d_first_gen, (uint64_t)n, generations, cone_max, (int32_t *)nullptr, -1);
+                         d_first_gen, (uint64_t)n, generations, cone_max);
       rc = launched("k_step_contains_split launch");
       if (rc != LIFEAPI_OK) return rc;
     }

@@ -580,7 +580,7 @@ constexpr uint32_t kConeRowsWindowGens = 3;
 // profiles/r06/ab/)
 constexpr uint32_t kConeWholeWinGens = 8;
 
-// The filter's report word for a target (host.hpp cone_class_slot): the
+// Round 5's launch report word for a target (the tuning build's hint_k): the
 // window K (64: the whole board) in bits 0-7, and for a whole board the
 // row-window class (cone_rows: 4, 2, 1 universes per register, 0 none) in
 // bits 8-15 and its first row y0 in bits 16-21.
@@ -590,20 +590,6 @@ __device__ __forceinline__ int32_t report_word(uint32_t K, int pk, uint32_t y0 =
   return (int32_t)K | (pk << 8) | (pk ? (int32_t)(y0 & 63u) << 16 : 0);
 }
 
-// The report of a target the split pair answers (step.hip: more generations
-// than k_cone_adapt takes unless the last report allows it): one wave
-// computes what k_cone_adapt's first wave would report and writes it, so
-// that the next call on this target can choose.
-__device__ __forceinline__ int32_t cone_report(uint64_t care_col, uint32_t gens) {
-  if (cone_whole(care_col, gens)) {
-    uint32_t y0 = 0;
-    const int pk = cone_rows(care_col, gens, y0);
-    return report_word(kWave, pk, y0);
-  }
-  uint32_t xs = 0, K = kWave, y0 = 0;
-  cone_window(care_col, gens, xs, K);
-  return report_word(K, cone_rows(care_col, gens, y0), y0);
-}
 // The light-cone pass (cone_kernels.hpp; here for the iterated search
 // loop's low-layout kernel, below).  One wave's chunks of UPW universes u0 .. u0 + UPW - 1, u0 = u_first,
 // u_first + u_step, ... (< n), under the window (xs = first loaded column,
@@ -799,16 +785,14 @@ __device__ __forceinline__ void cone_wave_rows(const uint64_t *in, const uint64_
 // traffic is the exchange area, a different 2 KiB.
 // WIN (no final states, 3 <= gens < 16): a target whose care rows, widened
 // by the light cone, fit 32 rows (cone_rows) takes the window split layout
-// (cone_split.hpp) on its column window; cls: the report word of this
-// target (host.hpp cone_class_slot), written by wave 0 when it differs from
-// cls_last (what the host last read), so that the next call can choose.
+// (cone_split.hpp) on its column window -- or, on a whole board below
+// kConeWholeWinGens generations, the packed LDS-DMA row pass.
 template <int S, int NET, int ASM = 0, bool PF = false, bool WIN = false>
 __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *in, uint64_t *fin,
                                                                 const uint64_t *__restrict__ wanted,
                                                                 const uint64_t *__restrict__ unwanted,
                                                                 uint32_t *__restrict__ first, uint64_t n,
-                                                                uint32_t gens, uint32_t cone_max, int32_t *cls,
-                                                                int32_t cls_last) {
+                                                                uint32_t gens, uint32_t cone_max) {
   constexpr int P = S / 2;
   constexpr uint32_t every = P == 1 ? ~0u : P == 2 ? 0x55555555u : P == 4 ? 0x11111111u : 0x01010101u;
   // 4 KiB of LDS per wave: the exchange area of the generation loops
@@ -823,10 +807,6 @@ __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *
   // the cone test first: after the row window's, it costs kContainsHi 6
   // VGPRs, 70 -> 76)
   const uint64_t care_col = wanted[lane] | unwanted[lane];
-  if (cls && blockIdx.x == 0 && wib == 0) {
-    const int32_t word = cone_report(care_col, gens);
-    if (lane == 0 && word != cls_last) *reinterpret_cast<volatile int32_t *>(cls) = word;
-  }
   if constexpr (WIN) {
     if (!fin && gens >= kConeRowsWindowGens && gens < 16u) {
       uint32_t y0w = 0;

@@ -821,16 +821,14 @@ def test_stable_passes_8_byte_aligned_batch(hip, port):
 
 
 def test_filter_launch_form_follows_the_target(hip, port):
-    """The search filter picks its launch form by what the last launch on the
-    same target pointers reported (cone_kernels.hpp launch_cone_adapt AUTO):
-    the first call on a whole-board target runs the capped form, the next ones
-    the LDS form on the uncapped grid; rewriting the target in place to a
-    small one leaves one call on the stale form, which must still be exact.
-    From 3 generations the waves after the first take the row window from the
-    report (cone_kernels.hpp kConeHintGens): a small target in the whole-board
-    target's rows runs on that stale window in those waves and on its own
-    window in the first -- overlapping chunks, both exact.  Every call against
-    the oracle, at 1, 2, 3 and 5 generations, ragged n."""
+    """One pair of target buffers rewritten in place between calls, as a
+    search loop does: round 5 picked the launch form from the last call's
+    report on the same pointers (a stale form had to stay exact); from round 6
+    no form depends on a report -- every wave of the one launch picks its pass
+    from the target it reads (step.hip: k_cone_adapt's DMA form at 1-2
+    generations, the merged split kernel from 3) -- and every call must be
+    exact whatever the previous target was.  Every call against the oracle,
+    at 1, 2, 3 and 5 generations, ragged n."""
     n = 70001
     x = port.fill(n, seed=91) & port.fill(n, seed=92)
     d = to_dev(x)

@@ -244,6 +244,9 @@ def summarize(manifest, *dirs):
             out["salu_per_universe"] = c["SQ_INSTS_SALU"] / n
         if "FETCH_SIZE" in c:
             out["fetch_bytes_per_universe"] = c["FETCH_SIZE"] * 1024 * 2.0 / n  # (x 2: MI355X_MICROARCH.md HBM)
+        if c.get("TCC_HIT_sum") is not None and c.get("TCC_MISS_sum") is not None:
+            tot = c["TCC_HIT_sum"] + c["TCC_MISS_sum"]
+            out["tcc_hit_rate"] = c["TCC_HIT_sum"] / tot if tot else None
         if "SQ_WAVE_CYCLES" in c and "SQ_WAVES" in c and c["SQ_WAVES"]:
             for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU"):
                 if k in c:

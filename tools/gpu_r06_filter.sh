@@ -22,5 +22,7 @@ pmc() {  # name counters
 pmc sq "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"
 pmc sq2 "SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_LDS"
 pmc fetch "FETCH_SIZE"
-PMC_JSON="$O/pmc_filter.json" python3 "$P" summarize "$O/sq.manifest" "$O/sq" "$O/sq2" "$O/fetch" > "$O/pmc.jsonl" || exit 5
+pmc tcc "TCC_HIT_sum TCC_MISS_sum"
+PMC_JSON="$O/pmc_filter.json" python3 "$P" summarize "$O/sq.manifest" "$O/sq" "$O/sq2" "$O/fetch" "$O/tcc" \
+  > "$O/pmc.jsonl" || exit 5
 echo "summary ok"

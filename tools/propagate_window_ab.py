@@ -1,7 +1,8 @@
-"""A/B: LifeStable Propagate (LifeStable.hpp:718-729) with every PropagateStep
+"""A/B: LifeStable Propagate (LifeStable.hpp:718-729; PASS=stabilise:
+StabiliseOptions, :677-693) with every iteration
 on the whole columns against the steps after the first on a 32-row window
 around the cells the step before changed (stable_kernels.hpp
-stable_step_window; tuning build k_stable<4, false / true>), and the
+stable_iter_window; tuning build k_stable<4, false / true>, k_stable_dma<5, ...>), and the
 product's launch, on 1M LifeStables of tools/rows_bench.py's two inputs
 (fresh options on still lifes; a search's next node).  Per form: planes
 and flags checked equal to the whole-column form; times back to back (4
@@ -37,14 +38,20 @@ def main():
     scrub = bench.Scrub(RT())
     st = stable_inputs(n)
     inputs = {"fresh options": st, "next node": stable_next_node(st)}
-    forms = {"whole": lambda w: tune.stable_pass(w, 14, 0, xcd_chunk=True),
-             "window": lambda w: tune.stable_pass(w, 15, 0, xcd_chunk=True),
-             "shipped": lambda w: hip.stable_pass(w, "propagate")}
+    which = os.environ.get("PASS", "propagate")
+    if which == "propagate":
+        forms = {"whole": lambda w: tune.stable_pass(w, 14, 0, xcd_chunk=True),
+                 "window": lambda w: tune.stable_pass(w, 15, 0, xcd_chunk=True),
+                 "shipped": lambda w: hip.stable_pass(w, "propagate")}
+    else:  # StabiliseOptions: the shipped LDS-DMA form, whole columns against the window
+        forms = {"whole": lambda w: tune.stable_pass(w, 37, 0, upw=1),
+                 "window": lambda w: tune.stable_pass(w, 38, 0, upw=1),
+                 "shipped": lambda w: hip.stable_pass(w, "stabilise")}
     works = [st.clone() for _ in range(4)]
     for iname, src in inputs.items():
         ref = src.clone()
         ref_flags = forms["whole"](ref).clone()
-        row = {"input": iname, "objects": n}
+        row = {"pass": which, "input": iname, "objects": n}
         for fname, fn in forms.items():
             w = src.clone()
             fl = fn(w)

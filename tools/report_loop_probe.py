@@ -1,11 +1,13 @@
 """The search filter's launch report in a loop that rewrites its target
 (ADVICE r05 items 1-2).
 
-The filter picks its launch form from the report word of the last call on
-the same target buffers (host.hip cone_class_slot, keyed on the wanted /
-unwanted pointers and the generation count).  A loop that writes a new
-target into one pair of device buffers before every call always reads the
-previous target's report.  This probe times three loops over the same
+Round 5's filter picked its launch form from the report word of the last
+call on the same target buffers (keyed on the wanted / unwanted pointers and
+the generation count); a loop that writes a new target into one pair of
+device buffers before every call always read the previous target's report
+(profiles/r06/report_loop_reported.jsonl: +13-20 % per call).  Round 6 reads
+no report (step.hip), so the three loops should match
+(profiles/r06/report_loop_unified.jsonl).  This probe times three loops over the same
 sequence of calls -- 1M config-2 universes, targets cycling block (4 x 4
 window), one-row whole board, full height (bench.py's), at 1, 2, 5 and 8
 generations:

@@ -31,17 +31,17 @@ int cone_by_shape(const uint64_t *in, const uint64_t *w, const uint64_t *u, OutT
     return launch_cone_adapt<8, FIRST, OutT, true>(in, w, u, out, n, gens, cus, st, cap, kWave, 0, rmax >> 8);
   // upw 7: upw 0 (the capped form) without the row-window passes
   if (upw == 7 && rmax == 8)
-    return launch_cone_adapt<8, FIRST, OutT, false, false, false>(in, w, u, out, n, gens, cus, st, cap);
+    return launch_cone_adapt<8, FIRST, OutT, false, false>(in, w, u, out, n, gens, cus, st, cap);
   // upw 8: upw 0 (the capped form) with the window split layout (cone_split.hpp) for row windows
   if (upw == 8 && rmax == 8)
-    return launch_cone_adapt<8, FIRST, OutT, false, false, true, true>(in, w, u, out, n, gens, cus, st, cap);
+    return launch_cone_adapt<8, FIRST, OutT, false, true, true>(in, w, u, out, n, gens, cus, st, cap);
   // upw 9: upw 5 (the whole-board LDS form told its report, rmax >> 8) with the window split layout
   if (upw == 9 && (rmax & 0xFF) == 8)
-    return launch_cone_adapt<8, FIRST, OutT, true, false, true, true>(in, w, u, out, n, gens, cus, st, cap, kWave, 0,
+    return launch_cone_adapt<8, FIRST, OutT, true, true, true>(in, w, u, out, n, gens, cus, st, cap, kWave, 0,
                                                                       rmax >> 8);
   // upw 2: upw 1 without the packed row-window pass (cone_wave_rows_dma): every whole-board target full
   if (upw == 2 && rmax == 8)
-    return launch_cone_adapt<8, FIRST, OutT, true, false, false>(in, w, u, out, n, gens, cus, st, cap);
+    return launch_cone_adapt<8, FIRST, OutT, true, false>(in, w, u, out, n, gens, cus, st, cap);
   LIFEAPI_CONE(8, 8)
   LIFEAPI_CONE(16, 4)
   LIFEAPI_CONE(16, 8)
@@ -207,13 +207,11 @@ int lifeapi_tune_search_iter(const uint64_t *d_in, const uint64_t *d_wanted, con
   if (rc != LIFEAPI_OK) return rc;
   const dim3 grid(grid_for((n + 3) / 4, cus, split_cap));
   hipLaunchKernelGGL((k_step_contains_split<8, kContainsNet, kContainsLo>), grid, dim3(kBlock), 0, (hipStream_t)stream,
-                     d_in, (uint64_t *)nullptr, d_wanted, d_unwanted, d_first, (uint64_t)n, gens, kConeIterColumns,
-                     (int32_t *)nullptr, -1);
+                     d_in, (uint64_t *)nullptr, d_wanted, d_unwanted, d_first, (uint64_t)n, gens, kConeIterColumns);
   rc = launched("k_step_contains_split (tuning) launch");
   if (rc != LIFEAPI_OK) return rc;
   hipLaunchKernelGGL((k_step_contains_split<8, kContainsNet, kContainsHi>), grid, dim3(kBlock), 0, (hipStream_t)stream,
-                     d_in, (uint64_t *)nullptr, d_wanted, d_unwanted, d_first, (uint64_t)n, gens, kConeIterColumns,
-                     (int32_t *)nullptr, -1);
+                     d_in, (uint64_t *)nullptr, d_wanted, d_unwanted, d_first, (uint64_t)n, gens, kConeIterColumns);
   return launched("k_step_contains_split (tuning) launch");
 }
 

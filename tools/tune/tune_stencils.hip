@@ -124,17 +124,20 @@ int lifeapi_tune_stable_pass(uint64_t *d_planes, uint8_t *d_flags, size_t n, int
   // 16 + k: pass k, nt fetch, counted waits; 24 + k: plain fetch, counted;
   // 32 + k: nt fetch, counted, the changed lines stored 16 bytes per lane
   // through the image (U = 1 only); k in {0, 4} for the plain fetch
-  if (pass >= 16 && pass <= 37) {
+  // 38 / 39: StabiliseOptions / Propagate as 37 / 36 with the iterations
+  // after the first on a 32-row window (PW = true; the product ships PW = false)
+  if (pass >= 16 && pass <= 39) {
     if (!d_planes || !d_flags || !aligned8(d_planes)) return fail(LIFEAPI_E_INVALID, "bad argument%s");
     int cus = 0, rc = device_cus(cus);
     if (rc != LIFEAPI_OK) return rc;
     using Fn = void (*)(uint64_t *, uint8_t *, uint64_t, uint32_t, uint32_t);
-    const Fn fns[22] = {k_stable_dma<0>, k_stable_dma<1>, k_stable_dma<2>, k_stable_dma<3>, k_stable_dma<4>,
+    const Fn fns[24] = {k_stable_dma<0>, k_stable_dma<1>, k_stable_dma<2>, k_stable_dma<3>, k_stable_dma<4>,
                         k_stable_dma<5>, nullptr, nullptr,
                         k_stable_dma<0, 0>, nullptr, nullptr, nullptr, k_stable_dma<4, 0>, nullptr, nullptr, nullptr,
                         k_stable_dma<0, 2, true, true>, k_stable_dma<1, 2, true, true>,
                         k_stable_dma<2, 2, true, true>, k_stable_dma<3, 2, true, true>,
-                        k_stable_dma<4, 2, true, true>, k_stable_dma<5, 2, true, true>};
+                        k_stable_dma<4, 2, true, true>, k_stable_dma<5, 2, true, true>,
+                        k_stable_dma<5, 2, true, true, true>, k_stable_dma<4, 2, true, true, true>};
     if (!fns[pass - 16]) return fail(LIFEAPI_E_INVALID, "no such k_stable_dma variant%s");
     int res = 0;
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&res, fns[pass - 16], kBlock, 0);
@@ -160,7 +163,7 @@ int lifeapi_tune_stable_pass(uint64_t *d_planes, uint8_t *d_flags, size_t n, int
   // pass 8 + k: pass k with the prefetching loop (k_stable_pf<k>)
   // pass 14 / 15: Propagate with every step on the whole columns / the steps
   // after the first on a 32-row window (k_stable<4, PW>; the product ships
-  // kPropagateWindow)
+  // PW = kPropagateWindow = false)
   if (!d_planes || !d_flags || !aligned8(d_planes) || pass < 0 || pass > 15 || (pass > 5 && pass < 8))
     return fail(LIFEAPI_E_INVALID, "bad argument to lifeapi_tune_stable_pass%s");
   int cus = 0, rc = device_cus(cus);

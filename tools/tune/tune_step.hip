@@ -539,7 +539,7 @@ int lifeapi_tune_step_contains(const uint64_t *d_in, uint64_t *d_final, const ui
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
   using Fn = void (*)(const uint64_t *, uint64_t *, const uint64_t *, const uint64_t *, uint32_t *, uint64_t, uint32_t,
-                      uint32_t, int32_t *, int32_t);
+                      uint32_t);
   const Fn fns[9] = {k_step_contains_split<8, kContainsNet, 0>, k_step_contains_split<8, kContainsNet, 1>,
                      k_step_contains_split<8, kContainsNet, 2>, k_step_contains_split<8, kContainsNet, 3>,
                      k_step_contains_split<8, kContainsNet, 4>, k_step_contains_split<8, kContainsNet, 5>,
@@ -547,7 +547,7 @@ int lifeapi_tune_step_contains(const uint64_t *d_in, uint64_t *d_final, const ui
                      k_step_contains_split<8, kContainsNet, 8>};
   if (variant < 0 || variant > 8) return fail(LIFEAPI_E_INVALID, "unknown contains variant%s");
   hipLaunchKernelGGL(fns[variant], dim3(grid_for((n + 3) / 4, cus, 0)), dim3(kBlock), 0, (hipStream_t)stream, d_in,
-                     d_final, d_wanted, d_unwanted, d_first_gen, (uint64_t)n, generations, 0u, (int32_t *)nullptr, -1);
+                     d_final, d_wanted, d_unwanted, d_first_gen, (uint64_t)n, generations, 0u);
   return launched("k_step_contains_split (tuning) launch");
 }
 
@@ -611,12 +611,12 @@ int lifeapi_tune_step_contains_pair(const uint64_t *d_in, uint64_t *d_final, con
   if (rc != LIFEAPI_OK) return rc;
   hipLaunchKernelGGL((k_step_contains_split<8, kContainsNet, 7>), dim3(grid_for((n + 3) / 4, cus, cap_lo)),
                      dim3(kBlock), 0, (hipStream_t)stream, d_in, d_final, d_wanted, d_unwanted, d_first_gen,
-                     (uint64_t)n, generations, 0u, (int32_t *)nullptr, -1);
+                     (uint64_t)n, generations, 0u);
   rc = launched("k_step_contains_split (tuning) launch");
   if (rc != LIFEAPI_OK) return rc;
   hipLaunchKernelGGL((k_step_contains_split<8, kContainsNet, 8>), dim3(grid_for((n + 3) / 4, cus, cap_hi)),
                      dim3(kBlock), 0, (hipStream_t)stream, d_in, d_final, d_wanted, d_unwanted, d_first_gen,
-                     (uint64_t)n, generations, 0u, (int32_t *)nullptr, -1);
+                     (uint64_t)n, generations, 0u);
   return launched("k_step_contains_split (tuning) launch");
 }
 
@@ -637,7 +637,7 @@ int lifeapi_tune_filter_iter(const uint64_t *d_in, const uint64_t *d_wanted, con
   const int cap = variant & 0xFF;
   const bool pf = (variant & 0x100) != 0, hi_only = (variant & 0x200) != 0, lo_only = (variant & 0x400) != 0;
   using Fn = void (*)(const uint64_t *, uint64_t *, const uint64_t *, const uint64_t *, uint32_t *, uint64_t, uint32_t,
-                      uint32_t, int32_t *, int32_t);
+                      uint32_t);
   const Fn lo = pf ? k_step_contains_split<8, kContainsNet, kContainsLo, true>
                    : k_step_contains_split<8, kContainsNet, kContainsLo>;
   const Fn hi = pf ? k_step_contains_split<8, kContainsNet, kContainsHi, true>
@@ -650,14 +650,13 @@ int lifeapi_tune_filter_iter(const uint64_t *d_in, const uint64_t *d_wanted, con
                        : (pf ? k_step_contains_split<8, kContainsNet, kContainsAll, true>
                              : k_step_contains_split<8, kContainsNet, kContainsAll>);
     hipLaunchKernelGGL(all, grid, dim3(kBlock), 0, (hipStream_t)stream, d_in, nullptr, d_wanted, d_unwanted,
-                       d_first_gen, (uint64_t)n, generations, 32u, (int32_t *)nullptr, -1);
+                       d_first_gen, (uint64_t)n, generations, 32u);
     return launched("k_step_contains_split (tuning) launch");
   }
   for (int k = 0; k < 2; ++k) {
     if ((k == 0 && hi_only) || (k == 1 && lo_only)) continue;
     hipLaunchKernelGGL(k == 0 ? lo : hi, grid, dim3(kBlock), 0, (hipStream_t)stream, d_in, nullptr, d_wanted,
-                       d_unwanted, d_first_gen, (uint64_t)n, generations, 32u, (int32_t *)nullptr,
-                       -1);  // (cone_max: cone_kernels.hpp kConeIterColumns)
+                       d_unwanted, d_first_gen, (uint64_t)n, generations, 32u);  // (cone_max: cone_kernels.hpp kConeIterColumns)
     rc = launched("k_step_contains_split (tuning) launch");
     if (rc != LIFEAPI_OK) return rc;
   }
