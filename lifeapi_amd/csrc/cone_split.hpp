@@ -201,25 +201,137 @@ __device__ __forceinline__ uint32_t win_batch_gen(uint32_t b) {
   else return (b >> 3) & 1u;
 }
 
+// Generations g_begin + 1 .. g_end of one register set (P lanes per
+// universe), the test after each: a universe's first clean generation goes
+// to lane base + (its group) U + (its index) of `mine`, and `found` (bit =
+// that lane) keeps it from being recorded again.
+template <int P, int R>
+__device__ __forceinline__ void win_gens(uint32_t (&r)[8], const uint32_t (&tw)[8], const uint32_t (&tm)[8],
+                                         uint32_t g_begin, uint32_t g_end, uint32_t &mine, uint64_t &found,
+                                         uint32_t base, int lane) {
+  constexpr int GPS = kWave / P;
+  constexpr int U = 256 / R;
+  constexpr int GPB = R == 32 ? 4 : 2;  // generations per batch word
+  constexpr uint32_t kRot = 8;          // one row group
+  constexpr uint32_t kDiff = ((TA ^ TB) & TC) & 0xFF;  // (s ^ wanted) & care
+  constexpr uint32_t kOr3 = (TA | TB | TC) & 0xFF;
+  constexpr uint32_t fold_mask = R == 32 ? 0xFFu : 0x00FF00FFu;  // one bit per universe after the fold
+  // per group: the bits of the universes answered before this call, in every
+  // generation of a batch word (R = 32: universe u at u + 8 m; R = 16:
+  // universe 2 v + h at 16 h + v + 8 m)
+  uint32_t foundrep[GPS];
+#pragma unroll
+  for (int g = 0; g < GPS; ++g) {
+    const uint32_t fu = (uint32_t)(found >> (base + (uint32_t)g * U)) & ((1u << U) - 1u);
+    if constexpr (R == 32) {
+      foundrep[g] = fu * 0x01010101u;
+    } else {
+      uint32_t rep = 0;
+      for (uint32_t t = fu; t; t &= t - 1) {  // (rare)
+        const uint32_t u = (uint32_t)__builtin_ctz(t);
+        rep |= 0x0101u << (16u * (u & 1u) + (u >> 1));
+      }
+      foundrep[g] = rep;
+    }
+  }
+  for (uint32_t g0 = g_begin; g0 < g_end; g0 += GPB) {
+    const uint32_t nb = g_end - g0 < (uint32_t)GPB ? g_end - g0 : (uint32_t)GPB;  // (wave-uniform)
+    uint32_t acc = 0;
+#pragma unroll
+    for (int m = 0; m < GPB; ++m) {
+      if ((uint32_t)m >= nb) break;
+      uint32_t h0[8], h1[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t L = dpp_prev(r[i]), Rt = dpp_next(r[i]);
+        h0[i] = lut3<kXor3>(L, r[i], Rt);
+        h1[i] = lut3<kMaj>(L, r[i], Rt);
+      }
+      const uint32_t h0u0 = __builtin_amdgcn_alignbit(h0[7], h0[7], 32 - kRot);  // rotl 8: row group k - 1
+      const uint32_t h1u0 = __builtin_amdgcn_alignbit(h1[7], h1[7], 32 - kRot);
+      const uint32_t h0d7 = __builtin_amdgcn_alignbit(h0[0], h0[0], kRot);       // rotr 8: row group k + 1
+      const uint32_t h1d7 = __builtin_amdgcn_alignbit(h1[0], h1[0], kRot);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t u0v = i ? h0[i - 1] : h0u0, d0v = i < 7 ? h0[i + 1] : h0d7;
+        const uint32_t u1v = i ? h1[i - 1] : h1u0, d1v = i < 7 ? h1[i + 1] : h1d7;
+        r[i] = life_tail6(u0v, h0[i], d0v, u1v, h1[i], d1v, r[i]);
+      }
+      uint32_t d[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) d[i] = lut3<kDiff>(r[i], tw[i], tm[i]);
+      const uint32_t D = lut3<kOr3>(lut3<kOr3>(d[0], d[1], d[2]), lut3<kOr3>(d[3], d[4], d[5]), d[6] | d[7]);
+      uint32_t f;
+      if constexpr (R == 32) {
+        f = D | __builtin_amdgcn_alignbit(D, D, 16);
+        f = f | __builtin_amdgcn_alignbit(f, f, 8);
+      } else {
+        f = D | __builtin_amdgcn_alignbit(D, D, 8);
+      }
+      acc |= (f & fold_mask) << (8 * m);
+    }
+    // the OR over each group's P lanes: every lane of an 8-lane half
+    // (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror), of a 16-lane row
+    // (row_mirror), then the rows by v_readlane
+    uint32_t v = acc;
+    v |= dpp_mov<0xB1>(v);
+    v |= dpp_mov<0x4E>(v);
+    v |= dpp_mov<0x141>(v);
+    if constexpr (P >= 16) v |= dpp_mov<0x140>(v);
+    uint32_t vmask = 0;  // the batch word's bits of generations g0 + 1 .. g0 + nb
+#pragma unroll
+    for (int m = 0; m < GPB; ++m)
+      if ((uint32_t)m < nb) vmask |= fold_mask << (8 * m);
+#pragma unroll
+    for (int g = 0; g < GPS; ++g) {
+      uint32_t w = 0;
+      if constexpr (P <= 16) {
+        w = (uint32_t)__builtin_amdgcn_readlane((int)v, g * P);
+      } else {
+#pragma unroll
+        for (int t = 0; t < P / 16; ++t) w |= (uint32_t)__builtin_amdgcn_readlane((int)v, g * P + 16 * t);
+      }
+      uint32_t c = ~w & vmask & ~foundrep[g];
+      while (c) {  // (rare) hits: the first clean generation of each new universe
+        const uint32_t b = (uint32_t)__builtin_ctz(c);
+        const uint32_t idx = base + (uint32_t)g * U + win_universe<R>(b);
+        if (!((found >> idx) & 1ull)) {
+          found |= 1ull << idx;
+          if ((uint32_t)lane == idx) mine = g0 + win_batch_gen<R>(b) + 1u;
+          // this universe's bits in every generation of a batch word
+          foundrep[g] |= R == 32 ? 0x01010101u << (b & 7u) : 0x0101u << (b & 0x17u);
+        }
+        c &= c - 1;
+      }
+    }
+  }
+}
+
 // One wave's passes over universes u_first, u_first + u_step, ... (chunks of
 // UPS = (64 / P) (256 / R) universes, one register set each).  out[u] = the
 // first generation in 1..gens whose state contains the target, 0 = never.
 // xs / K: the column window (K <= P), y0: the first window row (WRAP: the
 // window crosses row 63), as cone_wave_rows.
-template <int P, int R, bool WRAP, typename OutT>
+//
+// SHRINK: the light cone narrows by two columns a generation; once the
+// columns still needed, K - 2 g1, fit P / 2 lanes, two register sets become
+// one: chunks of 2 UPS universes, each set stepped g1 generations and parked
+// in the wave's LDS (`stash`, 4 KiB), then read back as one set of P / 2
+// lanes per universe (lane j2 of new group 2 s + q takes lane q P + g1 + j2
+// of set s -- the window's first g1 columns dropped) and stepped the rest:
+// every later generation at half the issue slots.  The target is loaded
+// again in each layout (a cached 512-byte read) rather than held twice.
+template <int P, int R, bool WRAP, bool SHRINK, typename OutT>
 __device__ __forceinline__ void cone_wave_split(const uint64_t *in, const uint64_t *__restrict__ wanted,
                                                 const uint64_t *__restrict__ unwanted, OutT *__restrict__ out,
                                                 uint64_t n, uint64_t u_first, uint64_t u_step, uint32_t gens,
-                                                uint32_t xs, uint32_t K, uint32_t y0, int lane) {
-  constexpr int GPS = kWave / P;                 // groups (universe columns) per wave
-  constexpr int U = 256 / R;                     // universes per register per group
-  constexpr int UPS = GPS * U;                   // universes per register set
-  constexpr int GPB = R == 32 ? 4 : 2;           // generations per batch word
-  constexpr uint32_t kRot = 8;                   // one row group
-  static_assert(UPS <= kWave, "one answer per lane");
-  static_assert(P >= 8 && P <= kWave, "8 .. 64 lanes per universe");
-  constexpr uint32_t kDiff = ((TA ^ TB) & TC) & 0xFF;  // (s ^ wanted) & care
-  constexpr uint32_t kOr3 = (TA | TB | TC) & 0xFF;
+                                                uint32_t xs, uint32_t K, uint32_t y0, int lane, uint32_t *stash) {
+  constexpr int GPS = kWave / P;  // groups (universe columns) per wave
+  constexpr int U = 256 / R;      // universes per register per group
+  constexpr int UPS = GPS * U;    // universes per register set
+  constexpr int CH = SHRINK ? 2 * UPS : UPS;  // universes per chunk
+  static_assert(CH <= kWave, "one answer per lane");
+  static_assert(P >= 8 && P <= kWave && (!SHRINK || P >= 16), "8 .. 64 lanes per universe");
   constexpr uint32_t rmask = R == 32 ? ~0u : 0xFFFFu;
   const uint32_t j = (uint32_t)lane & (P - 1), q = (uint32_t)lane / P;
   const uint32_t col = (xs + j) & (kWave - 1);
@@ -229,141 +341,110 @@ __device__ __forceinline__ void cone_wave_split(const uint64_t *in, const uint64
     const W w = split(v);
     return (WRAP ? __builtin_amdgcn_alignbit(w.lo, w.hi, sh) : __builtin_amdgcn_alignbit(w.hi, w.lo, sh)) & rmask;
   };
-  // the target in the same layout, replicated over the universes
-  uint32_t tw[8], tm[8];
-  {
-    const uint64_t w64 = live ? wanted[col] : 0ull, m64 = live ? (w64 | unwanted[col]) : 0ull;
+  // the target in the same layout, replicated over the universes: window
+  // column jj in this lane
+  auto target = [&](uint32_t jj, uint32_t (&tw_)[8], uint32_t (&tm_)[8]) __attribute__((always_inline)) {
+    const uint32_t c = (xs + jj) & (kWave - 1);
+    const uint64_t w64 = jj < K ? wanted[c] : 0ull, m64 = jj < K ? (w64 | unwanted[c]) : 0ull;
     uint32_t ew[U], em[U];
     const uint32_t cw = cut(w64), cm = cut(m64);
 #pragma unroll
     for (int u = 0; u < U; ++u) ew[u] = cw, em[u] = cm;
-    win_pack<R>(ew, tw);
-    win_pack<R>(em, tm);
-  }
-  const uint32_t fold_mask = R == 32 ? 0xFFu : 0x00FF00FFu;  // one bit per universe after the fold
+    win_pack<R>(ew, tw_);
+    win_pack<R>(em, tm_);
+  };
+  auto load_set = [&](uint64_t ub, uint32_t (&r)[8]) __attribute__((always_inline)) {
+    uint32_t e[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t uu = ub + (uint64_t)q * U + u;
+      e[u] = (live && uu < n) ? cut(__builtin_nontemporal_load(in + uu * kWave + col)) : 0u;
+    }
+    win_pack<R>(e, r);
+  };
+  uint32_t tw[8], tm[8];
+  if constexpr (!SHRINK) target(j, tw, tm);
+  // SHRINK: the generation after which the needed columns fit P / 2 lanes
+  const uint32_t g1 = SHRINK ? (K - P / 2 + 1) / 2 : gens;
   for (uint64_t u0 = u_first; u0 < n; u0 += u_step) {
-    uint32_t r[8];
-    {
-      uint32_t e[U];
-      const uint64_t ub = u0 + (uint64_t)q * U;
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint64_t uu = ub + u;
-        e[u] = (live && uu < n) ? cut(__builtin_nontemporal_load(in + uu * kWave + col)) : 0u;
+    uint32_t mine = 0;   // lane L: the answer of universe u0 + L
+    uint64_t found = 0;  // chunk-local universes already answered
+    if constexpr (!SHRINK) {
+      uint32_t r[8];
+      load_set(u0, r);
+      win_gens<P, R>(r, tw, tm, 0u, gens, mine, found, 0u, lane);
+    } else {
+      constexpr int P2 = P / 2;
+      using V4 = __attribute__((ext_vector_type(4))) uint32_t;
+      V4 *const st = reinterpret_cast<V4 *>(stash);  // set s, lane L: st[128 s + 2 L], [+ 1]
+      {
+        uint32_t jj = j;  // (opaque: loaded again per chunk, not held across the merged phase)
+        asm volatile("" : "+v"(jj));
+        target(jj, tw, tm);
       }
-      win_pack<R>(e, r);
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        uint32_t r[8];
+        load_set(u0 + (uint64_t)s * UPS, r);
+        win_gens<P, R>(r, tw, tm, 0u, g1, mine, found, (uint32_t)(s * UPS), lane);
+        st[128 * s + 2 * lane] = V4{r[0], r[1], r[2], r[3]};
+        st[128 * s + 2 * lane + 1] = V4{r[4], r[5], r[6], r[7]};
+      }
+      // lane L of the merged set: group q2 = L / P2 (set q2 / GPS, its group
+      // q2 % GPS), column j2 = L % P2 of the narrowed window
+      const uint32_t q2 = (uint32_t)lane / P2, j2 = (uint32_t)lane & (P2 - 1);
+      const uint32_t src = 128u * (q2 / GPS) + 2u * ((q2 % GPS) * P + g1 + j2);
+      const V4 a = st[src], b = st[src + 1];
+      uint32_t r2[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      target(g1 + j2, tw, tm);
+      win_gens<P2, R>(r2, tw, tm, g1, gens, mine, found, 0u, lane);
     }
-    uint32_t mine = 0;      // lane L: the answer of universe u0 + L
-    uint64_t found = 0;     // set-local universes already answered
-    uint32_t foundrep[GPS];  // per group: the found universes' bits in a batch word
-#pragma unroll
-    for (int g = 0; g < GPS; ++g) foundrep[g] = 0;
-    for (uint32_t g0 = 0; g0 < gens; g0 += GPB) {
-      const uint32_t nb = gens - g0 < (uint32_t)GPB ? gens - g0 : (uint32_t)GPB;  // (wave-uniform)
-      uint32_t acc = 0;
-#pragma unroll
-      for (int m = 0; m < GPB; ++m) {
-        if ((uint32_t)m >= nb) break;
-        uint32_t h0[8], h1[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const uint32_t L = dpp_prev(r[i]), Rt = dpp_next(r[i]);
-          h0[i] = lut3<kXor3>(L, r[i], Rt);
-          h1[i] = lut3<kMaj>(L, r[i], Rt);
-        }
-        const uint32_t h0u0 = __builtin_amdgcn_alignbit(h0[7], h0[7], 32 - kRot);  // rotl 8: row group k - 1
-        const uint32_t h1u0 = __builtin_amdgcn_alignbit(h1[7], h1[7], 32 - kRot);
-        const uint32_t h0d7 = __builtin_amdgcn_alignbit(h0[0], h0[0], kRot);       // rotr 8: row group k + 1
-        const uint32_t h1d7 = __builtin_amdgcn_alignbit(h1[0], h1[0], kRot);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const uint32_t u0v = i ? h0[i - 1] : h0u0, d0v = i < 7 ? h0[i + 1] : h0d7;
-          const uint32_t u1v = i ? h1[i - 1] : h1u0, d1v = i < 7 ? h1[i + 1] : h1d7;
-          r[i] = life_tail6(u0v, h0[i], d0v, u1v, h1[i], d1v, r[i]);
-        }
-        uint32_t d[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) d[i] = lut3<kDiff>(r[i], tw[i], tm[i]);
-        const uint32_t D = lut3<kOr3>(lut3<kOr3>(d[0], d[1], d[2]), lut3<kOr3>(d[3], d[4], d[5]), d[6] | d[7]);
-        uint32_t f;
-        if constexpr (R == 32) {
-          f = D | __builtin_amdgcn_alignbit(D, D, 16);
-          f = f | __builtin_amdgcn_alignbit(f, f, 8);
-        } else {
-          f = D | __builtin_amdgcn_alignbit(D, D, 8);
-        }
-        acc |= (f & fold_mask) << (8 * m);
-      }
-      // the OR over each group's P lanes: every lane of an 8-lane half
-      // (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror), of a 16-lane row
-      // (row_mirror), then the rows by v_readlane
-      uint32_t v = acc;
-      v |= dpp_mov<0xB1>(v);
-      v |= dpp_mov<0x4E>(v);
-      v |= dpp_mov<0x141>(v);
-      if constexpr (P >= 16) v |= dpp_mov<0x140>(v);
-      uint32_t vmask = 0;  // the batch word's bits of generations g0 + 1 .. g0 + nb
-#pragma unroll
-      for (int m = 0; m < GPB; ++m)
-        if ((uint32_t)m < nb) vmask |= fold_mask << (8 * m);
-#pragma unroll
-      for (int g = 0; g < GPS; ++g) {
-        uint32_t w = 0;
-        if constexpr (P <= 16) {
-          w = (uint32_t)__builtin_amdgcn_readlane((int)v, g * P);
-        } else {
-#pragma unroll
-          for (int t = 0; t < P / 16; ++t) w |= (uint32_t)__builtin_amdgcn_readlane((int)v, g * P + 16 * t);
-        }
-        uint32_t c = ~w & vmask & ~foundrep[g];
-        while (c) {  // (rare) hits: the first clean generation of each new universe
-          const uint32_t b = (uint32_t)__builtin_ctz(c);
-          const uint32_t uu = win_universe<R>(b), idx = (uint32_t)g * U + uu;
-          if (!((found >> idx) & 1ull)) {
-            found |= 1ull << idx;
-            if ((uint32_t)lane == idx) mine = g0 + win_batch_gen<R>(b) + 1u;
-            // this universe's bits in every generation of a batch word
-            foundrep[g] |= R == 32 ? 0x01010101u << (b & 7u) : 0x0101u << (b & 0x17u);
-          }
-          c &= c - 1;
-        }
-      }
-    }
-    if (lane < UPS && u0 + (uint64_t)lane < n) out[u0 + lane] = (OutT)mine;
+    if (lane < CH && u0 + (uint64_t)lane < n) out[u0 + lane] = (OutT)mine;
   }
 }
 
-// The pass for a window (R = 32 rows for row class 1, 16 for classes 2 and
-// 4; P = the lanes per universe the K columns need, >= 16 for R = 16: one
-// answer per lane), this wave's sets from wave index `wave` of `nw`, sets of
-// (64 / P) (256 / R) universes.
 template <typename OutT>
 __device__ __forceinline__ void cone_split_pass(const uint64_t *in, const uint64_t *__restrict__ wanted,
                                                 const uint64_t *__restrict__ unwanted, OutT *__restrict__ out,
                                                 uint64_t n, uint64_t wave, uint64_t nw, uint32_t gens, uint32_t xs,
-                                                uint32_t K, int pk, uint32_t y0, int lane) {
-  auto run = [&](auto p_c, auto r_c) __attribute__((always_inline)) {
+                                                uint32_t K, int pk, uint32_t y0, int lane,
+                                                uint32_t *stash = nullptr) {
+  auto run = [&](auto p_c, auto r_c, auto s_c) __attribute__((always_inline)) {
     constexpr int Pc = decltype(p_c)::value, Rc = decltype(r_c)::value;
-    constexpr uint64_t UPS = (uint64_t)(kWave / Pc) * (256 / Rc);
-    if (wave * UPS >= n) return;
+    constexpr bool Sc = decltype(s_c)::value;
+    constexpr uint64_t CH = (uint64_t)(kWave / Pc) * (256 / Rc) * (Sc ? 2 : 1);
+    if (wave * CH >= n) return;
     if (y0 >= 32u)
-      cone_wave_split<Pc, Rc, true>(in, wanted, unwanted, out, n, wave * UPS, nw * UPS, gens, xs, K, y0, lane);
+      cone_wave_split<Pc, Rc, true, Sc>(in, wanted, unwanted, out, n, wave * CH, nw * CH, gens, xs, K, y0, lane, stash);
     else
-      cone_wave_split<Pc, Rc, false>(in, wanted, unwanted, out, n, wave * UPS, nw * UPS, gens, xs, K, y0, lane);
+      cone_wave_split<Pc, Rc, false, Sc>(in, wanted, unwanted, out, n, wave * CH, nw * CH, gens, xs, K, y0, lane, stash);
   };
   using I8 = std::integral_constant<int, 8>;
   using I16 = std::integral_constant<int, 16>;
   using I32 = std::integral_constant<int, 32>;
   using I64 = std::integral_constant<int, 64>;
+  using T = std::true_type;
+  using F = std::false_type;
+  // the columns fit half the lanes before the last generation: K - 2 g1 <=
+  // P / 2 with g1 < gens (and 2 UPS answers fit the wave's 64 lanes); a
+  // caller without a stash never shrinks
+    // (LIFE_SHRINK_MASK: bit i enables the i-th shrinking form below; the A/B
+  // build without any, tools/gpu_r06f.sh, compiles with 0.  1M universes,
+  // 4 x 4 block, alone: 8 / 13 generations 0.097 / 0.137 ms against 0.110 /
+  // 0.153; other targets within +-3 %, profiles/r06/shrink_ab/)
+#ifndef LIFE_SHRINK_MASK
+#define LIFE_SHRINK_MASK 31
+#endif
+  auto shrinks = [&](uint32_t P, int bit) { return ((LIFE_SHRINK_MASK >> bit) & 1) && stash && K > P / 2 && (K - P / 2 + 1) / 2 < gens; };
   if (pk == 1) {
-    if (K <= 8u) return run(I8{}, I32{});
-    if (K <= 16u) return run(I16{}, I32{});
-    if (K <= 32u) return run(I32{}, I32{});
-    return run(I64{}, I32{});
+    if (K <= 8u) return run(I8{}, I32{}, F{});
+    if (K <= 16u) return shrinks(16, 0) ? run(I16{}, I32{}, T{}) : run(I16{}, I32{}, F{});
+    if (K <= 32u) return shrinks(32, 1) ? run(I32{}, I32{}, T{}) : run(I32{}, I32{}, F{});
+    return shrinks(64, 2) ? run(I64{}, I32{}, T{}) : run(I64{}, I32{}, F{});
   }
-  if (K <= 16u) return run(I16{}, I16{});
-  if (K <= 32u) return run(I32{}, I16{});
-  return run(I64{}, I16{});
+  if (K <= 16u) return run(I16{}, I16{}, F{});
+  if (K <= 32u) return shrinks(32, 3) ? run(I32{}, I16{}, T{}) : run(I32{}, I16{}, F{});
+  return shrinks(64, 4) ? run(I64{}, I16{}, T{}) : run(I64{}, I16{}, F{});
 }
 
 }  // namespace

@@ -788,7 +788,10 @@ __device__ __forceinline__ void cone_wave_rows(const uint64_t *in, const uint64_
 // (cone_split.hpp) on its column window -- or, on a whole board below
 // kConeWholeWinGens generations, the packed LDS-DMA row pass.
 template <int S, int NET, int ASM = 0, bool PF = false, bool WIN = false>
-__global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *in, uint64_t *fin,
+// (amdgpu_waves_per_eu(7): the shrinking window pass (cone_split.hpp) lifts
+// the kernel's allocation 72 -> 76 VGPRs on its own, a wave per SIMD for
+// every target; held at 72 it spills 12 bytes, reloaded once per chunk)
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) void k_step_contains_split(const uint64_t *in, uint64_t *fin,
                                                                 const uint64_t *__restrict__ wanted,
                                                                 const uint64_t *__restrict__ unwanted,
                                                                 uint32_t *__restrict__ first, uint64_t n,
@@ -837,7 +840,8 @@ __global__ __launch_bounds__(kBlock) void k_step_contains_split(const uint64_t *
             return y0w >= 32u ? rows(P1{}, T{}) : rows(P1{}, F{});
           }
         }
-        return cone_split_pass(in, wanted, unwanted, first, n, wave, nw, gens, xs, K, pk, y0w, lane);
+        return cone_split_pass(in, wanted, unwanted, first, n, wave, nw, gens, xs, K, pk, y0w, lane,
+                               reinterpret_cast<uint32_t *>(wave_lds[wib]));
       }
     }
   }

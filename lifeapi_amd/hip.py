@@ -19,7 +19,9 @@ import torch  # noqa: F401  (must precede loading the HIP library)
 
 from .layout import N
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "liblifeapi_hip.so")
+# (LIFEAPI_HIP_LIB: another build of the same library, for A/B probes under tools/)
+LIB_PATH = os.environ.get("LIFEAPI_HIP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                             "liblifeapi_hip.so")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(

@@ -190,6 +190,43 @@ def test_step_contains_random_windows_vs_reference(hip, R, port):
         assert 1 <= exp[0] <= 3
 
 
+@pytest.mark.parametrize("gens", [3, 4, 5, 7, 8, 11, 15])
+def test_filter_shrinking_windows_vs_reference(hip, R, port, gens):
+    """the window split pass that halves its lanes once the light cone's
+    columns fit (cone_split.hpp SHRINK): column windows of every lane class
+    (K = w + 2 gens in 9..16, 17..32, 33..63), row windows of 32 and (up to
+    7 generations) 16 rows, across the column and row seams; universes that
+    are universe 0 stepped 1..k - 1 generations hit before and after the
+    merge, in both halves of a chunk, at a ragged batch end"""
+    rng = np.random.default_rng(1000 + gens)
+    n = 1000 + gens
+    x = port.fill(n, seed=gens) & port.fill(n, seed=gens + 50)
+    lanes = [(9, 16), (17, 32), (33, 63)]
+    for t in range(18):
+        lo, hi = lanes[t % 3]
+        w = int(rng.integers(max(1, lo - 2 * gens), max(2, hi - 2 * gens + 1)))
+        w = min(w, 64 - 2 * gens - 1)
+        x0 = int(rng.integers(64)) if t % 2 else 64 - w // 2  # across column 63 every other target
+        rmax = 16 if gens <= 7 and t % 4 == 1 else 32
+        h = int(rng.integers(1, rmax - 2 * gens + 1))
+        y0 = int(rng.integers(64)) if t % 3 else 64 - h // 2
+        rows = np.uint64(sum(1 << ((y0 + i) % 64) for i in range(h)))
+        box = np.zeros(64, np.uint64)
+        box[[(x0 + i) % 64 for i in range(w)]] = rows
+        k = int(rng.integers(1, gens + 1))
+        at = rng.choice(n, size=k, replace=False)  # at[d]: x[src] stepped d generations
+        src = int(at[0])
+        for d in range(1, k):
+            x[at[d]] = port.step_batch(x[src:src + 1], d)[0]
+        ahead = port.step_batch(x[src:src + 1], k)[0]
+        wv, uv = ahead & box, box & ~ahead
+        first, _ = hip.step_contains(to_dev(x), to_dev(wv[None]), to_dev(uv[None]), gens)
+        exp, _ = R.step_contains_batch(x, wv, uv, gens, nthreads=THREADS)
+        got = first.cpu().numpy().astype(np.uint32)
+        assert (got == exp).all(), (t, w, x0, h, y0, k, np.nonzero(got != exp)[0][:8])
+        assert 1 <= exp[src] <= k
+
+
 @pytest.mark.parametrize("gens", [1, 2, 13])
 @pytest.mark.parametrize("which", [0, 1])
 def test_step_contains_in_place_vs_reference(hip, R, port, which, gens):
