@@ -176,17 +176,17 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
     // * care rows that fit 32 with the light cone (cone_rows): on a whole
     //   board below kConeWholeWinGens generations the packed LDS-DMA pass
     //   (cone_wave_rows_dma), else the window split layout (cone_split.hpp)
-    //   on the column window;
+    //   on the column window, on half the lanes once the cone's columns fit;
     // * else a cone of <= 32 columns: the natural layout on the cone
     //   (cone_wave);
     // * else the 8-way row split with the test fused (the loop its row
     //   window picks), the next group of universes fetched into LDS while
     //   this one steps.
     // 1M universes, median of 5 x 10 back to back (tools/filter_iter_probe.py,
-    // profiles/r06/): block + ring at 3 / 5 / 8 / 13 generations 0.036 / 0.053
-    // / 0.110 / 0.153 ms (round 5: 0.047 / 0.057 / 0.154 / 0.222), a
-    // full-height target 0.176 / 0.237 / 0.327 / 0.465 (0.18 / 0.24 / 0.32 /
-    // 0.47 on the split pair).
+    // profiles/r06/): block + ring at 3 / 5 / 8 / 13 generations 0.042 / 0.058
+    // / 0.096 / 0.137 ms (round 5: 0.047 / 0.057 / 0.154 / 0.222;
+    // profiles/r06/shrink_ab/), a full-height target 0.179 / 0.235 / 0.309 /
+    // 0.435 (0.18 / 0.24 / 0.32 / 0.47 on the split pair).
     using Fn = void (*)(const uint64_t *, uint64_t *, const uint64_t *, const uint64_t *, uint32_t *, uint64_t,
                         uint32_t, uint32_t);
     const Fn fn = aligned16(d_in) ? k_step_contains_split<8, kContainsNet, kContainsAll, true, true>

@@ -890,12 +890,11 @@ def test_filter_whole_board_row_windows(hip, port, rows, gens_list):
     16 or 32 rows takes the packed row-window pass (cone_kernels.hpp
     cone_wave_rows_dma: 4, 2 or 1 universes per 32-bit register, shifts for
     the vertical neighbours) in the LDS form; windows across row 63 and across
-    the 32-bit halves; every call against the oracle (first call the capped
-    form, the next two the LDS form), ragged n.  From 3 generations the first
-    call takes the merged split kernel (step.hip: its waves run the window
-    split layout, cone_split.hpp, and wave 0 writes the target's report), the
-    next ones k_cone_adapt (the LDS-DMA packed form below kConeWholeWinGens,
-    the window split layout from it on)."""
+    the 32-bit halves; every call against the oracle, three calls each
+    (round 5's calls differed by the launch report; round 6's are one form),
+    ragged n.  From 3 generations the merged split kernel (step.hip): the
+    LDS-DMA packed pass below kConeWholeWinGens, the window split layout
+    (cone_split.hpp) from it on."""
     n = 70001
     x = port.fill(n, seed=93) & port.fill(n, seed=94) & port.fill(n, seed=95)
     d = to_dev(x)

@@ -164,10 +164,9 @@ def test_config3_search_loop_vs_reference_digest(hip):
 
 
 def test_step_contains_random_windows_vs_reference(hip, R, port):
-    """the shipped filter (round 6: the merged split kernel on the first call
-    on a target, k_cone_adapt's window split layout once a report carries a
-    row window -- and the target buffers are reused, so calls read the last
-    target's report) on 48 targets with random row windows (1..12 rows, also
+    """the shipped filter (round 6: one launch of the merged split kernel,
+    whose waves pick the pass from the target they read -- no launch report)
+    on 48 targets with random row windows (1..12 rows, also
     20 and 64, anywhere including across the row seam) and columns:
     each target is universe 0's box after 3 generations, so universe 0 hits;
     first-hit generations and final states against the reference's loop"""
@@ -375,7 +374,7 @@ def test_iterated_search_loop_cone_and_split_vs_reference(hip, R, port, w, gens)
         dw, du = to_dev(tw[None]), to_dev(tu[None])
         exp_first, exp_fin = R.step_contains_batch(x, tw, tu, gens, nthreads=THREADS)
         dx = to_dev(x)
-        for call in range(2):  # the second call takes the form the first one's report picked
+        for call in range(2):  # (round 5: the second call took the form the first one's report picked)
             first, _ = hip.step_contains(dx, dw, du, gens)
             got = first.cpu().numpy().astype(np.uint32)
             assert (got == exp_first).all(), (w, gens, x0, call, np.nonzero(got != exp_first)[0][:8])
@@ -395,8 +394,8 @@ def test_iterated_search_loop_cone_and_split_vs_reference(hip, R, port, w, gens)
                                       (40, 2, 4), (40, 12, 7), (64, 3, 14)])
 def test_iterated_search_loop_short_targets_vs_reference(hip, R, port, w, h, gens):
     """gens > 2, no final states, targets of w columns x h rows (cyclic, at
-    the seams), each called twice (no report, then the form the report
-    picks): rows that fit 32 with the light cone take the window split
+    the seams), each called twice (round 5's two calls differed by the
+    launch report): rows that fit 32 with the light cone take the window split
     layout (cone_split.hpp; the round-6 shapes cover P = 8 / 16 / 32 / 64
     lanes x R = 32 / 16 rows), narrower cones of taller targets the natural
     layout's cone pass, the rest the 8-way row split that their height
@@ -420,7 +419,7 @@ def test_iterated_search_loop_short_targets_vs_reference(hip, R, port, w, h, gen
         dw, du = to_dev(tw[None]), to_dev(tu[None])
         exp_first, _ = R.step_contains_batch(x, tw, tu, gens, nthreads=THREADS)
         dx = to_dev(x)
-        for call in range(2):  # the second call takes the form the first one's report picked
+        for call in range(2):  # (round 5: the second call took the form the first one's report picked)
             first, _ = hip.step_contains(dx, dw, du, gens)
             got = first.cpu().numpy().astype(np.uint32)
             assert (got == exp_first).all(), (w, h, gens, x0, y0, call, np.nonzero(got != exp_first)[0][:8])

@@ -42,7 +42,8 @@ for s in ${STEPS:-test smoke bench}; do
   rehearse8)
     LIFEAPI_BENCH_BACKEND=gloo timeout -k 10 600 python bench.py --gpus 8 --steps 10 --warmup 3 \
       > "$O/dist_rehearsal8.json" 2> "$O/dist_rehearsal8.err" || { tail -30 "$O/dist_rehearsal8.err"; exit 6; } ;;
-  rows)
+  rows)  # (priced on this call's filter PMC table when the filterpmc step ran before it)
+    [ -f "$O/filterpmc/pmc_filter.json" ] && export LIFEAPI_PMC_FILTER="$O/filterpmc/pmc_filter.json"
     timeout -k 10 300 python tools/rows_bench.py > "$O/rows_bench.jsonl" 2> "$O/rows_bench.err" \
       || { tail -20 "$O/rows_bench.err"; exit 7; } ;;
   trace)

@@ -20,7 +20,8 @@ import sys
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT_DIR)
 import bench  # noqa: E402
 import lifeapi_amd.hip as hip  # noqa: E402
 
@@ -121,8 +122,9 @@ def both(name, n, nbytes, fn, extra=None, pmc=None):
     report(name, n, nbytes, timed(fn), extra, scrubbed(fn), pmc=pmc)
 
 
-PMC_FILTER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "r06",
-                          "pmc_filter.json")
+# (LIFEAPI_PMC_FILTER: a table collected earlier in the same GPU call, tools/gpu_r06.sh)
+PMC_FILTER = os.environ.get("LIFEAPI_PMC_FILTER") or os.path.join(
+    os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "r06", "pmc_filter.json")
 
 
 def pmc_filter_row(target, gens, algo_bytes):
@@ -139,7 +141,7 @@ def pmc_filter_row(target, gens, algo_bytes):
     if not r or "valu_per_universe" not in r:
         return None
     fetched = r.get("fetch_bytes_per_universe", 0.0) + 4
-    return max(algo_bytes, fetched), r["valu_per_universe"], "profiles/r06/pmc_filter.json"
+    return max(algo_bytes, fetched), r["valu_per_universe"], os.path.relpath(PMC_FILTER, ROOT_DIR)
 
 
 def stable_inputs(n):
