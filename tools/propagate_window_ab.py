@@ -2,7 +2,8 @@
 StabiliseOptions, :677-693) with every iteration
 on the whole columns against the steps after the first on a 32-row window
 around the cells the step before changed (stable_kernels.hpp
-stable_iter_window; tuning build k_stable<4, false / true>, k_stable_dma<5, ...>), and the
+stable_iter_window; tuning build k_stable<4, false / true>, k_stable_dma<5, ...>,
+k_stable<5, true, false / true>), and the
 product's launch, on 1M LifeStables of tools/rows_bench.py's two inputs
 (fresh options on still lifes; a search's next node).  Per form: planes
 and flags checked equal to the whole-column form; times back to back (4
@@ -46,6 +47,10 @@ def main():
     else:  # StabiliseOptions: the shipped LDS-DMA form, whole columns against the window
         forms = {"whole": lambda w: tune.stable_pass(w, 37, 0, upw=1),
                  "window": lambda w: tune.stable_pass(w, 38, 0, upw=1),
+                 # k_stable (no LDS-DMA), whole columns / the later rounds on
+                 # the window with the columns stashed in LDS
+                 "k_whole": lambda w: tune.stable_pass(w, 6, 0, xcd_chunk=True),
+                 "k_window": lambda w: tune.stable_pass(w, 7, 0, xcd_chunk=True),
                  "shipped": lambda w: hip.stable_pass(w, "stabilise")}
     works = [st.clone() for _ in range(4)]
     for iname, src in inputs.items():
