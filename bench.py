@@ -858,10 +858,11 @@ def _cone_cells(wanted: np.ndarray, unwanted: np.ndarray, gens: int) -> int:
 def secondary_filter_iter(hip, rt):
     """The iterated search filter (LifeTarget.hpp:44-51,
     LifeAPI.hpp:877-881): 1M config-2 universes, Step() then Contains(target)
-    after every generation up to 3-13 generations, first hits only, on three
-    targets: bench's block + ring (a 4 x 4 care window), its one-row
-    whole-board target, and a full-height one (16 dead cells, one in every
-    fourth row: no window of any kind).  Each call is timed alone after a 768
+    after every generation up to 1-13 generations, first hits only, on three
+    targets: bench's block + ring (a 4 x 4 care window) at 5 / 8 / 13, its
+    one-row whole-board target at 5 / 8, and a full-height one (16 dead
+    cells, one in every fourth row: no window of any kind) at 1 / 2 / 3 / 5
+    / 8 generations.  Each call is timed alone after a 768
     MiB scrub (median of 10) and back to back; the answers of the first and
     the second call on each target (the first call has no launch report yet)
     are checked against the reference's own loop (tests/golden/golden.json
@@ -877,7 +878,7 @@ def secondary_filter_iter(hip, rt):
     x = hip.fill_random(n, seed=2, device=rt.device, stream=rt.stream)
     scrub = Scrub(rt)
     out = {"workload": f"config2 input: {n} universes, the search loop Step() then Contains(target) up to "
-                       "3-13 generations, first hits only",
+                       "1-13 generations, first hits only",
            "timing": "alone: 3 warm, 10 timed calls each after a 768 MiB scrub, events around the call, "
                      "median; b2b: 20 calls back to back",
            "targets": {}}

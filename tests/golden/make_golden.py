@@ -279,7 +279,7 @@ def full_height_target():
     return w, u
 
 
-FILTER_ITER_GENS = {"block": (5, 8, 13), "whole_board": (5, 8), "full_height": (3, 5, 8)}
+FILTER_ITER_GENS = {"block": (5, 8, 13), "whole_board": (5, 8), "full_height": (1, 2, 3, 5, 8)}
 
 
 def filter_iter_digests() -> dict:

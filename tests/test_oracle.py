@@ -503,3 +503,26 @@ def test_prelude_build_matches_minimal_recipe(ref, port):
         assert (pa == pb).all(), which
     for u in range(len(st)):
         assert (a.stable_vulnerable(st[u]) == b.stable_vulnerable(st[u])).all()
+
+
+def test_filter_iter_digests_from_the_port(port, meta):
+    """bench.py secondary_filter_iter's digests (the reference's own Step() +
+    Contains loop, make_golden.py filter_iter_digests) reproduced by the
+    restatement: first-hit generations of every target at every generation
+    count on the full 1M config-2 input"""
+    d = meta["digests"]["config2_filter_iter"]
+    x = port.fill(d["universes"], d["seed"])
+    for name, t in d["targets"].items():
+        w, u = (np.array([int(v, 16) for v in t[k]], dtype=np.uint64) for k in ("wanted", "unwanted"))
+        care = w | u
+        gens = sorted(int(g) for g in t["gens"])
+        first, s = np.zeros(len(x), np.uint32), x
+        for g in range(1, gens[-1] + 1):
+            s = port.step_batch(s, 1, nthreads=8)
+            hit = (((s ^ w) & care) == 0).all(axis=1)
+            first[(first == 0) & hit] = g
+            if str(g) in t["gens"]:
+                got = np.where(first <= g, first, 0).astype(np.uint64)
+                want = t["gens"][str(g)]
+                assert int((got > 0).sum()) == want["hits"], (name, g)
+                assert f"{port.digest(got):016x}" == want["first_digest"], (name, g)
