@@ -321,7 +321,16 @@ __device__ __forceinline__ void win_gens(uint32_t (&r)[8], const uint32_t (&tw)[
 // of set s -- the window's first g1 columns dropped) and stepped the rest:
 // every later generation at half the issue slots.  The target is loaded
 // again in each layout (a cached 512-byte read) rather than held twice.
-template <int P, int R, bool WRAP, bool SHRINK, typename OutT>
+//
+// DMA (the whole board, P = 64 and R = 32: chunks of 8 universes = 4 KiB, a
+// 16-byte aligned batch): the chunks arrive by LDS-DMA into `stash`
+// (dma_fetch_pass), the next one fetched as soon as this one is read out, so
+// its loads run under this chunk's generations instead of stalling the wave
+// at every chunk's start.  1M universes, the one-row whole-board target
+// (row windows of 32 rows), same box: 8 / 13 generations 0.197 / 0.280 ->
+// 0.180 / 0.266 ms back to back; every other target within +-3 %
+// (profiles/r06/win_dma_ab/).
+template <int P, int R, bool WRAP, bool SHRINK, typename OutT, bool DMA = false>
 __device__ __forceinline__ void cone_wave_split(const uint64_t *in, const uint64_t *__restrict__ wanted,
                                                 const uint64_t *__restrict__ unwanted, OutT *__restrict__ out,
                                                 uint64_t n, uint64_t u_first, uint64_t u_step, uint32_t gens,
@@ -332,6 +341,7 @@ __device__ __forceinline__ void cone_wave_split(const uint64_t *in, const uint64
   constexpr int CH = SHRINK ? 2 * UPS : UPS;  // universes per chunk
   static_assert(CH <= kWave, "one answer per lane");
   static_assert(P >= 8 && P <= kWave && (!SHRINK || P >= 16), "8 .. 64 lanes per universe");
+  static_assert(!DMA || (P == kWave && R == 32 && !SHRINK), "the LDS-DMA form: whole columns, 8 universes");
   constexpr uint32_t rmask = R == 32 ? ~0u : 0xFFFFu;
   const uint32_t j = (uint32_t)lane & (P - 1), q = (uint32_t)lane / P;
   const uint32_t col = (xs + j) & (kWave - 1);
@@ -364,6 +374,28 @@ __device__ __forceinline__ void cone_wave_split(const uint64_t *in, const uint64
   };
   uint32_t tw[8], tm[8];
   if constexpr (!SHRINK) target(j, tw, tm);
+  if constexpr (DMA) {
+    uint64_t *const img = reinterpret_cast<uint64_t *>(stash);  // universe m of the chunk: img[m * 64 + column]
+    if (u_first < n) dma_fetch_pass<UPS>(in, n, u_first, lane, img);
+    int after = 0;  // vector-memory ops issued after the pending fetch (the chunk's answer store)
+    for (uint64_t u0 = u_first; u0 < n; u0 += u_step) {
+      if (after) __builtin_amdgcn_s_waitcnt(kWaitVm1);
+      else __builtin_amdgcn_s_waitcnt(kWaitVm0);
+      uint32_t e[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) e[u] = cut(img[u * kWave + lane]);  // (past n: universe n - 1 again)
+      __builtin_amdgcn_s_waitcnt(kWaitLgkm0);  // read out before the next fetch lands
+      if (u0 + u_step < n) dma_fetch_pass<UPS>(in, n, u0 + u_step, lane, img);
+      uint32_t r[8];
+      win_pack<R>(e, r);
+      uint32_t mine = 0;
+      uint64_t found = 0;
+      win_gens<P, R>(r, tw, tm, 0u, gens, mine, found, 0u, lane);
+      if (lane < UPS && u0 + (uint64_t)lane < n) out[u0 + lane] = (OutT)mine;
+      after = 1;  // (lane 0 stores: u0 < n)
+    }
+    return;
+  }
   // SHRINK: the generation after which the needed columns fit P / 2 lanes
   const uint32_t g1 = SHRINK ? (K - P / 2 + 1) / 2 : gens;
   for (uint64_t u0 = u_first; u0 < n; u0 += u_step) {
@@ -408,17 +440,20 @@ __device__ __forceinline__ void cone_split_pass(const uint64_t *in, const uint64
                                                 const uint64_t *__restrict__ unwanted, OutT *__restrict__ out,
                                                 uint64_t n, uint64_t wave, uint64_t nw, uint32_t gens, uint32_t xs,
                                                 uint32_t K, int pk, uint32_t y0, int lane,
-                                                uint32_t *stash = nullptr) {
-  auto run = [&](auto p_c, auto r_c, auto s_c) __attribute__((always_inline)) {
+                                                uint32_t *stash = nullptr, bool dma = false) {
+  auto run4 = [&](auto p_c, auto r_c, auto s_c, auto d_c) __attribute__((always_inline)) {
     constexpr int Pc = decltype(p_c)::value, Rc = decltype(r_c)::value;
-    constexpr bool Sc = decltype(s_c)::value;
+    constexpr bool Sc = decltype(s_c)::value, Dc = decltype(d_c)::value;
     constexpr uint64_t CH = (uint64_t)(kWave / Pc) * (256 / Rc) * (Sc ? 2 : 1);
     if (wave * CH >= n) return;
     if (y0 >= 32u)
-      cone_wave_split<Pc, Rc, true, Sc>(in, wanted, unwanted, out, n, wave * CH, nw * CH, gens, xs, K, y0, lane, stash);
+      cone_wave_split<Pc, Rc, true, Sc, OutT, Dc>(in, wanted, unwanted, out, n, wave * CH, nw * CH, gens, xs, K, y0,
+                                                  lane, stash);
     else
-      cone_wave_split<Pc, Rc, false, Sc>(in, wanted, unwanted, out, n, wave * CH, nw * CH, gens, xs, K, y0, lane, stash);
+      cone_wave_split<Pc, Rc, false, Sc, OutT, Dc>(in, wanted, unwanted, out, n, wave * CH, nw * CH, gens, xs, K, y0,
+                                                   lane, stash);
   };
+  auto run = [&](auto p_c, auto r_c, auto s_c) __attribute__((always_inline)) { run4(p_c, r_c, s_c, std::false_type{}); };
   using I8 = std::integral_constant<int, 8>;
   using I16 = std::integral_constant<int, 16>;
   using I32 = std::integral_constant<int, 32>;
@@ -440,7 +475,14 @@ __device__ __forceinline__ void cone_split_pass(const uint64_t *in, const uint64
     if (K <= 8u) return run(I8{}, I32{}, F{});
     if (K <= 16u) return shrinks(16, 0) ? run(I16{}, I32{}, T{}) : run(I16{}, I32{}, F{});
     if (K <= 32u) return shrinks(32, 1) ? run(I32{}, I32{}, T{}) : run(I32{}, I32{}, F{});
-    return shrinks(64, 2) ? run(I64{}, I32{}, T{}) : run(I64{}, I32{}, F{});
+    if (shrinks(64, 2)) return run(I64{}, I32{}, T{});
+    // (dma: a 16-byte aligned batch with the stash; the whole board only,
+    // whose chunks are 4 KiB; LIFE_WIN_DMA=0 builds the A/B without it)
+#ifndef LIFE_WIN_DMA
+#define LIFE_WIN_DMA 1
+#endif
+    if (LIFE_WIN_DMA && dma && stash && K == (uint32_t)kWave) return run4(I64{}, I32{}, F{}, T{});
+    return run(I64{}, I32{}, F{});
   }
   if (K <= 16u) return run(I16{}, I16{}, F{});
   if (K <= 32u) return shrinks(32, 3) ? run(I32{}, I16{}, T{}) : run(I32{}, I16{}, F{});

@@ -176,7 +176,8 @@ int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
     // * care rows that fit 32 with the light cone (cone_rows): on a whole
     //   board below kConeWholeWinGens generations the packed LDS-DMA pass
     //   (cone_wave_rows_dma), else the window split layout (cone_split.hpp)
-    //   on the column window, on half the lanes once the cone's columns fit;
+    //   on the column window, on half the lanes once the cone's columns fit
+    //   (a whole board's chunks fetched by LDS-DMA);
     // * else a cone of <= 32 columns: the natural layout on the cone
     //   (cone_wave);
     // * else the 8-way row split with the test fused (the loop its row

@@ -841,7 +841,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) voi
           }
         }
         return cone_split_pass(in, wanted, unwanted, first, n, wave, nw, gens, xs, K, pk, y0w, lane,
-                               reinterpret_cast<uint32_t *>(wave_lds[wib]));
+                               reinterpret_cast<uint32_t *>(wave_lds[wib]), PF);
       }
     }
   }
