@@ -172,6 +172,37 @@ def test_reductions_on_8_byte_aligned_batches(hip, port, n):
         assert (to_host(out) == port.fill(n, 3, 77, mode)).all()
 
 
+@pytest.mark.parametrize("gens", [1, 2, 3, 5, 8, 13])
+def test_filter_on_8_byte_aligned_batches(hip, port, gens):
+    """The search filter without final states takes LDS-DMA forms on 16-byte
+    aligned batches (k_cone_adapt's DMA form at 1-2 generations, the merged
+    split kernel's prefetch and the whole-board window pass's DMA chunks
+    from 3) and 8-byte loads otherwise: a block + ring (column window, the
+    shrinking pass), a one-row whole board (row window) and a full-height
+    target (no window) on both alignments, ragged n, against the oracle"""
+    n = 1001
+    x = port.fill(n, seed=300 + gens) & port.fill(n, seed=400 + gens)
+    bw, bu = np.zeros(64, np.uint64), np.zeros(64, np.uint64)
+    bw[10] = bw[11] = np.uint64(3 << 40)
+    bu[9:13] = np.uint64(15 << 39)
+    bu &= ~bw
+    ru = np.zeros(64, np.uint64)
+    ru[0::3] = np.uint64(1 << 10)
+    fu = np.zeros(64, np.uint64)
+    for y in range(0, 64, 4):
+        fu[(3 * y) % 64] |= np.uint64(1 << y)
+    for w, u in ((bw, bu), (np.zeros(64, np.uint64), ru), (np.zeros(64, np.uint64), fu)):
+        res, s = np.zeros(n, np.uint32), x.copy()
+        for g in range(1, gens + 1):
+            s = port.step_batch(s, 1, nthreads=8)
+            hit = (((s ^ w) & (w | u)) == 0).all(axis=1)
+            res[(res == 0) & hit] = g
+        for d in (to_dev(x), _off8(x)):
+            first, _ = hip.step_contains(d, to_dev(w[None]), to_dev(u[None]), gens)
+            got = first.cpu().numpy().astype(np.uint32)
+            assert (got == res).all(), (gens, d.data_ptr() % 16, int(np.count_nonzero(u)), int((got != res).sum()))
+
+
 def test_step_contains(hip, port):
     # blinkers: contained every second generation
     b = np.zeros(64, np.uint64)
