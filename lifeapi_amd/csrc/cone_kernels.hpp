@@ -143,8 +143,7 @@ __device__ __forceinline__ void cone_wave_full_dma(const uint64_t *in, uint64_t 
 
 // (cone_wave_rows_dma: cone_split.hpp)
 
-// (cone_rows, kConeHintGens, kConeRowsWindowGens and the report word:
-// step_kernels.hpp)
+// (cone_rows and kConeRowsWindowGens: step_kernels.hpp)
 
 // UPW universes per wave (one-shot grid of ceil(n / UPW) waves), every wave
 // choosing its lane layout from the window (wave-uniform: the target is the
@@ -196,18 +195,10 @@ __global__ __launch_bounds__(kBlock) void k_cone(const uint64_t *in, const uint6
 template <int RMAX, bool FIRST, typename OutT, bool A16 = false, bool DMA = false, bool ROWS = true, bool WIN = false>
 __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const uint64_t *__restrict__ wanted,
                                                        const uint64_t *__restrict__ unwanted, OutT *__restrict__ out,
-                                                       uint64_t n, uint32_t gens, uint32_t kmax, uint32_t cap_waves,
-                                                       int32_t *cls, int32_t cls_last) {
+                                                       uint64_t n, uint32_t gens, uint32_t kmax, uint32_t cap_waves) {
   const int lane = threadIdx.x & (kWave - 1);
   const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
-  // the first wave reports the window K to the host (host.hpp cone_class_slot)
-  // when it differs from what the host last read there: a write to host
-  // memory holds the launch's end by a PCIe round trip, so a target that
-  // keeps its window costs it once
-  auto report = [&](int32_t word) __attribute__((always_inline)) {
-    if (cls && wave == 0 && lane == 0 && word != cls_last) *reinterpret_cast<volatile int32_t *>(cls) = word;
-  };
   // (the smallest chunk any path takes: a wave starting past n has no work)
   // (WIN: the window split layout's sets are as small as 8 universes, 64
   // lanes x 32 rows)
@@ -224,49 +215,16 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
     __shared__ uint64_t img_all[kWavesPerBlock][RMAX * kWave];
     uint64_t *img = img_all[__builtin_amdgcn_readfirstlane(threadIdx.x / kWave)];
     const uint64_t c = 2 * RMAX;
-    // the last launch on this target reported a whole board: the wave's first
-    // pass is fetched before the window tests, which then run under it (a
-    // wave that turns out not to need it waits for it before leaving: LDS-DMA
-    // still in flight must not outlive the wave's LDS)
-    // (WIN: a whole board whose report carries a row class from
-    // kConeRowsWindowGens generations on takes the split window, which loads
-    // by itself)
-    const bool win_hint = WIN && FIRST && gens >= kConeWholeWinGens && ((cls_last >> 8) & 0xFF) != 0;
-    const bool early = (cls_last & 0xFF) == kReportWhole && !win_hint && wave * c < n;
-    if (early) dma_fetch_pass<RMAX>(in, n, wave * c, lane, img);
-    auto leave = [&]() __attribute__((always_inline)) {
-      if (early) __builtin_amdgcn_s_waitcnt(kWaitVm0);
-    };
-    // the row window: from kConeHintGens generations on, every wave but the
-    // first takes the one the last report on this target gave, once one
-    // ballot shows the care rows inside its exact interior (the row-window
-    // pass is exact for any columns, so the whole-board test is not needed
-    // then); the first wave, and every wave without such a report, find it
-    // themselves
+    // (round 5 fetched a whole board's first pass before these tests when the
+    // last launch on the same target pointers had reported one; round 6 reads
+    // no report)
     int pk = 0;
     uint32_t y0 = 0;
-    bool whole = false, hinted = false;
-    if constexpr (FIRST && ROWS) {
-      const int hpk = (cls_last >> 8) & 0xFF;
-      if (wave != 0 && gens >= kConeHintGens && report_whole(cls_last) && hpk && gens < 16u &&
-          2u * gens < 32u / (uint32_t)hpk) {
-        const uint32_t hy0 = ((uint32_t)cls_last >> 16) & 63u, inner_w = 32u / (uint32_t)hpk - 2u * gens;
-        const uint64_t inner = rotr64((1ull << inner_w) - 1ull, (64u - ((hy0 + gens) & 63u)) & 63u);
-        if (__ballot((care_col & ~inner) != 0ull) == 0ull) pk = hpk, y0 = hy0, whole = hinted = true;
-      }
-    }
-    if (!hinted) {
-      whole = cone_whole(care_col, g);
-      if (whole) {
-        if constexpr (FIRST) pk = cone_rows(care_col, gens, y0);
-        report(report_word(kWave, pk, y0));
-      }
-    }
-    if (whole) {
-      if (kmax < (uint32_t)kWave) return leave();
+    if (cone_whole(care_col, g)) {
+      if constexpr (FIRST) pk = cone_rows(care_col, gens, y0);
+      if (kmax < (uint32_t)kWave) return;
       if constexpr (FIRST && WIN) {
         if (pk > 0 && gens >= kConeWholeWinGens) {  // (its sets may be 8 universes: before the chunk test)
-          leave();
           if (cap_waves) {
             if (wave >= cap_waves) return;
             nw = nw < cap_waves ? nw : cap_waves;
@@ -274,11 +232,11 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
           return split_pass(pk, y0, nw);
         }
       }
-      if (wave * c >= n) return leave();
+      if (wave * c >= n) return;
       if constexpr (FIRST && ROWS) {
         auto rows = [&](auto pk_c, auto wrap_c) __attribute__((always_inline)) {
           cone_wave_rows_dma<RMAX, decltype(pk_c)::value, decltype(wrap_c)::value>(
-              in, w64, m64, out, n, wave * c, nw * c, gens, y0, lane, img, early);
+              in, w64, m64, out, n, wave * c, nw * c, gens, y0, lane, img, false);
         };
         using T = std::true_type;
         using F = std::false_type;
@@ -289,27 +247,18 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
         if (pk == 2) return y0 >= 32u ? rows(P2{}, T{}) : rows(P2{}, F{});
         if (pk == 1) return y0 >= 32u ? rows(P1{}, T{}) : rows(P1{}, F{});
       }
-      return cone_wave_full_dma<RMAX, FIRST>(in, w64, m64, out, n, wave * c, nw * c, gens, lane, img, early);
+      return cone_wave_full_dma<RMAX, FIRST>(in, w64, m64, out, n, wave * c, nw * c, gens, lane, img, false);
     }
     if (cap_waves) {
-      if (wave >= cap_waves) return leave();
+      if (wave >= cap_waves) return;
       nw = nw < cap_waves ? nw : cap_waves;
     }
     cone_window(care_col, g, xs, K);
-    {
-      int wpk = 0;
-      uint32_t wy0 = 0;
-      if constexpr (FIRST) {
-        if (cls && wave == 0) wpk = cone_rows(care_col, gens, wy0);  // (only the report needs it)
-      }
-      report(report_word(K, wpk, wy0));
-    }
-    if (K > kmax) return leave();
+    if (K > kmax) return;
     if (K == (uint32_t)kWave) {
-      if (wave * c >= n) return leave();
-      return cone_wave_full_dma<RMAX, FIRST>(in, w64, m64, out, n, wave * c, nw * c, gens, lane, img, early);
+      if (wave * c >= n) return;
+      return cone_wave_full_dma<RMAX, FIRST>(in, w64, m64, out, n, wave * c, nw * c, gens, lane, img, false);
     }
-    leave();
   } else {
     int pk = 0;
     uint32_t y0 = 0;
@@ -317,12 +266,11 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
       cone_window(care_col, g, xs, K);
       // (the row window of a column window: cone_wave_rows, below)
       if constexpr (FIRST && ROWS) {
-        if (gens >= kConeRowsWindowGens || (cls && wave == 0)) pk = cone_rows(care_col, gens, y0);
+        if (gens >= kConeRowsWindowGens) pk = cone_rows(care_col, gens, y0);
       }
-    } else if constexpr (FIRST) {
-      if ((ROWS && gens >= kConeRowsWindowGens) || (cls && wave == 0)) pk = cone_rows(care_col, gens, y0);
+    } else if constexpr (FIRST && ROWS) {
+      if (gens >= kConeRowsWindowGens) pk = cone_rows(care_col, gens, y0);
     }
-    report(report_word(K, pk, y0));
     if (K > kmax) return;
     if constexpr (FIRST && ROWS) {
       // a column window of more than 4 columns (the whole board too, in this
@@ -395,31 +343,17 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
 // profiles/r04/r04g/cone_grid_ab.jsonl), 16 per wave best for 14-30 columns.
 constexpr int kConeSets = 8;
 constexpr int kConeAdaptBlocksPerCU = 16;
-// The search filter without final states takes k_cone_adapt alone up to
-// this many generations (step.hip); beyond, the split-layout pair.  Batches
-// of at most kConeAloneSmallUniverses take it up to kConeAloneGensSmall:
-// same process (tools/ab/search_iter_caps_ab.py, profiles/r04/r04an), at 5-6
-// generations k_cone_adapt / split pair = 0.65-0.94 on a 4-column and a
-// whole-board target at 64K-128K, 0.83-1.02 at 256K, but 1.07-1.14 on the
-// whole board at 512K.
-constexpr uint32_t kConeAloneGens = 4, kConeAloneGensSmall = 6;  // (round 5's routing; the tuning build's A/Bs)
+// (Round 5 routed the filter without final states by the generation count,
+// the batch size and the last launch report: k_cone_adapt alone up to 4
+// generations (6 for batches of at most 256K), the row-window passes up to
+// 15, the split pair beyond; its constants and measurements are in the git
+// history and DESIGN.md 3.2.)
 // Round 6: the merged split kernel (step.hip, 3+ generations without final
 // states) on a grid of at most this many blocks per CU looping over the
 // batch (1M universes: 16 and 32 within 1-3 % of each other on every
 // target, 8 up to 9 % slower on the one-row whole board; profiles/r06/ab/)
 constexpr int kFilterIterBlocksPerCU = 16;
 // (kConeWholeWinGens: step_kernels.hpp)
-// Beyond those, up to this many generations (exclusive), a whole-board target
-// whose row window fits 32 rows (cone_rows) keeps k_cone_adapt (step.hip).
-constexpr uint32_t kConeRowsMaxGens = 16;
-// ... and so does a column window of 5-63 columns whose rows fit
-// (cone_wave_rows, the capped form): 1M universes, bench.py's block target
-// (4 x 4) at 5 / 8 / 13 generations 0.060 / 0.151 / 0.225 ms against 0.096 /
-// 0.231 / 0.363 on the split pair, 40 x 3 columns at 5 / 8 0.159 / 0.228
-// against 0.229 / 0.300 (tools/filter_gens_ab.py,
-// profiles/r05/gens/gens_ab_window_rows.jsonl).
-constexpr bool kConeRowsWindowRoute = true;
-constexpr uint64_t kConeAloneSmallUniverses = 1u << 18;
 // The iterated search loop (gens > 2, no final states) steps the light cone
 // while it spans at most this many columns (P <= 32 lanes per universe: at
 // most half the natural layout's work per universe-generation, against the
@@ -434,8 +368,8 @@ static_assert(kConeIterColumns <= 32, "kContainsLo's cone passes take P <= 32");
 // idles, and the working one is faster capped from 256K universes on.
 constexpr int kSplitIterBlocksPerCU = 32;
 // The tuning build's separate-launch form of the same (k_cone before the
-// pair): 8 universes per wave, at most 16 blocks per CU.
-constexpr int kConeIterUniverses = 8, kConeIterBlocksPerCU = 16;
+// pair): 8 universes per wave.
+constexpr int kConeIterUniverses = 8;
 
 // Launches k_cone on a one-shot grid.
 template <int UPW, int RMAX, bool FIRST, typename OutT, bool PIPE = false>
@@ -460,22 +394,18 @@ int launch_cone(const uint64_t *d_in, const uint64_t *d_wanted, const uint64_t *
 // per CU (0: no cap).  DMA: a whole-board window takes cone_wave_full_dma
 // when the batch is 16-byte aligned, on a grid of at most dma_blocks_per_cu
 // blocks per CU (0: uncapped; blocks_per_cu then caps the waves of a
-// windowed target).  hint_k: the tuning build's stand-in for round 5's
-// launch report (the last launch's window word: a whole board fetches its
-// first pass before the window tests; -1 none).
+// windowed target).
 template <int RMAX, bool FIRST, typename OutT, bool DMA = false, bool ROWS = true, bool WIN = false>
 int launch_cone_adapt(const uint64_t *d_in, const uint64_t *d_wanted, const uint64_t *d_unwanted, OutT *d_out,
                       size_t n, uint32_t gens, int cus, hipStream_t stream, int blocks_per_cu,
-                      uint32_t kmax = kWave, int dma_blocks_per_cu = 0, int hint_k = -1) {
+                      uint32_t kmax = kWave, int dma_blocks_per_cu = 0) {
   const dim3 grid(grid_for((n + 15) / 16, cus, blocks_per_cu));
-  int32_t *const cls = nullptr;
-  const int last_k = hint_k;
   if constexpr (DMA) {
     if (aligned16(d_in)) {
       const uint32_t cap_waves = blocks_per_cu > 0 ? (uint32_t)(cus * blocks_per_cu * kWavesPerBlock) : 0u;
       hipLaunchKernelGGL((k_cone_adapt<RMAX, FIRST, OutT, true, true, ROWS, WIN>),
                          dim3(grid_for((n + 15) / 16, cus, dma_blocks_per_cu)), dim3(kBlock), 0, stream, d_in,
-                         d_wanted, d_unwanted, d_out, (uint64_t)n, gens, kmax, cap_waves, cls, (int32_t)last_k);
+                         d_wanted, d_unwanted, d_out, (uint64_t)n, gens, kmax, cap_waves);
       return launched("k_cone_adapt launch");
     }
   }
@@ -484,12 +414,12 @@ int launch_cone_adapt(const uint64_t *d_in, const uint64_t *d_wanted, const uint
   if (a16) {
     if constexpr (!FIRST) {
       hipLaunchKernelGGL((k_cone_adapt<RMAX, FIRST, OutT, true, false, ROWS, WIN>), grid, dim3(kBlock), 0, stream, d_in,
-                         d_wanted, d_unwanted, d_out, (uint64_t)n, gens, kmax, 0u, cls, (int32_t)last_k);
+                         d_wanted, d_unwanted, d_out, (uint64_t)n, gens, kmax, 0u);
       return launched("k_cone_adapt launch");
     }
   }
   hipLaunchKernelGGL((k_cone_adapt<RMAX, FIRST, OutT, false, false, ROWS, WIN>), grid, dim3(kBlock), 0, stream, d_in,
-                     d_wanted, d_unwanted, d_out, (uint64_t)n, gens, kmax, 0u, cls, (int32_t)last_k);
+                     d_wanted, d_unwanted, d_out, (uint64_t)n, gens, kmax, 0u);
   return launched("k_cone_adapt launch");
 }
 

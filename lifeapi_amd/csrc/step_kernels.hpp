@@ -560,35 +560,16 @@ __device__ __forceinline__ int cone_rows(uint64_t care_col, uint32_t gens, uint3
   return need <= 8u ? 4 : need <= 16u ? 2 : need <= 32u ? 1 : 0;
 }
 
-// Waves after the first take the row window from the last report from this
-// many generations on.  1M universes, bench.py's whole-board target, each
-// launch alone after a scrub, interleaved with the same launch finding the
-// window itself (tools/filter_interleave.py rows_hint / rows_early,
-// profiles/r05/hint/): 3 / 4 / 5 / 8 generations 0.081 / 0.096 / 0.109 /
-// 0.188 ms against 0.095 / 0.108 / 0.122 / 0.194; at 1 generation no
-// difference (0.083-0.085 both), at 2 it costs 4 % (0.086 against 0.082,
-// unexplained; every series on the box agreed).
-constexpr uint32_t kConeHintGens = 3;
 // A column window (5-32 columns) takes the row window too from this many
 // generations on (cone_wave_rows; below it the pass is not VALU-bound).
 constexpr uint32_t kConeRowsWindowGens = 3;
-// A whole board whose report carries a row window takes k_cone_adapt's
-// LDS-DMA packed form (cone_wave_rows_dma) below this many generations, the
+// A whole board whose care rows fit a row window takes the LDS-DMA packed
+// form (cone_wave_rows_dma) below this many generations, the
 // window split layout (cone_split.hpp) from it on (one-row target, 1M
 // universes: 3 / 5 generations 0.080 / 0.116 ms against 0.102 / 0.113 for
 // the split window; 8 / 13: 0.203 / 0.289 against 0.199 / 0.279;
 // profiles/r06/ab/)
 constexpr uint32_t kConeWholeWinGens = 8;
-
-// Round 5's launch report word for a target (the tuning build's hint_k): the
-// window K (64: the whole board) in bits 0-7, and for a whole board the
-// row-window class (cone_rows: 4, 2, 1 universes per register, 0 none) in
-// bits 8-15 and its first row y0 in bits 16-21.
-constexpr int32_t kReportWhole = kWave;
-__device__ __forceinline__ bool report_whole(int32_t word) { return (word & 0xFF) == kReportWhole; }
-__device__ __forceinline__ int32_t report_word(uint32_t K, int pk, uint32_t y0 = 0) {
-  return (int32_t)K | (pk << 8) | (pk ? (int32_t)(y0 & 63u) << 16 : 0);
-}
 
 // The light-cone pass (cone_kernels.hpp; here for the iterated search
 // loop's low-layout kernel, below).  One wave's chunks of UPW universes u0 .. u0 + UPW - 1, u0 = u_first,

@@ -4,15 +4,10 @@ whole-board target (golden.json digests.config2_filter: row 10 of every third
 column) at 1, 2 and 4 generations.  Per rep, every form in turn: a 768 MiB
 scrub (bench.Scrub), then the launch alone between a pair of events; the
 forms alternate launch by launch, so that a clock or fabric state that drifts
-over a series falls on all of them alike.  Forms: shipped
-(launch form by the target's last report: the LDS form, packed row window),
+over a series falls on all of them alike.  Forms: shipped,
 rows / norows (tuning build cone shapes upw 1 / 2: the LDS form with and
 without the packed row-window pass), rows_capC (upw 3: rows on a grid of at
-most C blocks per CU looping over the batch), rows_early (upw 4: rows with
-the first pass fetched before the window tests, as the shipped launch does
-after a whole-board report), rows_hint (upw 5: rows_early given the report
-word the shipped launch gets, so that all waves but the first take the row
-window from it after one ballot), probe_sS (with PROBE=1: the pass with no
+most C blocks per CU looping over the batch), probe_sS (with PROBE=1: the pass with no
 window search and s_sleep(S) after each next-pass fetch, tune_cone.hip
 k_rows_probe), capped (upw 0, 16 blocks per CU), and
 Contains (shipped, and the LDS form).  One JSON line per generation count:
@@ -65,17 +60,10 @@ def main():
             u[0::3] = np.uint64(1) << np.uint64(row10)
             tw.zero_()
             tu.copy_(torch.from_numpy(u.view(np.int64)[None].copy()))
-        # the report word the shipped launch passes back after its first call
-        # (cone_kernels.hpp report_word): the care row r widened by gens
-        r = 10 if row10 is None else row10
-        need = 1 + 2 * gens
-        pk = 4 if need <= 8 else 2 if need <= 16 else 1 if need <= 32 else 0
-        hint = 64 | (pk << 8) | ((((r - gens) & 63) << 16) if pk else 0)
+        r = 10 if row10 is None else row10  # the care row (the probe's window starts gens above it)
         forms = {
             "shipped": lambda: hip.step_contains(x, tw, tu, gens)[0],
             "rows": lambda: tune.cone(x, tw, tu, gens, 1, 8, first=True),
-            "rows_early": lambda: tune.cone(x, tw, tu, gens, 4, 8, first=True),
-            "rows_hint": lambda: tune.cone(x, tw, tu, gens, 5, 8 | (hint << 8), first=True),
             "rows_cap16": lambda: tune.cone(x, tw, tu, gens, 16003, 8, first=True),
             "norows": lambda: tune.cone(x, tw, tu, gens, 2, 8, first=True),
             "capped": lambda: tune.cone(x, tw, tu, gens, 16000, 8, first=True),

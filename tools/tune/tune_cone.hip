@@ -23,22 +23,13 @@ int cone_by_shape(const uint64_t *in, const uint64_t *w, const uint64_t *u, OutT
   // upw 3: upw 1 with the whole-board grid capped at `cap` blocks per CU
   if (upw == 3 && rmax == 8)
     return launch_cone_adapt<8, FIRST, OutT, true>(in, w, u, out, n, gens, cus, st, 0, kWave, cap);
-  // upw 4: upw 1 told that the target is a whole board (the first pass fetched before the window tests)
-  if (upw == 4 && rmax == 8)
-    return launch_cone_adapt<8, FIRST, OutT, true>(in, w, u, out, n, gens, cus, st, cap, kWave, 0, kWave);
-  // upw 5: upw 4 with rmax >> 8 as the last report word (the row-window hint: K | class << 8 | y0 << 16)
-  if (upw == 5 && (rmax & 0xFF) == 8)
-    return launch_cone_adapt<8, FIRST, OutT, true>(in, w, u, out, n, gens, cus, st, cap, kWave, 0, rmax >> 8);
+  // (upw 4, 5, 9: round 5's forms told the last launch report; removed with it)
   // upw 7: upw 0 (the capped form) without the row-window passes
   if (upw == 7 && rmax == 8)
     return launch_cone_adapt<8, FIRST, OutT, false, false>(in, w, u, out, n, gens, cus, st, cap);
   // upw 8: upw 0 (the capped form) with the window split layout (cone_split.hpp) for row windows
   if (upw == 8 && rmax == 8)
     return launch_cone_adapt<8, FIRST, OutT, false, true, true>(in, w, u, out, n, gens, cus, st, cap);
-  // upw 9: upw 5 (the whole-board LDS form told its report, rmax >> 8) with the window split layout
-  if (upw == 9 && (rmax & 0xFF) == 8)
-    return launch_cone_adapt<8, FIRST, OutT, true, true, true>(in, w, u, out, n, gens, cus, st, cap, kWave, 0,
-                                                                      rmax >> 8);
   // upw 2: upw 1 without the packed row-window pass (cone_wave_rows_dma): every whole-board target full
   if (upw == 2 && rmax == 8)
     return launch_cone_adapt<8, FIRST, OutT, true, false>(in, w, u, out, n, gens, cus, st, cap);
