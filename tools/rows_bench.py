@@ -7,7 +7,7 @@ events around the launch only, median of 10.
 
 The LifeStable passes write back only the lines they change,
 so their rows are priced on the bytes each pass really moves, measured by
-PMC on the same inputs (profiles/r05/pmc_rows.json, tools/pmc_rows.py:
+PMC on the same inputs (profiles/r06/pmc_rows.json, tools/pmc_rows.py:
 FETCH_SIZE x 2 + WRITE_SIZE per LifeStable), and carry the VALU side beside
 it: SQ_INSTS_VALU per LifeStable / (1024 SIMDs x one wave64 instruction per
 2 clocks at 2.4 GHz = 1.2288e12 per second).  `bound_frac` = max(bytes time,
@@ -60,8 +60,8 @@ def scrubbed(fn, prep=None):
 
 PEAK = 8000.0  # GB/s
 VALU_PEAK = 1024 * 2.4e9 / 2  # wave64 VALU instructions per second (MI355X_MICROARCH.md: 2 clocks each)
-PMC_ROWS = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "r05",
-                        "pmc_rows.json")
+PMC_ROWS = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "r06",
+                        "pmc_rows.json")  # (tools/gpu_r05_pmc.sh on round 6's kernels)
 
 
 def pmc_row(name):
@@ -73,7 +73,7 @@ def pmc_row(name):
         return None
     if not r:
         return None
-    return r["hbm_bytes_per_object"], r["valu_per_object"], "profiles/r05/pmc_rows.json"
+    return r["hbm_bytes_per_object"], r["valu_per_object"], "profiles/r06/pmc_rows.json"
 
 
 K = 10  # launches per timing, back to back (the bench's own way: launch gaps hidden by the queue)
