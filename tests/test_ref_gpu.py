@@ -424,3 +424,50 @@ def test_iterated_search_loop_short_targets_vs_reference(hip, R, port, w, h, gen
             got = first.cpu().numpy().astype(np.uint32)
             assert (got == exp_first).all(), (w, h, gens, x0, y0, call, np.nonzero(got != exp_first)[0][:8])
         assert 1 <= exp_first[0] <= gens
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_filter_fuzz_vs_reference(hip, R, port, seed):
+    """The search filter (first hits only) on 40 random targets per seed
+    against the reference's own Step() + Contains loop: 1-15 generations;
+    targets of one to five boxes (1-20 columns x 1-24 rows each, anywhere,
+    across both seams), sometimes a row band over every column, sometimes
+    wanted cells only or unwanted only; each target cut from a universe of
+    the batch a few generations ahead, so that hits occur; ragged batches
+    on both alignments.  Every pass the one launch picks (natural cone,
+    window split with and without shrinking, whole-board rows, LDS-DMA
+    chunks, 8-way split) meets targets of its class here."""
+    rng = np.random.default_rng(7000 + seed)
+    for t in range(40):
+        n = int(rng.integers(60, 700))
+        x = port.fill(n, seed=int(rng.integers(1 << 30))) & port.fill(n, seed=int(rng.integers(1 << 30)))
+        gens = int(rng.integers(1, 16))
+        box = np.zeros(64, np.uint64)
+        if rng.random() < 0.2:  # a band of rows over every column (a whole-board target)
+            y0, h = int(rng.integers(64)), int(rng.integers(1, 6))
+            box[:] = np.uint64(sum(1 << ((y0 + i) % 64) for i in range(h)))
+            box[rng.random(64) < 0.5] = 0
+        else:
+            for _ in range(int(rng.integers(1, 6))):
+                x0, w = int(rng.integers(64)), int(rng.integers(1, 21))
+                y0, h = int(rng.integers(64)), int(rng.integers(1, 25))
+                rows = np.uint64(sum(1 << ((y0 + i) % 64) for i in range(h)))
+                for c in range(w):
+                    box[(x0 + c) % 64] |= rows
+        src = int(rng.integers(n))
+        ahead = port.step_batch(x[src:src + 1], int(rng.integers(1, gens + 1)))[0]
+        tw, tu = ahead & box, box & ~ahead
+        kind = rng.random()
+        if kind < 0.1:
+            tu[:] = 0
+        elif kind < 0.2:
+            tw[:] = 0
+        exp, _ = R.step_contains_batch(x, tw, tu, gens, nthreads=THREADS)
+        for d in (to_dev(x), None):
+            if d is None:  # 8-byte aligned only
+                t8 = torch.zeros(x.size + 1, dtype=torch.int64, device="cuda")
+                d = t8[1:].view(n, 64)
+                d.copy_(to_dev(x))
+            first, _ = hip.step_contains(d, to_dev(tw[None]), to_dev(tu[None]), gens)
+            got = first.cpu().numpy().astype(np.uint32)
+            assert (got == exp).all(), (seed, t, gens, n, d.data_ptr() % 16, np.nonzero(got != exp)[0][:8])
