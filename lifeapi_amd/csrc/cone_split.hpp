@@ -39,11 +39,28 @@
 // batch.  A universe is clean at a generation iff its bit is 0 in the
 // group's word; hits (rare) take a scalar slow path that records the first
 // clean generation of every universe not yet found.
+//
+// Round 6 additions (cone_wave_split): the shrinking pass (two register sets
+// merged onto half the lanes once the cone's columns fit them) and, on a
+// whole board, chunks fetched by LDS-DMA while the last one steps.
 #pragma once
 
 #include <type_traits>
 
 #include "device.hpp"
+
+// A/B switches of the round-6 forms (the tuning probes' builds without them):
+// LIFE_SHRINK_MASK bit i enables the i-th shrinking form of cone_split_pass
+// (0: none; 1M universes, 4 x 4 block, alone: 8 / 13 generations 0.097 /
+// 0.137 ms against 0.110 / 0.153, other targets within +-3 %,
+// profiles/r06/shrink_ab/, tools/gpu_r06f.sh); LIFE_WIN_DMA=0 builds the
+// whole-board window pass without its LDS-DMA chunks (tools/gpu_r06h.sh).
+#ifndef LIFE_SHRINK_MASK
+#define LIFE_SHRINK_MASK 31
+#endif
+#ifndef LIFE_WIN_DMA
+#define LIFE_WIN_DMA 1
+#endif
 
 namespace lifeapi_impl {
 namespace {
@@ -453,7 +470,9 @@ __device__ __forceinline__ void cone_split_pass(const uint64_t *in, const uint64
       cone_wave_split<Pc, Rc, false, Sc, OutT, Dc>(in, wanted, unwanted, out, n, wave * CH, nw * CH, gens, xs, K, y0,
                                                    lane, stash);
   };
-  auto run = [&](auto p_c, auto r_c, auto s_c) __attribute__((always_inline)) { run4(p_c, r_c, s_c, std::false_type{}); };
+  auto run = [&](auto p_c, auto r_c, auto s_c) __attribute__((always_inline)) {
+    run4(p_c, r_c, s_c, std::false_type{});
+  };
   using I8 = std::integral_constant<int, 8>;
   using I16 = std::integral_constant<int, 16>;
   using I32 = std::integral_constant<int, 32>;
@@ -463,24 +482,16 @@ __device__ __forceinline__ void cone_split_pass(const uint64_t *in, const uint64
   // the columns fit half the lanes before the last generation: K - 2 g1 <=
   // P / 2 with g1 < gens (and 2 UPS answers fit the wave's 64 lanes); a
   // caller without a stash never shrinks
-    // (LIFE_SHRINK_MASK: bit i enables the i-th shrinking form below; the A/B
-  // build without any, tools/gpu_r06f.sh, compiles with 0.  1M universes,
-  // 4 x 4 block, alone: 8 / 13 generations 0.097 / 0.137 ms against 0.110 /
-  // 0.153; other targets within +-3 %, profiles/r06/shrink_ab/)
-#ifndef LIFE_SHRINK_MASK
-#define LIFE_SHRINK_MASK 31
-#endif
-  auto shrinks = [&](uint32_t P, int bit) { return ((LIFE_SHRINK_MASK >> bit) & 1) && stash && K > P / 2 && (K - P / 2 + 1) / 2 < gens; };
+  auto shrinks = [&](uint32_t P, int bit) {
+    return ((LIFE_SHRINK_MASK >> bit) & 1) && stash && K > P / 2 && (K - P / 2 + 1) / 2 < gens;
+  };
   if (pk == 1) {
     if (K <= 8u) return run(I8{}, I32{}, F{});
     if (K <= 16u) return shrinks(16, 0) ? run(I16{}, I32{}, T{}) : run(I16{}, I32{}, F{});
     if (K <= 32u) return shrinks(32, 1) ? run(I32{}, I32{}, T{}) : run(I32{}, I32{}, F{});
     if (shrinks(64, 2)) return run(I64{}, I32{}, T{});
     // (dma: a 16-byte aligned batch with the stash; the whole board only,
-    // whose chunks are 4 KiB; LIFE_WIN_DMA=0 builds the A/B without it)
-#ifndef LIFE_WIN_DMA
-#define LIFE_WIN_DMA 1
-#endif
+    // whose chunks are 4 KiB)
     if (LIFE_WIN_DMA && dma && stash && K == (uint32_t)kWave) return run4(I64{}, I32{}, F{}, T{});
     return run(I64{}, I32{}, F{});
   }
