@@ -88,10 +88,13 @@ int lifeapi_contains_batch_dev(const uint64_t *d_states, const uint64_t *d_wante
                                const uint64_t *d_unwanted, uint8_t *d_out, size_t n,
                                void *stream);
 /* fused Step^gens + Contains: d_out[u] = first generation g in 1..gens at
- * which Stepped(g) contains the target, or 0 if none; d_final (may be NULL)
- * receives Stepped(gens).  With d_final NULL (the search filter) only the
- * columns within gens of the target's care columns are read and stepped
- * when gens <= 4, or when those columns number at most 32.                */
+ * which Stepped(g) contains the target, or 0 if none (all 0 for gens = 0);
+ * d_final (may be NULL) receives Stepped(gens).  With d_final NULL (the
+ * search filter) only the target's light cone is read and stepped: at 1-2
+ * generations the columns within gens of its care columns, from 3 the
+ * columns of a cone of at most 32 columns and the rows of a cone that fits
+ * 32 rows; a target with neither is stepped whole.  Nothing is remembered
+ * between calls: the target buffers may be rewritten between them.         */
 int lifeapi_step_contains_batch_dev(const uint64_t *d_in, uint64_t *d_final,
                                     const uint64_t *d_wanted, const uint64_t *d_unwanted,
                                     uint32_t *d_first_gen, size_t n, uint32_t generations,

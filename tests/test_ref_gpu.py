@@ -471,3 +471,23 @@ def test_filter_fuzz_vs_reference(hip, R, port, seed):
             first, _ = hip.step_contains(d, to_dev(tw[None]), to_dev(tu[None]), gens)
             got = first.cpu().numpy().astype(np.uint32)
             assert (got == exp).all(), (seed, t, gens, n, d.data_ptr() % 16, np.nonzero(got != exp)[0][:8])
+
+
+def test_filter_zero_generations_vs_reference(hip, R, port):
+    """generations = 0: the loop `for g in 1..gens` never runs -- every answer
+    0 and d_final = Stepped(0) = the input, in every launch form (the cone
+    kernel without final states, the streaming filter with them), whatever the
+    target (one contained by every universe included)"""
+    n = 333
+    x = port.fill(n, seed=55)
+    targets = [(np.zeros(64, np.uint64), np.zeros(64, np.uint64)),  # the empty target: contained by all
+               (x[0].copy(), np.zeros(64, np.uint64))]
+    for w, u in targets:
+        exp_first, exp_fin = R.step_contains_batch(x, w, u, 0)
+        assert not exp_first.any()
+        first, _ = hip.step_contains(to_dev(x), to_dev(w[None]), to_dev(u[None]), 0)
+        assert not first.cpu().numpy().any()
+        fin = torch.empty((n, 64), dtype=torch.int64, device="cuda")
+        first, _ = hip.step_contains(to_dev(x), to_dev(w[None]), to_dev(u[None]), 0, final=fin)
+        assert not first.cpu().numpy().any()
+        _check(to_host(fin), exp_fin, "Stepped(0)")
