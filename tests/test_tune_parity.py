@@ -291,3 +291,21 @@ def test_cone_full_dma_ragged(tune, port, rmax, n):
                 want[(want == 0) & hit] = g
             got = tune.cone(d, to_dev(tw[None]), to_dev(tu[None]), gens, 1, rmax).cpu().numpy()
         assert (got.astype(want.dtype) == want).all(), (gens, np.nonzero(got != want)[0][:8])
+
+
+# k_stable's measured alternatives (stable_kernels.hpp): StabiliseOptions with
+# every round on the whole columns / the later rounds on the 32-row window
+# (tuning passes 6 / 7), Propagate whole / windowed (14 / 15, the product
+# ships 15's form) and windowed with plane-selective stores (40)
+@pytest.mark.parametrize("which,pname", [(6, "stabilise"), (7, "stabilise"), (14, "propagate"), (15, "propagate"),
+                                         (40, "propagate")])
+@pytest.mark.parametrize("n", [5, 20003])
+def test_stable_window_forms(tune, hip, port, which, pname, n):
+    from test_gpu_parity import _stable_cases
+    x = _stable_cases(port, n, seed=23 + n % 7)
+    w = hip.STABLE_PASSES.index(pname)
+    want, wfl = port.stable_pass(x, w)
+    d = to_dev(x).reshape(n, 640)
+    fl = tune.stable_pass(d, which, 0, xcd_chunk=True).cpu().numpy()
+    assert (to_host(d).reshape(n, 640) == want).all(), (which, pname)
+    assert (fl == wfl).all(), (which, pname)

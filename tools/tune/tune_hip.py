@@ -118,15 +118,17 @@ lib.lifeapi_tune_stable_vulnerable.restype = _int
 
 
 def stable_pass(planes: torch.Tensor, which: int, blocks_per_cu: int, max_iters: int = 0, stream=None,
-                reverse: bool = False, xcd_chunk: bool = False, store_all: bool = False, upw: int = 0):
+                reverse: bool = False, xcd_chunk: bool = False, store_all: bool = False, upw: int = 0,
+                no_store: bool = False):
     """store_all: every line stored (round 3's k_stable), else only the lines
-    holding a changed column (the shipped form)"""
+    holding a changed column (the shipped form); no_store (k_stable only): no
+    plane stored -- a timing probe, the planes are left wrong"""
     n = planes.numel() // (10 * 64)
     flags = torch.empty(n, dtype=torch.uint8, device=planes.device)
     hip._check(lib.lifeapi_tune_stable_pass(planes.data_ptr(), flags.data_ptr(), n, which, max_iters,
                                             blocks_per_cu, hip._stream(stream),
                                             (1 if reverse else 0) | (2 if xcd_chunk else 0) | (4 if store_all else 0)
-                                            | (upw << 8)))
+                                            | (8 if no_store else 0) | (upw << 8)))
     return flags
 
 
