@@ -296,11 +296,9 @@ def test_cone_full_dma_ragged(tune, port, rmax, n):
 # k_stable's measured alternatives (stable_kernels.hpp): StabiliseOptions with
 # every round on the whole columns / the later rounds on the 32-row window
 # (tuning passes 6 / 7), Propagate whole / windowed (14 / 15, the product
-# ships 15's form), windowed with plane-selective stores (40) and with the
-# first step's tests deferred (41: _stable_cases holds inconsistent objects,
-# so both its fast path and its restore-and-redo path run)
+# ships 15's form) and windowed with plane-selective stores (40)
 @pytest.mark.parametrize("which,pname", [(6, "stabilise"), (7, "stabilise"), (14, "propagate"), (15, "propagate"),
-                                         (40, "propagate"), (41, "propagate")])
+                                         (40, "propagate")])
 @pytest.mark.parametrize("n", [5, 20003])
 def test_stable_window_forms(tune, hip, port, which, pname, n):
     from test_gpu_parity import _stable_cases

@@ -3,8 +3,7 @@ windowed Propagate (tuning build k_stable<4, true>, pass 15) on a search's
 next node against the same launch storing no plane (mode bit 3: a timing
 probe whose planes are left wrong), the same storing a plane's dirty line
 only where that plane changed (pass 40, the unmodified object re-read at
-the end to compare), the same with the first step's tests deferred (pass
-41), and against SynchroniseStateKnown and
+the end to compare), and against SynchroniseStateKnown and
 SignalNeighbours on the same input (read-mostly passes).  1M LifeStables,
 each launch on its own fresh copy, back to back (4 per timing, median of 7)
 and alone after a 768 MiB scrub (median of 8).  One JSON line."""
@@ -44,7 +43,6 @@ def main():
              "window": lambda w: tune.stable_pass(w, 15, 0, xcd_chunk=True),
              "window_no_store": lambda w: tune.stable_pass(w, 15, 0, xcd_chunk=True, no_store=True),
              "window_plane_stores": lambda w: tune.stable_pass(w, 40, 0, xcd_chunk=True),
-             "window_deferred": lambda w: tune.stable_pass(w, 41, 0, xcd_chunk=True),
              "whole_no_store": lambda w: tune.stable_pass(w, 14, 0, xcd_chunk=True, no_store=True),
              "sync": lambda w: hip.stable_pass(w, "sync"),
              "signal": lambda w: hip.stable_pass(w, "signal")}

@@ -167,20 +167,17 @@ int lifeapi_tune_stable_pass(uint64_t *d_planes, uint8_t *d_flags, size_t n, int
   // with every round on the whole columns / the rounds after the first on
   // the window, columns stashed in LDS (k_stable<5, PW, SW>)
   // pass 40: Propagate as 15, each plane's dirty line stored only where the
-  // plane changed (k_stable<4, true, false, true>); 41: as 15 with the first
-  // step's tests deferred (k_stable<4, true, false, false, true>)
-  if (!d_planes || !d_flags || !aligned8(d_planes) || pass < 0 || (pass > 15 && pass != 40 && pass != 41))
+  // plane changed (k_stable<4, true, false, true>)
+  if (!d_planes || !d_flags || !aligned8(d_planes) || pass < 0 || (pass > 15 && pass != 40))
     return fail(LIFEAPI_E_INVALID, "bad argument to lifeapi_tune_stable_pass%s");
   int cus = 0, rc = device_cus(cus);
   if (rc != LIFEAPI_OK) return rc;
   using Fn = void (*)(uint64_t *, uint8_t *, uint64_t, uint32_t, uint32_t);
-  const Fn fns[18] = {k_stable<0>, k_stable<1>, k_stable<2>, k_stable<3>, k_stable<4>, k_stable<5>,
+  const Fn fns[17] = {k_stable<0>, k_stable<1>, k_stable<2>, k_stable<3>, k_stable<4>, k_stable<5>,
                       k_stable<5, true, false>, k_stable<5, true, true>,
                       k_stable_pf<0>, k_stable_pf<1>, k_stable_pf<2>, k_stable_pf<3>, k_stable_pf<4>, k_stable_pf<5>,
-                      k_stable<4, false>, k_stable<4, true>, k_stable<4, true, false, true>,
-                      k_stable<4, true, false, false, true>};
+                      k_stable<4, false>, k_stable<4, true>, k_stable<4, true, false, true>};
   if (pass == 40) pass = 16;
-  if (pass == 41) pass = 17;
   // blocks_per_cu < 0: uncapped grid, at most -blocks_per_cu blocks resident
   // per CU (unused dynamic LDS out of the CU's 160 KiB)
   unsigned lds = 0;
