@@ -491,3 +491,42 @@ def test_filter_zero_generations_vs_reference(hip, R, port):
         first, _ = hip.step_contains(to_dev(x), to_dev(w[None]), to_dev(u[None]), 0, final=fin)
         assert not first.cpu().numpy().any()
         _check(to_host(fin), exp_fin, "Stepped(0)")
+
+
+@pytest.mark.parametrize("gens", [3, 7, 8, 12, 15, 16, 17])
+def test_filter_window_boundaries_vs_reference(hip, R, port, gens):
+    """The routing edges of the iterated filter: care rows whose light cone
+    needs exactly 8 / 16 / 32 rows or one more (the packed fields, R = 16 / 32
+    windows, none), column windows whose cone is exactly 16 / 32 / 63 columns
+    or one more (P = 16 / 32 / 64 and the whole board), a whole board at the
+    kConeWholeWinGens edge, and 16 / 17 generations (the window passes stop
+    at 15), each across the seams; against the reference's own loop"""
+    n = 389
+    x = port.fill(n, seed=900 + gens) & port.fill(n, seed=950 + gens)
+    cases = []
+    for need in (8, 9, 16, 17, 32, 33):
+        h = need - 2 * gens
+        if h >= 1:
+            cases.append(("rows", h, None))
+    for kc in (16, 17, 32, 33, 63, 64):
+        w = kc - 2 * gens
+        if 1 <= w <= 64:
+            cases.append(("cols", 3, w))
+    cases.append(("whole", 1, 64))
+    for t, (kind, h, w) in enumerate(cases):
+        y0 = (61 + 7 * t) % 64
+        x0 = (62 + 5 * t) % 64
+        rows = np.uint64(sum(1 << ((y0 + i) % 64) for i in range(h)))
+        box = np.zeros(64, np.uint64)
+        if kind == "rows":
+            box[0::3] = rows  # a whole board whose rows may fit a window
+        else:
+            for c in range(w):
+                box[(x0 + c) % 64] = rows
+        src = (17 * t) % n
+        ahead = port.step_batch(x[src:src + 1], max(1, gens // 2))[0]
+        tw, tu = ahead & box, box & ~ahead
+        exp, _ = R.step_contains_batch(x, tw, tu, gens, nthreads=THREADS)
+        first, _ = hip.step_contains(to_dev(x), to_dev(tw[None]), to_dev(tu[None]), gens)
+        got = first.cpu().numpy().astype(np.uint32)
+        assert (got == exp).all(), (gens, kind, h, w, np.nonzero(got != exp)[0][:8])
