@@ -192,7 +192,14 @@ __global__ __launch_bounds__(kBlock) void k_cone(const uint64_t *in, const uint6
 // WIN: from kConeRowsWindowGens generations on, a target whose rows fit
 // 32 (16) takes the window split layout (cone_split.hpp cone_wave_split) on
 // the capped grid instead of the packed row-window passes.
-template <int RMAX, bool FIRST, typename OutT, bool A16 = false, bool DMA = false, bool ROWS = true, bool WIN = false>
+// EARLY (DMA): a whole board's first pass is fetched as soon as the
+// whole-board test passes, so the row-window search runs under it.  1M
+// universes, back to back, against the tuning build's EARLY = false
+// (profiles/r06/ab/early_fetch.jsonl): full-height and random whole boards at
+// 2 generations 0.133 / 0.132 ms against 0.138 / 0.139, the one-row target
+// and 1 generation within +-3 %, small targets unchanged.
+template <int RMAX, bool FIRST, typename OutT, bool A16 = false, bool DMA = false, bool ROWS = true, bool WIN = false,
+          bool EARLY = true>
 __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const uint64_t *__restrict__ wanted,
                                                        const uint64_t *__restrict__ unwanted, OutT *__restrict__ out,
                                                        uint64_t n, uint32_t gens, uint32_t kmax, uint32_t cap_waves) {
@@ -215,12 +222,17 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
     __shared__ uint64_t img_all[kWavesPerBlock][RMAX * kWave];
     uint64_t *img = img_all[__builtin_amdgcn_readfirstlane(threadIdx.x / kWave)];
     const uint64_t c = 2 * RMAX;
-    // (round 5 fetched a whole board's first pass before these tests when the
-    // last launch on the same target pointers had reported one; round 6 reads
-    // no report)
+    // (round 5 fetched a whole board's first pass before the whole-board test
+    // when the last launch on the same target pointers had reported one;
+    // round 6 reads no report and fetches it right after that test, DESIGN.md
+    // 3.2)
     int pk = 0;
     uint32_t y0 = 0;
     if (cone_whole(care_col, g)) {
+      // (not before a pass that loads by itself: the window split layout)
+      const bool early = EARLY && kmax >= (uint32_t)kWave && wave * c < n &&
+                         !(WIN && FIRST && gens >= kConeWholeWinGens);
+      if (early) dma_fetch_pass<RMAX>(in, n, wave * c, lane, img);
       if constexpr (FIRST) pk = cone_rows(care_col, gens, y0);
       if (kmax < (uint32_t)kWave) return;
       if constexpr (FIRST && WIN) {
@@ -236,7 +248,7 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
       if constexpr (FIRST && ROWS) {
         auto rows = [&](auto pk_c, auto wrap_c) __attribute__((always_inline)) {
           cone_wave_rows_dma<RMAX, decltype(pk_c)::value, decltype(wrap_c)::value>(
-              in, w64, m64, out, n, wave * c, nw * c, gens, y0, lane, img, false);
+              in, w64, m64, out, n, wave * c, nw * c, gens, y0, lane, img, early);
         };
         using T = std::true_type;
         using F = std::false_type;
@@ -247,7 +259,7 @@ __global__ __launch_bounds__(kBlock) void k_cone_adapt(const uint64_t *in, const
         if (pk == 2) return y0 >= 32u ? rows(P2{}, T{}) : rows(P2{}, F{});
         if (pk == 1) return y0 >= 32u ? rows(P1{}, T{}) : rows(P1{}, F{});
       }
-      return cone_wave_full_dma<RMAX, FIRST>(in, w64, m64, out, n, wave * c, nw * c, gens, lane, img, false);
+      return cone_wave_full_dma<RMAX, FIRST>(in, w64, m64, out, n, wave * c, nw * c, gens, lane, img, early);
     }
     if (cap_waves) {
       if (wave >= cap_waves) return;
@@ -395,7 +407,7 @@ int launch_cone(const uint64_t *d_in, const uint64_t *d_wanted, const uint64_t *
 // when the batch is 16-byte aligned, on a grid of at most dma_blocks_per_cu
 // blocks per CU (0: uncapped; blocks_per_cu then caps the waves of a
 // windowed target).
-template <int RMAX, bool FIRST, typename OutT, bool DMA = false, bool ROWS = true, bool WIN = false>
+template <int RMAX, bool FIRST, typename OutT, bool DMA = false, bool ROWS = true, bool WIN = false, bool EARLY = true>
 int launch_cone_adapt(const uint64_t *d_in, const uint64_t *d_wanted, const uint64_t *d_unwanted, OutT *d_out,
                       size_t n, uint32_t gens, int cus, hipStream_t stream, int blocks_per_cu,
                       uint32_t kmax = kWave, int dma_blocks_per_cu = 0) {
@@ -403,7 +415,7 @@ int launch_cone_adapt(const uint64_t *d_in, const uint64_t *d_wanted, const uint
   if constexpr (DMA) {
     if (aligned16(d_in)) {
       const uint32_t cap_waves = blocks_per_cu > 0 ? (uint32_t)(cus * blocks_per_cu * kWavesPerBlock) : 0u;
-      hipLaunchKernelGGL((k_cone_adapt<RMAX, FIRST, OutT, true, true, ROWS, WIN>),
+      hipLaunchKernelGGL((k_cone_adapt<RMAX, FIRST, OutT, true, true, ROWS, WIN, EARLY>),
                          dim3(grid_for((n + 15) / 16, cus, dma_blocks_per_cu)), dim3(kBlock), 0, stream, d_in,
                          d_wanted, d_unwanted, d_out, (uint64_t)n, gens, kmax, cap_waves);
       return launched("k_cone_adapt launch");

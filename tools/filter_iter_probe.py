@@ -106,6 +106,7 @@ def forms(x, tw, tu, gens):
     # passes (cone_wave_rows) against the window split layout (cone_split.hpp)
     # the 1-2 generation filter's LDS form on the capped grid (no report needed)
     fs["dma_capped16"] = lambda: tune.cone(x, tw, tu, gens, 16003, 8, first=True)
+    fs["dma_capped16_late"] = lambda: tune.cone(x, tw, tu, gens, 16010, 8, first=True)  # (no early fetch)
     fs["dma_capped8"] = lambda: tune.cone(x, tw, tu, gens, 8003, 8, first=True)
     fs["rows_capped"] = lambda: tune.cone(x, tw, tu, gens, 16000, 8, first=True)
     fs["win_capped"] = lambda: tune.cone(x, tw, tu, gens, 16008, 8, first=True)

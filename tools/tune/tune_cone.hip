@@ -23,6 +23,10 @@ int cone_by_shape(const uint64_t *in, const uint64_t *w, const uint64_t *u, OutT
   // upw 3: upw 1 with the whole-board grid capped at `cap` blocks per CU
   if (upw == 3 && rmax == 8)
     return launch_cone_adapt<8, FIRST, OutT, true>(in, w, u, out, n, gens, cus, st, 0, kWave, cap);
+  // upw 10: upw 3 with the whole board's first pass fetched only after the
+  // row-window search (EARLY = false)
+  if (upw == 10 && rmax == 8)
+    return launch_cone_adapt<8, FIRST, OutT, true, true, false, false>(in, w, u, out, n, gens, cus, st, 0, kWave, cap);
   // (upw 4, 5, 9: round 5's forms told the last launch report; removed with it)
   // upw 7: upw 0 (the capped form) without the row-window passes
   if (upw == 7 && rmax == 8)
