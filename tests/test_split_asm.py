@@ -127,7 +127,7 @@ def test_simulated_windowed_contains(port, h, late):
     assert (got == _to_split(_rot_rows(s, y0))).all()
 
 
-@pytest.mark.parametrize("lay,h", [("high", h) for h in range(1, 8)] + [("low", h) for h in range(1, g.LOW_H + 1)])
+@pytest.mark.parametrize("lay,h", [("high", h) for h in range(1, 9)] + [("low", h) for h in range(1, g.LOW_H + 1)])
 def test_simulated_batched_contains(port, h, lay):
     """split_contains_asm_batch_h<h> / _batch_lo (the test batched over eight
     generations: a nibble per generation, one DPP lane OR and one scalar
@@ -179,3 +179,31 @@ def test_batched_dpp_chain_reaches_lane_63():
         for line in g.batch_chain():
             g._dpp(v, line)
         assert v[a, 63] == 1 << (lane % 32), lane
+
+
+@pytest.mark.parametrize("rows", [0x1111111111111111, 0x8000400020001001, (1 << 64) - 1])
+def test_simulated_batched_contains_any_target(port, rows):
+    """split_contains_asm_batch_h8 on targets with no row window (care rows
+    every fourth row, five scattered rows, every row): each generation's OR
+    of differences folded onto a nibble before the block's lane OR; against
+    the oracle's step-then-Contains loop at every remainder of 8"""
+    care = np.zeros(64, np.uint64)
+    for c in (3, 17, 40, 63):
+        care[c] = np.uint64(rows)
+    base = port.fill(1, seed=4242)[0]
+    wanted = port.step_batch(base[None], 11)[0] & care
+    unwanted = care & ~wanted
+    x = np.stack([base, port.step_batch(base[None], 3)[0], port.step_batch(base[None], 8)[0],
+                  port.fill(1, seed=4343)[0]])
+    W, M = _to_split(np.stack([wanted] * 4)), _to_split(np.stack([wanted | unwanted] * 4))
+    for gens in (0, 1, 5, 8, 9, 11, 16, 19):
+        exp, s = [0] * 4, x.copy()
+        for k in range(1, gens + 1):
+            s = port.step_batch(s, 1)
+            for u in range(4):
+                if not exp[u] and (((s[u] ^ wanted) & (wanted | unwanted)) == 0).all():
+                    exp[u] = k
+        got, hits = g.simulate_batch(_to_split(x), W, M, gens, g.S)
+        assert hits == exp, (hex(rows), gens, hits, exp)
+        assert (got == _to_split(s)).all()
+    assert exp[0] == 11 and exp[1] == 8 and exp[2] == 3, exp

@@ -545,12 +545,19 @@ def simulate_contains(r, w, m, gens, lean=False, h=S, late=False):
 # The block word needs one register, free in both layouts: w[7] (h <= 7) or
 # v60 (low).
 ACC_HI, ACC_LO = 60, 60
+# h = 8 (any target: every register differenced, w[7] in v60 taken): the
+# block word in v68, one VGPR past the lean loop's 68; each generation's OR
+# of differences is folded onto its low nibble first (rotates by 16, 8, 4:
+# the universe index, bit & 3, is kept), 6 VALU, then packed as above
+ACC_H8 = 68
 KB = 8             # generations per block
 BATCH_MAX_H = 7
 OR2 = 0xFC         # a | b
 
 
-def _acc():
+def _acc(h=None):
+    if _LAYOUT["name"] == "high" and h == S:
+        return ACC_H8
     return {"low": ACC_LO, "high": ACC_HI}[_LAYOUT["name"]]
 
 
@@ -565,9 +572,28 @@ def _or_into(d, dst, al):
     return lines + [op(dst, a, b, c, OR3)]
 
 
+def batch_x_full(k, al):
+    """batch_x for h = 8: the eight differences OR-ed in place (their
+    temps reused), folded onto the low nibble, then packed"""
+    acc = _acc(S)
+    wr, mr = _wm()
+    d = [al.get(j) for j in range(S)]
+    lines = [op(d[j], R[j], wr[j], mr[j], DIFF) for j in range(S)]
+    x, t = d[6], d[7]
+    lines += [op(d[0], d[0], d[1], d[2], OR3), op(d[3], d[3], d[4], d[5], OR3), op(x, d[6], t, d[0], OR3),
+              op(x, x, d[3], d[3], OR3)]
+    for sh in (16, 8, 4):
+        lines += [f"v_alignbit_b32 v{t}, v{x}, v{x}, {sh}", op(x, x, t, t, OR3)]
+    if k == 0:
+        return lines + [f"v_and_b32 v{acc}, 15, v{x}"]
+    return lines + [f"v_and_b32 v{t}, 15, v{x}", f"v_lshl_or_b32 v{acc}, v{t}, {4 * k}, v{acc}"]
+
+
 def batch_x(h, k, al):
     """generation k of the block: ACC = x_k (k = 0) or ACC |= x_k << 4k,
     x_k = OR_j (r_j ^ w_j) & m_j over the h care registers"""
+    if h == S:
+        return batch_x_full(k, al)
     acc = _acc()
     wr, mr = _wm()
     if h == 1 and k == 0:
@@ -582,9 +608,9 @@ def batch_x(h, k, al):
     return lines + _or_into(d, x, al) + [f"v_lshl_or_b32 v{acc}, v{x}, {4 * k}, v{acc}"]
 
 
-def batch_chain():
+def batch_chain(h=None):
     """the lane OR of the block word into lane 63 (six in-place DPP ORs)"""
-    a = _acc()
+    a = _acc(h)
     return [f"v_or_b32_dpp v{a}, v{a}, v{a} row_shr:{n} row_mask:0xf bank_mask:0xf" for n in (1, 2, 4, 8)] + \
            [f"v_or_b32_dpp v{a}, v{a}, v{a} row_bcast:15 row_mask:0xa bank_mask:0xf",
             f"v_or_b32_dpp v{a}, v{a}, v{a} row_bcast:31 row_mask:0xc bank_mask:0xf"]
@@ -616,14 +642,14 @@ def batch_slowpath(lbl, back):
 def batch_block(h):
     """eight generations; the first carries the previous block's lane OR and
     scalar test between its h-layer's VALU"""
-    acc = _acc()
+    acc = _acc(h)
     out = []
     for k in range(KB):
         b = body(DEFAULT)
         if k:
             b.remove("s_sub_u32 %[g], %[g], 1")
         else:   # the pending chain, two VALU apart (DPP reads a fresh VGPR after 2 wait states)
-            chain = batch_chain() + [f"v_readlane_b32 %[rl], v{acc}, 63"]
+            chain = batch_chain(h) + [f"v_readlane_b32 %[rl], v{acc}, 63"]
             valu = [i for i, l in enumerate(b) if l.startswith("v_")]
             pos = {valu[2 * i]: c for i, c in enumerate(chain[:6])}
             pos[valu[13]] = chain[6]
@@ -644,11 +670,11 @@ def batch_block(h):
 
 
 def batch_text(h):
-    acc = _acc()
-    assert 1 <= h <= {"low": LOW_H, "high": BATCH_MAX_H}[_LAYOUT["name"]]
+    acc = _acc(h)
+    assert 1 <= h <= {"low": LOW_H, "high": S}[_LAYOUT["name"]]
     lean = [l.replace("%[g]", "%[rem]") for l in contains_body(True, h)]
     flush = []
-    for c in batch_chain():
+    for c in batch_chain(h):
         flush += [c, "s_nop 1"]
     flush += [f"v_readlane_b32 %[rl], v{acc}, 63"] + batch_check(10, 11)
     return (["s_cmp_eq_u32 %[g], 0", "s_cbranch_scc1 2f"] + prologue(DEFAULT) +
@@ -675,13 +701,13 @@ def emit_batch(h):
                     [f'"{{v{mr[j]}}}"(m[{j}])' for j in range(nt)] +
                     [f'[m{u}] "s"(0x11111111u << {u})' for u in range(P)])
     used = set(wr[:nt] + mr[:nt])
-    extra = {"low": [ACC_LO], "high": W_REGS + M_REGS}[lay]
+    extra = {"low": [ACC_LO], "high": W_REGS + M_REGS + ([ACC_H8] if h == S else [])}[lay]
     pinned = sorted({x for x in L + RR + H1 + H0 + [H0U, H0D, H1U, H1D] + TEMPS + extra} - used)
     clob = ", ".join(f'"v{x}"' for x in pinned)
     name = {"low": "split_contains_asm_batch_lo", "high": f"split_contains_asm_batch_h{h}"}[lay]
     note = {"low": ";\n// the low register layout (any target of at most 4 rows)", "high": ""}[lay]
     return f"""
-// The lean test batched over eight generations (rows 0..{h - 1}): per block one
+// The lean test batched over eight generations ({"any target" if h == S else f"rows 0..{h - 1}"}): per block one
 // lane OR (DPP) and one scalar test of a word holding a nibble per generation{note}.
 __device__ __forceinline__ void {name}(uint32_t (&r)[8], const uint32_t (&w)[8],
                                    const uint32_t (&m)[8], uint32_t gens, uint32_t a_self,
@@ -816,6 +842,9 @@ def simulate_batch(r, w, m, gens, h):
                 assert bsel < 8
                 out |= ((src >> np.uint64(8 * bsel)) & np.uint64(0xFF)) << np.uint64(8 * i)
             v[d] = out.astype(np.uint32)
+        elif mn == "v_and_b32":
+            d, a = int(args[0].strip()[1:]), int(args[2].strip()[1:])
+            v[d] = v[a] & np.uint32(int(args[1]))
         elif mn == "v_lshl_or_b32":
             d, a = (int(x) for x in re.findall(r"v(\d+)", l)[:2])
             c = int(re.findall(r"v(\d+)", l)[2])
@@ -948,7 +977,7 @@ _SIG_TWO = "(uint32_t (&a)[8], uint32_t (&b)[8], uint32_t gens, uint32_t a_self,
 # what the product include defines: the step loop, the full lean test (any
 # target), the batched test for windows of 5..7 rows and, in the low layout,
 # for windows of at most 4 rows; everything else is the tuning build's
-PRODUCT_BATCH_H = range(LOW_H + 1, BATCH_MAX_H + 1)
+PRODUCT_BATCH_H = list(range(LOW_H + 1, BATCH_MAX_H + 1)) + [S]
 
 
 def _ablation_decls():
@@ -982,8 +1011,10 @@ def emit():
 // (schedule "{VARIANTS[0]}").  The same loop with the fused Contains test
 // (k_step_contains_split): split_contains_asm_batch_lo (a target window of at
 // most 4 rows, the test batched over eight generations, 61 VGPRs pinned),
-// split_contains_asm_batch_h<5..7> (windows of 5..7 rows, 68 pinned) and
-// split_contains_asm_lean (any target, per generation, 68 pinned).  The measured
+// split_contains_asm_batch_h<5..7> (windows of 5..7 rows, 68 pinned),
+// split_contains_asm_batch_h8 (any target, each generation's differences
+// folded onto a nibble, 69 pinned) and split_contains_asm_lean (any target,
+// per generation, 68 pinned).  The measured
 // alternatives (other schedules, two groups per wave, the round-1 contains
 // bookkeeping, the per-generation test on narrower windows, a late scalar
 // test) are generated into tools/tune/split_asm_tune.inc for the tuning
