@@ -481,14 +481,11 @@ constexpr int kContainsLo = 7, kContainsHi = 8;
 // VGPRs (7 waves per SIMD), which costs the low layout nothing measurable
 // (6 above: the low layout's occupancy alone gained nothing)
 constexpr int kContainsAll = 9;
-// Targets with no row window of at most 7 rows (kContainsHi and
-// kContainsAll): the test batched over eight generations with each
-// generation's differences folded onto a nibble (split_asm.inc
-// split_contains_asm_batch_h8) instead of the lean per-generation test;
-// LIFE_BATCH_H8=0 builds the A/B without it
-#ifndef LIFE_BATCH_H8
-#define LIFE_BATCH_H8 1
-#endif
+// (Measured, commit 5278498: targets with no row window of at most 7 rows
+// batched over eight generations, each generation's differences folded onto
+// a nibble, instead of the lean per-generation test -- no gain, 1M x 3-13
+// generations within -2 .. +3 %, profiles/r06/batch_h8_ab/; the lean test
+// stays.  tools/tune/split_asm_tune.inc keeps split_contains_asm_batch_h8.)
 // the light-cone path of kContainsLo (cone_max below): universes per wave chunk
 // (Measured in the compiler's allocation, not shipped: the whole board in the
 // natural layout for wider cones at <= 4 generations -- 10-35 % faster there
@@ -1010,14 +1007,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) voi
       if (h == 5) LIFEAPI_RUN(split_contains_asm_batch_h5);
       else if (h == 6) LIFEAPI_RUN(split_contains_asm_batch_h6);
       else if (h == 7) LIFEAPI_RUN(split_contains_asm_batch_h7);
-      else if (LIFE_BATCH_H8) LIFEAPI_RUN(split_contains_asm_batch_h8);
       else LIFEAPI_RUN(split_contains_asm_lean);
     } else if constexpr (ASM == kContainsAll) {
       if (h <= kLowRows) LIFEAPI_RUN(split_contains_asm_batch_lo);
       else if (h == 5) LIFEAPI_RUN(split_contains_asm_batch_h5);
       else if (h == 6) LIFEAPI_RUN(split_contains_asm_batch_h6);
       else if (h == 7) LIFEAPI_RUN(split_contains_asm_batch_h7);
-      else if (LIFE_BATCH_H8) LIFEAPI_RUN(split_contains_asm_batch_h8);
       else LIFEAPI_RUN(split_contains_asm_lean);
     } else if constexpr (ASM == 7) {
       LIFEAPI_RUN(split_contains_asm_batch_lo);

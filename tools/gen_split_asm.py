@@ -977,7 +977,7 @@ _SIG_TWO = "(uint32_t (&a)[8], uint32_t (&b)[8], uint32_t gens, uint32_t a_self,
 # what the product include defines: the step loop, the full lean test (any
 # target), the batched test for windows of 5..7 rows and, in the low layout,
 # for windows of at most 4 rows; everything else is the tuning build's
-PRODUCT_BATCH_H = list(range(LOW_H + 1, BATCH_MAX_H + 1)) + [S]
+PRODUCT_BATCH_H = range(LOW_H + 1, BATCH_MAX_H + 1)
 
 
 def _ablation_decls():
@@ -1011,10 +1011,8 @@ def emit():
 // (schedule "{VARIANTS[0]}").  The same loop with the fused Contains test
 // (k_step_contains_split): split_contains_asm_batch_lo (a target window of at
 // most 4 rows, the test batched over eight generations, 61 VGPRs pinned),
-// split_contains_asm_batch_h<5..7> (windows of 5..7 rows, 68 pinned),
-// split_contains_asm_batch_h8 (any target, each generation's differences
-// folded onto a nibble, 69 pinned) and split_contains_asm_lean (any target,
-// per generation, 68 pinned).  The measured
+// split_contains_asm_batch_h<5..7> (windows of 5..7 rows, 68 pinned) and
+// split_contains_asm_lean (any target, per generation, 68 pinned).  The measured
 // alternatives (other schedules, two groups per wave, the round-1 contains
 // bookkeeping, the per-generation test on narrower windows, a late scalar
 // test) are generated into tools/tune/split_asm_tune.inc for the tuning
@@ -1043,11 +1041,13 @@ def emit_tune():
 // (split_contains_asm); the per-generation lean test on windows of 1..7 rows
 // (split_contains_asm_lean_h<h>, and _lo in the low layout), with its scalar
 // part late (split_contains_asm_lean_late[_h<h>]); the batched test in the
-// full layout on windows of 1..4 rows (split_contains_asm_batch_h<1..4>).
+// full layout on windows of 1..4 rows (split_contains_asm_batch_h<1..4>) and
+// on any target, differences folded onto a nibble (split_contains_asm_batch_h8:
+// no gain over the lean test, profiles/r06/batch_h8_ab/).
 #pragma once
 
 namespace lifeapi_impl {{
-{fns}{emit2()}{emit_contains()}{"".join(emit_contains(True, h) for h in range(1, S))}{"".join(emit_contains(True, h, True) for h in range(1, S + 1))}{"".join(emit_batch(h) for h in range(1, LOW_H + 1))}{_low_lean()}
+{fns}{emit2()}{emit_contains()}{"".join(emit_contains(True, h) for h in range(1, S))}{"".join(emit_contains(True, h, True) for h in range(1, S + 1))}{"".join(emit_batch(h) for h in list(range(1, LOW_H + 1)) + [S])}{_low_lean()}
 }}  // namespace lifeapi_impl
 """
 
