@@ -530,3 +530,122 @@ def test_filter_window_boundaries_vs_reference(hip, R, port, gens):
         first, _ = hip.step_contains(to_dev(x), to_dev(tw[None]), to_dev(tu[None]), gens)
         got = first.cpu().numpy().astype(np.uint32)
         assert (got == exp).all(), (gens, kind, h, w, np.nonzero(got != exp)[0][:8])
+
+
+def _stable_next_nodes(R, port, n, seed):
+    """LifeStables as a search meets them: still lifes with an unknown window
+    (anywhere, across the row and column seams, 4-44 rows tall), propagated
+    to their fixpoint by the reference, then one unknown cell decided ON or
+    OFF -- Propagate from there changes rows near that cell (the window
+    steps, stable_kernels.hpp stable_iter_window), or, in tall windows,
+    more rows than the window holds (the whole-column fallback)"""
+    rng = np.random.default_rng(seed)
+    blocks = port.parse("2o$2o!")
+    x = np.zeros((n, 10, 64), np.uint64)
+    for u in range(n):
+        st = np.zeros(64, np.uint64)
+        for _ in range(int(rng.integers(3, 9))):
+            bx, by = int(rng.integers(16)) * 4, int(rng.integers(16)) * 4
+            st |= np.roll(blocks, bx) << np.uint64(by) | (np.roll(blocks, bx) >> np.uint64((64 - by) % 64) if by else 0)
+        w0, h0 = int(rng.integers(3, 24)), int(rng.integers(4, 45))
+        x0, y0 = int(rng.integers(64)), int(rng.integers(64))
+        rows = np.uint64(sum(1 << ((y0 + i) % 64) for i in range(h0)))
+        unk = np.zeros(64, np.uint64)
+        for c in range(w0):
+            unk[(x0 + c) % 64] = rows
+        x[u, 0], x[u, 1] = st & ~unk, unk
+        obj = np.ascontiguousarray(x[u].reshape(640))
+        R.stable_pass(obj, 4)  # the parent: propagated to its fixpoint
+        x[u] = obj.reshape(10, 64)
+        cols = np.nonzero(x[u, 1])[0]
+        if cols.size:
+            c = int(rng.choice(cols))
+            bits = [b for b in range(64) if (int(x[u, 1, c]) >> b) & 1]
+            b = int(rng.choice(bits))
+            x[u, 1, c] &= ~np.uint64(1 << b)
+            if rng.random() < 0.5:
+                x[u, 0, c] |= np.uint64(1 << b)  # decided ON
+            else:
+                x[u, 0, c] &= ~np.uint64(1 << b)  # decided OFF
+    return x.reshape(n, 640)
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_stable_next_node_passes_vs_reference(hip, R, port, seed):
+    """Propagate (its steps after the first on a 32-row window, or the whole
+    columns when the changed rows do not fit), StabiliseOptions and
+    PropagateStep on next nodes against the reference's own LifeStable
+    members (LifeStable.hpp:677-729), object by object: planes and the
+    PropagateResult flags, on both alignments"""
+    n = 160
+    x = _stable_next_nodes(R, port, n, 500 + seed)
+    for name, which in (("propagate", 4), ("stabilise", 5), ("step", 3)):
+        want, wfl = x.copy(), np.zeros(n, np.uint8)
+        for u in range(n):
+            obj = np.ascontiguousarray(want[u])
+            wfl[u] = R.stable_pass(obj, which)
+            want[u] = obj
+        for aligned in (True, False):
+            if aligned:
+                d = to_dev(x).reshape(n, 640)
+            else:
+                t8 = torch.zeros(x.size + 1, dtype=torch.int64, device="cuda")
+                d = t8[1:].view(n, 640)
+                d.copy_(to_dev(x).reshape(n, 640))
+            fl = hip.stable_pass(d, name).cpu().numpy()
+            got = to_host(d).reshape(n, 640)
+            bad = np.nonzero((got != want).any(axis=1) | (fl != wfl))[0]
+            assert bad.size == 0, (name, aligned, bad[:8], fl[bad[:4]], wfl[bad[:4]])
+
+
+def test_propagate_cascades_vs_reference(hip, R, port):
+    """Propagate on LifeStables whose fixpoint takes many steps: still lifes
+    (blocks, beehives, loaves, boats, tubs on an 8-cell lattice) under a
+    large unknown region (10-40 rows and columns, across the seams) with a
+    few of its cells decided ON or OFF, so that forcing chains run through
+    the region step after step -- the windowed steps (a window of the rows
+    within 2 RHO = 6 of the previous step's changes, the band within RHO = 3
+    trusted) must reach the reference's fixpoint and flags exactly; both
+    alignments"""
+    rng = np.random.default_rng(8080)
+    pats = [port.parse(t) for t in ("2o$2o!", "b2o$o2bo$b2o!", "b2o$o2bo$bobo$2bo!", "2o$obo$bo!", "bo$obo$bo!")]
+    n = 400
+    x = np.zeros((n, 10, 64), np.uint64)
+    for u in range(n):
+        st = np.zeros(64, np.uint64)
+        for gx in range(8):
+            for gy in range(8):
+                if rng.random() < 0.55:
+                    pt = pats[int(rng.integers(len(pats)))]
+                    st |= np.roll(pt, 8 * gx + 1) << np.uint64(8 * gy + 1)
+        unk = np.zeros(64, np.uint64)
+        y0, h = int(rng.integers(64)), int(rng.integers(10, 41))
+        rows = np.uint64(sum(1 << ((y0 + i) % 64) for i in range(h)))
+        x0, w = int(rng.integers(64)), int(rng.integers(10, 41))
+        for c in range(w):
+            unk[(x0 + c) % 64] = rows
+        state = st & ~unk
+        for _ in range(int(rng.integers(1, 4))):  # decided cells inside the region
+            c, b = (x0 + int(rng.integers(w))) % 64, (y0 + int(rng.integers(h))) % 64
+            unk[c] &= ~np.uint64(1 << b)
+            if rng.random() < 0.5:
+                state[c] |= np.uint64(1 << b)
+        x[u, 0], x[u, 1] = state, unk
+    x = x.reshape(n, 640)
+    want, wfl = x.copy(), np.zeros(n, np.uint8)
+    for u in range(n):
+        obj = np.ascontiguousarray(want[u])
+        wfl[u] = R.stable_pass(obj, 4)
+        want[u] = obj
+    assert (wfl & 1).sum() > n // 10, int((wfl & 1).sum())  # consistent ones among them
+    for aligned in (True, False):
+        if aligned:
+            d = to_dev(x).reshape(n, 640)
+        else:
+            t8 = torch.zeros(x.size + 1, dtype=torch.int64, device="cuda")
+            d = t8[1:].view(n, 640)
+            d.copy_(to_dev(x).reshape(n, 640))
+        fl = hip.stable_pass(d, "propagate").cpu().numpy()
+        got = to_host(d).reshape(n, 640)
+        bad = np.nonzero((got != want).any(axis=1) | (fl != wfl))[0]
+        assert bad.size == 0, (aligned, bad[:8], fl[bad[:4]], wfl[bad[:4]])
