@@ -14,6 +14,7 @@ own RandomState(), or are hand-placed seam cases.  The fixtures are data only
 """
 from __future__ import annotations
 
+import glob
 import json
 import os
 import sys
@@ -551,8 +552,26 @@ def rle_fixture():
                         parse_text=ptext, parse_offsets=poff, parsed=parsed)
 
 
+def stable_window_fixture():
+    """stable_window.npz: LifeStables on which Propagate's window width
+    matters -- found by tools/stable_window_mutant_search.py on the GPU (the
+    shipped library against a build trusting only 1 row of the window;
+    inputs kept in stable_window_inputs/) -- with the reference's own
+    Propagate (LifeStable.hpp:718-729) planes and flags"""
+    xs = [np.load(f) for f in sorted(glob.glob(os.path.join(HERE, "stable_window_inputs", "*.npy")))]
+    x = np.concatenate(xs).reshape(-1, 640)
+    out, flags = x.copy(), np.zeros(len(x), np.uint8)
+    for u in range(len(x)):
+        obj = np.ascontiguousarray(out[u])
+        flags[u] = R.stable_pass(obj, 4)
+        out[u] = obj
+    np.savez_compressed(os.path.join(HERE, "stable_window.npz"), input=x, propagate=out, flags=flags)
+
+
 if __name__ == "__main__":
-    if "--only-rle" in sys.argv:
+    if "--only-stable-window" in sys.argv:
+        stable_window_fixture()
+    elif "--only-rle" in sys.argv:
         rle_fixture()
     elif "--only-digests" in sys.argv:  # refresh golden.json["digests"] only
         gj = os.path.join(HERE, "golden.json")

@@ -947,3 +947,23 @@ def test_filter_whole_board_row_windows(hip, port, rows, gens_list):
                 torch.cuda.synchronize()
                 got = first.cpu().numpy().astype(np.uint32)
                 assert (got == res).all(), (rows, gens, call, int(w.any()), int((got != res).sum()))
+
+
+def test_propagate_window_sensitive_fixture(hip):
+    """Propagate on the LifeStables of tests/golden/stable_window.npz --
+    next nodes on which a window trusting fewer rows than the analysis's
+    RHO = 3 goes wrong (found by tools/stable_window_mutant_search.py) --
+    against the reference's answers; both alignments"""
+    import os
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "stable_window.npz"))
+    x, n = g["input"], g["input"].shape[0]
+    for aligned in (True, False):
+        if aligned:
+            d = to_dev(x).reshape(n, 640)
+        else:
+            t8 = torch.zeros(x.size + 1, dtype=torch.int64, device="cuda")
+            d = t8[1:].view(n, 640)
+            d.copy_(to_dev(x).reshape(n, 640))
+        fl = hip.stable_pass(d, "propagate").cpu().numpy()
+        got = to_host(d).reshape(n, 640)
+        assert (got == g["propagate"]).all() and (fl == g["flags"]).all(), aligned

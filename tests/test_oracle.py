@@ -526,3 +526,12 @@ def test_filter_iter_digests_from_the_port(port, meta):
                 want = t["gens"][str(g)]
                 assert int((got > 0).sum()) == want["hits"], (name, g)
                 assert f"{port.digest(got):016x}" == want["first_digest"], (name, g)
+
+
+def test_stable_window_fixture(port):
+    """tests/golden/stable_window.npz (LifeStables on which Propagate's
+    window width matters, with the reference's answers): the restatement's
+    Propagate agrees"""
+    g = load("stable_window.npz")
+    got, fl = port.stable_pass(g["input"], 4)
+    assert (got == g["propagate"]).all() and (fl == g["flags"]).all()
