@@ -68,7 +68,7 @@ def main():
             "norows": lambda: tune.cone(x, tw, tu, gens, 2, 8, first=True),
             "capped": lambda: tune.cone(x, tw, tu, gens, 16000, 8, first=True),
             **({f"probe_s{sl}": (lambda sl=sl: tune.rows_probe(x, tw, tu, gens, (r - gens) & 63, sl))
-                for sl in (0, 2, 8)} if pk == 4 and os.environ.get("PROBE") else {}),
+                for sl in (0, 2, 8)} if os.environ.get("PROBE") else {}),
             "contains": lambda: hip.contains(x, tw, tu),
             "contains_lds": lambda: tune.cone(x, tw, tu, 0, 1, 8, first=False),
         }
