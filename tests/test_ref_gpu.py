@@ -649,3 +649,30 @@ def test_propagate_cascades_vs_reference(hip, R, port):
         got = to_host(d).reshape(n, 640)
         bad = np.nonzero((got != want).any(axis=1) | (fl != wfl))[0]
         assert bad.size == 0, (aligned, bad[:8], fl[bad[:4]], wfl[bad[:4]])
+
+
+def test_propagate_window_at_every_row_offset_vs_reference(hip, R, port):
+    """The window's first row y0 at every offset: next nodes rolled down the
+    torus by each of 0..63 rows (every plane's column words rotated), so that
+    the window steps start on both sides of the columns' 64-row seam and
+    exactly on it (y0 = 0 and 32, where stable_kernels.hpp place_rows leaves
+    one word half to the band mask) -- Propagate and StabiliseOptions against
+    the reference's own members, planes and flags"""
+    base = _stable_next_nodes(R, port, 12, 777).reshape(12, 10, 64)
+    rolled = []
+    for r in range(64):
+        s = np.uint64(r)
+        rolled.append(base if r == 0 else (base << s) | (base >> np.uint64(64 - r)))
+    x = np.ascontiguousarray(np.stack(rolled, 1).reshape(-1, 640))
+    n = x.shape[0]
+    for name, which in (("propagate", 4), ("stabilise", 5)):
+        want, wfl = x.copy(), np.zeros(n, np.uint8)
+        for u in range(n):
+            obj = np.ascontiguousarray(want[u])
+            wfl[u] = R.stable_pass(obj, which)
+            want[u] = obj
+        d = to_dev(x).reshape(n, 640)
+        fl = hip.stable_pass(d, name).cpu().numpy()
+        got = to_host(d).reshape(n, 640)
+        bad = np.nonzero((got != want).any(axis=1) | (fl != wfl))[0]
+        assert bad.size == 0, (name, bad[:8] // 64, bad[:8] % 64, fl[bad[:4]], wfl[bad[:4]])
